@@ -1,0 +1,264 @@
+/*
+ * pdeinv.h — C ABI of the MI355X-native hot path of shenzebang/PDE-inverse-problem.
+ *
+ * The reference is pure Python/JAX: its hot path is XLA-generated code
+ * behind Python callables. Each entry point below replaces one of those callables and
+ * cites the reference interface it stands in for (paths relative to the reference root).
+ *
+ * Conventions:
+ *   - every pointer named d_* / "device" is a device (HBM) pointer owned by the caller;
+ *     the library never allocates on the hot path — workspace sizes are queried first;
+ *   - work is enqueued on the caller's hipStream_t (passed as void*), nothing blocks;
+ *   - return 0 on success, a negative pdeinv_status on failure; the message is in
+ *     pdeinv_last_error() (thread-local). Python maps INVALID -> ValueError,
+ *     UNSUPPORTED -> NotImplementedError, HIP -> RuntimeError, mirroring the reference's
+ *     exception types (…_OU.py:138 ValueError, consistency.py:25 NotImplementedError);
+ *   - all arithmetic the reference does in fp32 is fp32 here; cross-particle sums are
+ *     accumulated fp32 per thread / block and fp64 across blocks;
+ *   - results are deterministic given (seed, counter_offset, particle ids): no float
+ *     atomics, every reduction has a fixed order.
+ *
+ * RNG stream layout (Philox4x32-10, Random123; replaces jax.random threefry, which
+ * cannot be reproduced bit-for-bit without JAX — SURVEY.md §8(c) P7):
+ *   key = {lo32(seed), hi32(seed)}
+ *   simulator normals, update s (0..n_steps) of global particle p, 4-normal block j:
+ *       ctr = {lo32(p), hi32(p), counter_offset + s, j}
+ *   simulator time shift tau0 of particle p:
+ *       ctr = {lo32(p), hi32(p), counter_offset, 0x80000000}
+ *       (McKean–Vlasov: one shared tau0 for the interacting ensemble, p = UINT64_MAX;
+ *        with d_shift_u, u[0] is used)
+ *   Gaussian sampler, sample r (global row), 4-normal block j:
+ *       ctr = {lo32(r), hi32(r), counter_offset, 0x40000000 | j}
+ *   u32 -> uniform:  u = (x >> 8) * 2^-24 in [0,1)
+ *   u32 pair (a,b) -> 2 normals (Box–Muller): u1 = ((a>>8)+1)*2^-24 in (0,1],
+ *       u2 = (b>>8)*2^-24, r = sqrt(-2 ln u1), (r cos 2πu2, r sin 2πu2)
+ *   Philox block j = (x0,x1,x2,x3) yields normals 4j..4j+3 from pairs (x0,x1),(x2,x3).
+ */
+#ifndef PDEINV_H
+#define PDEINV_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PDEINV_ABI_VERSION 1
+#define PDEINV_MAX_DIM 16          /* d (configuration-space dimension) */
+#define PDEINV_MAX_PARAMS 256      /* floats of potential parameters passed by value */
+
+typedef enum {
+  PDEINV_OK = 0,
+  PDEINV_ERR_INVALID = -1,     /* bad argument / shape  -> ValueError          */
+  PDEINV_ERR_UNSUPPORTED = -2, /* unsupported kind/dim  -> NotImplementedError */
+  PDEINV_ERR_HIP = -3          /* HIP runtime failure   -> RuntimeError        */
+} pdeinv_status;
+
+typedef enum {
+  /* grad U(q) = A (q - c); params = A[d*d] row-major, then c[d] (optional, see has_center).
+     KOU: A = tilde_F (…_OU.py:15-19, V_true_fn :130-138). */
+  PDEINV_POT_QUADRATIC = 0,
+  /* GMM: U(x) = -logsumexp_k(-|x-mu_k|^2 / (2 sigma^2)); grad by the analytic softmax form.
+     params = mu[K*d] row-major (core/potential.py:32-61). */
+  PDEINV_POT_GMM = 1,
+  /* McKean–Vlasov quadratic interaction: grad U(q_i) = A (q_i - xbar), xbar read from device
+     (one all-reduced mean per update). params = A[d*d]. */
+  PDEINV_POT_MEANFIELD_QUADRATIC = 2,
+  /* U = 0 (core/potential.py VoidPotential). */
+  PDEINV_POT_NONE = 3
+} pdeinv_potential_kind;
+
+typedef struct {
+  int32_t kind;        /* pdeinv_potential_kind */
+  int32_t n_centers;   /* K for GMM (<= PDEINV_MAX_PARAMS / d) */
+  float sigma;         /* GMM component std (reference: 1, …_GMM.py:76-78) */
+  int32_t has_center;  /* QUADRATIC: params[d*d .. d*d+d) is c */
+  const float* params; /* HOST pointer, copied by value into the kernel arguments */
+} pdeinv_potential;
+
+/* ---------------------------------------------------------------------------------------
+ * Simulator — replaces utils/sampling_utils.py:25-52 underdamped_langevin_dynamics_scan
+ * (vmapped per particle) and its update_step :6-22.
+ *   per particle: tau0 = U*dt; one update of h = tau0, n_steps-1 updates of h = dt, one of
+ *   h = dt - tau0 (total T = n_steps*dt); each update
+ *       p' = p - h*gradU(q) + sqrt(h)*noise_scale*xi - gamma*p*h ;  q' = q + h*p'
+ *   traj[s] is the state after update s (s = 0..n_steps-1), tau[s] = tau0 + s*dt,
+ *   last = state after update n_steps.
+ * Layout: z0 [N, 2d] (x first, v second; row stride ld_z0 floats, >= 2d).
+ *         traj [n_steps, N, 2d] TIME-MAJOR (coalesced stores; the reference's [N, n, 2d]
+ *         is traj.permute(1,0,2)); tau [n_steps, N]; last [N, 2d]. Each output nullable.
+ * Moments (optional, fused — the KFP residual then needs no re-read of traj): when
+ * d_moments != NULL the kernel accumulates, for the three sample sets
+ *   set 0 = z0 ("initial"), set 1 = traj ("0T"), set 2 = last ("terminal"),
+ * the fp64 vector [count, sum z (2d), sum z_i z_j (i<=j, row-major upper triangle)]
+ * (pdeinv_moment_len(2d) doubles per set) into d_moments[3][len]. Requires d_workspace of
+ * pdeinv_sde_workspace_bytes() bytes.
+ * --------------------------------------------------------------------------------------- */
+typedef struct {
+  int64_t n_particles;      /* N in this call (may be 0) */
+  int64_t particle_offset;  /* global id of row 0 (rank sharding: ids are rank-count invariant) */
+  int32_t dim;              /* d, 1..PDEINV_MAX_DIM */
+  int32_t n_steps;          /* n >= 1 */
+  float dt;                 /* T / n */
+  float gamma;              /* friction (KOU 1.0 …_OU.py:21; GMM 0.5 …_GMM.py:17) */
+  float noise_scale;        /* sqrt(2) (sampling_utils.py:14) */
+  int32_t random_shift;     /* 1: tau0 ~ U(0,dt) (reference); 0: tau0 = 0 */
+  uint64_t seed;
+  uint32_t counter_offset;  /* advance by n_steps+1 between calls */
+  int64_t ld_z0;            /* row stride of z0 in floats (0 => 2d) */
+  pdeinv_potential potential;
+  const float* d_noise;     /* nullable: explicit xi [n_steps+1, N, d] (parity mode) */
+  const float* d_shift_u;   /* nullable: explicit u [N] in [0,1) for tau0 = u*dt */
+  const float* d_meanfield; /* MEANFIELD only: xbar [n_steps+1, d] fp32, one row per update */
+} pdeinv_sde_desc;
+
+int pdeinv_moment_len(int m); /* 1 + m + m(m+1)/2 */
+size_t pdeinv_sde_workspace_bytes(const pdeinv_sde_desc* desc);
+int pdeinv_sde_simulate(const pdeinv_sde_desc* desc, const float* d_z0, float* d_traj,
+                        float* d_tau, float* d_last, void* d_workspace, double* d_moments,
+                        void* stream);
+
+/* McKean–Vlasov stepping (one update per call; the mean-field xbar of the current state is
+ * an input so that ranks can all-reduce it between calls — SURVEY.md §8(e)).
+ * Reads z [N,2d] (state before the update), writes z_out [N,2d] (may alias traj row), and
+ * accumulates the fp64 partial [count, sum x (d)] of the NEW positions into d_xsum
+ * (pdeinv_mf_workspace_bytes()). h selects the update kind: 0 = tau0 step, 1 = dt step,
+ * 2 = final dt - tau0 step; s is the update index (RNG counter). */
+size_t pdeinv_mf_workspace_bytes(const pdeinv_sde_desc* desc);
+int pdeinv_mf_step(const pdeinv_sde_desc* desc, int32_t s, const float* d_z, float* d_z_out,
+                   float* d_tau_row, const float* d_tau0, const double* d_xbar_sum,
+                   void* d_workspace, double* d_xsum, void* stream);
+/* tau0 per particle (u*dt from the shift stream, or d_shift_u) -> d_tau0 [N]. */
+int pdeinv_sde_tau0(const pdeinv_sde_desc* desc, float* d_tau0, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Generic moment reduction of a sample set (rows of m floats, row stride ld floats) —
+ * the reduction behind every parametric-quadratic residual term
+ * (methods/consistency_instances/kinetic_fokker_planck.py:33-58) for data that did not come
+ * out of the fused simulator (offline subsample, exact Gaussian samples).
+ * Output: d_out[pdeinv_moment_len(m)] fp64 (count, sums, upper-triangle products).
+ * --------------------------------------------------------------------------------------- */
+size_t pdeinv_moments_workspace_bytes(int64_t n_rows, int32_t m);
+int pdeinv_moments(const float* d_z, int64_t n_rows, int32_t m, int64_t ld, void* d_workspace,
+                   double* d_out, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * KFP residual, parametric quadratic V_theta(x) = x . Dense_d(x) = x^T K x + b^T x
+ * (…_OU.py:209-220), grad V = S x + b, Hessian S = K + K^T.
+ * Replaces kinetic_fokker_planck.py:11-69 value_and_grad_fn for this model: every term of
+ * loss_fn (:33-50) and loss_ground_truth_fn (:52-58) is an expectation of a polynomial of
+ * degree <= 2 in z, so all of them — and d loss / d(K,b) — follow exactly from the three
+ * moment sets (init, 0T, terminal). d_moments: [3][pdeinv_moment_len(2d)] fp64 sums
+ * (possibly all-reduced over ranks). d_theta = [K (d*d, flax layout [in,out]), b (d)] fp32.
+ * Outputs: d_out[PDEINV_KFP_NOUT] fp32, d_grad [d*d + d] fp32 (same layout as theta).
+ * --------------------------------------------------------------------------------------- */
+enum {
+  PDEINV_KFP_LOSS = 0,
+  PDEINV_KFP_LOSS_GT = 1,        /* "loss ground truth" */
+  PDEINV_KFP_GRAD_NORM = 2,
+  PDEINV_KFP_NABLA = 3,          /* E_0T |grad V_theta|^2 */
+  PDEINV_KFP_HESSIAN = 4,        /* E_0T v^T H v */
+  PDEINV_KFP_FRICTION = 5,       /* gamma * E_0T grad V_theta . v */
+  PDEINV_KFP_NABLA_TRUE = 6,     /* E_0T |grad V*|^2 */
+  PDEINV_KFP_INITIAL = 7,        /* E_init grad V_theta . v */
+  PDEINV_KFP_TERMINAL = 8,       /* E_term grad V_theta . v */
+  PDEINV_KFP_NOUT = 9
+};
+
+typedef struct {
+  int32_t dim;
+  float gamma;
+  float total_time;          /* T (divides the boundary terms, :48-50) */
+  const float* tilde_F;      /* HOST [d*d]: grad V* = tilde_F x (V_true, …_OU.py:130-138) */
+} pdeinv_kfp_quad_desc;
+
+int pdeinv_residual_kfp_quadratic(const pdeinv_kfp_quad_desc* desc, const double* d_moments,
+                                  const float* d_theta, float* d_out, float* d_grad,
+                                  void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * KFP residual, parametric GMM V_theta(x) = -logsumexp_k(-|x-mu_k|^2/(2 sigma^2)) with
+ * learnable mu [K,d] (…_GMM.py:214-234), true potential GMM(mu*) (…_GMM.py:94-102).
+ * Fused per-sample forward (grad V, v^T H v, grad V . v, grad V*) and the analytic adjoint
+ * d/d mu (replaces jax.value_and_grad, kinetic_fokker_planck.py:60-61).
+ * Sets: initial [n_init,2d], terminal [n_term,2d], 0T [n_0T,2d], each with its row stride.
+ * Coefficients (c_*) weight the per-sample terms so that the accumulators are the loss and
+ * gradient directly:  loss = sum_0T(c_nabla T1 + c_hess T2 + c_fric T3 + c_true Tt)
+ *                          + c_init sum_init T3 + c_term sum_term T3.
+ * (reference: c_nabla = 1/M, c_hess = -2/M, c_fric = 2 gamma/M, c_true = 1/M,
+ *  c_init = -2/(T B_i), c_term = 2/(T B_t)). The fp64 accumulator d_acc has
+ * PDEINV_GMM_NACC + K*d entries and may be all-reduced before pdeinv_residual_kfp_gmm_finalize.
+ * --------------------------------------------------------------------------------------- */
+enum {
+  PDEINV_GMM_ACC_LOSS = 0,     /* weighted loss (all terms) */
+  PDEINV_GMM_ACC_LOSS_GT = 1,  /* c_true * sum |grad V* - grad V|^2 */
+  PDEINV_GMM_ACC_NABLA = 2,    /* c_true * sum T1 (unweighted mean when c_true = 1/M) */
+  PDEINV_GMM_ACC_HESSIAN = 3,  /* c_true * sum T2 */
+  PDEINV_GMM_ACC_FRICTION = 4, /* c_true * sum T3 */
+  PDEINV_GMM_ACC_NABLA_TRUE = 5,
+  PDEINV_GMM_ACC_INITIAL = 6,  /* sum_init T3 / n_init */
+  PDEINV_GMM_ACC_TERMINAL = 7, /* sum_term T3 / n_term */
+  PDEINV_GMM_NACC = 8
+};
+
+typedef struct {
+  int32_t dim;
+  int32_t n_centers;         /* K of the model */
+  float sigma;               /* model sigma (reference 1) */
+  int32_t n_centers_true;    /* K* */
+  float sigma_true;
+  const float* mus_true;     /* HOST [K* * d] */
+  float gamma;               /* friction (…_GMM.py:17), reported in the FRICTION slot */
+  float c_nabla, c_hess, c_fric, c_true, c_init, c_term;
+} pdeinv_kfp_gmm_desc;
+
+size_t pdeinv_residual_kfp_gmm_workspace_bytes(const pdeinv_kfp_gmm_desc* desc, int64_t n_init,
+                                               int64_t n_term, int64_t n_0T);
+int pdeinv_residual_kfp_gmm(const pdeinv_kfp_gmm_desc* desc, const float* d_init,
+                            int64_t n_init, int64_t ld_init, const float* d_term,
+                            int64_t n_term, int64_t ld_term, const float* d_0T, int64_t n_0T,
+                            int64_t ld_0T, const float* d_mus, void* d_workspace,
+                            double* d_acc, void* stream);
+/* d_acc -> d_out[PDEINV_KFP_NOUT] (same slots as the quadratic residual), d_grad [K*d]. */
+int pdeinv_residual_kfp_gmm_finalize(const pdeinv_kfp_gmm_desc* desc, const double* d_acc,
+                                     float* d_out, float* d_grad, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * GMM potential value and gradient over a batch — GMMPotential.value/.gradient
+ * (core/potential.py:48-61; V_true_fn of …_GMM.py:94-102). Either output nullable.
+ * --------------------------------------------------------------------------------------- */
+int pdeinv_gmm_potential(int32_t dim, int32_t n_centers, float sigma, const float* mus_host,
+                         const float* d_x, int64_t n, int64_t ld, float* d_value,
+                         float* d_grad, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Exact Gaussian sampler — core/distribution.py:52-65 Gaussian.sample: z = C^{1/2} xi + mu.
+ * d_mean [m], d_cov_half [m*m] row-major (device); out [n, m]; rows are global ids
+ * row_offset + r (rank sharding). m <= 2*PDEINV_MAX_DIM.
+ * --------------------------------------------------------------------------------------- */
+int pdeinv_gaussian_sample(int64_t n, int32_t m, uint64_t seed, uint32_t counter_offset,
+                           int64_t row_offset, const float* d_mean, const float* d_cov_half,
+                           float* d_out, void* stream);
+
+/* Raw Philox4x32-10 blocks for the KAT / stream tests: block i uses
+ * ctr = {lo32(i), hi32(i), ctr_z, ctr_w}; out [n_blocks, 4] u32. */
+int pdeinv_philox_fill(uint64_t seed, uint32_t ctr_z, uint32_t ctr_w, int64_t n_blocks,
+                       uint32_t* d_out, void* stream);
+
+/* Strided time/trajectory subsample gather (consistency.py:97-118, offline mode):
+ * out[r*n_t + t] = traj_tm[time_idx[t], traj_idx[r]] for a time-major traj [n, N, m]. */
+int pdeinv_gather_subsample(const float* d_traj, int64_t n_particles, int32_t n_steps,
+                            int32_t m, const int32_t* d_traj_idx, int64_t n_traj_sel,
+                            const int32_t* d_time_idx, int32_t n_time_sel, float* d_out,
+                            void* stream);
+
+int pdeinv_abi_version(void);
+const char* pdeinv_last_error(void);
+/* HIP runtime version the library is running against (detects a second HIP runtime). */
+int pdeinv_runtime_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PDEINV_H */

@@ -1,0 +1,419 @@
+"""NumPy restatement of the reference hot path — CPU ORACLE (test infrastructure only).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this module, and
+only as the checker / CPU baseline. The product package (pde-inverse-problem_amd/) never does.
+
+Parity status: the reference is JAX, which is absent from this image, so no
+reference output can be produced here and the reference ships no golden vectors
+(SURVEY.md §4). This restatement is pinned instead by closed-form known answers:
+  * the exact law of the semi-implicit Euler–Maruyama chain (em_chain_moments), which the
+    sample-path restatement must reproduce — an identity, not a tolerance fit;
+  * the continuous OU moments (ou_mean_cov), i.e. the reference's own odeint solution
+    (…_OU.py:73-106) in closed form, to which the chain converges at O(dt);
+  * the finite-difference checks of the reference's only test script
+    (test_partial_s_log_density.py:241-311), here asserted;
+  * the loss == "loss ground truth" identity in expectation (kinetic_fokker_planck.py:33-58).
+Bit-level parity with JAX's threefry streams is "parity unpinned".
+
+Functions cite the reference file:line they follow (paths relative to the reference root).
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+from scipy.linalg import expm
+
+SQRT2 = math.sqrt(2.0)
+
+
+# --------------------------------------------------------------------------------------
+# simulator: utils/sampling_utils.py:6-52
+# --------------------------------------------------------------------------------------
+def grad_quadratic(A, c=None):
+    """grad U(q) = A (q - c) — V_true_fn of …_OU.py:130-138 is 0.5 x^T tilde_F x."""
+    A = np.asarray(A)
+
+    def g(q):
+        y = q if c is None else q - c
+        return y @ A.T
+
+    return g
+
+
+def gmm_value_grad(x, mus, sigma=1.0):
+    """core/potential.py:32-37: V = -logsumexp_k(-|x-mu_k|^2/(2 sigma^2)), grad = sum_k w_k (x-mu_k)/sigma^2."""
+    x = np.asarray(x)
+    diff = x[..., None, :] - mus  # [..., K, d]
+    a = -np.sum(diff * diff, axis=-1) / (2.0 * sigma * sigma)
+    amax = np.max(a, axis=-1, keepdims=True)
+    e = np.exp(a - amax)
+    den = np.sum(e, axis=-1, keepdims=True)
+    w = e / den
+    value = -(amax[..., 0] + np.log(den[..., 0]))
+    grad = np.sum(w[..., None] * diff, axis=-2) / (sigma * sigma)
+    return value, grad
+
+
+def grad_gmm(mus, sigma=1.0):
+    mus = np.asarray(mus)
+    return lambda q: gmm_value_grad(q, mus, sigma)[1]
+
+
+def update_step(q, p, h, grad_fn, gamma, xi, noise_scale=SQRT2):
+    """utils/sampling_utils.py:6-22 (h may be per-particle [N,1])."""
+    g = grad_fn(q)
+    noise = noise_scale * xi
+    p_new = p - h * g + np.sqrt(h) * noise - gamma * p * h
+    q_new = q + h * p_new
+    return q_new, p_new
+
+
+def sde_scan(z0, n_steps, dt, gamma, grad_fn, xi, u, noise_scale=SQRT2, dtype=np.float64,
+             random_shift=True):
+    """utils/sampling_utils.py:25-52 for all particles at once, with explicit noise.
+
+    z0 [N, 2d]; xi [n_steps+1, N, d] standard normals (update s uses xi[s]); u [N] in [0,1).
+    Returns (last [N,2d], traj [n_steps, N, 2d] time-major, tau [n_steps, N]).
+    """
+    z0 = np.asarray(z0, dtype=dtype)
+    N, m = z0.shape
+    d = m // 2
+    dt = dtype(dt)
+    gamma = dtype(gamma)
+    ns = dtype(noise_scale)
+    q, p = z0[:, :d].copy(), z0[:, d:].copy()
+    tau0 = (np.asarray(u, dtype=dtype) * dt) if random_shift else np.zeros(N, dtype=dtype)
+    traj = np.empty((n_steps, N, m), dtype=dtype)
+    for s in range(n_steps + 1):
+        if s == 0:
+            h = tau0[:, None]
+        elif s == n_steps:
+            h = (dt - tau0)[:, None]
+        else:
+            h = dt
+        q, p = update_step(q, p, h, grad_fn, gamma, np.asarray(xi[s], dtype=dtype), ns)
+        if s < n_steps:
+            traj[s, :, :d] = q
+            traj[s, :, d:] = p
+    last = np.concatenate([q, p], axis=1)
+    tau = (tau0[None, :] + (np.arange(n_steps, dtype=dtype) * dt)[:, None]).astype(dtype)
+    return last, traj, tau
+
+
+# --------------------------------------------------------------------------------------
+# KOU problem constants and analytic moments: example_problems/kinetic_fokker_planck_example_OU.py
+# --------------------------------------------------------------------------------------
+def ou_configuration(tilde_F, gamma=1.0, P_x0=1.0, P_v0=1.0, L_scale=2.0):
+    """…_OU.py:15-70: F = [[0, I], [-tilde_F, -gamma I]], L = diag(0, L_scale I), m0 = 0."""
+    tilde_F = np.asarray(tilde_F, dtype=np.float64)
+    d = tilde_F.shape[0]
+    I = np.eye(d)
+    Z = np.zeros((d, d))
+    F = np.block([[Z, I], [-tilde_F, -gamma * I]])
+    L = np.block([[Z, Z], [Z, L_scale * I]])
+    m0 = np.zeros(2 * d)
+    P0 = np.block([[P_x0 * I, Z], [Z, P_v0 * I]])
+    return dict(gamma_friction=gamma, tilde_F=tilde_F, F=F, L=L, m_0=m0, P_0=P0,
+                m_x_0=np.zeros(d), P_x_0=P_x0 * I)
+
+
+def ou_mean_cov(t, cfg):
+    """Closed form of OU_process (…_OU.py:73-93): m' = F m, P' = F P + P F^T + L.
+
+    m(t) = e^{Ft} m0; P(t) = e^{Ft} P0 e^{F^T t} + int_0^t e^{Fs} L e^{F^T s} ds, the integral by
+    Van Loan's block exponential (exact to rounding, where the reference uses dopri5 odeint).
+    """
+    F, L, m0, P0 = cfg["F"], cfg["L"], cfg["m_0"], cfg["P_0"]
+    n = F.shape[0]
+    E = expm(F * t)
+    blk = np.zeros((2 * n, 2 * n))
+    blk[:n, :n] = -F
+    blk[:n, n:] = L
+    blk[n:, n:] = F.T
+    V = expm(blk * t)
+    Q = V[n:, n:].T @ V[:n, n:]
+    m = E @ m0
+    P = E @ P0 @ E.T + Q
+    return m, 0.5 * (P + P.T)
+
+
+def em_step_matrices(tilde_F, gamma, h, noise_scale=SQRT2):
+    """Exact law of one semi-implicit update with grad U = tilde_F q (sampling_utils.py:17-20):
+    z' = A(h) z + B(h) xi, A = [[I - h^2 F~, h(1-gamma h) I], [-h F~, (1-gamma h) I]], B = sqrt(h) ns [h I; I]."""
+    d = tilde_F.shape[0]
+    I = np.eye(d)
+    A = np.block([[I - h * h * tilde_F, h * (1 - gamma * h) * I], [-h * tilde_F, (1 - gamma * h) * I]])
+    B = math.sqrt(h) * noise_scale * np.vstack([h * I, I])
+    return A, B
+
+
+def em_chain_moments(tilde_F, gamma, dt, n_steps, m0, P0, noise_scale=SQRT2, random_shift=True,
+                     n_gl=8):
+    """Exact mean / second moment of every traj row and of `last` for the chain restated by
+    sde_scan with grad U = tilde_F q, averaged over tau0 = u dt, u ~ U(0,1).
+
+    Entries are polynomials in tau0 of degree <= 8, so n_gl >= 5 Gauss–Legendre nodes are exact.
+    Returns (mean_traj [n,2d], second_traj [n,2d,2d], mean_last [2d], second_last [2d,2d]).
+    """
+    tilde_F = np.asarray(tilde_F, dtype=np.float64)
+    m = 2 * tilde_F.shape[0]
+    nodes, weights = np.polynomial.legendre.leggauss(n_gl)
+    us = 0.5 * (nodes + 1.0) if random_shift else np.array([0.0])
+    ws = 0.5 * weights if random_shift else np.array([1.0])
+    A_dt, B_dt = em_step_matrices(tilde_F, gamma, dt, noise_scale)
+    mean_tr = np.zeros((n_steps, m))
+    sec_tr = np.zeros((n_steps, m, m))
+    mean_last = np.zeros(m)
+    sec_last = np.zeros((m, m))
+    for u, w in zip(us, ws):
+        t0 = u * dt
+        A0, B0 = em_step_matrices(tilde_F, gamma, t0, noise_scale)
+        mu = A0 @ m0
+        P = A0 @ P0 @ A0.T + B0 @ B0.T
+        for s in range(n_steps):
+            if s > 0:
+                mu = A_dt @ mu
+                P = A_dt @ P @ A_dt.T + B_dt @ B_dt.T
+            mean_tr[s] += w * mu
+            sec_tr[s] += w * (P + np.outer(mu, mu))
+        A1, B1 = em_step_matrices(tilde_F, gamma, dt - t0, noise_scale)
+        mu_l = A1 @ mu
+        P_l = A1 @ P @ A1.T + B1 @ B1.T
+        mean_last += w * mu_l
+        sec_last += w * (P_l + np.outer(mu_l, mu_l))
+    return mean_tr, sec_tr, mean_last, sec_last
+
+
+# --------------------------------------------------------------------------------------
+# moments layout of include/pdeinv.h
+# --------------------------------------------------------------------------------------
+def moments(z):
+    """[count, sum z, sum z_i z_j (i<=j)] in fp64."""
+    z = np.asarray(z, dtype=np.float64).reshape(-1, np.shape(z)[-1])
+    m = z.shape[1]
+    iu = np.triu_indices(m)
+    S2 = z.T @ z
+    return np.concatenate([[z.shape[0]], z.sum(0), S2[iu]])
+
+
+def unpack_moments(vec, m):
+    vec = np.asarray(vec, dtype=np.float64)
+    n = vec[0]
+    mean = vec[1:1 + m] / n
+    S = np.zeros((m, m))
+    iu = np.triu_indices(m)
+    S[iu] = vec[1 + m:]
+    S = S + S.T - np.diag(np.diag(S))
+    return n, mean, S / n
+
+
+# --------------------------------------------------------------------------------------
+# KFP residual: methods/consistency_instances/kinetic_fokker_planck.py:11-69
+# --------------------------------------------------------------------------------------
+def kfp_quadratic_samples(K, b, z_init, z_term, z_0T, tilde_F, gamma, T):
+    """Per-sample fp64 restatement of loss_fn (:33-50) and loss_ground_truth_fn (:52-58) for
+    V_theta(x) = x . (x K + b) (…_OU.py:209-220): grad V = (K+K^T) x + b, Hessian K+K^T."""
+    K = np.asarray(K, np.float64); b = np.asarray(b, np.float64)
+    S = K + K.T
+    d = K.shape[0]
+
+    def split(z):
+        z = np.asarray(z, np.float64)
+        return z[:, :d], z[:, d:]
+
+    xi, vi = split(z_init); xt, vt = split(z_term); x0, v0 = split(z_0T)
+    gV = lambda x: x @ S.T + b
+    gT = lambda x: x @ np.asarray(tilde_F, np.float64).T
+    parts = dict(
+        initial=np.mean(np.sum(gV(xi) * vi, -1)) if len(xi) else 0.0,
+        terminal=np.mean(np.sum(gV(xt) * vt, -1)) if len(xt) else 0.0,
+        nabla=np.mean(np.sum(gV(x0) ** 2, -1)),
+        hessian=np.mean(np.einsum("ni,ij,nj->n", v0, S, v0)),
+        friction=np.mean(np.sum(gV(x0) * v0, -1)) * gamma,
+        nabla_true=np.mean(np.sum(gT(x0) ** 2, -1)),
+    )
+    loss = (parts["nabla"] - 2 * parts["hessian"] + 2 * parts["friction"] + parts["nabla_true"]
+            + (-2 * parts["initial"] + 2 * parts["terminal"]) / T)
+    loss_gt = np.mean(np.sum((gT(x0) - gV(x0)) ** 2, -1))
+    return loss, loss_gt, parts
+
+
+def kfp_quadratic_from_moments(K, b, mom_init, mom_0T, mom_term, tilde_F, gamma, T):
+    """The same loss and its exact gradient d/d(K,b) from the three moment sets."""
+    K = np.asarray(K, np.float64); b = np.asarray(b, np.float64)
+    F = np.asarray(tilde_F, np.float64)
+    d = K.shape[0]
+    S = K + K.T
+
+    def blocks(mom):
+        n, mean, M = unpack_moments(mom, 2 * d)
+        return mean[:d], mean[d:], M[:d, :d], M[:d, d:], M[d:, d:]
+
+    ex, ev, Mxx, Mxv, Mvv = blocks(mom_0T)
+    _, evi, _, Mxvi, _ = blocks(mom_init)
+    _, evt, _, Mxvt, _ = blocks(mom_term)
+    nabla = np.trace(S @ Mxx @ S) + 2 * b @ S @ ex + b @ b
+    hess = np.trace(S @ Mvv)
+    fric_raw = np.trace(S @ Mxv) + b @ ev
+    init = np.trace(S @ Mxvi) + b @ evi
+    term = np.trace(S @ Mxvt) + b @ evt
+    true = np.trace(F @ Mxx @ F.T)
+    loss = nabla - 2 * hess + 2 * gamma * fric_raw + true + (-2 * init + 2 * term) / T
+    D = F - S
+    loss_gt = np.trace(D @ Mxx @ D.T) - 2 * b @ D @ ex + b @ b
+    G = (S @ Mxx + Mxx @ S + 2 * np.outer(b, ex)) - 2 * Mvv + 2 * gamma * Mxv.T \
+        + (-2 * Mxvi.T + 2 * Mxvt.T) / T
+    gK = G + G.T
+    gb = (2 * S @ ex + 2 * b) + 2 * gamma * ev + (-2 * evi + 2 * evt) / T
+    parts = dict(nabla=nabla, hessian=hess, friction=gamma * fric_raw, nabla_true=true,
+                 initial=init, terminal=term)
+    return loss, loss_gt, gK, gb, parts
+
+
+# --------------------------------------------------------------------------------------
+# KFP residual with the parametric GMM model (…_GMM.py:214-234)
+# --------------------------------------------------------------------------------------
+def gmm_terms(x, v, mus, sigma=1.0):
+    """Per-sample grad V, v^T Hess V v for V = -logsumexp (analytic: H = I/s^2 - Cov_w(mu)/s^4)."""
+    x = np.asarray(x, np.float64); v = np.asarray(v, np.float64)
+    diff = x[:, None, :] - mus[None]
+    a = -np.sum(diff ** 2, -1) / (2 * sigma ** 2)
+    a -= a.max(-1, keepdims=True)
+    w = np.exp(a); w /= w.sum(-1, keepdims=True)
+    s2 = 1.0 / sigma ** 2
+    mbar = w @ mus
+    g = s2 * (x - mbar)
+    pk = v @ mus.T
+    pbar = np.sum(w * pk, -1)
+    vHv = s2 * np.sum(v * v, -1) - s2 * s2 * (np.sum(w * pk * pk, -1) - pbar ** 2)
+    return g, vHv
+
+
+def kfp_gmm_loss(mus, z_init, z_term, z_0T, mus_true, gamma, T, sigma=1.0, sigma_true=1.0):
+    """loss_fn (:33-50) / loss_ground_truth_fn (:52-58) with V_theta = GMM(mus), V* = GMM(mus_true)."""
+    mus = np.asarray(mus, np.float64)
+    d = mus.shape[1]
+    z_init = np.asarray(z_init, np.float64); z_term = np.asarray(z_term, np.float64)
+    z_0T = np.asarray(z_0T, np.float64)
+    x0, v0 = z_0T[:, :d], z_0T[:, d:]
+    g0, h0 = gmm_terms(x0, v0, mus, sigma)
+    gt = gmm_value_grad(x0, np.asarray(mus_true, np.float64), sigma_true)[1]
+    parts = dict(nabla=np.mean(np.sum(g0 ** 2, -1)), hessian=np.mean(h0),
+                 friction=gamma * np.mean(np.sum(g0 * v0, -1)),
+                 nabla_true=np.mean(np.sum(gt ** 2, -1)))
+    for name, z in (("initial", z_init), ("terminal", z_term)):
+        if len(z):
+            gz, _ = gmm_terms(z[:, :d], z[:, d:], mus, sigma)
+            parts[name] = np.mean(np.sum(gz * z[:, d:], -1))
+        else:
+            parts[name] = 0.0
+    loss = (parts["nabla"] - 2 * parts["hessian"] + 2 * parts["friction"] + parts["nabla_true"]
+            + (-2 * parts["initial"] + 2 * parts["terminal"]) / T)
+    loss_gt = np.mean(np.sum((gt - g0) ** 2, -1))
+    return loss, loss_gt, parts
+
+
+def fd_grad(fn, theta, eps=1e-5):
+    """Central finite differences in fp64 (replaces jax.value_and_grad as the checker)."""
+    theta = np.asarray(theta, np.float64)
+    g = np.zeros_like(theta)
+    it = np.nditer(theta, flags=["multi_index"])
+    for _ in it:
+        idx = it.multi_index
+        tp = theta.copy(); tp[idx] += eps
+        tm = theta.copy(); tm[idx] -= eps
+        g[idx] = (fn(tp) - fn(tm)) / (2 * eps)
+    return g
+
+
+# --------------------------------------------------------------------------------------
+# score / log-density terms: kinetic_mckean_vlasov_example_quadratic.py:18-191,
+# test_partial_s_log_density.py:142-164
+# --------------------------------------------------------------------------------------
+def _xmarginal(s, cfg):
+    d = cfg["tilde_F"].shape[0]
+    mean, cov = ou_mean_cov(s, cfg)
+    F, L = cfg["F"], cfg["L"]
+    dm = F @ mean
+    d2m = F @ dm
+    dP = F @ cov + cov @ F.T + L
+    d2P = F @ dP + dP @ F.T
+    return (mean[:d], cov[:d, :d], dm[:d], d2m[:d], dP[:d, :d], d2P[:d, :d])
+
+
+def log_density(s, x, cfg):
+    """test_partial_s_log_density.py:142-153: log N(x; m_1(s), P_11(s))."""
+    m1, P11, *_ = _xmarginal(s, cfg)
+    Pinv = np.linalg.inv(P11)
+    r = m1 - np.asarray(x, np.float64)
+    quad = np.einsum("...i,ij,...j->...", r, Pinv, r)
+    return -0.5 * quad - 0.5 * np.log(np.linalg.det(2 * np.pi * P11))
+
+
+def partial_s_log_density(s, x, cfg):
+    """kinetic_mckean_vlasov_example_quadratic.py:51-69."""
+    m1, P11, dm1, _, dP11, _ = _xmarginal(s, cfg)
+    Pinv = np.linalg.inv(P11)
+    dPinv = -Pinv @ dP11 @ Pinv
+    r = m1 - np.asarray(x, np.float64)
+    term1 = -np.einsum("i,ij,...j->...", dm1, Pinv, r)
+    term2 = -0.5 * np.trace(dP11 @ Pinv)
+    term3 = -0.5 * np.einsum("...i,ij,...j->...", r, dPinv, r)
+    return term1 + term2 + term3
+
+
+def partial_s2_log_density(s, x, cfg):
+    """kinetic_mckean_vlasov_example_quadratic.py:120-177."""
+    m1, P11, dm1, d2m1, dP11, d2P11 = _xmarginal(s, cfg)
+    Pinv = np.linalg.inv(P11)
+    dPinv = -Pinv @ dP11 @ Pinv
+    d2Pinv = -Pinv @ d2P11 @ Pinv + 2 * Pinv @ dP11 @ Pinv @ dP11 @ Pinv
+    x = np.asarray(x, np.float64)
+    r = m1 - x
+    term1 = (-np.einsum("i,ij,...j->...", d2m1, Pinv, r) - np.einsum("i,ij,...j->...", dm1, dPinv, r)
+             - dm1 @ Pinv @ dm1)
+    term2 = -0.5 * np.einsum("...i,ij,...j->...", -r, d2Pinv, -r) - np.einsum("...i,ij,j->...", r, dPinv, dm1)
+    term3 = 0.5 * np.trace(Pinv @ dP11 @ Pinv @ dP11) - 0.5 * np.trace(Pinv @ d2P11)
+    return term1 + term2 + term3
+
+
+# --------------------------------------------------------------------------------------
+# KMV residual: methods/consistency_instances/kinetic_mckean_vlasov.py:11-120 (pairwise, O(n^2))
+# --------------------------------------------------------------------------------------
+def kmv_pairwise_loss(K, b, x, v, tau, cfg):
+    """Literal restatement with the [m, n, n_time, d] pairwise tensor (:20-23, :74-97), for
+    Phi_theta(y) = y . (y K + b) (…_quadratic.py:205-216), Phi* = 0.5 y^T tilde_F y (:193-203).
+    x, v: [n, n_time, d]; tau [n_time]."""
+    K = np.asarray(K, np.float64); b = np.asarray(b, np.float64)
+    S = K + K.T
+    F = cfg["tilde_F"]
+    gamma = cfg["gamma_friction"]
+    x = np.asarray(x, np.float64); v = np.asarray(v, np.float64)
+    y = x[None] - x[:, None]  # [m, n, T, d] (x_minus_ref, :23)
+    gPhi = y @ S.T + b
+    Phi = np.einsum("...i,ij,...j->...", y, K, y) + y @ b
+    gTrue = y @ F.T
+    loss_nabla = np.mean(np.sum(np.mean(gPhi, 0) ** 2, -1))
+    loss_hess = np.mean(np.einsum("nti,ij,ntj->nt", v, S, v))  # Hessian constant in j
+    ps = np.stack([partial_s_log_density(t, x[:, k], cfg) for k, t in enumerate(tau)], 1)
+    ps2 = np.stack([partial_s2_log_density(t, x[:, k], cfg) for k, t in enumerate(tau)], 1)
+    loss_value = np.mean(np.mean(Phi, 0) * (ps2 + ps ** 2 + gamma * ps))
+    loss_true = np.mean(np.sum(np.mean(gTrue, 0) ** 2, -1))
+    loss = loss_nabla - 2 * loss_hess + 2 * loss_value + loss_true
+    loss_gt = np.mean(np.sum((np.mean(gTrue, 0) - np.mean(gPhi, 0)) ** 2, -1))
+    return loss, loss_gt
+
+
+# --------------------------------------------------------------------------------------
+# problem constants
+# --------------------------------------------------------------------------------------
+def problem_constants(d, seed=2217):
+    """tilde_F = G G^T, G ~ N(0,1)^{d x (d+1)} (…_OU.py:16-19 distribution, numpy PCG64 stream)."""
+    G = np.random.default_rng(seed).standard_normal((d, d + 1))
+    return G @ G.T
+
+
+def gmm_centres(d, K, seed=2217, lo=-4.0, hi=4.0):
+    """mu_k ~ U[-4, 4]^d (…_GMM.py:22-23, 52-59 distribution)."""
+    return np.random.default_rng(seed + 1).uniform(lo, hi, size=(K, d))

@@ -1,0 +1,125 @@
+// common.h — device helpers shared by the pdeinv HIP kernels (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "../../include/pdeinv.h"
+
+namespace pdeinv {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+constexpr int kBlock = 256;          // 4 waves of 64
+constexpr int kWave = 64;
+constexpr int kWavesPerBlock = kBlock / kWave;
+
+// ---- error plumbing (host) ------------------------------------------------------------
+void set_error(const std::string& msg);
+int fail(int code, const std::string& msg);
+int check_launch(const char* what);
+
+#define PDEINV_REQUIRE(cond, code, msg) \
+  do {                                  \
+    if (!(cond)) return ::pdeinv::fail((code), (msg)); \
+  } while (0)
+
+// ---- Philox4x32-10 (Random123) ----------------------------------------------------------
+constexpr uint32_t kM0 = 0xD2511F53u, kM1 = 0xCD9E8D57u;
+constexpr uint32_t kW0 = 0x9E3779B9u, kW1 = 0xBB67AE85u;
+
+__device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t hi0 = __umulhi(kM0, c.x), lo0 = kM0 * c.x;
+    const uint32_t hi1 = __umulhi(kM1, c.z), lo1 = kM1 * c.z;
+    c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
+    k0 += kW0;
+    k1 += kW1;
+  }
+  return c;
+}
+
+// u32 -> [0,1) with 24 random bits (exact in fp32; identical on host and device).
+__device__ __forceinline__ float u32_unit(uint32_t x) { return (float)(x >> 8) * 0x1p-24f; }
+
+// Box–Muller on the hardware transcendentals: v_log_f32 is log2, v_sin/v_cos take revolutions.
+__device__ __forceinline__ void box_muller(uint32_t a, uint32_t b, float& z0, float& z1) {
+  const float u1 = (float)((a >> 8) + 1u) * 0x1p-24f;  // (0, 1]
+  const float u2 = (float)(b >> 8) * 0x1p-24f;         // [0, 1)
+  const float r = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));
+  z0 = r * __builtin_amdgcn_cosf(u2);
+  z1 = r * __builtin_amdgcn_sinf(u2);
+}
+
+// ---- wave / block reductions ------------------------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// Reduce the N per-thread values over the block and store the block sum of value c < n_write
+// to partials[c * n_blocks + block] (column-major slab: the fp64 reducer then reads each
+// column contiguously). N is compile-time so `vals` stays in VGPRs (a runtime index would
+// demote the whole array to scratch). `lds` holds kWavesPerBlock * N floats. All threads call.
+template <int N>
+__device__ __forceinline__ void block_reduce_to_slab(const float (&vals)[N], int n_write, float* lds,
+                                                     float* partials, int block, int n_blocks) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = threadIdx.x / kWave;
+  __syncthreads();  // lds may still be read by a previous call
+#pragma unroll
+  for (int c = 0; c < N; ++c) {
+    if (c < n_write) {
+      const float s = wave_sum(vals[c]);
+      if (lane == 0) lds[wave * N + c] = s;
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < n_write; c += kBlock) {
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < kWavesPerBlock; ++w) s += lds[w * N + c];
+    partials[(int64_t)c * n_blocks + block] = s;
+  }
+}
+
+// ---- moments layout -----------------------------------------------------------------------
+__host__ __device__ constexpr int moment_len(int m) { return 1 + m + m * (m + 1) / 2; }
+
+template <int M>
+struct MomentAcc {
+  float v[moment_len(M)];
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int i = 0; i < moment_len(M); ++i) v[i] = 0.f;
+  }
+  __device__ __forceinline__ void add(const float* z, float w) {  // w = 1 (active) or 0
+    v[0] += w;
+#pragma unroll
+    for (int i = 0; i < M; ++i) v[1 + i] = fmaf(w, z[i], v[1 + i]);
+    int o = 1 + M;
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      const float wz = w * z[i];
+#pragma unroll
+      for (int j = i; j < M; ++j) {
+        v[o] = fmaf(wz, z[j], v[o]);
+        ++o;
+      }
+    }
+  }
+};
+
+// fp64 column reducer launched after any kernel that wrote a partial slab.
+void launch_slab_reduce(const float* partials, int n_blocks, int n_cols, double* out,
+                        hipStream_t stream);
+
+inline int grid_for(int64_t n, int64_t per_block = kBlock) {
+  return (int)((n + per_block - 1) / per_block);
+}
+
+}  // namespace pdeinv

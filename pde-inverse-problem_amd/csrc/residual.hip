@@ -1,0 +1,512 @@
+// residual.hip — PDE-consistency residuals and their parameter gradients (gfx950).
+//
+// Replaces methods/consistency_instances/kinetic_fokker_planck.py:11-69 (value_and_grad_fn):
+// the reference evaluates grad V_theta (vmap(grad)), v^T Hess V_theta v (vmap(jvp∘grad)) and
+// grad V* per sample and then differentiates the whole loss with jax.value_and_grad. Here
+//  * the parametric quadratic model reduces exactly to moments (moments.hip / the fused
+//    simulator) plus this O(d^3) finalize, and
+//  * the parametric GMM model runs one fused per-sample pass with the analytic adjoint
+//    d loss / d mu, HBM-bound on the 8d bytes per sample.
+#include <math.h>
+
+#include "common.h"
+
+namespace pdeinv {
+
+// =========================================================================================
+// KFP residual, V_theta(x) = x^T K x + b^T x — finalize from the three moment sets
+// =========================================================================================
+struct KfpQuadArgs {
+  int d;
+  float gamma, T;
+  float F[PDEINV_MAX_DIM * PDEINV_MAX_DIM];
+};
+
+struct SetMoments {
+  double n, mean[2 * PDEINV_MAX_DIM];
+  double M[2 * PDEINV_MAX_DIM][2 * PDEINV_MAX_DIM];  // E[z z^T]
+};
+
+__device__ void unpack_set(const double* v, int m, SetMoments& s) {
+  s.n = v[0];
+  const double inv = s.n > 0 ? 1.0 / s.n : 0.0;
+  for (int i = 0; i < m; ++i) s.mean[i] = v[1 + i] * inv;
+  int o = 1 + m;
+  for (int i = 0; i < m; ++i)
+    for (int j = i; j < m; ++j) {
+      s.M[i][j] = v[o] * inv;
+      s.M[j][i] = v[o] * inv;
+      ++o;
+    }
+}
+
+// One thread: d <= 16, O(d^3) work. Gradient derivation in oracle/numpy_ref.py
+// kfp_quadratic_from_moments (checked there against central finite differences).
+__global__ void kfp_quadratic_finalize_kernel(KfpQuadArgs a, const double* __restrict__ mom,
+                                              const float* __restrict__ theta,
+                                              float* __restrict__ out, float* __restrict__ grad) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const int d = a.d, m = 2 * d, L = moment_len(m);
+  SetMoments si, s0, st;
+  unpack_set(mom, m, si);
+  unpack_set(mom + L, m, s0);
+  unpack_set(mom + 2 * L, m, st);
+  double S[PDEINV_MAX_DIM][PDEINV_MAX_DIM], b[PDEINV_MAX_DIM];
+  for (int i = 0; i < d; ++i) {
+    b[i] = theta[d * d + i];
+    for (int j = 0; j < d; ++j) S[i][j] = (double)theta[i * d + j] + (double)theta[j * d + i];
+  }
+  // SM = S Mxx, tr(S Mxx S), b^T S ex, ...
+  double SM[PDEINV_MAX_DIM][PDEINV_MAX_DIM];
+  for (int i = 0; i < d; ++i)
+    for (int j = 0; j < d; ++j) {
+      double t = 0;
+      for (int k = 0; k < d; ++k) t += S[i][k] * s0.M[k][j];
+      SM[i][j] = t;
+    }
+  double nabla = 0, bSe = 0, bb = 0, hess = 0, fric = 0, init = 0, term = 0, tru = 0, gt = 0;
+  double Sex[PDEINV_MAX_DIM];
+  for (int i = 0; i < d; ++i) {
+    double t = 0;
+    for (int k = 0; k < d; ++k) t += S[i][k] * s0.mean[k];
+    Sex[i] = t;
+    bSe += b[i] * t;
+    bb += b[i] * b[i];
+  }
+  for (int i = 0; i < d; ++i)
+    for (int j = 0; j < d; ++j) {
+      nabla += SM[i][j] * S[j][i];
+      hess += S[i][j] * s0.M[d + j][d + i];  // tr(S Mvv)
+      fric += S[i][j] * s0.M[j][d + i];      // tr(S Mxv), Mxv[j][i] = E[x_j v_i]
+      init += S[i][j] * si.M[j][d + i];
+      term += S[i][j] * st.M[j][d + i];
+    }
+  nabla += 2 * bSe + bb;
+  for (int i = 0; i < d; ++i) {
+    fric += b[i] * s0.mean[d + i];
+    init += b[i] * si.mean[d + i];
+    term += b[i] * st.mean[d + i];
+  }
+  // V* = 0.5 x^T F x (F symmetric): E|F x|^2 and E|(F - S) x - b|^2
+  double Dm[PDEINV_MAX_DIM][PDEINV_MAX_DIM];
+  for (int i = 0; i < d; ++i)
+    for (int j = 0; j < d; ++j) Dm[i][j] = (double)a.F[i * d + j] - S[i][j];
+  for (int i = 0; i < d; ++i) {
+    double fx2 = 0, dx2 = 0, de = 0;
+    for (int j = 0; j < d; ++j) {
+      de += Dm[i][j] * s0.mean[j];
+      for (int k = 0; k < d; ++k) {
+        fx2 += (double)a.F[i * d + j] * s0.M[j][k] * (double)a.F[i * d + k];
+        dx2 += Dm[i][j] * s0.M[j][k] * Dm[i][k];
+      }
+    }
+    tru += fx2;
+    gt += dx2 - 2 * b[i] * de;
+  }
+  gt += bb;
+  const double g = a.gamma, T = a.T;
+  const double loss = nabla - 2 * hess + 2 * g * fric + tru + (-2 * init + 2 * term) / T;
+  // d loss / d S (entries independent) then d/dK = G + G^T
+  double G[PDEINV_MAX_DIM][PDEINV_MAX_DIM];
+  for (int i = 0; i < d; ++i)
+    for (int j = 0; j < d; ++j) {
+      double sm_ms = 0;
+      for (int k = 0; k < d; ++k) sm_ms += S[i][k] * s0.M[k][j] + s0.M[i][k] * S[k][j];
+      G[i][j] = sm_ms + 2 * b[i] * s0.mean[j] - 2 * s0.M[d + i][d + j] + 2 * g * s0.M[d + i][j] +
+                (-2 * si.M[d + i][j] + 2 * st.M[d + i][j]) / T;
+    }
+  double gn = 0;
+  for (int i = 0; i < d; ++i)
+    for (int j = 0; j < d; ++j) {
+      const double gk = G[i][j] + G[j][i];
+      grad[i * d + j] = (float)gk;
+      gn += gk * gk;
+    }
+  for (int i = 0; i < d; ++i) {
+    const double gb = 2 * Sex[i] + 2 * b[i] + 2 * g * s0.mean[d + i] +
+                      (-2 * si.mean[d + i] + 2 * st.mean[d + i]) / T;
+    grad[d * d + i] = (float)gb;
+    gn += gb * gb;
+  }
+  out[PDEINV_KFP_LOSS] = (float)loss;
+  out[PDEINV_KFP_LOSS_GT] = (float)gt;
+  out[PDEINV_KFP_GRAD_NORM] = (float)sqrt(gn);
+  out[PDEINV_KFP_NABLA] = (float)nabla;
+  out[PDEINV_KFP_HESSIAN] = (float)hess;
+  out[PDEINV_KFP_FRICTION] = (float)(g * fric);
+  out[PDEINV_KFP_NABLA_TRUE] = (float)tru;
+  out[PDEINV_KFP_INITIAL] = (float)init;
+  out[PDEINV_KFP_TERMINAL] = (float)term;
+}
+
+// =========================================================================================
+// KFP residual, V_theta = GMM(mu) — fused per-sample forward + analytic adjoint
+// =========================================================================================
+struct GmmResArgs {
+  int K, KT;
+  float s2, nh_s2_l2e, s2t, nh_s2t_l2e;  // 1/sigma^2 and -0.5/sigma^2*log2(e)
+  int64_t n0, ni, nt, ld0, ldi, ldt;
+  const float* z0T;
+  const float* zi;
+  const float* zt;
+  float c_nabla, c_hess, c_fric, c_true, c_init, c_term, inv_ni, inv_nt;
+  float mus_true[PDEINV_MAX_PARAMS];
+};
+
+constexpr int kGmmGridCap = 1024;
+
+// softmax weights w_k of a_k = -|x - mu_k|^2 / (2 s^2); returns sum_k w_k mu_k in mbar.
+template <int D, int KM>
+__device__ __forceinline__ void gmm_softmax(const float* x, const float (*mu)[D], int K, float nh,
+                                            float* w, float* mbar) {
+  float amax = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < KM; ++k) {
+    if (k < K) {
+      float d2 = 0.f;
+#pragma unroll
+      for (int i = 0; i < D; ++i) {
+        const float t = x[i] - mu[k][i];
+        d2 = fmaf(t, t, d2);
+      }
+      w[k] = d2 * nh;
+      amax = fmaxf(amax, w[k]);
+    }
+  }
+  float den = 0.f;
+#pragma unroll
+  for (int k = 0; k < KM; ++k) {
+    if (k < K) {
+      w[k] = __builtin_amdgcn_exp2f(w[k] - amax);
+      den += w[k];
+    } else {
+      w[k] = 0.f;
+    }
+  }
+  const float inv = 1.f / den;
+#pragma unroll
+  for (int i = 0; i < D; ++i) mbar[i] = 0.f;
+#pragma unroll
+  for (int k = 0; k < KM; ++k) {
+    w[k] *= inv;
+#pragma unroll
+    for (int i = 0; i < D; ++i) mbar[i] = fmaf(w[k], mu[k][i], mbar[i]);
+  }
+}
+
+template <int D, int KM>
+__global__ __launch_bounds__(kBlock) void kfp_gmm_kernel(GmmResArgs a, const float* __restrict__ mus,
+                                                         float* __restrict__ partials) {
+  constexpr int NS = PDEINV_GMM_NACC;
+  float mu[KM][D];
+  float mut[KM][D];
+#pragma unroll
+  for (int k = 0; k < KM; ++k)
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      mu[k][i] = (k < a.K) ? mus[k * D + i] : 0.f;
+      mut[k][i] = (k < a.KT) ? a.mus_true[k * D + i] : 0.f;
+    }
+  float acc[NS + KM * D];
+#pragma unroll
+  for (int c = 0; c < NS + KM * D; ++c) acc[c] = 0.f;
+
+  const int64_t total = a.n0 + a.ni + a.nt;
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  const float s2 = a.s2;
+  for (int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x; r < total; r += stride) {
+    int set;
+    const float* row;
+    if (r < a.n0) { set = 0; row = a.z0T + r * a.ld0; }
+    else if (r < a.n0 + a.ni) { set = 1; row = a.zi + (r - a.n0) * a.ldi; }
+    else { set = 2; row = a.zt + (r - a.n0 - a.ni) * a.ldt; }
+    float x[D], v[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) { x[i] = row[i]; v[i] = row[D + i]; }
+
+    float w[KM], mbar[D];
+    gmm_softmax<D, KM>(x, mu, a.K, a.nh_s2_l2e, w, mbar);
+    float e[D], g[D], T1 = 0.f, T3 = 0.f, vv = 0.f;
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      e[i] = x[i] - mbar[i];
+      g[i] = s2 * e[i];
+      T1 = fmaf(g[i], g[i], T1);
+      T3 = fmaf(g[i], v[i], T3);
+      vv = fmaf(v[i], v[i], vv);
+    }
+    float pk[KM], em[KM], pbar = 0.f, wp2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+      float p = 0.f, q = 0.f;
+#pragma unroll
+      for (int i = 0; i < D; ++i) { p = fmaf(mu[k][i], v[i], p); q = fmaf(mu[k][i], e[i], q); }
+      pk[k] = p;
+      em[k] = q;
+      pbar = fmaf(w[k], p, pbar);
+      wp2 = fmaf(w[k] * p, p, wp2);
+    }
+    const float s4 = s2 * s2;
+    const float T2 = s2 * vv - s4 * (wp2 - pbar * pbar);  // v^T (I/s^2 - Cov_w(mu)/s^4) v
+
+    const float c1 = set == 0 ? a.c_nabla : 0.f;
+    const float c2 = set == 0 ? a.c_hess : 0.f;
+    const float c3 = set == 0 ? a.c_fric : (set == 1 ? a.c_init : a.c_term);
+    // adjoint: F_k = d f / d w_k, explicit d f / d mu_j, then softmax chain rule
+    float Fk[KM], Fbar = 0.f;
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+      Fk[k] = -2.f * c1 * s4 * em[k] - c2 * s4 * (pk[k] * pk[k] - 2.f * pbar * pk[k]) - c3 * s2 * pk[k];
+      Fbar = fmaf(w[k], Fk[k], Fbar);
+    }
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+      const float cw = w[k] * (Fk[k] - Fbar) * s2;
+      const float ce = -2.f * c1 * s4 * w[k];
+      const float cv = -w[k] * (2.f * c2 * s4 * (pk[k] - pbar) + c3 * s2);
+#pragma unroll
+      for (int i = 0; i < D; ++i)
+        acc[NS + k * D + i] += cw * (x[i] - mu[k][i]) + ce * e[i] + cv * v[i];
+    }
+    acc[PDEINV_GMM_ACC_LOSS] += c1 * T1 + c2 * T2 + c3 * T3;
+    if (set == 0) {
+      float wt[KM], mbt[D];
+      gmm_softmax<D, KM>(x, mut, a.KT, a.nh_s2t_l2e, wt, mbt);
+      float Tt = 0.f, Tgt = 0.f;
+#pragma unroll
+      for (int i = 0; i < D; ++i) {
+        const float gt = a.s2t * (x[i] - mbt[i]);
+        Tt = fmaf(gt, gt, Tt);
+        Tgt = fmaf(gt - g[i], gt - g[i], Tgt);
+      }
+      acc[PDEINV_GMM_ACC_LOSS] += a.c_true * Tt;
+      acc[PDEINV_GMM_ACC_LOSS_GT] += a.c_true * Tgt;
+      acc[PDEINV_GMM_ACC_NABLA] += a.c_true * T1;
+      acc[PDEINV_GMM_ACC_HESSIAN] += a.c_true * T2;
+      acc[PDEINV_GMM_ACC_FRICTION] += a.c_true * T3;
+      acc[PDEINV_GMM_ACC_NABLA_TRUE] += a.c_true * Tt;
+    } else if (set == 1) {
+      acc[PDEINV_GMM_ACC_INITIAL] += a.inv_ni * T3;
+    } else {
+      acc[PDEINV_GMM_ACC_TERMINAL] += a.inv_nt * T3;
+    }
+  }
+  __shared__ float lds[kWavesPerBlock * (NS + KM * D)];
+  block_reduce_to_slab(acc, NS + a.K * D, lds, partials, blockIdx.x, gridDim.x);
+}
+
+__global__ void kfp_gmm_finalize_kernel(int n_grad, float gamma, const double* __restrict__ acc,
+                                        float* __restrict__ out, float* __restrict__ grad) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  double gn = 0.0;
+  for (int k = 0; k < n_grad; ++k) {
+    const double g = acc[PDEINV_GMM_NACC + k];
+    grad[k] = (float)g;
+    gn += g * g;
+  }
+  out[PDEINV_KFP_LOSS] = (float)acc[PDEINV_GMM_ACC_LOSS];
+  out[PDEINV_KFP_LOSS_GT] = (float)acc[PDEINV_GMM_ACC_LOSS_GT];
+  out[PDEINV_KFP_GRAD_NORM] = (float)sqrt(gn);
+  out[PDEINV_KFP_NABLA] = (float)acc[PDEINV_GMM_ACC_NABLA];
+  out[PDEINV_KFP_HESSIAN] = (float)acc[PDEINV_GMM_ACC_HESSIAN];
+  out[PDEINV_KFP_FRICTION] = (float)(gamma * acc[PDEINV_GMM_ACC_FRICTION]);
+  out[PDEINV_KFP_NABLA_TRUE] = (float)acc[PDEINV_GMM_ACC_NABLA_TRUE];
+  out[PDEINV_KFP_INITIAL] = (float)acc[PDEINV_GMM_ACC_INITIAL];
+  out[PDEINV_KFP_TERMINAL] = (float)acc[PDEINV_GMM_ACC_TERMINAL];
+}
+
+// =========================================================================================
+// GMM potential value / gradient over a batch (core/potential.py:48-61)
+// =========================================================================================
+struct GmmPotArgs {
+  int K;
+  float s2, nh_s2_l2e;
+  int64_t n, ld;
+  float mus[PDEINV_MAX_PARAMS];
+};
+
+template <int D>
+__global__ __launch_bounds__(kBlock) void gmm_potential_kernel(GmmPotArgs a, const float* __restrict__ x_in,
+                                                               float* __restrict__ value,
+                                                               float* __restrict__ grad) {
+  const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (r >= a.n) return;
+  float x[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) x[i] = x_in[r * a.ld + i];
+  float al[16], amax = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    if (k < a.K) {
+      float d2 = 0.f;
+#pragma unroll
+      for (int i = 0; i < D; ++i) {
+        const float t = x[i] - a.mus[k * D + i];
+        d2 = fmaf(t, t, d2);
+      }
+      al[k] = d2 * a.nh_s2_l2e;
+      amax = fmaxf(amax, al[k]);
+    }
+  }
+  float den = 0.f, accm[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) accm[i] = 0.f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    if (k < a.K) {
+      const float e = __builtin_amdgcn_exp2f(al[k] - amax);
+      den += e;
+#pragma unroll
+      for (int i = 0; i < D; ++i) accm[i] = fmaf(e, a.mus[k * D + i], accm[i]);
+    }
+  }
+  // V = -logsumexp(a) = -(amax + log(den)) in natural units
+  if (value) value[r] = -(amax + __builtin_amdgcn_logf(den)) * 0.6931471805599453f;
+  if (grad) {
+    const float inv = 1.f / den;
+#pragma unroll
+    for (int i = 0; i < D; ++i) grad[r * D + i] = a.s2 * (x[i] - accm[i] * inv);
+  }
+}
+
+}  // namespace pdeinv
+
+using namespace pdeinv;
+
+extern "C" int pdeinv_residual_kfp_quadratic(const pdeinv_kfp_quad_desc* d, const double* mom,
+                                             const float* theta, float* out, float* grad,
+                                             void* stream) {
+  PDEINV_REQUIRE(d != nullptr, PDEINV_ERR_INVALID, "kfp_quadratic: null descriptor");
+  PDEINV_REQUIRE(d->dim >= 1 && d->dim <= PDEINV_MAX_DIM, PDEINV_ERR_UNSUPPORTED,
+                 "kfp_quadratic: dim must be in [1, 16]");
+  PDEINV_REQUIRE(mom && theta && out && grad, PDEINV_ERR_INVALID, "kfp_quadratic: null pointer");
+  PDEINV_REQUIRE(d->tilde_F != nullptr, PDEINV_ERR_INVALID, "kfp_quadratic: tilde_F is null");
+  PDEINV_REQUIRE(std::isfinite(d->total_time) && d->total_time > 0.f, PDEINV_ERR_INVALID,
+                 "kfp_quadratic: total_time must be > 0");
+  KfpQuadArgs a{};
+  a.d = d->dim;
+  a.gamma = d->gamma;
+  a.T = d->total_time;
+  for (int k = 0; k < d->dim * d->dim; ++k) a.F[k] = d->tilde_F[k];
+  hipLaunchKernelGGL(kfp_quadratic_finalize_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, a, mom,
+                     theta, out, grad);
+  return check_launch("kfp_quadratic_finalize_kernel");
+}
+
+static int gmm_grid(int64_t total) {
+  int g = grid_for(total);
+  return g < 1 ? 1 : (g > kGmmGridCap ? kGmmGridCap : g);
+}
+
+static int gmm_km(int D, int K) {
+  int km = K <= 4 ? 4 : (K <= 8 ? 8 : 16);
+  while (km * D > 128 && km > 4) km /= 2;
+  return (K <= km) ? km : 0;
+}
+
+extern "C" size_t pdeinv_residual_kfp_gmm_workspace_bytes(const pdeinv_kfp_gmm_desc* d, int64_t ni,
+                                                          int64_t nt, int64_t n0) {
+  if (!d || d->dim < 1 || d->n_centers < 1) return 0;
+  return (size_t)(PDEINV_GMM_NACC + d->n_centers * d->dim) * gmm_grid(ni + nt + n0) * sizeof(float);
+}
+
+template <int D, int KM>
+static void launch_gmm(const GmmResArgs& a, const float* mus, float* ws, int g, hipStream_t st) {
+  hipLaunchKernelGGL((kfp_gmm_kernel<D, KM>), dim3(g), dim3(kBlock), 0, st, a, mus, ws);
+}
+
+template <int D>
+static int dispatch_gmm(int km, const GmmResArgs& a, const float* mus, float* ws, int g, hipStream_t st) {
+  if (km == 4) launch_gmm<D, 4>(a, mus, ws, g, st);
+  else if (km == 8) launch_gmm<D, 8>(a, mus, ws, g, st);
+  else if constexpr (D <= 8) launch_gmm<D, 16>(a, mus, ws, g, st);
+  else return fail(PDEINV_ERR_UNSUPPORTED, "kfp_gmm: n_centers too large for dim");
+  return PDEINV_OK;
+}
+
+extern "C" int pdeinv_residual_kfp_gmm(const pdeinv_kfp_gmm_desc* d, const float* zi, int64_t ni,
+                                       int64_t ldi, const float* zt, int64_t nt, int64_t ldt,
+                                       const float* z0, int64_t n0, int64_t ld0, const float* mus,
+                                       void* ws, double* acc, void* stream) {
+  PDEINV_REQUIRE(d != nullptr, PDEINV_ERR_INVALID, "kfp_gmm: null descriptor");
+  const int D = d->dim;
+  PDEINV_REQUIRE(D >= 1 && D <= 16, PDEINV_ERR_UNSUPPORTED, "kfp_gmm: dim must be in [1, 16]");
+  PDEINV_REQUIRE(d->n_centers >= 1 && d->n_centers_true >= 1 && d->n_centers_true <= 16,
+                 PDEINV_ERR_UNSUPPORTED, "kfp_gmm: need 1 <= n_centers, n_centers_true <= 16");
+  const int km = gmm_km(D, d->n_centers >= d->n_centers_true ? d->n_centers : d->n_centers_true);
+  PDEINV_REQUIRE(km > 0, PDEINV_ERR_UNSUPPORTED, "kfp_gmm: n_centers * dim exceeds 128 registers");
+  PDEINV_REQUIRE(ni >= 0 && nt >= 0 && n0 >= 1, PDEINV_ERR_INVALID, "kfp_gmm: 0T set must be non-empty");
+  PDEINV_REQUIRE(mus && ws && acc && z0 && (ni == 0 || zi) && (nt == 0 || zt), PDEINV_ERR_INVALID,
+                 "kfp_gmm: null pointer");
+  PDEINV_REQUIRE(d->mus_true != nullptr, PDEINV_ERR_INVALID, "kfp_gmm: mus_true is null");
+  PDEINV_REQUIRE(d->sigma > 0.f && d->sigma_true > 0.f, PDEINV_ERR_INVALID, "kfp_gmm: sigma must be > 0");
+  GmmResArgs a{};
+  a.K = d->n_centers;
+  a.KT = d->n_centers_true;
+  a.s2 = 1.f / (d->sigma * d->sigma);
+  a.nh_s2_l2e = -0.5f * a.s2 * 1.4426950408889634f;
+  a.s2t = 1.f / (d->sigma_true * d->sigma_true);
+  a.nh_s2t_l2e = -0.5f * a.s2t * 1.4426950408889634f;
+  a.n0 = n0; a.ni = ni; a.nt = nt;
+  a.ld0 = ld0 ? ld0 : 2 * D; a.ldi = ldi ? ldi : 2 * D; a.ldt = ldt ? ldt : 2 * D;
+  PDEINV_REQUIRE(a.ld0 >= 2 * D && a.ldi >= 2 * D && a.ldt >= 2 * D, PDEINV_ERR_INVALID,
+                 "kfp_gmm: row stride < 2*dim");
+  a.z0T = z0; a.zi = zi; a.zt = zt;
+  a.c_nabla = d->c_nabla; a.c_hess = d->c_hess; a.c_fric = d->c_fric; a.c_true = d->c_true;
+  a.c_init = d->c_init; a.c_term = d->c_term;
+  a.inv_ni = ni ? 1.f / (float)ni : 0.f;
+  a.inv_nt = nt ? 1.f / (float)nt : 0.f;
+  for (int k = 0; k < d->n_centers_true * D; ++k) a.mus_true[k] = d->mus_true[k];
+  hipStream_t st = (hipStream_t)stream;
+  const int g = gmm_grid(n0 + ni + nt);
+  float* wsf = (float*)ws;
+  int rc = PDEINV_OK;
+  switch (D) {
+#define CASE(DD) case DD: rc = dispatch_gmm<DD>(km, a, mus, wsf, g, st); break;
+    CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) CASE(10) CASE(12) CASE(16)
+#undef CASE
+    default:
+      return fail(PDEINV_ERR_UNSUPPORTED, "kfp_gmm: dim must be one of 1-8, 10, 12, 16");
+  }
+  if (rc) return rc;
+  rc = check_launch("kfp_gmm_kernel");
+  if (rc) return rc;
+  launch_slab_reduce(wsf, g, PDEINV_GMM_NACC + a.K * D, acc, st);
+  return check_launch("slab_reduce_kernel");
+}
+
+extern "C" int pdeinv_residual_kfp_gmm_finalize(const pdeinv_kfp_gmm_desc* d, const double* acc,
+                                                float* out, float* grad, void* stream) {
+  PDEINV_REQUIRE(d && acc && out && grad, PDEINV_ERR_INVALID, "kfp_gmm_finalize: null pointer");
+  hipLaunchKernelGGL(kfp_gmm_finalize_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream,
+                     d->n_centers * d->dim, d->gamma, acc, out, grad);
+  return check_launch("kfp_gmm_finalize_kernel");
+}
+
+extern "C" int pdeinv_gmm_potential(int32_t D, int32_t K, float sigma, const float* mus_host,
+                                    const float* x, int64_t n, int64_t ld, float* value,
+                                    float* grad, void* stream) {
+  PDEINV_REQUIRE(D >= 1 && D <= 16 && K >= 1 && K <= 16 && K * D <= PDEINV_MAX_PARAMS,
+                 PDEINV_ERR_UNSUPPORTED, "gmm_potential: need dim <= 16, 1 <= K <= 16");
+  PDEINV_REQUIRE(sigma > 0.f && mus_host != nullptr, PDEINV_ERR_INVALID, "gmm_potential: bad sigma / mus");
+  PDEINV_REQUIRE(n >= 0, PDEINV_ERR_INVALID, "gmm_potential: n < 0");
+  if (n == 0) return PDEINV_OK;
+  PDEINV_REQUIRE(x != nullptr, PDEINV_ERR_INVALID, "gmm_potential: x is null");
+  GmmPotArgs a{};
+  a.K = K;
+  a.s2 = 1.f / (sigma * sigma);
+  a.nh_s2_l2e = -0.5f * a.s2 * 1.4426950408889634f;
+  a.n = n;
+  a.ld = ld ? ld : D;
+  PDEINV_REQUIRE(a.ld >= D, PDEINV_ERR_INVALID, "gmm_potential: ld < dim");
+  for (int k = 0; k < K * D; ++k) a.mus[k] = mus_host[k];
+  hipStream_t st = (hipStream_t)stream;
+  switch (D) {
+#define CASE(DD) case DD: hipLaunchKernelGGL(gmm_potential_kernel<DD>, dim3(grid_for(n)), dim3(kBlock), 0, st, a, x, value, grad); break;
+    CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) CASE(10) CASE(12) CASE(16)
+#undef CASE
+    default:
+      return fail(PDEINV_ERR_UNSUPPORTED, "gmm_potential: dim must be one of 1-8, 10, 12, 16");
+  }
+  return check_launch("gmm_potential_kernel");
+}

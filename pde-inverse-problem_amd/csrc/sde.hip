@@ -1,0 +1,490 @@
+// sde.hip — the Euler–Maruyama particle simulator (gfx950).
+//
+// Replaces utils/sampling_utils.py:25-52 (underdamped_langevin_dynamics_scan, vmapped over
+// particles, lax.scan over steps) and update_step :6-22. XLA runs one scan body per step and
+// round-trips the state through HBM each time; here one thread owns one particle for all
+// n_steps+1 updates, the state lives in VGPRs, the noise is Philox4x32-10 in registers, and
+// the only HBM traffic is the z0 read and the time-major trajectory / tau / last stores
+// ((8d + 4) B per particle-update).
+//
+// Optionally the same kernel accumulates the moment sets (initial = z0, 0T = traj,
+// terminal = last) that the parametric-quadratic residual needs, so the KFP residual
+// (kinetic_fokker_planck.py:33-58) costs no second pass over the trajectory.
+#include <math.h>
+
+#include "common.h"
+
+namespace pdeinv {
+
+struct SdeArgs {
+  int64_t N, poff, ld_z0;
+  int32_t n_steps, random_shift, K, has_center;
+  float dt, gamma, ns, neg_half_inv_s2_log2e, inv_s2;
+  uint32_t k0, k1, ctr_off;
+  const float* noise;
+  const float* shift_u;
+  float params[PDEINV_MAX_PARAMS + PDEINV_MAX_DIM];
+};
+
+constexpr int kMaxGmmK = 16;
+
+// d standard normals for update s of particle (plo, phi) — stream layout of include/pdeinv.h.
+template <int D>
+__device__ __forceinline__ void gen_normals(const SdeArgs& a, uint32_t plo, uint32_t phi,
+                                            uint32_t s, int64_t i, float* xi) {
+  if (a.noise) {
+    const float* src = a.noise + ((int64_t)s * a.N + i) * D;
+#pragma unroll
+    for (int k = 0; k < D; ++k) xi[k] = src[k];
+    return;
+  }
+#pragma unroll
+  for (int j = 0; 4 * j < D; ++j) {
+    const uint4 r = philox4x32_10(make_uint4(plo, phi, a.ctr_off + s, (uint32_t)j), a.k0, a.k1);
+    float z[4];
+    box_muller(r.x, r.y, z[0], z[1]);
+    box_muller(r.z, r.w, z[2], z[3]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (4 * j + k < D) xi[4 * j + k] = z[k];
+  }
+}
+
+// grad U(q) = A (q - c)   (KOU: A = tilde_F, …_OU.py:130-138)
+template <int D>
+__device__ __forceinline__ void grad_quadratic(const SdeArgs& a, const float* q, float* g) {
+  float y[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) y[k] = a.has_center ? q[k] - a.params[D * D + k] : q[k];
+#pragma unroll
+  for (int r = 0; r < D; ++r) {
+    float acc = 0.f;
+#pragma unroll
+    for (int c = 0; c < D; ++c) acc = fmaf(a.params[r * D + c], y[c], acc);
+    g[r] = acc;
+  }
+}
+
+// grad of U = -logsumexp_k(-|q-mu_k|^2/(2 s^2)) = (q - sum_k w_k mu_k) / s^2
+// (core/potential.py:32-37; the softmax form of the commented analytic gradient :39-43).
+// Centres are kernel arguments (scalar loads); exponents in log2 units for v_exp_f32.
+template <int D>
+__device__ __forceinline__ void grad_gmm(const SdeArgs& a, const float* q, float* g) {
+  float al[kMaxGmmK];
+  float amax = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < kMaxGmmK; ++k) {
+    if (k < a.K) {
+      float d2 = 0.f;
+#pragma unroll
+      for (int i = 0; i < D; ++i) {
+        const float t = q[i] - a.params[k * D + i];
+        d2 = fmaf(t, t, d2);
+      }
+      al[k] = d2 * a.neg_half_inv_s2_log2e;
+      amax = fmaxf(amax, al[k]);
+    }
+  }
+  float den = 0.f, acc[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) acc[i] = 0.f;
+#pragma unroll
+  for (int k = 0; k < kMaxGmmK; ++k) {
+    if (k < a.K) {
+      const float e = __builtin_amdgcn_exp2f(al[k] - amax);
+      den += e;
+#pragma unroll
+      for (int i = 0; i < D; ++i) acc[i] = fmaf(e, a.params[k * D + i], acc[i]);
+    }
+  }
+  const float inv = 1.0f / den;
+#pragma unroll
+  for (int i = 0; i < D; ++i) g[i] = a.inv_s2 * (q[i] - acc[i] * inv);
+}
+
+template <int D>
+__device__ __forceinline__ void store_row(float* dst, const float* z) {
+  constexpr int M = 2 * D;
+  if constexpr (M % 4 == 0) {
+#pragma unroll
+    for (int k = 0; k < M; k += 4)
+      __builtin_nontemporal_store(f32x4{z[k], z[k + 1], z[k + 2], z[k + 3]},
+                                  reinterpret_cast<f32x4*>(dst + k));
+  } else {
+#pragma unroll
+    for (int k = 0; k < M; k += 2)
+      __builtin_nontemporal_store(f32x2{z[k], z[k + 1]}, reinterpret_cast<f32x2*>(dst + k));
+  }
+}
+
+__device__ __forceinline__ float tau_value(float tau0, int s, float dt) {
+#pragma clang fp contract(off)
+  return tau0 + (float)s * dt;  // tau_0 + arange(n)*dt, two roundings (sampling_utils.py:48)
+}
+
+__device__ __forceinline__ float shift_u(const SdeArgs& a, uint32_t plo, uint32_t phi, int64_t i) {
+  if (a.shift_u) return a.shift_u[i];
+  const uint4 r = philox4x32_10(make_uint4(plo, phi, a.ctr_off, 0x80000000u), a.k0, a.k1);
+  return u32_unit(r.x);
+}
+
+template <int D, int POT, bool MOM>
+__global__ __launch_bounds__(kBlock) void sde_simulate_kernel(SdeArgs a, const float* __restrict__ z0,
+                                                              float* __restrict__ traj,
+                                                              float* __restrict__ tau,
+                                                              float* __restrict__ last,
+                                                              float* __restrict__ partials) {
+  constexpr int M = 2 * D;
+  const int64_t i_raw = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const bool active = i_raw < a.N;
+  const int64_t i = active ? i_raw : a.N - 1;  // inactive lanes compute on a valid row, store nothing
+  const float w = active ? 1.f : 0.f;
+  const uint64_t gid = (uint64_t)(a.poff + i);
+  const uint32_t plo = (uint32_t)gid, phi = (uint32_t)(gid >> 32);
+
+  float z[M];
+#pragma unroll
+  for (int k = 0; k < M; ++k) z[k] = z0[i * a.ld_z0 + k];
+
+  __shared__ float lds[kWavesPerBlock * moment_len(M > 16 ? 2 : M)];
+  const int nb = gridDim.x;
+  constexpr int L = moment_len(M > 16 ? 2 : M);
+  if constexpr (MOM) {
+    MomentAcc<M> init;
+    init.zero();
+    init.add(z, w);
+    block_reduce_to_slab(init.v, L, lds, partials, blockIdx.x, nb);
+  }
+
+  const float tau0 = a.random_shift ? shift_u(a, plo, phi, i) * a.dt : 0.f;
+  const float h_last = a.dt - tau0;
+
+  MomentAcc<(MOM ? M : 2)> acc;
+  acc.zero();
+
+  float* tr = traj ? traj + i * M : nullptr;
+  float* ta = tau ? tau + i : nullptr;
+  const int64_t tr_stride = a.N * M;
+
+  auto update = [&](float h, float sh, uint32_t s) {
+    float g[D], xi[D];
+    if constexpr (POT == PDEINV_POT_GMM) grad_gmm<D>(a, z, g);
+    else grad_quadratic<D>(a, z, g);
+    gen_normals<D>(a, plo, phi, s, i, xi);
+    const float gh = a.gamma * h;
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      const float p = z[D + k];
+      // p' = p - h*gradU + sqrt(h)*ns*xi - gamma*p*h ; q' = q + h*p'  (sampling_utils.py:17,20)
+      const float pn = fmaf(-gh, p, fmaf(sh, xi[k], fmaf(-h, g[k], p)));
+      z[D + k] = pn;
+      z[k] = fmaf(h, pn, z[k]);
+    }
+  };
+
+  // update 0: h = tau0 (sample at tau0)
+  update(tau0, sqrtf(tau0) * a.ns, 0u);
+  if (active) {
+    if (tr) store_row<D>(tr, z);
+    if (ta) __builtin_nontemporal_store(tau_value(tau0, 0, a.dt), ta);
+  }
+  if constexpr (MOM) acc.add(z, w);
+
+  const float sh_dt = sqrtf(a.dt) * a.ns;
+  for (int s = 1; s < a.n_steps; ++s) {
+    update(a.dt, sh_dt, (uint32_t)s);
+    if (active) {
+      if (tr) store_row<D>(tr + (int64_t)s * tr_stride, z);
+      if (ta) __builtin_nontemporal_store(tau_value(tau0, s, a.dt), ta + (int64_t)s * a.N);
+    }
+    if constexpr (MOM) acc.add(z, w);
+  }
+
+  // final update: h = dt - tau0, lands exactly at T = n*dt (sampling_utils.py:44-46)
+  update(h_last, sqrtf(h_last) * a.ns, (uint32_t)a.n_steps);
+  if (active && last) store_row<D>(last + i * M, z);
+
+  if constexpr (MOM) {
+    block_reduce_to_slab(acc.v, L, lds, partials + (int64_t)L * nb, blockIdx.x, nb);
+    MomentAcc<M> term;
+    term.zero();
+    term.add(z, w);
+    block_reduce_to_slab(term.v, L, lds, partials + (int64_t)2 * L * nb, blockIdx.x, nb);
+  }
+}
+
+// ---- McKean–Vlasov single update ---------------------------------------------------------
+// grad U(q_i) = A (q_i - xbar) with xbar = (sum x)/count of the ensemble BEFORE this update
+// (the pairwise mean  mean_j grad Phi*(x_i - x_j) of kinetic_mckean_vlasov.py:20-23 for
+// quadratic Phi*, evaluated in O(N)). Emits [count, sum x_new] partials for the next update.
+template <int D>
+__global__ __launch_bounds__(kBlock) void mf_step_kernel(SdeArgs a, int s, float tau0,
+                                                         const float* __restrict__ zin,
+                                                         float* __restrict__ zout,
+                                                         float* __restrict__ tau_row,
+                                                         const double* __restrict__ xbar_sum,
+                                                         float* __restrict__ partials) {
+  constexpr int M = 2 * D;
+  const int64_t i_raw = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const bool active = i_raw < a.N;
+  const int64_t i = active ? i_raw : a.N - 1;
+  const uint64_t gid = (uint64_t)(a.poff + i);
+  float z[M];
+#pragma unroll
+  for (int k = 0; k < M; ++k) z[k] = zin[i * M + k];
+  const double cnt = xbar_sum[0];
+  float y[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) y[k] = z[k] - (float)(xbar_sum[1 + k] / cnt);
+  float g[D];
+#pragma unroll
+  for (int r = 0; r < D; ++r) {
+    float acc = 0.f;
+#pragma unroll
+    for (int c = 0; c < D; ++c) acc = fmaf(a.params[r * D + c], y[c], acc);
+    g[r] = acc;
+  }
+  float xi[D];
+  gen_normals<D>(a, (uint32_t)gid, (uint32_t)(gid >> 32), (uint32_t)s, i, xi);
+  const float h = (s == 0) ? tau0 : ((s == a.n_steps) ? a.dt - tau0 : a.dt);
+  const float sh = sqrtf(h) * a.ns;
+  const float gh = a.gamma * h;
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    const float p = z[D + k];
+    const float pn = fmaf(-gh, p, fmaf(sh, xi[k], fmaf(-h, g[k], p)));
+    z[D + k] = pn;
+    z[k] = fmaf(h, pn, z[k]);
+  }
+  if (active) {
+    store_row<D>(zout + i * M, z);
+    if (tau_row) tau_row[i] = tau_value(tau0, s, a.dt);
+  }
+  float v[1 + D];
+  v[0] = active ? 1.f : 0.f;
+#pragma unroll
+  for (int k = 0; k < D; ++k) v[1 + k] = v[0] * z[k];
+  __shared__ float lds[kWavesPerBlock * (1 + D)];
+  block_reduce_to_slab(v, 1 + D, lds, partials, blockIdx.x, gridDim.x);
+}
+
+__global__ void tau0_kernel(SdeArgs a, float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= a.N) return;
+  const uint64_t gid = (uint64_t)(a.poff + i);
+  out[i] = a.random_shift ? shift_u(a, (uint32_t)gid, (uint32_t)(gid >> 32), i) * a.dt : 0.f;
+}
+
+// ---- host side ----------------------------------------------------------------------------
+static int build_args(const pdeinv_sde_desc* d, SdeArgs& a) {
+  PDEINV_REQUIRE(d != nullptr, PDEINV_ERR_INVALID, "sde: null descriptor");
+  PDEINV_REQUIRE(d->dim >= 1 && d->dim <= PDEINV_MAX_DIM, PDEINV_ERR_UNSUPPORTED,
+                 "sde: dim must be in [1, 16]");
+  PDEINV_REQUIRE(d->n_steps >= 1, PDEINV_ERR_INVALID, "sde: n_steps must be >= 1");
+  PDEINV_REQUIRE(d->n_particles >= 0, PDEINV_ERR_INVALID, "sde: n_particles must be >= 0");
+  PDEINV_REQUIRE(d->particle_offset >= 0, PDEINV_ERR_INVALID, "sde: particle_offset must be >= 0");
+  PDEINV_REQUIRE(std::isfinite(d->dt) && d->dt > 0.f, PDEINV_ERR_INVALID, "sde: dt must be > 0");
+  PDEINV_REQUIRE(std::isfinite(d->gamma) && std::isfinite(d->noise_scale), PDEINV_ERR_INVALID,
+                 "sde: gamma / noise_scale must be finite");
+  const int D = d->dim;
+  a = SdeArgs{};
+  a.N = d->n_particles;
+  a.poff = d->particle_offset;
+  a.ld_z0 = d->ld_z0 ? d->ld_z0 : 2 * D;
+  PDEINV_REQUIRE(a.ld_z0 >= 2 * D, PDEINV_ERR_INVALID, "sde: ld_z0 < 2*dim");
+  a.n_steps = d->n_steps;
+  a.random_shift = d->random_shift ? 1 : 0;
+  a.dt = d->dt;
+  a.gamma = d->gamma;
+  a.ns = d->noise_scale;
+  a.k0 = (uint32_t)d->seed;
+  a.k1 = (uint32_t)(d->seed >> 32);
+  a.ctr_off = d->counter_offset;
+  a.noise = d->d_noise;
+  a.shift_u = d->d_shift_u;
+  const pdeinv_potential& p = d->potential;
+  int n_params = 0;
+  switch (p.kind) {
+    case PDEINV_POT_QUADRATIC:
+    case PDEINV_POT_MEANFIELD_QUADRATIC:
+      a.has_center = (p.kind == PDEINV_POT_QUADRATIC && p.has_center) ? 1 : 0;
+      n_params = D * D + (a.has_center ? D : 0);
+      break;
+    case PDEINV_POT_GMM:
+      PDEINV_REQUIRE(p.n_centers >= 1 && p.n_centers <= kMaxGmmK &&
+                         p.n_centers * D <= PDEINV_MAX_PARAMS,
+                     PDEINV_ERR_UNSUPPORTED, "sde: GMM needs 1 <= n_centers <= 16");
+      PDEINV_REQUIRE(std::isfinite(p.sigma) && p.sigma > 0.f, PDEINV_ERR_INVALID,
+                     "sde: GMM sigma must be > 0");
+      a.K = p.n_centers;
+      a.inv_s2 = 1.0f / (p.sigma * p.sigma);
+      a.neg_half_inv_s2_log2e = -0.5f * a.inv_s2 * 1.4426950408889634f;
+      n_params = p.n_centers * D;
+      break;
+    case PDEINV_POT_NONE:
+      n_params = 0;  // quadratic with A = 0
+      break;
+    default:
+      return fail(PDEINV_ERR_UNSUPPORTED, "sde: unknown potential kind");
+  }
+  if (n_params) {
+    PDEINV_REQUIRE(p.params != nullptr, PDEINV_ERR_INVALID, "sde: potential params are null");
+    for (int k = 0; k < n_params; ++k) a.params[k] = p.params[k];
+  }
+  return PDEINV_OK;
+}
+
+static int sim_grid(int64_t N) { return grid_for(N); }
+
+}  // namespace pdeinv
+
+using namespace pdeinv;
+
+extern "C" int pdeinv_moment_len(int m) { return moment_len(m); }
+
+extern "C" size_t pdeinv_sde_workspace_bytes(const pdeinv_sde_desc* d) {
+  if (!d || d->dim < 1 || d->dim > 8 || d->n_particles <= 0) return 0;
+  return (size_t)3 * moment_len(2 * d->dim) * sim_grid(d->n_particles) * sizeof(float);
+}
+
+template <int D, int POT, bool MOM>
+static void launch_sim(const SdeArgs& a, const float* z0, float* traj, float* tau, float* last,
+                       float* ws, hipStream_t st) {
+  hipLaunchKernelGGL((sde_simulate_kernel<D, POT, MOM>), dim3(sim_grid(a.N)), dim3(kBlock), 0, st,
+                     a, z0, traj, tau, last, ws);
+}
+
+template <int D>
+static int dispatch_sim(const SdeArgs& a, int pot, bool mom, const float* z0, float* traj,
+                        float* tau, float* last, float* ws, hipStream_t st) {
+  if (pot == PDEINV_POT_GMM) {
+    if constexpr (D <= 8) {
+      if (mom) { launch_sim<D, PDEINV_POT_GMM, true>(a, z0, traj, tau, last, ws, st); return 0; }
+    }
+    launch_sim<D, PDEINV_POT_GMM, false>(a, z0, traj, tau, last, ws, st);
+  } else {
+    if constexpr (D <= 8) {
+      if (mom) { launch_sim<D, PDEINV_POT_QUADRATIC, true>(a, z0, traj, tau, last, ws, st); return 0; }
+    }
+    launch_sim<D, PDEINV_POT_QUADRATIC, false>(a, z0, traj, tau, last, ws, st);
+  }
+  return 0;
+}
+
+static bool aligned(const void* p, size_t a) { return p == nullptr || ((uintptr_t)p % a) == 0; }
+
+extern "C" int pdeinv_sde_simulate(const pdeinv_sde_desc* d, const float* z0, float* traj,
+                                   float* tau, float* last, void* ws, double* moments,
+                                   void* stream) {
+  SdeArgs a;
+  int rc = build_args(d, a);
+  if (rc) return rc;
+  PDEINV_REQUIRE(d->potential.kind != PDEINV_POT_MEANFIELD_QUADRATIC, PDEINV_ERR_INVALID,
+                 "sde: McKean–Vlasov runs through pdeinv_mf_step (one all-reduce per update)");
+  const int D = d->dim;
+  const bool mom = moments != nullptr;
+  PDEINV_REQUIRE(!mom || D <= 8, PDEINV_ERR_UNSUPPORTED, "sde: fused moments need dim <= 8");
+  hipStream_t st = (hipStream_t)stream;
+  const int L = moment_len(2 * D);
+  if (a.N == 0) {
+    if (mom && hipMemsetAsync(moments, 0, sizeof(double) * 3 * L, st) != hipSuccess)
+      return fail(PDEINV_ERR_HIP, "sde: hipMemsetAsync failed");
+    return PDEINV_OK;
+  }
+  PDEINV_REQUIRE(z0 != nullptr, PDEINV_ERR_INVALID, "sde: z0 is null");
+  PDEINV_REQUIRE(!mom || ws != nullptr, PDEINV_ERR_INVALID, "sde: moments need a workspace");
+  const size_t va = (D % 2 == 0) ? 16 : 8;
+  PDEINV_REQUIRE(aligned(traj, va) && aligned(last, va) && aligned(tau, 4), PDEINV_ERR_INVALID,
+                 "sde: traj/last must be 16-byte (even dim) or 8-byte (odd dim) aligned");
+  float* wsf = (float*)ws;
+  switch (D) {
+#define CASE(DD) case DD: dispatch_sim<DD>(a, d->potential.kind, mom, z0, traj, tau, last, wsf, st); break;
+    CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) CASE(10) CASE(12) CASE(16)
+#undef CASE
+    default:
+      return fail(PDEINV_ERR_UNSUPPORTED, "sde: dim must be one of 1-8, 10, 12, 16");
+  }
+  rc = check_launch("sde_simulate_kernel");
+  if (rc) return rc;
+  if (mom) {
+    launch_slab_reduce(wsf, sim_grid(a.N), 3 * L, moments, st);
+    rc = check_launch("slab_reduce_kernel");
+  }
+  return rc;
+}
+
+extern "C" size_t pdeinv_mf_workspace_bytes(const pdeinv_sde_desc* d) {
+  if (!d || d->dim < 1 || d->dim > PDEINV_MAX_DIM || d->n_particles <= 0) return 0;
+  return (size_t)(1 + d->dim) * sim_grid(d->n_particles) * sizeof(float);
+}
+
+static float shared_tau0_host(const SdeArgs& a, const pdeinv_sde_desc* d);
+
+extern "C" int pdeinv_mf_step(const pdeinv_sde_desc* d, int32_t s, const float* z, float* z_out,
+                              float* tau_row, const float* /*d_tau0*/, const double* xbar_sum,
+                              void* ws, double* xsum, void* stream) {
+  SdeArgs a;
+  int rc = build_args(d, a);
+  if (rc) return rc;
+  PDEINV_REQUIRE(d->potential.kind == PDEINV_POT_MEANFIELD_QUADRATIC, PDEINV_ERR_INVALID,
+                 "mf_step: potential must be MEANFIELD_QUADRATIC");
+  PDEINV_REQUIRE(s >= 0 && s <= d->n_steps, PDEINV_ERR_INVALID, "mf_step: s out of range");
+  PDEINV_REQUIRE(d->d_shift_u == nullptr, PDEINV_ERR_INVALID,
+                 "mf_step: the shared tau0 is drawn from the stream (shift_u unsupported)");
+  hipStream_t st = (hipStream_t)stream;
+  if (a.N == 0) {
+    if (xsum && hipMemsetAsync(xsum, 0, sizeof(double) * (1 + d->dim), st) != hipSuccess)
+      return fail(PDEINV_ERR_HIP, "mf_step: hipMemsetAsync failed");
+    return PDEINV_OK;
+  }
+  PDEINV_REQUIRE(z && z_out && xbar_sum && ws && xsum, PDEINV_ERR_INVALID, "mf_step: null pointer");
+  const float tau0 = shared_tau0_host(a, d);
+  const int D = d->dim;
+  const int g = sim_grid(a.N);
+  switch (D) {
+#define CASE(DD)                                                                           \
+  case DD:                                                                                 \
+    hipLaunchKernelGGL(mf_step_kernel<DD>, dim3(g), dim3(kBlock), 0, st, a, s, tau0, z, z_out, \
+                       tau_row, xbar_sum, (float*)ws);                                     \
+    break;
+    CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) CASE(10) CASE(12) CASE(16)
+#undef CASE
+    default:
+      return fail(PDEINV_ERR_UNSUPPORTED, "mf_step: dim must be one of 1-8, 10, 12, 16");
+  }
+  rc = check_launch("mf_step_kernel");
+  if (rc) return rc;
+  launch_slab_reduce((float*)ws, g, 1 + D, xsum, st);
+  return check_launch("slab_reduce_kernel");
+}
+
+// The interacting ensemble shares one clock: tau0 from global id UINT64_MAX (include/pdeinv.h).
+// Computed on the host with the same Philox so that every rank and every step agrees.
+static float shared_tau0_host(const SdeArgs& a, const pdeinv_sde_desc* d) {
+  if (!a.random_shift) return 0.f;
+  uint32_t c0 = 0xFFFFFFFFu, c1 = 0xFFFFFFFFu, c2 = a.ctr_off, c3 = 0x80000000u;
+  uint32_t k0 = a.k0, k1 = a.k1;
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)kM0 * c0, p1 = (uint64_t)kM1 * c2;
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0, n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    c1 = (uint32_t)p1;
+    c3 = (uint32_t)p0;
+    c0 = n0;
+    c2 = n2;
+    k0 += kW0;
+    k1 += kW1;
+  }
+  const float u = (float)(c0 >> 8) * 0x1p-24f;
+  (void)d;
+  return u * a.dt;
+}
+
+extern "C" int pdeinv_sde_tau0(const pdeinv_sde_desc* d, float* out, void* stream) {
+  SdeArgs a;
+  int rc = build_args(d, a);
+  if (rc) return rc;
+  if (a.N == 0) return PDEINV_OK;
+  PDEINV_REQUIRE(out != nullptr, PDEINV_ERR_INVALID, "sde_tau0: out is null");
+  hipLaunchKernelGGL(tau0_kernel, dim3(sim_grid(a.N)), dim3(kBlock), 0, (hipStream_t)stream, a, out);
+  return check_launch("tau0_kernel");
+}

@@ -1,0 +1,412 @@
+"""ctypes binding of libpdeinv.so (the C ABI in include/pdeinv.h).
+
+This is the only door from the Python mirror of the reference into the hot path. It fails
+loudly: if the library is missing, or a call is made without a GPU, it raises — there is no
+CPU fallback anywhere in the product path. Error codes map to the
+reference's exception types: INVALID -> ValueError, UNSUPPORTED -> NotImplementedError,
+HIP -> RuntimeError.
+
+PyTorch-ROCm is plumbing here: it owns device memory (caching allocator) and streams; every
+pointer handed to the library is a torch tensor's data_ptr() on the current stream. torch is
+imported before the library is dlopen'ed so that both share torch's libamdhip64.so.7.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+import subprocess
+from typing import Optional
+
+import numpy as np
+import torch
+
+_PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC_DIR = os.path.join(_PKG_DIR, "csrc")
+LIB_PATH = os.path.join(_PKG_DIR, "_build", "libpdeinv.so")
+
+PDEINV_OK, PDEINV_ERR_INVALID, PDEINV_ERR_UNSUPPORTED, PDEINV_ERR_HIP = 0, -1, -2, -3
+POT_QUADRATIC, POT_GMM, POT_MEANFIELD_QUADRATIC, POT_NONE = 0, 1, 2, 3
+MAX_DIM, MAX_PARAMS = 16, 256
+KFP_NOUT = 9
+KFP_SLOTS = ("loss", "loss ground truth", "grad_norm", "loss_nabla", "loss_Hessian",
+             "loss_friction", "loss_nabla_true", "loss_initial", "loss_terminal")
+GMM_NACC = 8
+SQRT2 = math.sqrt(2.0)
+
+# Every exported symbol of include/pdeinv.h (tests check the library exports all of them).
+EXPORTED_SYMBOLS = (
+    "pdeinv_moment_len", "pdeinv_sde_workspace_bytes", "pdeinv_sde_simulate",
+    "pdeinv_mf_workspace_bytes", "pdeinv_mf_step", "pdeinv_sde_tau0",
+    "pdeinv_moments_workspace_bytes", "pdeinv_moments", "pdeinv_residual_kfp_quadratic",
+    "pdeinv_residual_kfp_gmm_workspace_bytes", "pdeinv_residual_kfp_gmm",
+    "pdeinv_residual_kfp_gmm_finalize", "pdeinv_gmm_potential", "pdeinv_gaussian_sample",
+    "pdeinv_philox_fill", "pdeinv_gather_subsample", "pdeinv_abi_version", "pdeinv_last_error",
+    "pdeinv_runtime_version",
+)
+
+
+class PotentialDesc(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("n_centers", ctypes.c_int32), ("sigma", ctypes.c_float),
+                ("has_center", ctypes.c_int32), ("params", ctypes.c_void_p)]
+
+
+class SdeDesc(ctypes.Structure):
+    _fields_ = [("n_particles", ctypes.c_int64), ("particle_offset", ctypes.c_int64),
+                ("dim", ctypes.c_int32), ("n_steps", ctypes.c_int32), ("dt", ctypes.c_float),
+                ("gamma", ctypes.c_float), ("noise_scale", ctypes.c_float),
+                ("random_shift", ctypes.c_int32), ("seed", ctypes.c_uint64),
+                ("counter_offset", ctypes.c_uint32), ("ld_z0", ctypes.c_int64),
+                ("potential", PotentialDesc), ("d_noise", ctypes.c_void_p),
+                ("d_shift_u", ctypes.c_void_p), ("d_meanfield", ctypes.c_void_p)]
+
+
+class KfpQuadDesc(ctypes.Structure):
+    _fields_ = [("dim", ctypes.c_int32), ("gamma", ctypes.c_float), ("total_time", ctypes.c_float),
+                ("tilde_F", ctypes.c_void_p)]
+
+
+class KfpGmmDesc(ctypes.Structure):
+    _fields_ = [("dim", ctypes.c_int32), ("n_centers", ctypes.c_int32), ("sigma", ctypes.c_float),
+                ("n_centers_true", ctypes.c_int32), ("sigma_true", ctypes.c_float),
+                ("mus_true", ctypes.c_void_p), ("gamma", ctypes.c_float),
+                ("c_nabla", ctypes.c_float), ("c_hess", ctypes.c_float), ("c_fric", ctypes.c_float),
+                ("c_true", ctypes.c_float), ("c_init", ctypes.c_float), ("c_term", ctypes.c_float)]
+
+
+_lib = None
+
+
+def build(force: bool = False, jobs: int = 8) -> str:
+    """Compile libpdeinv.so in-tree (hipcc --offload-arch=gfx950)."""
+    args = ["make", "-C", CSRC_DIR, f"-j{jobs}"]
+    if force:
+        subprocess.check_call(["make", "-C", CSRC_DIR, "clean"])
+    subprocess.check_call(args)
+    return LIB_PATH
+
+
+def lib():
+    """The loaded library; raises if it was not built (no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"pdeinv native library missing at {LIB_PATH}; run __graft_entry__.build() "
+                           "(the hot path has no CPU fallback)")
+    L = ctypes.CDLL(LIB_PATH)
+    P, i32, i64, u32, u64, f32 = (ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32,
+                                  ctypes.c_uint64, ctypes.c_float)
+    sig = {
+        "pdeinv_moment_len": (i32, [i32]),
+        "pdeinv_sde_workspace_bytes": (ctypes.c_size_t, [P]),
+        "pdeinv_sde_simulate": (i32, [P, P, P, P, P, P, P, P]),
+        "pdeinv_mf_workspace_bytes": (ctypes.c_size_t, [P]),
+        "pdeinv_mf_step": (i32, [P, i32, P, P, P, P, P, P, P, P]),
+        "pdeinv_sde_tau0": (i32, [P, P, P]),
+        "pdeinv_moments_workspace_bytes": (ctypes.c_size_t, [i64, i32]),
+        "pdeinv_moments": (i32, [P, i64, i32, i64, P, P, P]),
+        "pdeinv_residual_kfp_quadratic": (i32, [P, P, P, P, P, P]),
+        "pdeinv_residual_kfp_gmm_workspace_bytes": (ctypes.c_size_t, [P, i64, i64, i64]),
+        "pdeinv_residual_kfp_gmm": (i32, [P, P, i64, i64, P, i64, i64, P, i64, i64, P, P, P, P]),
+        "pdeinv_residual_kfp_gmm_finalize": (i32, [P, P, P, P, P]),
+        "pdeinv_gmm_potential": (i32, [i32, i32, f32, P, P, i64, i64, P, P, P]),
+        "pdeinv_gaussian_sample": (i32, [i64, i32, u64, u32, i64, P, P, P, P]),
+        "pdeinv_philox_fill": (i32, [u64, u32, u32, i64, P, P]),
+        "pdeinv_gather_subsample": (i32, [P, i64, i32, i32, P, i64, P, i32, P, P]),
+        "pdeinv_abi_version": (i32, []),
+        "pdeinv_last_error": (ctypes.c_char_p, []),
+        "pdeinv_runtime_version": (i32, []),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    if L.pdeinv_abi_version() != 1:
+        raise RuntimeError("libpdeinv ABI version mismatch")
+    _lib = L
+    return _lib
+
+
+def _check(rc: int, what: str) -> None:
+    if rc == PDEINV_OK:
+        return
+    msg = f"{what}: {lib().pdeinv_last_error().decode(errors='replace')}"
+    if rc == PDEINV_ERR_INVALID:
+        raise ValueError(msg)
+    if rc == PDEINV_ERR_UNSUPPORTED:
+        raise NotImplementedError(msg)
+    raise RuntimeError(msg)
+
+
+def _require_gpu():
+    if not torch.cuda.is_available():
+        raise RuntimeError("pdeinv hot path needs a ROCm GPU (no CPU fallback)")
+
+
+def _dev(t: Optional[torch.Tensor], name: str, dtype=torch.float32) -> Optional[ctypes.c_void_p]:
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a device tensor")
+    if t.dtype != dtype:
+        raise ValueError(f"{name} must be {dtype}, got {t.dtype}")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _rows(t: torch.Tensor, name: str, m: int):
+    """A 2-D [n, m] view with unit inner stride; returns (ptr, n, ld)."""
+    if t.dim() != 2 or t.shape[1] != m:
+        raise ValueError(f"{name} must have shape [n, {m}], got {tuple(t.shape)}")
+    if t.shape[0] > 0 and t.stride(1) != 1:
+        raise ValueError(f"{name} must have unit stride along its last axis")
+    return _dev(t, name), t.shape[0], (t.stride(0) if t.shape[0] > 1 else m)
+
+
+def stream_handle() -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def moment_len(m: int) -> int:
+    return 1 + m + m * (m + 1) // 2
+
+
+def _host_f32(a) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(a, dtype=np.float32).ravel())
+
+
+# -----------------------------------------------------------------------------------------
+# simulator
+# -----------------------------------------------------------------------------------------
+def make_potential(kind: int, params=None, n_centers: int = 0, sigma: float = 1.0,
+                   has_center: bool = False):
+    host = _host_f32(np.zeros(1) if params is None else params)
+    desc = PotentialDesc(kind, int(n_centers), float(sigma), int(has_center),
+                         host.ctypes.data_as(ctypes.c_void_p))
+    return desc, host  # keep `host` alive while desc is used
+
+
+def sde_simulate(z0: torch.Tensor, n_steps: int, dt: float, gamma: float, potential: dict, *,
+                 seed: int, counter_offset: int = 0, particle_offset: int = 0,
+                 noise_scale: float = SQRT2, random_shift: bool = True,
+                 noise: Optional[torch.Tensor] = None, shift_u: Optional[torch.Tensor] = None,
+                 traj: bool = True, tau: bool = True, last: bool = True,
+                 moments: bool = False, out: Optional[dict] = None) -> dict:
+    """utils/sampling_utils.py:25-52 on the GPU. Returns time-major traj [n, N, 2d]."""
+    _require_gpu()
+    if z0.dim() != 2 or z0.shape[1] % 2:
+        raise ValueError("q0_p0 must be [N, 2d]")
+    N, m = z0.shape
+    d = m // 2
+    p_desc, p_host = make_potential(**potential)
+    desc = SdeDesc()
+    desc.n_particles = N
+    desc.particle_offset = int(particle_offset)
+    desc.dim = d
+    desc.n_steps = int(n_steps)
+    desc.dt = float(dt)
+    desc.gamma = float(gamma)
+    desc.noise_scale = float(noise_scale)
+    desc.random_shift = int(bool(random_shift))
+    desc.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+    desc.counter_offset = int(counter_offset) & 0xFFFFFFFF
+    z0p, _, ld = _rows(z0, "q0_p0", m) if N > 0 else (None, 0, m)
+    desc.ld_z0 = ld
+    desc.potential = p_desc
+    if noise is not None:
+        if tuple(noise.shape) != (n_steps + 1, N, d) or not noise.is_contiguous():
+            raise ValueError(f"noise must be contiguous [{n_steps + 1}, {N}, {d}]")
+        desc.d_noise = _dev(noise, "noise")
+    if shift_u is not None:
+        if tuple(shift_u.shape) != (N,) or not shift_u.is_contiguous():
+            raise ValueError(f"shift_u must be contiguous [{N}]")
+        desc.d_shift_u = _dev(shift_u, "shift_u")
+    dev = z0.device
+    res = {} if out is None else out
+    if traj and "traj" not in res:
+        res["traj"] = torch.empty((n_steps, N, m), device=dev, dtype=torch.float32)
+    if tau and "tau" not in res:
+        res["tau"] = torch.empty((n_steps, N), device=dev, dtype=torch.float32)
+    if last and "last" not in res:
+        res["last"] = torch.empty((N, m), device=dev, dtype=torch.float32)
+    ws = None
+    if moments:
+        if "moments" not in res:
+            res["moments"] = torch.empty((3, moment_len(m)), device=dev, dtype=torch.float64)
+        nbytes = lib().pdeinv_sde_workspace_bytes(ctypes.byref(desc))
+        ws = torch.empty(max(nbytes // 4, 1), device=dev, dtype=torch.float32)
+    rc = lib().pdeinv_sde_simulate(
+        ctypes.byref(desc), z0p, _dev(res.get("traj") if traj else None, "traj"),
+        _dev(res.get("tau") if tau else None, "tau"), _dev(res.get("last") if last else None, "last"),
+        _dev(ws, "workspace"), _dev(res.get("moments") if moments else None, "moments", torch.float64),
+        stream_handle())
+    del p_host
+    _check(rc, "pdeinv_sde_simulate")
+    return res
+
+
+def sde_tau0(N: int, dt: float, *, seed: int, counter_offset: int = 0, particle_offset: int = 0,
+             random_shift: bool = True, device="cuda") -> torch.Tensor:
+    _require_gpu()
+    desc = SdeDesc()
+    desc.n_particles = N
+    desc.particle_offset = particle_offset
+    desc.dim = 1
+    desc.n_steps = 1
+    desc.dt = dt
+    desc.noise_scale = SQRT2
+    desc.random_shift = int(random_shift)
+    desc.seed = seed
+    desc.counter_offset = counter_offset
+    desc.potential = PotentialDesc(POT_NONE, 0, 1.0, 0, None)
+    out = torch.empty(N, device=device, dtype=torch.float32)
+    _check(lib().pdeinv_sde_tau0(ctypes.byref(desc), _dev(out, "tau0"), stream_handle()), "pdeinv_sde_tau0")
+    return out
+
+
+def mf_step(desc: SdeDesc, s: int, z: torch.Tensor, z_out: torch.Tensor, tau_row, xbar_sum: torch.Tensor,
+            ws: torch.Tensor, xsum_out: torch.Tensor) -> None:
+    rc = lib().pdeinv_mf_step(ctypes.byref(desc), int(s), _dev(z, "z"), _dev(z_out, "z_out"),
+                              _dev(tau_row, "tau_row"), None, _dev(xbar_sum, "xbar_sum", torch.float64),
+                              _dev(ws, "workspace"), _dev(xsum_out, "xsum", torch.float64), stream_handle())
+    _check(rc, "pdeinv_mf_step")
+
+
+# -----------------------------------------------------------------------------------------
+# moments + residuals
+# -----------------------------------------------------------------------------------------
+def moments(z: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """[count, sum z, sum z_i z_j (i<=j)] fp64 of the rows of z ([..., m], inner stride 1)."""
+    _require_gpu()
+    m = z.shape[-1]
+    z2 = z.reshape(-1, m)
+    ptr, n, ld = _rows(z2, "z", m) if z2.shape[0] > 0 else (None, 0, m)
+    if out is None:
+        out = torch.empty(moment_len(m), device=z.device, dtype=torch.float64)
+    nbytes = lib().pdeinv_moments_workspace_bytes(n, m)
+    if nbytes == 0:
+        raise NotImplementedError(f"moments: m={m} unsupported (1..16)")
+    ws = torch.empty(nbytes // 4, device=z.device, dtype=torch.float32)
+    _check(lib().pdeinv_moments(ptr, n, m, ld, _dev(ws, "ws"), _dev(out, "out", torch.float64),
+                                stream_handle()), "pdeinv_moments")
+    return out
+
+
+def residual_kfp_quadratic(mom3: torch.Tensor, theta_flat: torch.Tensor, tilde_F, gamma: float,
+                           total_time: float):
+    """kinetic_fokker_planck.py:11-69 for V_theta = x.(xK+b); returns (out[9], grad_flat)."""
+    _require_gpu()
+    d = int(round(math.sqrt(theta_flat.numel() + 0.25) - 0.5))
+    if d * d + d != theta_flat.numel():
+        raise ValueError("theta must hold d*d + d values")
+    if tuple(mom3.shape) != (3, moment_len(2 * d)) or not mom3.is_contiguous():
+        raise ValueError("moments must be contiguous [3, moment_len(2d)] fp64")
+    F = _host_f32(tilde_F)
+    desc = KfpQuadDesc(d, float(gamma), float(total_time), F.ctypes.data_as(ctypes.c_void_p))
+    out = torch.empty(KFP_NOUT, device=mom3.device, dtype=torch.float32)
+    grad = torch.empty_like(theta_flat)
+    _check(lib().pdeinv_residual_kfp_quadratic(ctypes.byref(desc), _dev(mom3, "moments", torch.float64),
+                                               _dev(theta_flat.contiguous(), "theta"), _dev(out, "out"),
+                                               _dev(grad, "grad"), stream_handle()),
+           "pdeinv_residual_kfp_quadratic")
+    return out, grad
+
+
+def kfp_gmm_desc(dim, n_centers, mus_true, gamma, total_time, n_init, n_term, n_0T, sigma=1.0,
+                 sigma_true=1.0, world_scale=1.0):
+    """Descriptor with the reference's loss weights (kinetic_fokker_planck.py:33-50).
+    world_scale = 1/world_size turns per-rank sums into the pmap mean (trainer.py:52)."""
+    mt = _host_f32(mus_true)
+    M = float(n_0T)
+    c = dict(c_nabla=1.0 / M, c_hess=-2.0 / M, c_fric=2.0 * gamma / M, c_true=1.0 / M,
+             c_init=(-2.0 / (total_time * n_init)) if n_init else 0.0,
+             c_term=(2.0 / (total_time * n_term)) if n_term else 0.0)
+    c = {k: v * world_scale for k, v in c.items()}
+    desc = KfpGmmDesc(int(dim), int(n_centers), float(sigma), int(mt.size // dim), float(sigma_true),
+                      mt.ctypes.data_as(ctypes.c_void_p), float(gamma), c["c_nabla"], c["c_hess"],
+                      c["c_fric"], c["c_true"], c["c_init"], c["c_term"])
+    return desc, mt
+
+
+def residual_kfp_gmm(desc_keep, z_init: torch.Tensor, z_term: torch.Tensor, z_0T: torch.Tensor,
+                     mus: torch.Tensor) -> torch.Tensor:
+    """Fused per-sample GMM residual + adjoint -> fp64 accumulator [8 + K*d]."""
+    _require_gpu()
+    desc, _keep = desc_keep
+    d, K = desc.dim, desc.n_centers
+    m = 2 * d
+    pi, ni, ldi = _rows(z_init, "initial", m) if z_init.shape[0] else (None, 0, m)
+    pt, nt, ldt = _rows(z_term, "terminal", m) if z_term.shape[0] else (None, 0, m)
+    p0, n0, ld0 = _rows(z_0T, "0T", m)
+    if tuple(mus.shape) != (K, d):
+        raise ValueError(f"mus must be [{K}, {d}]")
+    nbytes = lib().pdeinv_residual_kfp_gmm_workspace_bytes(ctypes.byref(desc), ni, nt, n0)
+    ws = torch.empty(max(nbytes // 4, 1), device=z_0T.device, dtype=torch.float32)
+    acc = torch.empty(GMM_NACC + K * d, device=z_0T.device, dtype=torch.float64)
+    rc = lib().pdeinv_residual_kfp_gmm(ctypes.byref(desc), pi, ni, ldi, pt, nt, ldt, p0, n0, ld0,
+                                       _dev(mus.contiguous(), "mus"), _dev(ws, "ws"),
+                                       _dev(acc, "acc", torch.float64), stream_handle())
+    _check(rc, "pdeinv_residual_kfp_gmm")
+    return acc
+
+
+def residual_kfp_gmm_finalize(desc_keep, acc: torch.Tensor):
+    desc, _keep = desc_keep
+    out = torch.empty(KFP_NOUT, device=acc.device, dtype=torch.float32)
+    grad = torch.empty(desc.n_centers * desc.dim, device=acc.device, dtype=torch.float32)
+    _check(lib().pdeinv_residual_kfp_gmm_finalize(ctypes.byref(desc), _dev(acc, "acc", torch.float64),
+                                                  _dev(out, "out"), _dev(grad, "grad"), stream_handle()),
+           "pdeinv_residual_kfp_gmm_finalize")
+    return out, grad.view(desc.n_centers, desc.dim)
+
+
+# -----------------------------------------------------------------------------------------
+# potentials, samplers, streams
+# -----------------------------------------------------------------------------------------
+def gmm_potential(x: torch.Tensor, mus, sigma: float = 1.0, value: bool = True, grad: bool = True):
+    _require_gpu()
+    mh = np.asarray(mus, dtype=np.float32)
+    K, d = mh.shape
+    ptr, n, ld = _rows(x, "x", d) if x.shape[0] else (None, 0, d)
+    v = torch.empty(n, device=x.device, dtype=torch.float32) if value else None
+    g = torch.empty((n, d), device=x.device, dtype=torch.float32) if grad else None
+    mh = _host_f32(mh)
+    _check(lib().pdeinv_gmm_potential(d, K, float(sigma), mh.ctypes.data_as(ctypes.c_void_p), ptr, n, ld,
+                                      _dev(v, "value"), _dev(g, "grad"), stream_handle()),
+           "pdeinv_gmm_potential")
+    return v, g
+
+
+def gaussian_sample(n: int, mean: torch.Tensor, cov_half: torch.Tensor, *, seed: int,
+                    counter_offset: int = 0, row_offset: int = 0) -> torch.Tensor:
+    _require_gpu()
+    m = mean.shape[0]
+    out = torch.empty((n, m), device=mean.device, dtype=torch.float32)
+    _check(lib().pdeinv_gaussian_sample(int(n), int(m), int(seed) & 0xFFFFFFFFFFFFFFFF,
+                                        int(counter_offset) & 0xFFFFFFFF, int(row_offset),
+                                        _dev(mean.contiguous(), "mean"), _dev(cov_half.contiguous(), "cov_half"),
+                                        _dev(out, "out"), stream_handle()), "pdeinv_gaussian_sample")
+    return out
+
+
+def philox_fill(seed: int, ctr_z: int, ctr_w: int, n_blocks: int, device="cuda") -> torch.Tensor:
+    _require_gpu()
+    out = torch.empty((n_blocks, 4), device=device, dtype=torch.int32)
+    _check(lib().pdeinv_philox_fill(seed, ctr_z, ctr_w, n_blocks, _dev(out, "out", torch.int32),
+                                    stream_handle()), "pdeinv_philox_fill")
+    return out
+
+
+def gather_subsample(traj_tm: torch.Tensor, traj_idx: torch.Tensor, time_idx: torch.Tensor) -> torch.Tensor:
+    """consistency.py:97-118 gather from a time-major [n, N, m] trajectory -> [n_sel*n_t, m]."""
+    _require_gpu()
+    n, N, m = traj_tm.shape
+    if not traj_tm.is_contiguous():
+        raise ValueError("trajectory must be contiguous time-major [n, N, m]")
+    ti = traj_idx.to(torch.int32).contiguous()
+    si = time_idx.to(torch.int32).contiguous()
+    out = torch.empty((ti.numel() * si.numel(), m), device=traj_tm.device, dtype=torch.float32)
+    _check(lib().pdeinv_gather_subsample(_dev(traj_tm, "traj"), N, n, m, _dev(ti, "traj_idx", torch.int32),
+                                         ti.numel(), _dev(si, "time_idx", torch.int32), si.numel(),
+                                         _dev(out, "out"), stream_handle()), "pdeinv_gather_subsample")
+    return out

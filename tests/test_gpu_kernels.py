@@ -1,0 +1,246 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the CPU oracle.
+
+Tolerances (fp32 path vs fp32/fp64 restatement):
+  * Philox bits, tau, gathers: bit-exact;
+  * normals: |GPU - oracle| <= 2e-6 * (1 + |z|) (hardware v_log/v_sin vs libm, both fp32-rounded);
+  * explicit-noise trajectories after 100 steps: rtol = atol = 1e-5 vs the fp64 restatement
+    scaled by the state magnitude;
+  * Philox-mode trajectories vs the C oracle: 1e-4 abs (normals differ in the last ulps);
+  * moments / residuals: 1e-5 relative (fp32 accumulation, fp64 across blocks).
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import numpy_ref as nr
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _t(a, dtype=torch.float32):
+    return torch.as_tensor(np.ascontiguousarray(a), dtype=dtype, device=DEV)
+
+
+def test_runtime_shared_with_torch(native):
+    v = native.lib().pdeinv_runtime_version()
+    assert v > 0
+
+
+@pytest.mark.parametrize("cz,cw", [(0, 0), (5, 3), (0xFFFFFFFF, 0x80000000)])
+def test_philox_bits_exact(native, oracle_lib, cz, cw):
+    seed = 0x0123456789ABCDEF
+    n = 4099
+    g = native.philox_fill(seed, cz, cw, n).cpu().numpy().view(np.uint32)
+    o = oracle_lib.philox_fill(seed, cz, cw, n)
+    assert np.array_equal(g, o)
+
+
+def test_philox_kat_through_gpu(native):
+    g = native.philox_fill(0, 0, 0, 1).cpu().numpy().view(np.uint32)[0]
+    assert [hex(x) for x in g] == ["0x6627e8d5", "0xe169c58d", "0xbc57ac4c", "0x9b00dbd8"]
+
+
+@pytest.mark.parametrize("d", [1, 2, 3, 4, 8])
+def test_sde_explicit_noise_vs_restatement(native, d):
+    rng = np.random.default_rng(d)
+    N, n, T = 333, 100, 2.0
+    dt = T / n
+    F = nr.problem_constants(d)
+    z0 = rng.standard_normal((N, 2 * d)).astype(np.float32)
+    xi = rng.standard_normal((n + 1, N, d)).astype(np.float32)
+    u = rng.random(N).astype(np.float32)
+    res = native.sde_simulate(_t(z0), n, dt, 1.0, dict(kind=native.POT_QUADRATIC, params=F), seed=1,
+                              noise=_t(xi), shift_u=_t(u))
+    torch.cuda.synchronize()
+    last, traj, tau = nr.sde_scan(z0, n, dt, 1.0, nr.grad_quadratic(F), xi, u)
+    scale = np.abs(traj).max(axis=(0, 2), keepdims=True) + 1.0
+    assert np.max(np.abs(res["traj"].cpu().numpy() - traj) / scale) < 1e-5
+    assert np.max(np.abs(res["last"].cpu().numpy() - last) / (np.abs(last).max(1, keepdims=True) + 1)) < 1e-5
+    # tau = tau0 + s*dt with two fp32 roundings: bit-exact against the fp32 restatement
+    _, _, tau32 = nr.sde_scan(z0, n, dt, 1.0, nr.grad_quadratic(F), xi, u, dtype=np.float32)
+    assert np.array_equal(res["tau"].cpu().numpy(), tau32)
+
+
+@pytest.mark.parametrize("d,K", [(2, 3), (4, 3), (4, 8), (8, 8)])
+def test_sde_gmm_explicit_noise(native, d, K):
+    rng = np.random.default_rng(10 + d + K)
+    N, n, T = 257, 100, 2.0
+    dt = T / n
+    mus = nr.gmm_centres(d, K)
+    z0 = np.concatenate([2 * rng.standard_normal((N, d)), 0.3 * rng.standard_normal((N, d))], 1).astype(np.float32)
+    xi = rng.standard_normal((n + 1, N, d)).astype(np.float32)
+    u = rng.random(N).astype(np.float32)
+    res = native.sde_simulate(_t(z0), n, dt, 0.5, dict(kind=native.POT_GMM, params=mus, n_centers=K, sigma=1.0),
+                              seed=1, noise=_t(xi), shift_u=_t(u))
+    last, traj, _ = nr.sde_scan(z0, n, dt, 0.5, nr.grad_gmm(mus), xi, u)
+    scale = np.abs(traj).max(axis=(0, 2), keepdims=True) + 1.0
+    assert np.max(np.abs(res["traj"].cpu().numpy() - traj) / scale) < 1e-4
+
+
+@pytest.mark.parametrize("d", [2, 4, 8])
+def test_sde_philox_vs_c_oracle(native, oracle_lib, d):
+    rng = np.random.default_rng(100 + d)
+    N, n, T = 1000, 100, 2.0
+    dt = T / n
+    F = nr.problem_constants(d)
+    z0 = rng.standard_normal((N, 2 * d)).astype(np.float32)
+    seed, off, poff = 0xDEADBEEF12345, 77, 5_000_000_000
+    res = native.sde_simulate(_t(z0), n, dt, 1.0, dict(kind=native.POT_QUADRATIC, params=F), seed=seed,
+                              counter_offset=off, particle_offset=poff)
+    o = oracle_lib.sde_simulate(z0, n, dt, 1.0, "quadratic", F, seed=seed, counter_offset=off,
+                                particle_offset=poff)
+    assert np.array_equal(res["tau"].cpu().numpy(), o["tau"])  # same shift stream, same fp32 ops
+    assert np.max(np.abs(res["traj"].cpu().numpy() - o["traj"])) < 2e-4
+    assert np.max(np.abs(res["last"].cpu().numpy() - o["last"])) < 2e-4
+
+
+def test_sde_moments_match_discrete_chain(native):
+    """Philox-mode law == exact law of the chain, 5 sigma_MC."""
+    d, N, n, T = 4, 1 << 18, 100, 2.0
+    dt = T / n
+    F = nr.problem_constants(d)
+    z0 = native.gaussian_sample(N, _t(np.zeros(2 * d)), _t(np.eye(2 * d)), seed=3)
+    res = native.sde_simulate(z0, n, dt, 1.0, dict(kind=native.POT_QUADRATIC, params=F), seed=11,
+                              traj=True, tau=False, last=True)
+    mt, st, ml, sl = nr.em_chain_moments(F, 1.0, dt, n, np.zeros(2 * d), np.eye(2 * d))
+    for s in (0, 1, 50, n - 1):
+        z = res["traj"][s].double()
+        emp = (z.T @ z / N).cpu().numpy()
+        P = st[s]
+        sig = np.sqrt((np.outer(np.diag(P), np.diag(P)) + P ** 2) / N)
+        assert np.max(np.abs(emp - P) / sig) < 5.5, s
+        assert np.max(np.abs(z.mean(0).cpu().numpy() - mt[s]) / np.sqrt(np.diag(P) / N)) < 5.5
+    zl = res["last"].double()
+    emp = (zl.T @ zl / N).cpu().numpy()
+    sig = np.sqrt((np.outer(np.diag(sl), np.diag(sl)) + sl ** 2) / N)
+    assert np.max(np.abs(emp - sl) / sig) < 5.5
+
+
+@pytest.mark.parametrize("d", [1, 2, 4, 8])
+def test_fused_moments_equal_recomputed(native, d):
+    rng = np.random.default_rng(d)
+    N, n = 5003, 37
+    F = nr.problem_constants(d)
+    z0 = _t(rng.standard_normal((N, 2 * d)))
+    res = native.sde_simulate(z0, n, 0.02, 1.0, dict(kind=native.POT_QUADRATIC, params=F), seed=9,
+                              moments=True)
+    mom = res["moments"].cpu().numpy()
+    ref = [nr.moments(z0.cpu().numpy()), nr.moments(res["traj"].cpu().numpy()),
+           nr.moments(res["last"].cpu().numpy())]
+    for k in range(3):
+        assert np.allclose(mom[k], ref[k], rtol=2e-5, atol=1e-3 * max(1.0, ref[k][0] ** 0.5)), k
+
+
+@pytest.mark.parametrize("m", [2, 8, 16, 5])
+def test_moments_kernel_strided(native, m):
+    rng = np.random.default_rng(m)
+    big = _t(rng.standard_normal((70001, m + 3)))
+    view = big[:, :m]
+    got = native.moments(view).cpu().numpy()
+    ref = nr.moments(view.cpu().numpy())
+    assert np.allclose(got, ref, rtol=1e-5, atol=1e-2)
+
+
+def test_moments_empty(native):
+    got = native.moments(torch.empty((0, 8), device=DEV)).cpu().numpy()
+    assert np.all(got == 0)
+
+
+def test_residual_quadratic_vs_samples(native):
+    d, gamma, T = 4, 1.0, 2.0
+    rng = np.random.default_rng(0)
+    F = nr.problem_constants(d)
+    K = rng.standard_normal((d, d)).astype(np.float32)
+    b = rng.standard_normal(d).astype(np.float32)
+    zi, zt, z0 = (rng.standard_normal((n, 2 * d)).astype(np.float32) for n in (3000, 2000, 50000))
+    mom = torch.stack([native.moments(_t(z)) for z in (zi, z0, zt)])
+    theta = _t(np.concatenate([K.ravel(), b]))
+    out, grad = native.residual_kfp_quadratic(mom, theta, F, gamma, T)
+    out = out.cpu().numpy(); grad = grad.cpu().numpy()
+    loss, loss_gt, parts = nr.kfp_quadratic_samples(K, b, zi, zt, z0, F, gamma, T)
+    assert abs(out[0] - loss) < 1e-4 * (1 + abs(loss))
+    assert abs(out[1] - loss_gt) < 1e-4 * (1 + abs(loss_gt))
+    # gradient vs central finite differences of the per-sample restatement
+    def f(theta64):
+        return nr.kfp_quadratic_samples(theta64[:d * d].reshape(d, d), theta64[d * d:], zi, zt, z0, F, gamma, T)[0]
+    g_fd = nr.fd_grad(f, np.concatenate([K.ravel(), b]).astype(np.float64), eps=1e-4)
+    assert np.allclose(grad, g_fd, rtol=1e-4, atol=1e-3)
+    assert abs(out[2] - np.linalg.norm(g_fd)) < 1e-3 * (1 + np.linalg.norm(g_fd))
+
+
+@pytest.mark.parametrize("d,K,KT", [(2, 3, 3), (4, 8, 8), (4, 3, 8), (8, 8, 3)])
+def test_residual_gmm_vs_restatement(native, d, K, KT):
+    rng = np.random.default_rng(d * 10 + K)
+    gamma, T = 0.5, 2.0
+    mus_true = nr.gmm_centres(d, KT)
+    mus = rng.standard_normal((K, d))
+    zi = np.concatenate([2 * rng.standard_normal((1500, d)), 0.3 * rng.standard_normal((1500, d))], 1)
+    zt = rng.standard_normal((1200, 2 * d)) * 1.5
+    z0 = rng.standard_normal((20000, 2 * d)) * 1.5
+    zi, zt, z0 = (a.astype(np.float32) for a in (zi, zt, z0))
+    dk = native.kfp_gmm_desc(d, K, mus_true, gamma, T, len(zi), len(zt), len(z0))
+    acc = native.residual_kfp_gmm(dk, _t(zi), _t(zt), _t(z0), _t(mus))
+    out, grad = native.residual_kfp_gmm_finalize(dk, acc)
+    out = out.cpu().numpy(); grad = grad.cpu().numpy()
+    loss, loss_gt, parts = nr.kfp_gmm_loss(mus, zi, zt, z0, mus_true, gamma, T)
+    assert abs(out[0] - loss) < 2e-4 * (1 + abs(loss))
+    assert abs(out[1] - loss_gt) < 2e-4 * (1 + abs(loss_gt))
+    assert abs(out[4] - parts["hessian"]) < 2e-4 * (1 + abs(parts["hessian"]))
+    g_fd = nr.fd_grad(lambda th: nr.kfp_gmm_loss(th, zi, zt, z0, mus_true, gamma, T)[0], mus, eps=1e-5)
+    assert np.allclose(grad, g_fd, rtol=2e-3, atol=2e-4), np.abs(grad - g_fd).max()
+
+
+def test_gmm_potential(native, oracle_lib):
+    rng = np.random.default_rng(5)
+    d, K = 4, 8
+    mus = nr.gmm_centres(d, K)
+    x = (3 * rng.standard_normal((1000, d))).astype(np.float32)
+    v, g = native.gmm_potential(_t(x), mus)
+    vr, gr = nr.gmm_value_grad(x.astype(np.float64), mus)
+    assert np.allclose(v.cpu().numpy(), vr, rtol=1e-5, atol=1e-5)
+    assert np.allclose(g.cpu().numpy(), gr, rtol=1e-5, atol=1e-5)
+    # far from every centre: the max-shift keeps the softmax finite
+    far = _t(np.full((4, d), 40.0))
+    v2, g2 = native.gmm_potential(far, mus)
+    assert torch.isfinite(v2).all() and torch.isfinite(g2).all()
+
+
+@pytest.mark.parametrize("m", [8, 16, 5])
+def test_gaussian_sample_vs_oracle(native, oracle_lib, m):
+    rng = np.random.default_rng(m)
+    A = rng.standard_normal((m, m))
+    cov = A @ A.T + np.eye(m)
+    U, S, _ = np.linalg.svd(cov)
+    ch = (U @ np.diag(np.sqrt(S)) @ U.T).astype(np.float32)
+    mean = rng.standard_normal(m).astype(np.float32)
+    g = native.gaussian_sample(4096, _t(mean), _t(ch), seed=42, counter_offset=3, row_offset=1000).cpu().numpy()
+    o = oracle_lib.gaussian_sample(4096, mean, ch, 42, 3, 1000)
+    assert np.max(np.abs(g - o)) < 2e-5 * (1 + np.abs(o).max())
+
+
+def test_gather_subsample_exact(native):
+    rng = np.random.default_rng(1)
+    n, N, m = 40, 300, 8
+    traj = _t(rng.standard_normal((n, N, m)))
+    ti = torch.as_tensor(rng.permutation(N)[:60], device=DEV)
+    si = torch.as_tensor(np.arange(n // 5) * 5 + 2, device=DEV)
+    out = native.gather_subsample(traj, ti, si).cpu().numpy()
+    ref = traj.permute(1, 0, 2).cpu().numpy()[ti.cpu().numpy()][:, si.cpu().numpy(), :].reshape(-1, m)
+    assert np.array_equal(out, ref)
+
+
+def test_sde_edge_cases(native):
+    F = nr.problem_constants(2)
+    pot = dict(kind=native.POT_QUADRATIC, params=F)
+    res = native.sde_simulate(torch.empty((0, 4), device=DEV), 10, 0.1, 1.0, pot, seed=1, moments=True)
+    assert res["traj"].shape == (10, 0, 4) and torch.all(res["moments"] == 0)
+    one = native.sde_simulate(_t(np.ones((1, 4))), 1, 0.1, 1.0, pot, seed=1)
+    assert one["traj"].shape == (1, 1, 4) and torch.isfinite(one["last"]).all()
+    with pytest.raises(NotImplementedError):
+        native.sde_simulate(_t(np.ones((3, 22))), 5, 0.1, 1.0,
+                            dict(kind=native.POT_QUADRATIC, params=np.eye(11)), seed=1)
+    with pytest.raises(ValueError):
+        native.sde_simulate(_t(np.ones((3, 4))), 0, 0.1, 1.0, pot, seed=1)
