@@ -33,9 +33,10 @@ constexpr uint32_t kW0 = 0x9E3779B9u, kW1 = 0xBB67AE85u;
 __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
-    const uint32_t hi0 = __umulhi(kM0, c.x), lo0 = kM0 * c.x;
-    const uint32_t hi1 = __umulhi(kM1, c.z), lo1 = kM1 * c.z;
-    c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
+    // one v_mad_u64_u32 per product (hi and lo together) instead of v_mul_hi + v_mul_lo
+    const uint64_t p0 = (uint64_t)kM0 * c.x, p1 = (uint64_t)kM1 * c.z;
+    c = make_uint4((uint32_t)(p1 >> 32) ^ c.y ^ k0, (uint32_t)p1, (uint32_t)(p0 >> 32) ^ c.w ^ k1,
+                   (uint32_t)p0);
     k0 += kW0;
     k1 += kW1;
   }

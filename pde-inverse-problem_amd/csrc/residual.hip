@@ -22,121 +22,103 @@ struct KfpQuadArgs {
   float F[PDEINV_MAX_DIM * PDEINV_MAX_DIM];
 };
 
-struct SetMoments {
-  double n, mean[2 * PDEINV_MAX_DIM];
-  double M[2 * PDEINV_MAX_DIM][2 * PDEINV_MAX_DIM];  // E[z z^T]
+// Moment accessors over the packed fp64 layout [count, sum z (m), sum z_i z_j (i<=j)].
+struct MomView {
+  const double* v;
+  int m;
+  double inv;
+  __device__ MomView(const double* p, int m_) : v(p), m(m_), inv(p[0] > 0 ? 1.0 / p[0] : 0.0) {}
+  __device__ double mean(int i) const { return v[1 + i] * inv; }
+  __device__ double M(int i, int j) const {  // E[z_i z_j]
+    if (i > j) { const int t = i; i = j; j = t; }
+    return v[1 + m + i * m - i * (i - 1) / 2 + (j - i)] * inv;
+  }
 };
 
-__device__ void unpack_set(const double* v, int m, SetMoments& s) {
-  s.n = v[0];
-  const double inv = s.n > 0 ? 1.0 / s.n : 0.0;
-  for (int i = 0; i < m; ++i) s.mean[i] = v[1 + i] * inv;
-  int o = 1 + m;
-  for (int i = 0; i < m; ++i)
-    for (int j = i; j < m; ++j) {
-      s.M[i][j] = v[o] * inv;
-      s.M[j][i] = v[o] * inv;
-      ++o;
-    }
-}
-
-// One thread: d <= 16, O(d^3) work. Gradient derivation in oracle/numpy_ref.py
+// One block; thread t < d*d owns entry (i, j) = (t / d, t % d) of every d x d quantity, the
+// scalar terms are block sums. Gradient derivation: oracle/numpy_ref.py
 // kfp_quadratic_from_moments (checked there against central finite differences).
-__global__ void kfp_quadratic_finalize_kernel(KfpQuadArgs a, const double* __restrict__ mom,
-                                              const float* __restrict__ theta,
-                                              float* __restrict__ out, float* __restrict__ grad) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+__global__ __launch_bounds__(kBlock) void kfp_quadratic_finalize_kernel(KfpQuadArgs a,
+                                                                        const double* __restrict__ mom,
+                                                                        const float* __restrict__ theta,
+                                                                        float* __restrict__ out,
+                                                                        float* __restrict__ grad) {
   const int d = a.d, m = 2 * d, L = moment_len(m);
-  SetMoments si, s0, st;
-  unpack_set(mom, m, si);
-  unpack_set(mom + L, m, s0);
-  unpack_set(mom + 2 * L, m, st);
-  double S[PDEINV_MAX_DIM][PDEINV_MAX_DIM], b[PDEINV_MAX_DIM];
-  for (int i = 0; i < d; ++i) {
-    b[i] = theta[d * d + i];
-    for (int j = 0; j < d; ++j) S[i][j] = (double)theta[i * d + j] + (double)theta[j * d + i];
-  }
-  // SM = S Mxx, tr(S Mxx S), b^T S ex, ...
-  double SM[PDEINV_MAX_DIM][PDEINV_MAX_DIM];
-  for (int i = 0; i < d; ++i)
-    for (int j = 0; j < d; ++j) {
-      double t = 0;
-      for (int k = 0; k < d; ++k) t += S[i][k] * s0.M[k][j];
-      SM[i][j] = t;
-    }
-  double nabla = 0, bSe = 0, bb = 0, hess = 0, fric = 0, init = 0, term = 0, tru = 0, gt = 0;
-  double Sex[PDEINV_MAX_DIM];
-  for (int i = 0; i < d; ++i) {
-    double t = 0;
-    for (int k = 0; k < d; ++k) t += S[i][k] * s0.mean[k];
-    Sex[i] = t;
-    bSe += b[i] * t;
-    bb += b[i] * b[i];
-  }
-  for (int i = 0; i < d; ++i)
-    for (int j = 0; j < d; ++j) {
-      nabla += SM[i][j] * S[j][i];
-      hess += S[i][j] * s0.M[d + j][d + i];  // tr(S Mvv)
-      fric += S[i][j] * s0.M[j][d + i];      // tr(S Mxv), Mxv[j][i] = E[x_j v_i]
-      init += S[i][j] * si.M[j][d + i];
-      term += S[i][j] * st.M[j][d + i];
-    }
-  nabla += 2 * bSe + bb;
-  for (int i = 0; i < d; ++i) {
-    fric += b[i] * s0.mean[d + i];
-    init += b[i] * si.mean[d + i];
-    term += b[i] * st.mean[d + i];
-  }
-  // V* = 0.5 x^T F x (F symmetric): E|F x|^2 and E|(F - S) x - b|^2
-  double Dm[PDEINV_MAX_DIM][PDEINV_MAX_DIM];
-  for (int i = 0; i < d; ++i)
-    for (int j = 0; j < d; ++j) Dm[i][j] = (double)a.F[i * d + j] - S[i][j];
-  for (int i = 0; i < d; ++i) {
-    double fx2 = 0, dx2 = 0, de = 0;
-    for (int j = 0; j < d; ++j) {
-      de += Dm[i][j] * s0.mean[j];
-      for (int k = 0; k < d; ++k) {
-        fx2 += (double)a.F[i * d + j] * s0.M[j][k] * (double)a.F[i * d + k];
-        dx2 += Dm[i][j] * s0.M[j][k] * Dm[i][k];
-      }
-    }
-    tru += fx2;
-    gt += dx2 - 2 * b[i] * de;
-  }
-  gt += bb;
+  const MomView si(mom, m), s0(mom + L, m), st(mom + 2 * L, m);
+  auto S = [&](int i, int j) { return (double)theta[i * d + j] + (double)theta[j * d + i]; };
+  auto b = [&](int i) { return (double)theta[d * d + i]; };
+  auto F = [&](int i, int j) { return (double)a.F[i * d + j]; };
   const double g = a.gamma, T = a.T;
-  const double loss = nabla - 2 * hess + 2 * g * fric + tru + (-2 * init + 2 * term) / T;
-  // d loss / d S (entries independent) then d/dK = G + G^T
-  double G[PDEINV_MAX_DIM][PDEINV_MAX_DIM];
-  for (int i = 0; i < d; ++i)
-    for (int j = 0; j < d; ++j) {
-      double sm_ms = 0;
-      for (int k = 0; k < d; ++k) sm_ms += S[i][k] * s0.M[k][j] + s0.M[i][k] * S[k][j];
-      G[i][j] = sm_ms + 2 * b[i] * s0.mean[j] - 2 * s0.M[d + i][d + j] + 2 * g * s0.M[d + i][j] +
-                (-2 * si.M[d + i][j] + 2 * st.M[d + i][j]) / T;
+  // scalars: nabla, hess, fric(raw), init, term, true, gt, |grad|^2
+  double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int t = threadIdx.x;
+  if (t < d * d) {
+    const int i = t / d, j = t % d;
+    double SM = 0, MS = 0, SMji = 0, MSji = 0, FMF = 0, DMD = 0;
+    for (int k = 0; k < d; ++k) {
+      SM += S(i, k) * s0.M(k, j);
+      MS += s0.M(i, k) * S(k, j);
+      SMji += S(j, k) * s0.M(k, i);
+      MSji += s0.M(j, k) * S(k, i);
+      FMF += s0.M(j, k) * F(i, k);
+      DMD += s0.M(j, k) * (F(i, k) - S(i, k));
     }
-  double gn = 0;
-  for (int i = 0; i < d; ++i)
-    for (int j = 0; j < d; ++j) {
-      const double gk = G[i][j] + G[j][i];
-      grad[i * d + j] = (float)gk;
-      gn += gk * gk;
-    }
-  for (int i = 0; i < d; ++i) {
-    const double gb = 2 * Sex[i] + 2 * b[i] + 2 * g * s0.mean[d + i] +
-                      (-2 * si.mean[d + i] + 2 * st.mean[d + i]) / T;
-    grad[d * d + i] = (float)gb;
-    gn += gb * gb;
+    acc[0] = SM * S(j, i);                    // tr(S Mxx S)
+    acc[1] = S(i, j) * s0.M(d + j, d + i);    // tr(S Mvv)
+    acc[2] = S(i, j) * s0.M(j, d + i);        // tr(S Mxv), Mxv[j][i] = E[x_j v_i]
+    acc[3] = S(i, j) * si.M(j, d + i);
+    acc[4] = S(i, j) * st.M(j, d + i);
+    acc[5] = F(i, j) * FMF;                   // tr(F Mxx F^T)
+    acc[6] = (F(i, j) - S(i, j)) * DMD;       // tr(D Mxx D^T), D = F - S
+    // d loss / d S entries, then d/dK = G + G^T
+    const double Gij = SM + MS + 2 * b(i) * s0.mean(j) - 2 * s0.M(d + i, d + j) + 2 * g * s0.M(d + i, j) +
+                       (-2 * si.M(d + i, j) + 2 * st.M(d + i, j)) / T;
+    const double Gji = SMji + MSji + 2 * b(j) * s0.mean(i) - 2 * s0.M(d + j, d + i) + 2 * g * s0.M(d + j, i) +
+                       (-2 * si.M(d + j, i) + 2 * st.M(d + j, i)) / T;
+    const double gk = Gij + Gji;
+    grad[i * d + j] = (float)gk;
+    acc[7] = gk * gk;
   }
-  out[PDEINV_KFP_LOSS] = (float)loss;
-  out[PDEINV_KFP_LOSS_GT] = (float)gt;
-  out[PDEINV_KFP_GRAD_NORM] = (float)sqrt(gn);
-  out[PDEINV_KFP_NABLA] = (float)nabla;
-  out[PDEINV_KFP_HESSIAN] = (float)hess;
-  out[PDEINV_KFP_FRICTION] = (float)(g * fric);
-  out[PDEINV_KFP_NABLA_TRUE] = (float)tru;
-  out[PDEINV_KFP_INITIAL] = (float)init;
-  out[PDEINV_KFP_TERMINAL] = (float)term;
+  if (t < d) {
+    const int i = t;
+    double Sex = 0, De = 0;
+    for (int k = 0; k < d; ++k) {
+      Sex += S(i, k) * s0.mean(k);
+      De += (F(i, k) - S(i, k)) * s0.mean(k);
+    }
+    acc[0] += 2 * b(i) * Sex + b(i) * b(i);
+    acc[2] += b(i) * s0.mean(d + i);
+    acc[3] += b(i) * si.mean(d + i);
+    acc[4] += b(i) * st.mean(d + i);
+    acc[6] += -2 * b(i) * De + b(i) * b(i);
+    const double gb = 2 * Sex + 2 * b(i) + 2 * g * s0.mean(d + i) + (-2 * si.mean(d + i) + 2 * st.mean(d + i)) / T;
+    grad[d * d + i] = (float)gb;
+    acc[7] += gb * gb;
+  }
+  __shared__ double red[kWavesPerBlock][8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    double v = acc[c];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    if ((t & 63) == 0) red[t >> 6][c] = v;
+  }
+  __syncthreads();
+  if (t == 0) {
+    double r[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) r[c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+    const double nabla = r[0], hess = r[1], fric = r[2], init = r[3], term = r[4], tru = r[5];
+    out[PDEINV_KFP_LOSS] = (float)(nabla - 2 * hess + 2 * g * fric + tru + (-2 * init + 2 * term) / T);
+    out[PDEINV_KFP_LOSS_GT] = (float)r[6];
+    out[PDEINV_KFP_GRAD_NORM] = (float)sqrt(r[7]);
+    out[PDEINV_KFP_NABLA] = (float)nabla;
+    out[PDEINV_KFP_HESSIAN] = (float)hess;
+    out[PDEINV_KFP_FRICTION] = (float)(g * fric);
+    out[PDEINV_KFP_NABLA_TRUE] = (float)tru;
+    out[PDEINV_KFP_INITIAL] = (float)init;
+    out[PDEINV_KFP_TERMINAL] = (float)term;
+  }
 }
 
 // =========================================================================================
@@ -388,8 +370,8 @@ extern "C" int pdeinv_residual_kfp_quadratic(const pdeinv_kfp_quad_desc* d, cons
   a.gamma = d->gamma;
   a.T = d->total_time;
   for (int k = 0; k < d->dim * d->dim; ++k) a.F[k] = d->tilde_F[k];
-  hipLaunchKernelGGL(kfp_quadratic_finalize_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, a, mom,
-                     theta, out, grad);
+  hipLaunchKernelGGL(kfp_quadratic_finalize_kernel, dim3(1), dim3(kBlock), 0, (hipStream_t)stream, a,
+                     mom, theta, out, grad);
   return check_launch("kfp_quadratic_finalize_kernel");
 }
 

@@ -11,6 +11,7 @@
 // terminal = last) that the parametric-quadratic residual needs, so the KFP residual
 // (kinetic_fokker_planck.py:33-58) costs no second pass over the trajectory.
 #include <math.h>
+#include <stdlib.h>
 
 #include "common.h"
 
@@ -102,19 +103,52 @@ __device__ __forceinline__ void grad_gmm(const SdeArgs& a, const float* q, float
   for (int i = 0; i < D; ++i) g[i] = a.inv_s2 * (q[i] - acc[i] * inv);
 }
 
-template <int D>
+// Store modes for the per-step trajectory rows (M = 2d floats per particle):
+//  kStoreNT     — each lane stores its own row (M/4 dwordx4, nontemporal): one store
+//                 instruction covers 64 rows but only 16 of every 4*M bytes;
+//  kStorePlain  — the same with default-policy stores;
+//  kStoreStaged — the wave's 64 rows go through a 64*M*4-byte LDS slot so that every store
+//                 instruction writes 1 KiB contiguous (whole lines), nontemporal.
+enum { kStoreNT = 0, kStorePlain = 1, kStoreStaged = 2 };
+
+template <int D, int STORE>
 __device__ __forceinline__ void store_row(float* dst, const float* z) {
   constexpr int M = 2 * D;
   if constexpr (M % 4 == 0) {
 #pragma unroll
-    for (int k = 0; k < M; k += 4)
-      __builtin_nontemporal_store(f32x4{z[k], z[k + 1], z[k + 2], z[k + 3]},
-                                  reinterpret_cast<f32x4*>(dst + k));
+    for (int k = 0; k < M; k += 4) {
+      if constexpr (STORE == kStorePlain)
+        *reinterpret_cast<f32x4*>(dst + k) = f32x4{z[k], z[k + 1], z[k + 2], z[k + 3]};
+      else
+        __builtin_nontemporal_store(f32x4{z[k], z[k + 1], z[k + 2], z[k + 3]},
+                                    reinterpret_cast<f32x4*>(dst + k));
+    }
   } else {
 #pragma unroll
     for (int k = 0; k < M; k += 2)
       __builtin_nontemporal_store(f32x2{z[k], z[k + 1]}, reinterpret_cast<f32x2*>(dst + k));
   }
+}
+
+// Wave-cooperative store of 64 consecutive rows [wave_row0, wave_row0 + 64) of M floats:
+// row -> LDS (lane-private 4M bytes), then 16-byte chunk c = k*64 + lane -> global. Rows at or
+// beyond n_valid are not stored. LDS traffic of one wave only: no barrier needed.
+template <int D>
+__device__ __forceinline__ void store_rows_staged(float* wave_dst, const float* z, float* slot,
+                                                  int lane, int n_valid) {
+  constexpr int M = 2 * D;
+  static_assert(M % 4 == 0, "staged stores need 2d % 4 == 0");
+#pragma unroll
+  for (int k = 0; k < M; k += 4)
+    *reinterpret_cast<f32x4*>(slot + lane * M + k) = f32x4{z[k], z[k + 1], z[k + 2], z[k + 3]};
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int k = 0; k < M / 4; ++k) {
+    const int c = k * 64 + lane;  // 16-byte chunk within the wave's 64*M floats
+    const f32x4 v = *reinterpret_cast<const f32x4*>(slot + 4 * c);
+    if (4 * c < n_valid * M) __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(wave_dst + 4 * c));
+  }
+  __builtin_amdgcn_wave_barrier();
 }
 
 __device__ __forceinline__ float tau_value(float tau0, int s, float dt) {
@@ -128,7 +162,7 @@ __device__ __forceinline__ float shift_u(const SdeArgs& a, uint32_t plo, uint32_
   return u32_unit(r.x);
 }
 
-template <int D, int POT, bool MOM>
+template <int D, int POT, bool MOM, int STORE>
 __global__ __launch_bounds__(kBlock) void sde_simulate_kernel(SdeArgs a, const float* __restrict__ z0,
                                                               float* __restrict__ traj,
                                                               float* __restrict__ tau,
@@ -162,9 +196,19 @@ __global__ __launch_bounds__(kBlock) void sde_simulate_kernel(SdeArgs a, const f
   MomentAcc<(MOM ? M : 2)> acc;
   acc.zero();
 
-  float* tr = traj ? traj + i * M : nullptr;
+  constexpr bool kStaged = (STORE == kStoreStaged) && (M % 4 == 0);
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t wave_row0 = i_raw - lane;
+  const int n_valid = (int)((a.N - wave_row0) < kWave ? (a.N - wave_row0) : kWave);
+  __shared__ float stage[kStaged ? kBlock * M : 1];
+  float* slot = stage + (threadIdx.x - lane) * M;
+  float* tr = traj ? traj + (kStaged ? wave_row0 : i) * M : nullptr;
   float* ta = tau ? tau + i : nullptr;
   const int64_t tr_stride = a.N * M;
+  auto put = [&](float* dst) {
+    if constexpr (kStaged) store_rows_staged<D>(dst, z, slot, lane, n_valid);
+    else if (active) store_row<D, STORE>(dst, z);
+  };
 
   auto update = [&](float h, float sh, uint32_t s) {
     float g[D], xi[D];
@@ -184,25 +228,21 @@ __global__ __launch_bounds__(kBlock) void sde_simulate_kernel(SdeArgs a, const f
 
   // update 0: h = tau0 (sample at tau0)
   update(tau0, sqrtf(tau0) * a.ns, 0u);
-  if (active) {
-    if (tr) store_row<D>(tr, z);
-    if (ta) __builtin_nontemporal_store(tau_value(tau0, 0, a.dt), ta);
-  }
+  if (tr) put(tr);
+  if (active && ta) __builtin_nontemporal_store(tau_value(tau0, 0, a.dt), ta);
   if constexpr (MOM) acc.add(z, w);
 
   const float sh_dt = sqrtf(a.dt) * a.ns;
   for (int s = 1; s < a.n_steps; ++s) {
     update(a.dt, sh_dt, (uint32_t)s);
-    if (active) {
-      if (tr) store_row<D>(tr + (int64_t)s * tr_stride, z);
-      if (ta) __builtin_nontemporal_store(tau_value(tau0, s, a.dt), ta + (int64_t)s * a.N);
-    }
+    if (tr) put(tr + (int64_t)s * tr_stride);
+    if (active && ta) __builtin_nontemporal_store(tau_value(tau0, s, a.dt), ta + (int64_t)s * a.N);
     if constexpr (MOM) acc.add(z, w);
   }
 
   // final update: h = dt - tau0, lands exactly at T = n*dt (sampling_utils.py:44-46)
   update(h_last, sqrtf(h_last) * a.ns, (uint32_t)a.n_steps);
-  if (active && last) store_row<D>(last + i * M, z);
+  if (active && last) store_row<D, kStoreNT>(last + i * M, z);
 
   if constexpr (MOM) {
     block_reduce_to_slab(acc.v, L, lds, partials + (int64_t)L * nb, blockIdx.x, nb);
@@ -257,7 +297,7 @@ __global__ __launch_bounds__(kBlock) void mf_step_kernel(SdeArgs a, int s, float
     z[k] = fmaf(h, pn, z[k]);
   }
   if (active) {
-    store_row<D>(zout + i * M, z);
+    store_row<D, kStoreNT>(zout + i * M, z);
     if (tau_row) tau_row[i] = tau_value(tau0, s, a.dt);
   }
   float v[1 + D];
@@ -347,11 +387,22 @@ extern "C" size_t pdeinv_sde_workspace_bytes(const pdeinv_sde_desc* d) {
   return (size_t)3 * moment_len(2 * d->dim) * sim_grid(d->n_particles) * sizeof(float);
 }
 
+// Experiment knob (A/B of the store forms on the D = 4 quadratic kernel): PDEINV_STORE_MODE.
+static int store_mode_env() {
+  const char* e = getenv("PDEINV_STORE_MODE");
+  return e ? atoi(e) : -1;
+}
+
 template <int D, int POT, bool MOM>
 static void launch_sim(const SdeArgs& a, const float* z0, float* traj, float* tau, float* last,
                        float* ws, hipStream_t st) {
-  hipLaunchKernelGGL((sde_simulate_kernel<D, POT, MOM>), dim3(sim_grid(a.N)), dim3(kBlock), 0, st,
-                     a, z0, traj, tau, last, ws);
+  const dim3 g(sim_grid(a.N)), b(kBlock);
+  if constexpr (D == 4 && POT == PDEINV_POT_QUADRATIC) {
+    const int m = store_mode_env();
+    if (m == kStoreNT) { hipLaunchKernelGGL((sde_simulate_kernel<D, POT, MOM, kStoreNT>), g, b, 0, st, a, z0, traj, tau, last, ws); return; }
+    if (m == kStorePlain) { hipLaunchKernelGGL((sde_simulate_kernel<D, POT, MOM, kStorePlain>), g, b, 0, st, a, z0, traj, tau, last, ws); return; }
+  }
+  hipLaunchKernelGGL((sde_simulate_kernel<D, POT, MOM, kStoreStaged>), g, b, 0, st, a, z0, traj, tau, last, ws);
 }
 
 template <int D>

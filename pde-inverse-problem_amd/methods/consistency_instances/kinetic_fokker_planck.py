@@ -1,0 +1,113 @@
+"""KFP PDE-consistency residual (methods/consistency_instances/kinetic_fokker_planck.py).
+
+loss = E_0T|grad V_theta|^2 - 2 E_0T[v^T Hess V_theta v] + 2 gamma E_0T[grad V_theta . v]
+     + E_0T|grad V*|^2 + (2/T)(E_term - E_init)[grad V_theta . v]                     (:33-50)
+loss ground truth = E_0T |grad V* - grad V_theta|^2                                      (:52-58)
+
+The reference differentiates this with jax.value_and_grad over vmapped autodiff. Here each
+model kind has a fused native residual that returns the loss terms AND d loss / d theta:
+  * quadratic V_theta = x.(xK + b): all terms are moments of z (moments kernel, or fused into
+    the simulator) + an O(d^3) finalize kernel;
+  * GMM V_theta: one fused per-sample kernel with the analytic softmax adjoint.
+Multi-GPU: the fp64 pre-finalize sums are all-reduced (RCCL) — the pmap mean of trainer.py:52.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+from scipy.linalg import solve_sylvester
+
+from core.model import get_model
+from utils import distributed as dist
+from utils import native, prng
+
+
+def resolve_model(forward_fn):
+    """The reference passes `net.apply`; accept that bound method or the model itself."""
+    owner = getattr(forward_fn, "__self__", None)
+    model = owner if owner is not None and hasattr(owner, "residual_kind") else forward_fn
+    if not hasattr(model, "residual_kind"):
+        raise NotImplementedError("forward_fn must be a pdeinv model (or its .apply): the residual is a "
+                                  "fused native kernel per model family, there is no autodiff fallback")
+    return model
+
+
+def _result(out: torch.Tensor, grad_tree) -> dict:
+    return {"loss": out[native.KFP_SLOTS.index("loss")], "grad": grad_tree,
+            "grad_norm": out[native.KFP_SLOTS.index("grad_norm")],
+            "loss ground truth": out[native.KFP_SLOTS.index("loss ground truth")]}
+
+
+def kfp_moments(data: dict) -> torch.Tensor:
+    """[3, L] fp64 sums for (initial, 0T, terminal); fused-simulator moments are used as is."""
+    if data.get("moments") is not None:
+        return data["moments"]
+    return torch.stack([native.moments(data["initial"]), native.moments(data["0T"]),
+                        native.moments(data["terminal"])])
+
+
+def value_and_grad_fn(forward_fn, params, data, rng, pde_instance):
+    model = resolve_model(forward_fn)
+    ic = pde_instance.initial_configuration
+    gamma = float(ic["gamma_friction"])
+    T = float(pde_instance.total_evolving_time)
+    if model.residual_kind == "quadratic":
+        if "tilde_F" not in ic:
+            raise NotImplementedError("quadratic model needs a quadratic true potential (tilde_F)")
+        mom = dist.allreduce_sum(kfp_moments(data).contiguous())
+        out, grad = native.residual_kfp_quadratic(mom, model.flat(params), ic["tilde_F"], gamma, T)
+        return _result(out, model.unflat(grad))
+    if model.residual_kind == "gmm":
+        mus_true = pde_instance.potential.mus
+        n_i, n_t, n_0 = data["initial"].shape[0], data["terminal"].shape[0], data["0T"].shape[0]
+        desc = native.kfp_gmm_desc(model.dim, model.n_Gaussians, mus_true, gamma, T, n_i, n_t, n_0,
+                                   sigma=model.sigma, sigma_true=pde_instance.potential.sigma,
+                                   world_scale=1.0 / dist.world_size())
+        acc = native.residual_kfp_gmm(desc, data["initial"], data["terminal"], data["0T"], params["params"]["mus"])
+        acc = dist.allreduce_sum(acc)
+        if dist.world_size() > 1:  # the per-set means of the boundary terms are not pre-scaled
+            acc[native.GMM_NACC - 2:native.GMM_NACC] /= dist.world_size()
+        out, grad = native.residual_kfp_gmm_finalize(desc, acc)
+        return _result(out, {"params": {"mus": grad}})
+    raise NotImplementedError(f"no native KFP residual for model kind '{model.residual_kind}' yet "
+                              "(MLP hypothesis: SURVEY.md §8 a11, scheduled next)")
+
+
+def recover_quadratic_drift(moments3, gamma: float, T: float, d: int):
+    """Exact minimiser (S = K + K^T, b) of the quadratic-model loss given the three moment sets:
+    d loss/db = 0 gives b = -S E[x] + c, and d loss/dS = 0 the Lyapunov equation S C + C S = R with
+    C = Cov_0T(x). What Adam on this convex quadratic converges to (main.py:11-29)."""
+    mom = np.asarray(moments3.detach().cpu() if torch.is_tensor(moments3) else moments3, dtype=np.float64)
+    m = 2 * d
+
+    def unpack(v):
+        n = v[0]
+        mean = v[1:1 + m] / n
+        M = np.zeros((m, m))
+        M[np.triu_indices(m)] = v[1 + m:]
+        M = M + M.T - np.diag(np.diag(M))
+        return mean, M / n
+
+    ei, Mi = unpack(mom[0])
+    e0, M0 = unpack(mom[1])
+    et, Mt = unpack(mom[2])
+    ex, ev = e0[:d], e0[d:]
+    Mxx, Mxv, Mvv = M0[:d, :d], M0[:d, d:], M0[d:, d:]
+    c = -gamma * ev - (et[d:] - ei[d:]) / T
+    C = Mxx - np.outer(ex, ex)
+    R = (2 * Mvv - gamma * (Mxv.T + Mxv) + ((Mi[:d, d:].T + Mi[:d, d:]) - (Mt[:d, d:].T + Mt[:d, d:])) / T
+         - (np.outer(c, ex) + np.outer(ex, c)))
+    S = solve_sylvester(C, C, R)
+    S = 0.5 * (S + S.T)
+    return S, -S @ ex + c
+
+
+def test_fn(forward_fn, pde_instance, rng):
+    return {}  # kinetic_fokker_planck.py:72-92 returns {}
+
+
+def create_model_fn(pde_instance):
+    """kinetic_fokker_planck.py:96-104: params = net.init(PRNGKey(11), x)."""
+    net = get_model(pde_instance.cfg, DEBUG=False, pde_instance=pde_instance)
+    params = net.init(prng.PRNGKey(11), np.zeros(pde_instance.dim))
+    return net, params

@@ -1,0 +1,76 @@
+"""Data-parallel plumbing: one process per GPU, torch.distributed over RCCL (backend "nccl").
+
+Replaces the reference's `jax.pmap(value_and_grad_fn, in_axes=(None, 0))` followed by
+`jnp.mean(axis=0)` over the device axis (core/trainer.py:44-53). Particles are sharded by
+contiguous global-id ranges, so every rank's Philox streams are those of a single-process run
+over the same ids. The only exchanges are one all-reduce per residual evaluation (the fp64
+moment / loss-term sums and the parameter gradient, a few hundred bytes) and, for
+McKean–Vlasov, one all-reduce of sum(x) per simulator update.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def is_distributed() -> bool:
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+
+
+def rank() -> int:
+    return dist.get_rank() if is_distributed() else 0
+
+
+def world_size() -> int:
+    return dist.get_world_size() if is_distributed() else 1
+
+
+def init_from_env(backend: str = None) -> bool:
+    """Initialise from torchrun's env (RANK/WORLD_SIZE/MASTER_ADDR/MASTER_PORT); no-op for one rank."""
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    if ws <= 1 or dist.is_initialized():
+        return dist.is_initialized()
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    if backend == "nccl":
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+    dist.init_process_group(backend=backend)
+    return True
+
+
+def shard(n_global: int, r: int = None, w: int = None):
+    """Contiguous [offset, offset + n) share of n_global units for rank r of w."""
+    r = rank() if r is None else r
+    w = world_size() if w is None else w
+    base, rem = divmod(int(n_global), w)
+    n = base + (1 if r < rem else 0)
+    off = r * base + min(r, rem)
+    return off, n
+
+
+def allreduce_sum(t: torch.Tensor) -> torch.Tensor:
+    if is_distributed():
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return t
+
+
+def allreduce_mean(t: torch.Tensor) -> torch.Tensor:
+    if is_distributed():
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        t /= dist.get_world_size()
+    return t
+
+
+def allreduce_max_scalar(x: float, device=None) -> float:
+    if not is_distributed():
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def barrier():
+    if is_distributed():
+        dist.barrier()
