@@ -225,6 +225,50 @@ int pdeinv_residual_kfp_gmm_finalize(const pdeinv_kfp_gmm_desc* desc, const doub
                                      float* d_out, float* d_grad, void* stream);
 
 /* ---------------------------------------------------------------------------------------
+ * Batched moments: n_sets sample sets of n_rows rows each; row r of set t starts at
+ * z + t*set_stride + r*ld (floats). out [n_sets][pdeinv_moment_len(m)] fp64.
+ * The per-time-stamp moments behind the McKean–Vlasov residual (one set per time stamp):
+ * mean_j grad Phi(x_i - x_j) = S (x_i - xbar_t) + b for quadratic Phi
+ * (kinetic_mckean_vlasov.py:20-23, 74-97), so xbar_t and Cov_t replace the O(n^2) pairs.
+ * --------------------------------------------------------------------------------------- */
+size_t pdeinv_moments_batched_workspace_bytes(int64_t n_sets, int64_t n_rows, int32_t m);
+int pdeinv_moments_batched(const float* d_z, int64_t n_sets, int64_t n_rows, int32_t m,
+                           int64_t set_stride, int64_t ld, void* d_workspace, double* d_out,
+                           void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Score / log-density time derivatives of the Gaussian X-marginal N(m1(s), P11(s)) —
+ * partial_s_log_density_fn / partial_s2_log_density_fn
+ * (kinetic_mckean_vlasov_example_quadratic.py:18-191). Per time stamp t the host passes
+ * (from the closed-form OU moments) the coefficient row
+ *   [m1 (d), a1, beta1 (d), Gamma1 (d*d), a2, beta2 (d), Gamma2 (d*d)]   (PDEINV_KMV_NCOEF(d))
+ * with  ds log rho  = a1 + beta1 . r + r^T Gamma1 r,  ds2 log rho = a2 + beta2 . r + r^T Gamma2 r,
+ * r = m1 - x. Per particle the kernel evaluates both, c = ds2 + ds^2 + gamma ds (the weight
+ * of the Phi term, kinetic_mckean_vlasov.py:243-248), and accumulates per time stamp the
+ * fp64 vector [sum c, sum c x (d), sum c x_i x_j (i<=j)] (pdeinv_moment_len(d) doubles).
+ * Optional per-particle output d_ds [n_sets, n_rows, 2] = (ds log rho, ds2 log rho).
+ * --------------------------------------------------------------------------------------- */
+#define PDEINV_KMV_NCOEF(d) (3 * (d) + 2 + 2 * (d) * (d))
+size_t pdeinv_kmv_weights_workspace_bytes(int64_t n_sets, int64_t n_rows, int32_t dim);
+int pdeinv_kmv_weights(int32_t dim, float gamma, const float* d_coef, const float* d_z,
+                       int64_t n_sets, int64_t n_rows, int64_t set_stride, int64_t ld,
+                       float* d_ds, void* d_workspace, double* d_out, void* stream);
+
+/* KMV residual for Phi_theta(y) = y . Dense_d(y) (…_quadratic.py:205-216) from the per-time-stamp
+ * moments of z (mom [n_sets][moment_len(2d)]) and weighted stats (wst [n_sets][moment_len(d)]):
+ * loss (:74-97 of kinetic_mckean_vlasov.py), loss ground truth (:256-266) and d loss/d(K,b).
+ * Outputs d_out[PDEINV_KFP_NOUT] (INITIAL/TERMINAL slots unused = 0; FRICTION slot = the
+ * "2 * loss_value" term) and d_grad [d*d + d]. */
+typedef struct {
+  int32_t dim;
+  int32_t n_sets;
+  float gamma;
+  const float* tilde_F;  /* HOST [d*d]: Phi* = 0.5 y^T tilde_F y (…_quadratic.py:193-203) */
+} pdeinv_kmv_desc;
+int pdeinv_residual_kmv(const pdeinv_kmv_desc* desc, const double* d_mom, const double* d_wstats,
+                        const float* d_theta, float* d_out, float* d_grad, void* stream);
+
+/* ---------------------------------------------------------------------------------------
  * GMM potential value and gradient over a batch — GMMPotential.value/.gradient
  * (core/potential.py:48-61; V_true_fn of …_GMM.py:94-102). Either output nullable.
  * --------------------------------------------------------------------------------------- */

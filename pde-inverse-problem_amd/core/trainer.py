@@ -1,0 +1,124 @@
+"""Training loop (core/trainer.py of the reference): value_and_grad -> optimizer step -> log.
+
+`JaxTrainer` keeps the reference's name and constructor (trainer.py:14-29) so main.py-style
+drivers are unchanged. Differences of mechanism, not of behaviour:
+  * data parallelism is one process per GPU under torch.distributed (RCCL); the method's
+    value_and_grad_fn all-reduces its fp64 sums, which is the reference's pmap +
+    jnp.mean(axis=0) (trainer.py:44-53);
+  * the optimizer is optax's add_decayed_weights -> adam(b1=0.9, eps=1e-4) with a constant or
+    cosine(20000, alpha=1e-3) learning rate (main.py:11-29), applied to the parameter pytree on
+    the device; the EMA branch (trainer.py:87-103) is kept;
+  * metrics go to a local JSONL log (wandb is optional and not installed here).
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+import time
+
+import torch
+
+from core.model import compute_pytree_norm, tree_leaves, tree_map
+from utils import distributed as dist
+from utils import prng
+
+
+class Adam:
+    """optax.chain(add_decayed_weights(wd), adam(lr, b1=0.9, b2=0.999, eps=1e-4))."""
+
+    def __init__(self, learning_rate, weight_decay=0.0, b1=0.9, b2=0.999, eps=1e-4):
+        self.lr = learning_rate if callable(learning_rate) else (lambda step, v=float(learning_rate): v)
+        self.wd, self.b1, self.b2, self.eps = float(weight_decay), b1, b2, eps
+
+    def init(self, params):
+        z = lambda p: torch.zeros_like(p)
+        return {"count": 0, "mu": tree_map(z, params), "nu": tree_map(z, params)}
+
+    def update(self, grads, state, params):
+        count = state["count"] + 1
+        lr = self.lr(state["count"])
+        b1, b2, eps, wd = self.b1, self.b2, self.eps, self.wd
+        g_all = tree_map(lambda g, p: g + wd * p, grads, params)
+        mu = tree_map(lambda m, g: b1 * m + (1 - b1) * g, state["mu"], g_all)
+        nu = tree_map(lambda v, g: b2 * v + (1 - b2) * g * g, state["nu"], g_all)
+        c1, c2 = 1 - b1 ** count, 1 - b2 ** count
+        new = tree_map(lambda p, m, v: p - lr * (m / c1) / (torch.sqrt(v / c2) + eps), params, mu, nu)
+        return new, {"count": count, "mu": mu, "nu": nu}
+
+
+def cosine_decay_schedule(init_value, decay_steps, alpha):
+    """optax.cosine_decay_schedule."""
+    def f(step):
+        t = min(step, decay_steps) / decay_steps
+        return init_value * ((1 - alpha) * 0.5 * (1 + math.cos(math.pi * t)) + alpha)
+    return f
+
+
+def get_optimizer(optimizer_cfg):
+    """main.py:11-29."""
+    if optimizer_cfg.method != "SGD":
+        raise NotImplementedError
+    lr_cfg = optimizer_cfg.learning_rate
+    if lr_cfg.scheduling in ("None", None):
+        lr = float(lr_cfg.initial)
+    elif lr_cfg.scheduling == "cosine":
+        lr = cosine_decay_schedule(float(lr_cfg.initial), 20000, 0.001)
+    else:
+        raise NotImplementedError
+    return Adam(lr, weight_decay=float(optimizer_cfg.weight_decay), b1=0.9, eps=1e-4)
+
+
+class JaxTrainer:
+    def __init__(self, cfg, method, rng, optimizer, forward_fn, params, log_path=None):
+        self.cfg = cfg
+        self.forward_fn = forward_fn
+        self.params = params
+        self.optimizer = optimizer
+        self.method = method
+        self.rng = rng
+        self.log_path = log_path
+        self.history = []
+
+    def _log(self, record):
+        self.history.append(record)
+        if self.log_path and dist.rank() == 0:
+            with open(self.log_path, "a") as f:
+                f.write(json.dumps(record) + "\n")
+
+    def fit(self, number_of_iterations=None):
+        cfg = self.cfg
+        n_iter = int(number_of_iterations or cfg.train.number_of_iterations)
+        opt_state = self.optimizer.init(self.params)
+        use_ema = bool(cfg.train.optimizer.get("use_ema", False))
+        ema = None
+        test_freq = int(cfg.test.frequency)
+        verbose = bool(cfg.test.get("verbose", False))
+        t0 = time.perf_counter()
+        for epoch in range(n_iter):
+            rng = prng.fold_in(self.rng, epoch)  # trainer.py:80-83 (one key per iteration)
+            rng_train, rng_test, _ = prng.split(rng, 3)
+            v_g_etc = self.method.value_and_grad_fn(self.forward_fn, self.params, rng_train)
+            self.params, opt_state = self.optimizer.update(v_g_etc["grad"], opt_state, self.params)
+            if use_ema and epoch >= 40000:  # trainer.py:87-103, optax.ema(0.999)
+                if ema is None:
+                    ema = {"count": 0, "ema": tree_map(lambda p: p.clone(), self.params)}
+                ema["count"] += 1
+                c = 1 - 0.999 ** ema["count"]
+                ema["ema"] = tree_map(lambda e, p: 0.999 * e + 0.001 * p, ema["ema"], self.params)
+                self.params = tree_map(lambda e: e / c, ema["ema"])
+            v_g_etc.pop("grad")
+            v_g_etc["params_norm"] = compute_pytree_norm(self.params)
+            record = {k: float(v) for k, v in v_g_etc.items()}  # one host sync per iteration (:112)
+            assert not math.isnan(record["loss"])
+            record["step"] = epoch
+            if (epoch % test_freq == 0) or epoch >= n_iter - 3:
+                record.update({k: float(v) for k, v in self.method.test_fn(self.forward_fn, self.params, rng_test).items()})
+                if verbose and dist.rank() == 0:
+                    print(f"In epoch {epoch + 1: 5d}, " + ", ".join(f"{k} is {v: .3e}" for k, v in record.items()))
+            self._log(record)
+        self.elapsed = time.perf_counter() - t0
+        return self.params
+
+
+Trainer = JaxTrainer

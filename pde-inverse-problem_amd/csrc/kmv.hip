@@ -1,0 +1,294 @@
+// kmv.hip — McKean–Vlasov residual path (gfx950): per-time-stamp moments, the Gaussian
+// score / log-density time derivatives per particle, and the residual finalize.
+//
+// The reference forms all pairs x_i - x_j per time stamp ([m, n, n_time, d],
+// kinetic_mckean_vlasov.py:20-23) and triple-vmaps autodiff over them. For the quadratic
+// interaction Phi_theta(y) = y^T K y + b^T y every pairwise mean is a function of the time
+// stamp's moments, so the O(n^2) tensor becomes two streaming passes (moments, weights)
+// plus an O(n_time d^3) finalize — exact, not an approximation.
+#include <math.h>
+
+#include "common.h"
+
+namespace pdeinv {
+
+constexpr int kBatchedGridTarget = 2048;
+
+static int batched_bx(int64_t n_sets, int64_t n_rows) {
+  int64_t bx = (kBatchedGridTarget + n_sets - 1) / (n_sets > 0 ? n_sets : 1);
+  const int64_t need = (n_rows + kBlock - 1) / kBlock;
+  if (bx > need) bx = need;
+  if (bx < 1) bx = 1;
+  return (int)bx;
+}
+
+template <int M>
+__global__ __launch_bounds__(kBlock) void moments_batched_kernel(const float* __restrict__ z, int64_t n_rows,
+                                                                 int64_t set_stride, int64_t ld,
+                                                                 float* __restrict__ partials) {
+  MomentAcc<M> acc;
+  acc.zero();
+  const float* base = z + (int64_t)blockIdx.y * set_stride;
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x; r < n_rows; r += stride) {
+    const float* row = base + r * ld;
+    float v[M];
+#pragma unroll
+    for (int k = 0; k < M; ++k) v[k] = row[k];
+    acc.add(v, 1.f);
+  }
+  __shared__ float lds[kWavesPerBlock * moment_len(M)];
+  // set t owns columns [t*L, (t+1)*L) of the slab
+  block_reduce_to_slab(acc.v, moment_len(M), lds, partials + (int64_t)blockIdx.y * moment_len(M) * gridDim.x,
+                       blockIdx.x, gridDim.x);
+}
+
+// ds log rho = a1 + beta1.r + r^T G1 r ; ds2 log rho = a2 + beta2.r + r^T G2 r ; r = m1 - x.
+template <int D>
+__global__ __launch_bounds__(kBlock) void kmv_weights_kernel(float gamma, const float* __restrict__ coef,
+                                                             const float* __restrict__ z, int64_t n_rows,
+                                                             int64_t set_stride, int64_t ld,
+                                                             float* __restrict__ ds_out,
+                                                             float* __restrict__ partials) {
+  constexpr int NC = 3 * D + 2 + 2 * D * D;
+  const int t = blockIdx.y;
+  const float* c = coef + (int64_t)t * NC;  // wave-uniform: scalar loads
+  const float* m1 = c;
+  const float a1 = c[D];
+  const float* b1 = c + D + 1;
+  const float* G1 = c + 2 * D + 1;
+  const float a2 = c[2 * D + 1 + D * D];
+  const float* b2 = c + 2 * D + 2 + D * D;
+  const float* G2 = c + 3 * D + 2 + D * D;
+  MomentAcc<D> acc;
+  acc.zero();
+  const float* base = z + (int64_t)t * set_stride;
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x; r < n_rows; r += stride) {
+    const float* row = base + r * ld;
+    float x[D], rr[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      x[k] = row[k];
+      rr[k] = m1[k] - x[k];
+    }
+    float q1 = a1, q2 = a2;
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      float g1 = b1[i], g2 = b2[i];
+#pragma unroll
+      for (int j = 0; j < D; ++j) {
+        g1 = fmaf(G1[i * D + j], rr[j], g1);
+        g2 = fmaf(G2[i * D + j], rr[j], g2);
+      }
+      q1 = fmaf(g1, rr[i], q1);
+      q2 = fmaf(g2, rr[i], q2);
+    }
+    if (ds_out) {
+      float* o = ds_out + ((int64_t)t * n_rows + r) * 2;
+      o[0] = q1;
+      o[1] = q2;
+    }
+    const float w = q2 + q1 * q1 + gamma * q1;  // kinetic_mckean_vlasov.py:243-248
+    acc.add(x, w);
+  }
+  __shared__ float lds[kWavesPerBlock * moment_len(D)];
+  block_reduce_to_slab(acc.v, moment_len(D), lds, partials + (int64_t)t * moment_len(D) * gridDim.x, blockIdx.x,
+                       gridDim.x);
+}
+
+struct KmvArgs {
+  int d, n_sets;
+  float gamma;
+  float F[PDEINV_MAX_DIM * PDEINV_MAX_DIM];
+};
+
+// Per time stamp t: n_t, xbar_t, M_t = E_t[x x^T], C_t = M_t - xbar xbar^T from mom (z moments);
+// W_t, Wx_t, Wxx_t (sums) from wst. N = sum_t n_t.
+//   nabla = (1/N) sum_t n_t tr(S C_t S) + b.b        hess = tr(S Mvv)
+//   value = (1/N) sum_t [ 1/2 tr(S Wxx_t) - xbar_t^T S Wx_t + 1/2 W_t tr(S M_t) + b.(Wx_t - W_t xbar_t) ]
+//   true  = (1/N) sum_t n_t tr(F C_t F)              gt = (1/N) sum_t n_t tr(D C_t D^T) + b.b, D = F - S
+//   loss  = nabla - 2 hess + 2 value + true
+__global__ __launch_bounds__(kBlock) void kmv_finalize_kernel(KmvArgs a, const double* __restrict__ mom,
+                                                              const double* __restrict__ wst,
+                                                              const float* __restrict__ theta,
+                                                              float* __restrict__ out,
+                                                              float* __restrict__ grad) {
+  const int d = a.d, m = 2 * d, Lz = moment_len(m), Lw = moment_len(d);
+  auto S = [&](int i, int j) { return (double)theta[i * d + j] + (double)theta[j * d + i]; };
+  auto b = [&](int i) { return (double)theta[d * d + i]; };
+  auto F = [&](int i, int j) { return (double)a.F[i * d + j]; };
+  auto tri = [](int i, int j, int mm) {
+    if (i > j) { const int t = i; i = j; j = t; }
+    return i * mm - i * (i - 1) / 2 + (j - i);
+  };
+  // global counts and E[v v^T]
+  double Ntot = 0;
+  for (int t = 0; t < a.n_sets; ++t) Ntot += mom[(int64_t)t * Lz];
+  const double invN = Ntot > 0 ? 1.0 / Ntot : 0.0;
+  auto xbar = [&](int t, int i) {
+    const double* v = mom + (int64_t)t * Lz;
+    return v[0] > 0 ? v[1 + i] / v[0] : 0.0;
+  };
+  auto Mx = [&](int t, int i, int j) {  // E_t[x_i x_j]
+    const double* v = mom + (int64_t)t * Lz;
+    return v[0] > 0 ? v[1 + m + tri(i, j, m)] / v[0] : 0.0;
+  };
+  auto Cx = [&](int t, int i, int j) { return Mx(t, i, j) - xbar(t, i) * xbar(t, j); };
+  auto Mvv = [&](int i, int j) {
+    double s = 0;
+    for (int t = 0; t < a.n_sets; ++t) s += mom[(int64_t)t * Lz + 1 + m + tri(d + i, d + j, m)];
+    return s * invN;
+  };
+  auto W = [&](int t) { return wst[(int64_t)t * Lw]; };
+  auto Wx = [&](int t, int i) { return wst[(int64_t)t * Lw + 1 + i]; };
+  auto Wxx = [&](int t, int i, int j) { return wst[(int64_t)t * Lw + 1 + d + tri(i, j, d)]; };
+
+  double acc[7] = {0, 0, 0, 0, 0, 0, 0};  // nabla, hess, value, true, gt, |grad|^2, spare
+  const int tid = threadIdx.x;
+  if (tid < d * d) {
+    const int i = tid / d, j = tid % d;
+    double Gij = 0, Gji = 0;
+    for (int t = 0; t < a.n_sets; ++t) {
+      const double nt = mom[(int64_t)t * Lz] * invN;
+      double SC_ij = 0, CS_ij = 0, SC_ji = 0, CS_ji = 0, FC = 0, DC = 0;
+      for (int k = 0; k < d; ++k) {
+        SC_ij += S(i, k) * Cx(t, k, j);
+        CS_ij += Cx(t, i, k) * S(k, j);
+        SC_ji += S(j, k) * Cx(t, k, i);
+        CS_ji += Cx(t, j, k) * S(k, i);
+        FC += F(i, k) * Cx(t, k, j);
+        DC += (F(i, k) - S(i, k)) * Cx(t, k, j);
+      }
+      acc[0] += nt * SC_ij * S(j, i);                 // tr(S C S)
+      acc[3] += nt * FC * F(i, j);                    // tr(F C F^T)
+      acc[4] += nt * DC * (F(i, j) - S(i, j));        // tr(D C D^T)
+      // value: 1/2 tr(S Wxx) - xbar^T S Wx + 1/2 W tr(S M)
+      acc[2] += invN * (0.5 * S(i, j) * Wxx(t, j, i) - xbar(t, i) * S(i, j) * Wx(t, j) +
+                        0.5 * W(t) * S(i, j) * Mx(t, j, i));
+      Gij += nt * (SC_ij + CS_ij) + 2 * invN * (0.5 * Wxx(t, i, j) - xbar(t, i) * Wx(t, j) + 0.5 * W(t) * Mx(t, i, j));
+      Gji += nt * (SC_ji + CS_ji) + 2 * invN * (0.5 * Wxx(t, j, i) - xbar(t, j) * Wx(t, i) + 0.5 * W(t) * Mx(t, j, i));
+    }
+    const double mvv_ij = Mvv(i, j);
+    acc[1] = S(i, j) * mvv_ij;
+    Gij += -2 * mvv_ij;
+    Gji += -2 * mvv_ij;
+    const double gk = Gij + Gji;
+    grad[i * d + j] = (float)gk;
+    acc[5] = gk * gk;
+  }
+  if (tid < d) {
+    const int i = tid;
+    double wsum = 0;
+    for (int t = 0; t < a.n_sets; ++t) wsum += Wx(t, i) - W(t) * xbar(t, i);
+    acc[0] += b(i) * b(i);
+    acc[4] += b(i) * b(i);
+    acc[2] += invN * b(i) * wsum;
+    const double gb = 2 * b(i) + 2 * invN * wsum;
+    grad[d * d + i] = (float)gb;
+    acc[5] += gb * gb;
+  }
+  __shared__ double red[kWavesPerBlock][7];
+#pragma unroll
+  for (int c = 0; c < 7; ++c) {
+    double v = acc[c];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    if ((tid & 63) == 0) red[tid >> 6][c] = v;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    double r[7];
+#pragma unroll
+    for (int c = 0; c < 7; ++c) r[c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+    out[PDEINV_KFP_LOSS] = (float)(r[0] - 2 * r[1] + 2 * r[2] + r[3]);
+    out[PDEINV_KFP_LOSS_GT] = (float)r[4];
+    out[PDEINV_KFP_GRAD_NORM] = (float)sqrt(r[5]);
+    out[PDEINV_KFP_NABLA] = (float)r[0];
+    out[PDEINV_KFP_HESSIAN] = (float)r[1];
+    out[PDEINV_KFP_FRICTION] = (float)r[2];
+    out[PDEINV_KFP_NABLA_TRUE] = (float)r[3];
+    out[PDEINV_KFP_INITIAL] = 0.f;
+    out[PDEINV_KFP_TERMINAL] = 0.f;
+  }
+}
+
+}  // namespace pdeinv
+
+using namespace pdeinv;
+
+extern "C" size_t pdeinv_moments_batched_workspace_bytes(int64_t n_sets, int64_t n_rows, int32_t m) {
+  if (m < 1 || m > 16 || n_sets < 1 || n_rows < 0) return 0;
+  return (size_t)n_sets * moment_len(m) * batched_bx(n_sets, n_rows) * sizeof(float);
+}
+
+extern "C" int pdeinv_moments_batched(const float* z, int64_t n_sets, int64_t n_rows, int32_t m,
+                                      int64_t set_stride, int64_t ld, void* ws, double* out, void* stream) {
+  PDEINV_REQUIRE(m >= 1 && m <= 16, PDEINV_ERR_UNSUPPORTED, "moments_batched: m must be in [1, 16]");
+  PDEINV_REQUIRE(n_sets >= 1 && n_sets <= 65535 && n_rows >= 0, PDEINV_ERR_INVALID,
+                 "moments_batched: need 1 <= n_sets <= 65535, n_rows >= 0");
+  if (ld == 0) ld = m;
+  PDEINV_REQUIRE(ld >= m && set_stride >= 0, PDEINV_ERR_INVALID, "moments_batched: bad strides");
+  PDEINV_REQUIRE(out && ws && (n_rows == 0 || z), PDEINV_ERR_INVALID, "moments_batched: null pointer");
+  hipStream_t st = (hipStream_t)stream;
+  const int bx = batched_bx(n_sets, n_rows);
+  const dim3 g(bx, (unsigned)n_sets);
+  float* p = (float*)ws;
+  switch (m) {
+#define CASE(MM) case MM: hipLaunchKernelGGL(moments_batched_kernel<MM>, g, dim3(kBlock), 0, st, z, n_rows, set_stride, ld, p); break;
+    CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
+    CASE(9) CASE(10) CASE(11) CASE(12) CASE(13) CASE(14) CASE(15) CASE(16)
+#undef CASE
+  }
+  int rc = check_launch("moments_batched_kernel");
+  if (rc) return rc;
+  launch_slab_reduce(p, bx, (int)(n_sets * moment_len(m)), out, st);
+  return check_launch("slab_reduce_kernel");
+}
+
+extern "C" size_t pdeinv_kmv_weights_workspace_bytes(int64_t n_sets, int64_t n_rows, int32_t dim) {
+  if (dim < 1 || dim > 16 || n_sets < 1 || n_rows < 0) return 0;
+  return (size_t)n_sets * moment_len(dim) * batched_bx(n_sets, n_rows) * sizeof(float);
+}
+
+extern "C" int pdeinv_kmv_weights(int32_t D, float gamma, const float* coef, const float* z, int64_t n_sets,
+                                  int64_t n_rows, int64_t set_stride, int64_t ld, float* ds, void* ws,
+                                  double* out, void* stream) {
+  PDEINV_REQUIRE(D >= 1 && D <= 16, PDEINV_ERR_UNSUPPORTED, "kmv_weights: dim must be in [1, 16]");
+  PDEINV_REQUIRE(n_sets >= 1 && n_sets <= 65535 && n_rows >= 0, PDEINV_ERR_INVALID,
+                 "kmv_weights: need 1 <= n_sets <= 65535");
+  if (ld == 0) ld = 2 * D;
+  PDEINV_REQUIRE(ld >= D && set_stride >= 0, PDEINV_ERR_INVALID, "kmv_weights: bad strides");
+  PDEINV_REQUIRE(coef && out && ws && (n_rows == 0 || z), PDEINV_ERR_INVALID, "kmv_weights: null pointer");
+  hipStream_t st = (hipStream_t)stream;
+  const int bx = batched_bx(n_sets, n_rows);
+  const dim3 g(bx, (unsigned)n_sets);
+  float* p = (float*)ws;
+  switch (D) {
+#define CASE(DD) case DD: hipLaunchKernelGGL(kmv_weights_kernel<DD>, g, dim3(kBlock), 0, st, gamma, coef, z, n_rows, set_stride, ld, ds, p); break;
+    CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) CASE(10) CASE(12) CASE(16)
+#undef CASE
+    default:
+      return fail(PDEINV_ERR_UNSUPPORTED, "kmv_weights: dim must be one of 1-8, 10, 12, 16");
+  }
+  int rc = check_launch("kmv_weights_kernel");
+  if (rc) return rc;
+  launch_slab_reduce(p, bx, (int)(n_sets * moment_len(D)), out, st);
+  return check_launch("slab_reduce_kernel");
+}
+
+extern "C" int pdeinv_residual_kmv(const pdeinv_kmv_desc* d, const double* mom, const double* wst,
+                                   const float* theta, float* out, float* grad, void* stream) {
+  PDEINV_REQUIRE(d != nullptr, PDEINV_ERR_INVALID, "residual_kmv: null descriptor");
+  PDEINV_REQUIRE(d->dim >= 1 && d->dim <= 8, PDEINV_ERR_UNSUPPORTED, "residual_kmv: dim must be in [1, 8]");
+  PDEINV_REQUIRE(d->n_sets >= 1, PDEINV_ERR_INVALID, "residual_kmv: n_sets must be >= 1");
+  PDEINV_REQUIRE(mom && wst && theta && out && grad && d->tilde_F, PDEINV_ERR_INVALID, "residual_kmv: null pointer");
+  KmvArgs a{};
+  a.d = d->dim;
+  a.n_sets = d->n_sets;
+  a.gamma = d->gamma;
+  for (int k = 0; k < d->dim * d->dim; ++k) a.F[k] = d->tilde_F[k];
+  hipLaunchKernelGGL(kmv_finalize_kernel, dim3(1), dim3(kBlock), 0, (hipStream_t)stream, a, mom, wst, theta, out,
+                     grad);
+  return check_launch("kmv_finalize_kernel");
+}

@@ -20,6 +20,7 @@ import torch
 import methods.consistency_instances.kinetic_fokker_planck as kinetic_fokker_planck
 import methods.consistency_instances.kinetic_mckean_vlasov as kinetic_mckean_vlasov
 from api import Method
+from utils import distributed as dist
 from utils import native, prng
 
 INSTANCES = {
@@ -57,7 +58,13 @@ class ConsistencyBased(Method):
         needs_tau = self.cfg.pde_instance.name == "Kinetic-McKean-Vlasov"
         if pi.sample_mode == "online":
             rng_initial, rng_terminal, rng_0T = prng.split(rng, 3)
+            # every rank draws its own full batch, as every pmap device does (trainer.py:47-52):
+            # either from a rank-folded key or, where the sampler takes global particle ids,
+            # from the shared key at offset rank * batch (interacting systems need the shared key)
+            rank = dist.rank()
+            fold = (lambda k: prng.fold_in(k, rank)) if dist.world_size() > 1 else (lambda k: k)
             if pi.sample_scheme == "exact":
+                rng_initial, rng_terminal, rng_0T = fold(rng_initial), fold(rng_terminal), fold(rng_0T)
                 spec = {"random_time": int(tr.batch_size_0T),
                         "grid_time": (int(tr.n_time_stamps), int(tr.sample_per_time))}[tr.sample_mode]
                 data = {
@@ -67,17 +74,23 @@ class ConsistencyBased(Method):
                 }
                 if needs_tau:
                     data["tau_0T"] = pi.get_time_sample_ground_truth(rng_0T, spec)
+            elif pi.sample_scheme == "SDE" and hasattr(pi, "simulate_interacting"):
+                # McKean–Vlasov: the interacting system on a shared clock (one tau per time stamp)
+                B = int(tr.sample_per_time)
+                _, r = pi.simulate_interacting(rng_0T, B, particle_offset=rank * B)
+                data = {"0T_tm": r["traj"], "tau_0T": r["tau"][:, 0].double().cpu().numpy(),
+                        "shared_time": True}
             elif pi.sample_scheme == "SDE":
                 model = getattr(forward_fn, "__self__", forward_fn)
                 fused = getattr(model, "residual_kind", None) == "quadratic" and hasattr(pi, "simulate")
                 if fused:
-                    # every rank draws a full batch from its own (rank-folded) key, as every pmap
-                    # device does in the reference (trainer.py:47-52)
-                    _, r = pi.simulate(rng_0T, int(tr.batch_size_0T), traj=False, moments=True)
+                    B = int(tr.batch_size_0T)
+                    _, r = pi.simulate(rng_0T, B, particle_offset=rank * B, traj=False, moments=True)
                     data = {"moments": r["moments"]}
                 else:
                     data = {}
-                    data["initial"], data["terminal"], data["0T"] = pi.sample_ground_truth(rng_0T, int(tr.batch_size_0T))
+                    data["initial"], data["terminal"], data["0T"] = pi.sample_ground_truth(fold(rng_0T),
+                                                                                          int(tr.batch_size_0T))
             else:
                 raise ValueError("unknown sampling scheme")
         elif pi.sample_mode == "offline":

@@ -1,0 +1,75 @@
+"""KMV PDE-consistency residual (methods/consistency_instances/kinetic_mckean_vlasov.py).
+
+loss = mean_i |mean_j grad Phi_theta(x_i - x_j)|^2 - 2 mean_i mean_j v_i^T Hess Phi_theta v_i
+     + 2 mean_i [mean_j Phi_theta(x_i - x_j)] (ds2 log rho + (ds log rho)^2 + gamma ds log rho)
+     + mean_i |mean_j grad Phi*(x_i - x_j)|^2                                   (:74-97, pairs per time)
+For the quadratic Phi_theta every pairwise mean is a function of the time stamp's moments, so
+the [m, n, n_time, d] pair tensor of :20-23 is replaced by:
+  pass 1  pdeinv_moments_batched — per time stamp [count, sum z, sum z z^T];
+  pass 2  pdeinv_kmv_weights     — per particle ds/ds2 log rho (the score/log-density
+          evaluation) and per time stamp the c-weighted [sum c, sum c x, sum c x x^T];
+  final   pdeinv_residual_kmv    — loss, loss ground truth, d loss / d(K, b).
+Multi-GPU: with a shared clock (the simulated interacting system, sample_scheme SDE) the
+per-time-stamp sums are all-reduced before the finalize (the exact global loss); with
+per-rank random time stamps (exact sampler) each rank finalizes and the outputs are averaged,
+which is the reference's pmap mean (trainer.py:52).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from core.model import get_model
+from methods.consistency_instances.kinetic_fokker_planck import _result, resolve_model
+from utils import distributed as dist
+from utils import native, prng
+
+
+def layout(data: dict, d: int):
+    """(z, n_sets, n_rows, set_stride, ld) for either the time-major simulator output or the
+    reference's flattened [(i, t), 2d] sample order (x_0T.reshape(-1, n_time, d), :14-19)."""
+    tau = np.atleast_1d(np.asarray(data["tau_0T"], dtype=np.float64))
+    if "0T_tm" in data:
+        z = data["0T_tm"]
+        n_sets, n_rows = z.shape[0], z.shape[1]
+        return z, n_sets, n_rows, n_rows * 2 * d, 2 * d, tau
+    z = data["0T"].contiguous()
+    n_sets = len(tau)
+    n_rows = z.shape[0] // n_sets
+    return z, n_sets, n_rows, 2 * d, n_sets * 2 * d, tau
+
+
+def value_and_grad_fn(forward_fn, params, data, rng, pde_instance):
+    model = resolve_model(forward_fn)
+    if model.residual_kind != "quadratic":
+        raise NotImplementedError(f"no native KMV residual for model kind '{model.residual_kind}' "
+                                  "(general Phi: tiled N-body kernel, SURVEY.md §8(f) rank 3)")
+    d = pde_instance.dim
+    gamma = float(pde_instance.initial_configuration["gamma_friction"])
+    z, n_sets, n_rows, set_stride, ld, tau = layout(data, d)
+    mom = native.moments_batched(z, n_sets, n_rows, 2 * d, set_stride, ld)
+    coef = pde_instance.coefficients(tau, z.device)
+    wst, _ = native.kmv_weights(d, gamma, coef, z, n_sets, n_rows, set_stride, ld)
+    theta = model.flat(params)
+    F = pde_instance.initial_configuration["tilde_F"]
+    if data.get("shared_time", False):
+        both = dist.allreduce_sum(torch.cat([mom.reshape(-1), wst.reshape(-1)]))
+        mom = both[: mom.numel()].view_as(mom)
+        wst = both[mom.numel():].view_as(wst)
+        out, grad = native.residual_kmv(mom, wst, theta, F, gamma)
+    else:
+        out, grad = native.residual_kmv(mom, wst, theta, F, gamma)
+        if dist.world_size() > 1:
+            both = dist.allreduce_mean(torch.cat([out, grad]))
+            out, grad = both[: out.numel()], both[out.numel():]
+    return _result(out, model.unflat(grad))
+
+
+def test_fn(forward_fn, pde_instance, rng):
+    return {}  # kinetic_mckean_vlasov.py:123-144 returns {}
+
+
+def create_model_fn(pde_instance):
+    net = get_model(pde_instance.cfg, DEBUG=False, pde_instance=pde_instance)
+    params = net.init(prng.PRNGKey(11), np.zeros(pde_instance.dim))
+    return net, params

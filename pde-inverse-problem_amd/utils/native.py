@@ -42,7 +42,8 @@ EXPORTED_SYMBOLS = (
     "pdeinv_residual_kfp_gmm_workspace_bytes", "pdeinv_residual_kfp_gmm",
     "pdeinv_residual_kfp_gmm_finalize", "pdeinv_gmm_potential", "pdeinv_gaussian_sample",
     "pdeinv_philox_fill", "pdeinv_gather_subsample", "pdeinv_abi_version", "pdeinv_last_error",
-    "pdeinv_runtime_version",
+    "pdeinv_runtime_version", "pdeinv_moments_batched_workspace_bytes", "pdeinv_moments_batched",
+    "pdeinv_kmv_weights_workspace_bytes", "pdeinv_kmv_weights", "pdeinv_residual_kmv",
 )
 
 
@@ -63,6 +64,11 @@ class SdeDesc(ctypes.Structure):
 
 class KfpQuadDesc(ctypes.Structure):
     _fields_ = [("dim", ctypes.c_int32), ("gamma", ctypes.c_float), ("total_time", ctypes.c_float),
+                ("tilde_F", ctypes.c_void_p)]
+
+
+class KmvDesc(ctypes.Structure):
+    _fields_ = [("dim", ctypes.c_int32), ("n_sets", ctypes.c_int32), ("gamma", ctypes.c_float),
                 ("tilde_F", ctypes.c_void_p)]
 
 
@@ -117,6 +123,11 @@ def lib():
         "pdeinv_abi_version": (i32, []),
         "pdeinv_last_error": (ctypes.c_char_p, []),
         "pdeinv_runtime_version": (i32, []),
+        "pdeinv_moments_batched_workspace_bytes": (ctypes.c_size_t, [i64, i64, i32]),
+        "pdeinv_moments_batched": (i32, [P, i64, i64, i32, i64, i64, P, P, P]),
+        "pdeinv_kmv_weights_workspace_bytes": (ctypes.c_size_t, [i64, i64, i32]),
+        "pdeinv_kmv_weights": (i32, [i32, f32, P, P, i64, i64, i64, i64, P, P, P, P]),
+        "pdeinv_residual_kmv": (i32, [P, P, P, P, P, P, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -410,3 +421,98 @@ def gather_subsample(traj_tm: torch.Tensor, traj_idx: torch.Tensor, time_idx: to
                                          ti.numel(), _dev(si, "time_idx", torch.int32), si.numel(),
                                          _dev(out, "out"), stream_handle()), "pdeinv_gather_subsample")
     return out
+
+
+# -----------------------------------------------------------------------------------------
+# McKean–Vlasov residual path
+# -----------------------------------------------------------------------------------------
+def kmv_ncoef(d: int) -> int:
+    return 3 * d + 2 + 2 * d * d
+
+
+def _set_view(z: torch.Tensor, n_sets: int, n_rows: int, set_stride: int, ld: int, width: int):
+    if z.dtype != torch.float32 or not z.is_cuda:
+        raise ValueError("samples must be fp32 device tensors")
+    if z.stride(-1) != 1:
+        raise ValueError("samples must have unit inner stride")
+    need = (n_sets - 1) * set_stride + (n_rows - 1) * ld + width if n_rows > 0 else 0
+    avail = z.untyped_storage().nbytes() // 4 - z.storage_offset()
+    if need > avail:  # checked on the host: the kernel trusts these strides
+        raise ValueError("set/row strides run past the end of the sample buffer")
+
+
+def moments_batched(z: torch.Tensor, n_sets: int, n_rows: int, m: int, set_stride: int, ld: int) -> torch.Tensor:
+    """[n_sets, moment_len(m)] fp64: set t = rows z[t*set_stride + r*ld : +m] (floats)."""
+    _require_gpu()
+    _set_view(z, n_sets, n_rows, set_stride, ld, m)
+    nbytes = lib().pdeinv_moments_batched_workspace_bytes(n_sets, n_rows, m)
+    if nbytes == 0:
+        raise NotImplementedError(f"moments_batched: m={m} unsupported")
+    ws = torch.empty(nbytes // 4, device=z.device, dtype=torch.float32)
+    out = torch.empty((n_sets, moment_len(m)), device=z.device, dtype=torch.float64)
+    _check(lib().pdeinv_moments_batched(_dev(z, "z"), n_sets, n_rows, m, set_stride, ld, _dev(ws, "ws"),
+                                        _dev(out, "out", torch.float64), stream_handle()), "pdeinv_moments_batched")
+    return out
+
+
+def kmv_weights(d: int, gamma: float, coef: torch.Tensor, z: torch.Tensor, n_sets: int, n_rows: int,
+                set_stride: int, ld: int, want_ds: bool = False):
+    """Per time stamp [sum c, sum c x, sum c x x^T] fp64 (c = ds2 + ds^2 + gamma ds) and optionally
+    the per-particle (ds log rho, ds2 log rho) [n_sets, n_rows, 2]."""
+    _require_gpu()
+    if tuple(coef.shape) != (n_sets, kmv_ncoef(d)) or not coef.is_contiguous():
+        raise ValueError(f"coef must be contiguous [{n_sets}, {kmv_ncoef(d)}]")
+    _set_view(z, n_sets, n_rows, set_stride, ld, d)
+    nbytes = lib().pdeinv_kmv_weights_workspace_bytes(n_sets, n_rows, d)
+    ws = torch.empty(max(nbytes // 4, 1), device=z.device, dtype=torch.float32)
+    out = torch.empty((n_sets, moment_len(d)), device=z.device, dtype=torch.float64)
+    ds = torch.empty((n_sets, n_rows, 2), device=z.device, dtype=torch.float32) if want_ds else None
+    _check(lib().pdeinv_kmv_weights(d, float(gamma), _dev(coef, "coef"), _dev(z, "z"), n_sets, n_rows, set_stride,
+                                    ld, _dev(ds, "ds"), _dev(ws, "ws"), _dev(out, "out", torch.float64),
+                                    stream_handle()), "pdeinv_kmv_weights")
+    return out, ds
+
+
+def residual_kmv(mom: torch.Tensor, wst: torch.Tensor, theta_flat: torch.Tensor, tilde_F, gamma: float):
+    _require_gpu()
+    n_sets = mom.shape[0]
+    d = int(round(math.sqrt(theta_flat.numel() + 0.25) - 0.5))
+    if tuple(mom.shape) != (n_sets, moment_len(2 * d)) or tuple(wst.shape) != (n_sets, moment_len(d)):
+        raise ValueError("residual_kmv: moment shapes do not match theta's dimension")
+    F = _host_f32(tilde_F)
+    desc = KmvDesc(d, n_sets, float(gamma), F.ctypes.data_as(ctypes.c_void_p))
+    out = torch.empty(KFP_NOUT, device=mom.device, dtype=torch.float32)
+    grad = torch.empty_like(theta_flat)
+    _check(lib().pdeinv_residual_kmv(ctypes.byref(desc), _dev(mom.contiguous(), "mom", torch.float64),
+                                     _dev(wst.contiguous(), "wst", torch.float64), _dev(theta_flat.contiguous(), "theta"),
+                                     _dev(out, "out"), _dev(grad, "grad"), stream_handle()), "pdeinv_residual_kmv")
+    return out, grad
+
+
+def mf_desc(N: int, d: int, n_steps: int, dt: float, gamma: float, A, *, seed: int, counter_offset: int = 0,
+            particle_offset: int = 0, noise_scale: float = SQRT2, random_shift: bool = True,
+            noise: Optional[torch.Tensor] = None):
+    p_desc, p_host = make_potential(POT_MEANFIELD_QUADRATIC, A)
+    desc = SdeDesc()
+    desc.n_particles = N
+    desc.particle_offset = int(particle_offset)
+    desc.dim = d
+    desc.n_steps = int(n_steps)
+    desc.dt = float(dt)
+    desc.gamma = float(gamma)
+    desc.noise_scale = float(noise_scale)
+    desc.random_shift = int(bool(random_shift))
+    desc.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+    desc.counter_offset = int(counter_offset) & 0xFFFFFFFF
+    desc.ld_z0 = 2 * d
+    desc.potential = p_desc
+    if noise is not None:
+        if tuple(noise.shape) != (n_steps + 1, N, d) or not noise.is_contiguous():
+            raise ValueError(f"noise must be contiguous [{n_steps + 1}, {N}, {d}]")
+        desc.d_noise = _dev(noise, "noise")
+    return desc, p_host
+
+
+def mf_workspace(desc: SdeDesc, device) -> torch.Tensor:
+    nbytes = lib().pdeinv_mf_workspace_bytes(ctypes.byref(desc))
+    return torch.empty(max(nbytes // 4, 1), device=device, dtype=torch.float32)

@@ -1,0 +1,169 @@
+"""GPU tests of the reference-shaped host API (registry / problems / method / trainer) and of
+the McKean–Vlasov path, against the CPU oracle (oracle/numpy_ref.py, oracle/pdeinv_oracle.c).
+
+Tolerances: residual terms 1e-4 relative (fp32 sums, fp64 across blocks); ds log rho 1e-4
+relative to the term scale; mean-field trajectories 2e-4 absolute vs the C oracle.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import numpy_ref as nr
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _t(a):
+    return torch.as_tensor(np.ascontiguousarray(a), dtype=torch.float32, device=DEV)
+
+
+def _cfg(overrides):
+    from utils import config
+    return config.compose("config", overrides)
+
+
+def test_kmv_residual_vs_pairwise_restatement(native):
+    """Moment-form KMV residual == the reference's literal O(n^2) pairwise formulation."""
+    from example_problems.kinetic_mckean_vlasov_example_quadratic import KineticMcKeanVlasov
+    from methods.consistency_instances import kinetic_mckean_vlasov as kmv
+    from core.model import QuadraticModel
+    from utils import prng
+    d, n, n_t = 3, 300, 4
+    cfg = _cfg(["pde_instance=kinetic_mckean_vlasov", f"pde_instance.domain_dim={d}"])
+    pi = KineticMcKeanVlasov(cfg, prng.PRNGKey(0))
+    rng = np.random.default_rng(1)
+    x = rng.standard_normal((n, n_t, d)); v = rng.standard_normal((n, n_t, d))
+    tau = np.array([0.3, 0.7, 1.1, 1.9])
+    K = rng.standard_normal((d, d)) * 0.3; b = rng.standard_normal(d) * 0.2
+    z = np.concatenate([x, v], -1).reshape(-1, 2 * d)  # reference order rows (i, t)
+    model = QuadraticModel(d)
+    params = model.unflat(_t(np.concatenate([K.ravel(), b])))
+    res = kmv.value_and_grad_fn(model.apply, params, {"0T": _t(z), "tau_0T": tau}, None, pi)
+    cfg_np = nr.ou_configuration(pi.initial_configuration["tilde_F"], gamma=1.0)
+    loss, loss_gt = nr.kmv_pairwise_loss(K, b, x, v, tau, cfg_np)
+    assert abs(float(res["loss"]) - loss) < 2e-4 * (1 + abs(loss))
+    assert abs(float(res["loss ground truth"]) - loss_gt) < 2e-4 * (1 + abs(loss_gt))
+    g_fd = nr.fd_grad(lambda th: nr.kmv_pairwise_loss(th[:d * d].reshape(d, d), th[d * d:], x, v, tau, cfg_np)[0],
+                      np.concatenate([K.ravel(), b]), eps=1e-5)
+    g = torch.cat([res["grad"]["params"]["tilde_F"]["kernel"].reshape(-1), res["grad"]["params"]["tilde_F"]["bias"]])
+    assert np.allclose(g.cpu().numpy(), g_fd, rtol=1e-3, atol=1e-3)
+
+
+def test_partial_s_log_density_kat(native):
+    """test_partial_s_log_density.py:241-311 re-created and ASSERTED: d = 10, s = 0.1,
+    central differences delta = 1e-4 (ds) and 1e-3 (ds2), relative RMSE < 1e-3; plus a direct
+    comparison with the fp64 restatement."""
+    from example_problems.kinetic_mckean_vlasov_example_quadratic import KineticMcKeanVlasov
+    from utils import prng
+    d = 10
+    cfg = _cfg(["pde_instance=kinetic_mckean_vlasov", f"pde_instance.domain_dim={d}",
+                "pde_instance.total_evolving_time=1.0"])
+    pi = KineticMcKeanVlasov(cfg, prng.PRNGKey(0))
+    x = np.random.default_rng(0).uniform(size=(3, d))
+    s = 0.1
+    ds = pi.partial_s_log_density_fn(s, _t(x)).double().cpu().numpy()
+    ds2 = pi.partial_s2_log_density_fn(s, _t(x)).double().cpu().numpy()
+    cfg_np = nr.ou_configuration(pi.initial_configuration["tilde_F"], gamma=1.0)
+    fd1 = (nr.log_density(s + 1e-4, x, cfg_np) - nr.log_density(s - 1e-4, x, cfg_np)) / 2e-4
+    fd2 = (nr.partial_s_log_density(s + 1e-3, x, cfg_np) - nr.partial_s_log_density(s - 1e-3, x, cfg_np)) / 2e-3
+    ref1 = nr.partial_s_log_density(s, x, cfg_np); ref2 = nr.partial_s2_log_density(s, x, cfg_np)
+    assert np.sqrt(np.mean(((ref1 - fd1) / fd1) ** 2)) < 1e-3
+    assert np.sqrt(np.mean(((ref2 - fd2) / fd2) ** 2)) < 1e-3
+    assert np.max(np.abs(ds - ref1) / (1 + np.abs(ref1))) < 1e-4
+    assert np.max(np.abs(ds2 - ref2) / (1 + np.abs(ref2))) < 1e-3
+    # vector s, matrix x -> [n_x, n_s] like the reference's vmap order
+    both = pi.partial_s_log_density_fn(np.array([0.1, 0.5]), _t(x))
+    assert tuple(both.shape) == (3, 2)
+
+
+def test_mean_field_simulator_vs_c_oracle(native, oracle_lib):
+    from utils.mean_field import simulate_mean_field
+    from core.potential import MeanFieldQuadraticPotential
+    from utils import prng
+    d, N, n = 2, 2000, 50
+    A = nr.problem_constants(d)
+    z0 = np.random.default_rng(3).standard_normal((N, 2 * d)).astype(np.float32) + 0.5
+    key = prng.Key(0xABCDEF)
+    r = simulate_mean_field(_t(z0), n, 0.02, key, MeanFieldQuadraticPotential(A), 1.0, counter_offset=5)
+    o = oracle_lib.sde_simulate(z0, n, 0.02, 1.0, "meanfield", A, seed=key.seed, counter_offset=5)
+    assert np.array_equal(r["tau"].cpu().numpy(), o["tau"])
+    assert np.max(np.abs(r["traj"].cpu().numpy() - o["traj"])) < 2e-4
+    assert np.max(np.abs(r["last"].cpu().numpy() - o["last"])) < 2e-4
+
+
+def test_mean_field_equals_ou_for_centred_ensemble(native):
+    """with xbar_0 = vbar_0 = 0 the MV system's covariance is the OU chain's."""
+    from utils.mean_field import simulate_mean_field
+    from core.potential import MeanFieldQuadraticPotential
+    from utils import prng
+    d, N, n = 2, 1 << 17, 50
+    A = nr.problem_constants(d)
+    z0 = native.gaussian_sample(N, _t(np.zeros(2 * d)), _t(np.eye(2 * d)), seed=5)
+    z0 = z0 - z0.mean(0)
+    r = simulate_mean_field(z0, n, 0.02, prng.Key(9), MeanFieldQuadraticPotential(A), 1.0, random_shift=False)
+    P0 = (z0.double().T @ z0.double() / N).cpu().numpy()
+    mt, st, _, _ = nr.em_chain_moments(A, 1.0, 0.02, n, np.zeros(2 * d), P0, random_shift=False)
+    z = r["traj"][n - 1].double()
+    emp = (z.T @ z / N).cpu().numpy()
+    P = st[n - 1]
+    sig = np.sqrt((np.outer(np.diag(P), np.diag(P)) + P ** 2) / N)
+    assert np.max(np.abs(emp - P) / sig) < 5.5
+
+
+def _run(overrides, iters=3):
+    import main
+    cfg = _cfg(overrides + ["train.optimizer.learning_rate.initial=1e-2", "test.frequency=1000000"])
+    trainer, params = main.run(cfg, number_of_iterations=iters)
+    return trainer
+
+
+def test_trainer_kou_exact(native):
+    tr = _run(["pde_instance=kinetic_fokker_planck", "solver.train.batch_size_0T=20000",
+               "solver.train.batch_size_init=2000", "solver.train.batch_size_terminal=2000"])
+    assert len(tr.history) == 3 and all(np.isfinite(h["loss"]) for h in tr.history)
+
+
+def test_trainer_kou_sde_fused_converges(native):
+    """The fused simulate+moments path trains: loss ground truth decreases."""
+    tr = _run(["pde_instance=kinetic_fokker_planck", "pde_instance.sample_scheme=SDE",
+               "solver.train.batch_size_0T=50000", "train.optimizer.learning_rate.initial=5e-2"], iters=60)
+    gt = [h["loss ground truth"] for h in tr.history]
+    assert gt[-1] < 0.5 * gt[0]
+
+
+def test_trainer_gmm_online_and_offline(native):
+    for mode in ("online", "offline"):
+        tr = _run(["pde_instance=kinetic_fokker_planck", "pde_instance.potential=GMM", f"pde_instance.sample_mode={mode}",
+                   "pde_instance.n_steps=20", "solver.train.batch_size_0T=500", "pde_instance.sample_initial_size=5000",
+                   "pde_instance.sample_terminal_size=2000", "pde_instance.sample_0T_size=1000",
+                   "pde_instance.n_steps_terminal=40", "pde_instance.n_steps_0T=40"])
+        assert all(np.isfinite(h["loss"]) for h in tr.history)
+
+
+def test_trainer_kmv_exact_and_sde(native):
+    base = ["pde_instance=kinetic_mckean_vlasov", "pde_instance.domain_dim=2", "solver.train.sample_mode=grid_time",
+            "solver.train.sample_per_time=5000", "solver.train.n_time_stamps=1", "pde_instance.total_evolving_time=1"]
+    tr = _run(base)
+    assert all(np.isfinite(h["loss"]) for h in tr.history)
+    tr = _run(base + ["pde_instance.sample_scheme=SDE", "pde_instance.n_steps=20"])
+    assert all(np.isfinite(h["loss"]) for h in tr.history)
+
+
+def test_no_cpu_fallback_for_callables(native):
+    from utils.sampling_utils import underdamped_langevin_dynamics_scan
+    from utils import prng
+    with pytest.raises(NotImplementedError):
+        underdamped_langevin_dynamics_scan(_t(np.zeros((4, 4))), 5, 0.1, prng.Key(1), lambda q: q, 1.0)
+
+
+def test_reference_shaped_scan_outputs(native):
+    from utils.sampling_utils import underdamped_langevin_dynamics_scan
+    from core.potential import GMMPotential
+    from utils import prng
+    pot = GMMPotential(nr.gmm_centres(4, 3), 1.0)
+    last, traj, tau = underdamped_langevin_dynamics_scan(_t(np.zeros((64, 8))), 30, 0.05, prng.Key(3), pot.gradient, 0.5)
+    assert tuple(last.shape) == (64, 8) and tuple(traj.shape) == (64, 30, 8) and tuple(tau.shape) == (64, 30)
+    # tau = tau0 + k dt with tau0 in [0, dt)  (sampling_utils.py:32, 48)
+    t = tau.cpu().numpy()
+    assert np.all((t[:, 0] >= 0) & (t[:, 0] < 0.05)) and np.allclose(np.diff(t, axis=1), 0.05, atol=1e-6)
