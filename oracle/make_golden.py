@@ -1,0 +1,99 @@
+"""Generate tests/golden/*.npz from the fp64 NumPy restatement (oracle/numpy_ref.py).
+
+Test infrastructure only. The reference (JAX) cannot run in this image and ships no golden
+vectors, so these fixtures freeze the restatement's answers on fixed
+seeded inputs; the restatement itself is pinned by the closed-form checks in
+tests/test_oracle.py (exact EM-chain law, continuous OU moments, finite differences).
+
+    python oracle/make_golden.py        # rewrites tests/golden/
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+from oracle import numpy_ref as nr  # noqa: E402
+
+OUT = os.path.join(os.path.dirname(HERE), "tests", "golden")
+N, n, T = 64, 100, 2.0
+KEEP = np.r_[0, np.arange(9, n, 10)]  # stored trajectory rows
+
+
+def sde_case(name, d, gamma, grad_fn, params, seed, z0_scale=(1.0, 1.0), **extra):
+    rng = np.random.default_rng(seed)
+    z0 = np.concatenate([z0_scale[0] * rng.standard_normal((N, d)), z0_scale[1] * rng.standard_normal((N, d))],
+                        1).astype(np.float32)
+    xi = rng.standard_normal((n + 1, N, d)).astype(np.float32)
+    u = rng.random(N).astype(np.float32)
+    last, traj, _ = nr.sde_scan(z0, n, T / n, gamma, grad_fn, xi, u)
+    _, _, tau32 = nr.sde_scan(z0, n, T / n, gamma, grad_fn, xi, u, dtype=np.float32)
+    np.savez_compressed(os.path.join(OUT, f"sde_{name}.npz"), z0=z0, xi=xi, u=u, dt=T / n, gamma=gamma,
+                        params=np.asarray(params, np.float64), keep=KEEP, traj=traj[KEEP], last=last, tau=tau32,
+                        **extra)
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    for d in (2, 4, 8):
+        F = nr.problem_constants(d)
+        sde_case(f"kou_d{d}", d, 1.0, nr.grad_quadratic(F), F, 100 + d, kind="quadratic")
+    for K in (3, 8):
+        mus = nr.gmm_centres(4, K)
+        sde_case(f"gmm_d4_k{K}", 4, 0.5, nr.grad_gmm(mus), mus, 200 + K, z0_scale=(2.0, 0.3162), kind="gmm")
+
+    # KFP residual, quadratic model (kinetic_fokker_planck.py:33-58)
+    rng = np.random.default_rng(7)
+    d = 4
+    F = nr.problem_constants(d)
+    K = 0.3 * rng.standard_normal((d, d)); b = 0.2 * rng.standard_normal(d)
+    zi, zt, z0 = (rng.standard_normal((m, 2 * d)).astype(np.float32) for m in (500, 400, 3000))
+    loss, loss_gt, parts = nr.kfp_quadratic_samples(K, b, zi, zt, z0, F, 1.0, T)
+    g = nr.fd_grad(lambda th: nr.kfp_quadratic_samples(th[:16].reshape(4, 4), th[16:], zi, zt, z0, F, 1.0, T)[0],
+                   np.concatenate([K.ravel(), b]), eps=1e-6)
+    np.savez_compressed(os.path.join(OUT, "kfp_quadratic.npz"), K=K, b=b, zi=zi, zt=zt, z0=z0, F=F, gamma=1.0, T=T,
+                        loss=loss, loss_gt=loss_gt, grad=g)
+
+    # KFP residual, GMM model
+    mus_true = nr.gmm_centres(4, 3)
+    mus = rng.standard_normal((3, 4))
+    zi, zt, z0 = (1.5 * rng.standard_normal((m, 8)).astype(np.float32) for m in (400, 300, 2000))
+    loss, loss_gt, parts = nr.kfp_gmm_loss(mus, zi, zt, z0, mus_true, 0.5, T)
+    g = nr.fd_grad(lambda th: nr.kfp_gmm_loss(th, zi, zt, z0, mus_true, 0.5, T)[0], mus, eps=1e-6)
+    np.savez_compressed(os.path.join(OUT, "kfp_gmm.npz"), mus=mus, mus_true=mus_true, zi=zi, zt=zt, z0=z0, gamma=0.5,
+                        T=T, loss=loss, loss_gt=loss_gt, hessian=parts["hessian"], grad=g)
+
+    # KMV residual, literal pairwise formulation (kinetic_mckean_vlasov.py:11-120)
+    d, m_, nt = 2, 200, 3
+    F = nr.problem_constants(d)
+    cfg = nr.ou_configuration(F, gamma=1.0)
+    x = rng.standard_normal((m_, nt, d)); v = rng.standard_normal((m_, nt, d))
+    tau = np.array([0.25, 0.8, 1.6])
+    K = 0.3 * rng.standard_normal((d, d)); b = 0.2 * rng.standard_normal(d)
+    loss, loss_gt = nr.kmv_pairwise_loss(K, b, x, v, tau, cfg)
+    g = nr.fd_grad(lambda th: nr.kmv_pairwise_loss(th[:4].reshape(2, 2), th[4:], x, v, tau, cfg)[0],
+                   np.concatenate([K.ravel(), b]), eps=1e-6)
+    np.savez_compressed(os.path.join(OUT, "kmv_pairwise.npz"), K=K, b=b, x=x, v=v, tau=tau, F=F, loss=loss,
+                        loss_gt=loss_gt, grad=g)
+
+    # ds log rho KAT inputs/outputs (test_partial_s_log_density.py:241-311 shape: d = 10, s = 0.1)
+    d = 10
+    F = nr.problem_constants(d)
+    cfg = nr.ou_configuration(F, gamma=1.0)
+    xs = np.random.default_rng(0).uniform(size=(3, d))
+    np.savez_compressed(os.path.join(OUT, "dlogrho_d10.npz"), F=F, x=xs, s=0.1,
+                        ds=nr.partial_s_log_density(0.1, xs, cfg), ds2=nr.partial_s2_log_density(0.1, xs, cfg),
+                        logp=nr.log_density(0.1, xs, cfg))
+
+    # constants recipe
+    np.savez_compressed(os.path.join(OUT, "constants.npz"), **{f"tilde_F_d{d}": nr.problem_constants(d)
+                                                               for d in (2, 4, 8, 10)})
+    for f in sorted(os.listdir(OUT)):
+        print(f, os.path.getsize(os.path.join(OUT, f)))
+
+
+if __name__ == "__main__":
+    main()

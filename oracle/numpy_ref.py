@@ -417,3 +417,81 @@ def problem_constants(d, seed=2217):
 def gmm_centres(d, K, seed=2217, lo=-4.0, hi=4.0):
     """mu_k ~ U[-4, 4]^d (…_GMM.py:22-23, 52-59 distribution)."""
     return np.random.default_rng(seed + 1).uniform(lo, hi, size=(K, d))
+
+
+# --------------------------------------------------------------------------------------
+# derivations used by the kernels, restated in fp64 so the CPU suite can check them
+# --------------------------------------------------------------------------------------
+def kfp_gmm_grad_analytic(mus, z_init, z_term, z_0T, mus_true, gamma, T, sigma=1.0):
+    """The analytic adjoint of residual.hip kfp_gmm_kernel: d loss / d mu via the softmax chain
+    rule (F_k = df/dw_k, explicit d/dmu_j), per sample, summed with the loss weights."""
+    mus = np.asarray(mus, np.float64)
+    d = mus.shape[1]
+    s2 = 1.0 / sigma ** 2
+    s4 = s2 * s2
+    G = np.zeros_like(mus)
+
+    def acc(z, c1, c2, c3):
+        z = np.asarray(z, np.float64)
+        if len(z) == 0:
+            return
+        x, v = z[:, :d], z[:, d:]
+        diff = x[:, None, :] - mus[None]
+        a = -np.sum(diff ** 2, -1) * 0.5 * s2
+        a -= a.max(-1, keepdims=True)
+        w = np.exp(a); w /= w.sum(-1, keepdims=True)
+        mbar = w @ mus
+        e = x - mbar
+        pk = v @ mus.T
+        em = e @ mus.T
+        pbar = np.sum(w * pk, -1, keepdims=True)
+        Fk = -2 * c1 * s4 * em - c2 * s4 * (pk * pk - 2 * pbar * pk) - c3 * s2 * pk
+        Fbar = np.sum(w * Fk, -1, keepdims=True)
+        cw = w * (Fk - Fbar) * s2
+        ce = -2 * c1 * s4 * w
+        cv = -w * (2 * c2 * s4 * (pk - pbar) + c3 * s2)
+        G[:] += np.einsum("nk,nki->ki", cw, diff) + np.einsum("nk,ni->ki", ce, e) + np.einsum("nk,ni->ki", cv, v)
+
+    M = len(z_0T)
+    acc(z_0T, 1.0 / M, -2.0 / M, 2 * gamma / M)
+    if len(z_init):
+        acc(z_init, 0.0, 0.0, -2.0 / (T * len(z_init)))
+    if len(z_term):
+        acc(z_term, 0.0, 0.0, 2.0 / (T * len(z_term)))
+    return G
+
+
+def kmv_from_moments(K, b, x, v, tau, cfg):
+    """kmv.hip's formulation: per time stamp moments + c-weighted moments -> loss, loss_gt, grad."""
+    K = np.asarray(K, np.float64); b = np.asarray(b, np.float64)
+    S = K + K.T
+    F = cfg["tilde_F"]
+    gamma = cfg["gamma_friction"]
+    n, n_t, d = x.shape
+    N = n * n_t
+    nabla = hess = value = true = gt = 0.0
+    G = np.zeros((d, d)); gb = 2 * b.copy()
+    Mvv = np.einsum("nti,ntj->ij", v, v) / N
+    for t in range(n_t):
+        xt = x[:, t]
+        xbar = xt.mean(0)
+        M = xt.T @ xt / n
+        C = M - np.outer(xbar, xbar)
+        ds = partial_s_log_density(tau[t], xt, cfg)
+        ds2 = partial_s2_log_density(tau[t], xt, cfg)
+        c = ds2 + ds ** 2 + gamma * ds
+        W, Wx, Wxx = c.sum(), c @ xt, (xt * c[:, None]).T @ xt
+        w = n / N
+        nabla += w * np.trace(S @ C @ S)
+        true += w * np.trace(F @ C @ F.T)
+        D = F - S
+        gt += w * np.trace(D @ C @ D.T)
+        value += (0.5 * np.trace(S @ Wxx) - xbar @ S @ Wx + 0.5 * W * np.trace(S @ M) + b @ (Wx - W * xbar)) / N
+        G += w * (S @ C + C @ S) + 2 * (0.5 * Wxx - np.outer(xbar, Wx) + 0.5 * W * M) / N
+        gb += 2 * (Wx - W * xbar) / N
+    nabla += b @ b
+    gt += b @ b
+    hess = np.trace(S @ Mvv)
+    G += -2 * Mvv
+    loss = nabla - 2 * hess + 2 * value + true
+    return loss, gt, G + G.T, gb

@@ -1,0 +1,140 @@
+"""CPU tests of the host-side mirror: config composition, PRNG keys, registry, sharding,
+model init, the drift-recovery solve, and the C-ABI library's exported symbols."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_compose_defaults_and_overrides():
+    from utils import config
+    c = config.compose("config", [])
+    assert c.pde_instance.name == "Fokker-Planck" and c.solver.name == "ConsistencyBased"
+    assert c.train.optimizer.learning_rate.initial == 0.001 and c.seed == 1
+    c = config.compose("config", ["pde_instance=kinetic_mckean_vlasov", "pde_instance.domain_dim=2",
+                                  "train.optimizer.learning_rate.initial=1e-2", "backend.use_pmap_train=True",
+                                  "solver.train.sample_mode=grid_time", "estimation_mode=parametric", "seed=2"])
+    assert c.pde_instance.name == "Kinetic-McKean-Vlasov" and c.pde_instance.domain_dim == 2
+    assert c.train.optimizer.learning_rate.initial == 0.01 and c.backend.use_pmap_train is True
+    assert c.solver.train.sample_mode == "grid_time" and c.seed == 2
+    with pytest.raises(ValueError):
+        config.compose("config", ["pde_instance=nope"])
+
+
+@pytest.mark.parametrize("script", ["run_KOU.sh", "run_KGMM.sh", "parametric/KMV/run_quadratic_online.sh"])
+def test_reference_script_overrides_compose(script):
+    """The override lists of the reference's scripts/*.sh compose unchanged."""
+    from utils import config
+    overrides = {
+        "run_KOU.sh": ["pde_instance.domain_dim=4", "pde_instance.name=Kinetic-Fokker-Planck", "train.batch_size=250000",
+                       "solver.train.sample_per_time=250", "solver.train.n_time_stamps=100",
+                       "solver.train.batch_size_0T=250000", "solver.train.sample_mode=grid_time",
+                       "neural_network.hidden_dim=32", "train.optimizer.learning_rate.scheduling=cosine"],
+        "run_KGMM.sh": ["pde_instance.domain_dim=4", "pde_instance=kinetic_fokker_planck", "pde_instance.sample_mode=online",
+                        "pde_instance.potential=GMM", "pde_instance.n_steps=200", "solver.train.batch_size_0T=2500"],
+        "parametric/KMV/run_quadratic_online.sh": ["pde_instance.domain_dim=2", "pde_instance=kinetic_mckean_vlasov",
+                                                   "pde_instance.potential=Quadratic", "solver.train.sample_per_time=5000",
+                                                   "solver.train.n_time_stamps=1", "solver.train.batch_size_init=0"],
+    }[script]
+    c = config.compose("config", overrides)
+    assert c.pde_instance.domain_dim in (2, 4)
+
+
+def test_prng_split_is_deterministic_and_distinct():
+    from utils import prng
+    k = prng.PRNGKey(1)
+    a, b = prng.split(k)
+    assert prng.split(k) == [a, b] and a != b
+    assert len({x.seed for x in prng.split(k, 64)}) == 64
+    assert prng.fold_in(k, 0) != prng.fold_in(k, 1)
+
+
+def test_registry():
+    import registry
+    from utils import config
+    c = config.compose("config", ["pde_instance=kinetic_fokker_planck", "pde_instance.potential=GMM"])
+    assert registry.get_pde_instance(c).__module__.endswith("_GMM")
+    c = config.compose("config", [])
+    with pytest.raises(NotImplementedError):
+        registry.get_pde_instance(c)  # overdamped FP: out of scope, raises
+    c = config.compose("config", ["solver=PINN"])
+    with pytest.raises(NotImplementedError):
+        registry.get_method(c)
+
+
+@pytest.mark.parametrize("n,w", [(10, 3), (2 ** 21 * 8, 8), (5, 8), (0, 2)])
+def test_shard_partitions(n, w):
+    from utils import distributed as dist
+    parts = [dist.shard(n, r, w) for r in range(w)]
+    assert sum(p[1] for p in parts) == n
+    off = 0
+    for o, m in parts:
+        assert o == off
+        off += m
+
+
+def test_drift_recovery_is_exact_on_continuous_moments():
+    from methods.consistency_instances.kinetic_fokker_planck import recover_quadratic_drift
+    from oracle import numpy_ref as nr
+    d, T = 4, 2.0
+    F = nr.problem_constants(d)
+    cfg = nr.ou_configuration(F)
+    ts = (np.arange(2000) + 0.5) * T / 2000
+    M0 = np.mean([nr.ou_mean_cov(t, cfg)[1] for t in ts], 0)
+
+    def mom(P):
+        m = P.shape[0]
+        return np.concatenate([[1.0], np.zeros(m), P[np.triu_indices(m)]])
+    S, b = recover_quadratic_drift(np.stack([mom(cfg["P_0"]), mom(M0), mom(nr.ou_mean_cov(T, cfg)[1])]), 1.0, T, d)
+    assert np.abs(S - F).max() < 1e-5 and np.abs(b).max() < 1e-9
+
+
+def test_adam_matches_optax_semantics():
+    import torch
+    from core.trainer import Adam, cosine_decay_schedule
+    opt = Adam(0.1, weight_decay=0.01, eps=1e-4)
+    p = {"w": torch.tensor([1.0, -2.0])}
+    st = opt.init(p)
+    g = {"w": torch.tensor([0.5, 0.25])}
+    p1, st = opt.update(g, st, p)
+    gw = np.array([0.5, 0.25]) + 0.01 * np.array([1.0, -2.0])
+    m, v = 0.1 * gw, 0.001 * gw ** 2
+    want = np.array([1.0, -2.0]) - 0.1 * (m / 0.1) / (np.sqrt(v / 0.001) + 1e-4)
+    assert np.allclose(p1["w"].numpy(), want, rtol=1e-6)
+    f = cosine_decay_schedule(1.0, 20000, 1e-3)
+    assert f(0) == 1.0 and abs(f(20000) - 1e-3) < 1e-12 and abs(f(10000) - (0.5 * 0.999 + 1e-3)) < 1e-9
+
+
+def _header_functions():
+    txt = open(os.path.join(ROOT, "include", "pdeinv.h")).read()
+    return set(re.findall(r"^(?:int|size_t|const char\*)\s+(pdeinv_\w+)\(", txt, flags=re.M))
+
+
+def test_header_and_binding_agree():
+    from utils import native
+    assert _header_functions() == set(native.EXPORTED_SYMBOLS)
+
+
+def test_library_exports_every_header_symbol():
+    """The C-ABI shared library loads without a GPU and exports everything include/pdeinv.h declares."""
+    from utils import native
+    if not os.path.exists(native.LIB_PATH):
+        native.build()
+    lib = ctypes.CDLL(native.LIB_PATH)
+    missing = [s for s in _header_functions() if not hasattr(lib, s)]
+    assert not missing
+    lib.pdeinv_moment_len.restype = ctypes.c_int
+    assert lib.pdeinv_moment_len(8) == 45 and lib.pdeinv_abi_version() == 1
+
+
+def test_loader_fails_loudly_without_gpu():
+    import torch
+    from utils import native
+    if torch.cuda.is_available():
+        pytest.skip("has a GPU")
+    with pytest.raises(RuntimeError):
+        native.sde_simulate(torch.zeros((4, 4)), 3, 0.1, 1.0, dict(kind=0, params=np.eye(2)), seed=1)

@@ -1,0 +1,210 @@
+"""CPU tests: the oracle restatement against closed forms, the reference's own finite-difference
+check (test_partial_s_log_density.py, now asserted), Random123 KATs and the golden fixtures.
+No GPU needed."""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+from oracle import numpy_ref as nr
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+# Random123 philox4x32-10 known answers
+KATS = [
+    ((0, 0, 0, 0), (0, 0), (0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8)),
+    ((0xFFFFFFFF,) * 4, (0xFFFFFFFF,) * 2, (0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD)),
+    ((0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344), (0xA4093822, 0x299F31D0),
+     (0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1)),
+]
+
+
+@pytest.mark.parametrize("ctr,key,want", KATS)
+def test_philox_kat_c_oracle(oracle_lib, ctr, key, want):
+    assert tuple(int(x) for x in oracle_lib.philox(ctr, key)) == want
+
+
+@pytest.mark.parametrize("ctr,key,want", KATS)
+def test_philox_kat_host_prng(ctr, key, want):
+    from utils import prng
+    assert prng.philox4x32_10(ctr, key) == want
+
+
+def test_box_muller_normals_moments(oracle_lib):
+    z = np.concatenate([oracle_lib.sim_normals(11, p, 3, 8) for p in range(20000)])
+    assert abs(z.mean()) < 0.01 and abs(z.std() - 1) < 0.01
+    assert abs(np.mean(z ** 4) - 3) < 0.1
+
+
+@pytest.mark.parametrize("d", [1, 2, 4, 8])
+def test_c_oracle_equals_numpy_restatement(oracle_lib, d):
+    rng = np.random.default_rng(d)
+    N, n = 50, 60
+    F = nr.problem_constants(d)
+    z0 = rng.standard_normal((N, 2 * d)).astype(np.float32)
+    xi = rng.standard_normal((n + 1, N, d)).astype(np.float32)
+    u = rng.random(N).astype(np.float32)
+    o = oracle_lib.sde_simulate(z0, n, 0.02, 1.0, "quadratic", F, noise=xi, shift_u=u)
+    last, traj, _ = nr.sde_scan(z0, n, 0.02, 1.0, nr.grad_quadratic(F), xi, u)
+    assert np.max(np.abs(o["traj"] - traj) / (np.abs(traj).max() + 1)) < 1e-5
+
+
+def test_chain_law_matches_sample_paths():
+    """em_chain_moments is the exact law of sde_scan: check on 2e5 paths (5 sigma)."""
+    d, N, n = 2, 200000, 20
+    F = nr.problem_constants(d)
+    rng = np.random.default_rng(0)
+    z0 = rng.standard_normal((N, 2 * d))
+    xi = rng.standard_normal((n + 1, N, d))
+    u = rng.random(N)
+    last, traj, _ = nr.sde_scan(z0, n, 0.05, 1.0, nr.grad_quadratic(F), xi, u)
+    mt, st, ml, sl = nr.em_chain_moments(F, 1.0, 0.05, n, np.zeros(2 * d), np.eye(2 * d))
+    for s in (0, n - 1):
+        emp = traj[s].T @ traj[s] / N
+        sig = np.sqrt((np.outer(np.diag(st[s]), np.diag(st[s])) + st[s] ** 2) / N)
+        assert np.max(np.abs(emp - st[s]) / sig) < 5
+    emp = last.T @ last / N
+    sig = np.sqrt((np.outer(np.diag(sl), np.diag(sl)) + sl ** 2) / N)
+    assert np.max(np.abs(emp - sl) / sig) < 5
+
+
+def test_chain_converges_to_ou_weak_order_one():
+    """the terminal-covariance gap to the continuous OU law ~ dt."""
+    d, T = 4, 2.0
+    F = nr.problem_constants(d)
+    cfg = nr.ou_configuration(F)
+    _, P = nr.ou_mean_cov(T, cfg)
+    gaps = []
+    for n in (100, 200, 400):
+        _, _, _, sl = nr.em_chain_moments(F, 1.0, T / n, n, np.zeros(2 * d), np.eye(2 * d))
+        gaps.append(np.abs(sl - P).max())
+    assert 1.7 < gaps[0] / gaps[1] < 2.3 and 1.7 < gaps[1] / gaps[2] < 2.3
+
+
+def test_ou_closed_form_matches_ode():
+    """ou_mean_cov (Van Loan) == the reference's moment ODE (…_OU.py:78-86) integrated by RK45."""
+    from scipy.integrate import solve_ivp
+    F = nr.problem_constants(3)
+    cfg = nr.ou_configuration(F)
+    cfg["m_0"] = np.array([1.0, -0.5, 0.2, 0.0, 0.3, 0.0])
+    n = 6
+
+    def rhs(t, y):
+        m, P = y[:n], y[n:].reshape(n, n)
+        return np.concatenate([cfg["F"] @ m, (cfg["F"] @ P + P @ cfg["F"].T + cfg["L"]).ravel()])
+
+    sol = solve_ivp(rhs, (0, 1.3), np.concatenate([cfg["m_0"], cfg["P_0"].ravel()]), rtol=1e-10, atol=1e-12)
+    m, P = nr.ou_mean_cov(1.3, cfg)
+    assert np.allclose(m, sol.y[:n, -1], atol=1e-7) and np.allclose(P, sol.y[n:, -1].reshape(n, n), atol=1e-7)
+
+
+def test_quadratic_residual_moments_identity_and_gradient():
+    rng = np.random.default_rng(0)
+    d = 3
+    F = nr.problem_constants(d)
+    K, b = rng.standard_normal((d, d)), rng.standard_normal(d)
+    zi, zt, z0 = (rng.standard_normal((m, 2 * d)) for m in (300, 200, 1000))
+    loss, gt, _ = nr.kfp_quadratic_samples(K, b, zi, zt, z0, F, 0.7, 2.0)
+    l2, gt2, gK, gb, _ = nr.kfp_quadratic_from_moments(K, b, nr.moments(zi), nr.moments(z0), nr.moments(zt), F, 0.7, 2.0)
+    assert abs(loss - l2) < 1e-9 * (1 + abs(loss)) and abs(gt - gt2) < 1e-9 * (1 + abs(gt))
+    g_fd = nr.fd_grad(lambda th: nr.kfp_quadratic_samples(th[:9].reshape(3, 3), th[9:], zi, zt, z0, F, 0.7, 2.0)[0],
+                      np.concatenate([K.ravel(), b]))
+    assert np.allclose(np.concatenate([gK.ravel(), gb]), g_fd, rtol=1e-6, atol=1e-6)
+
+
+def test_loss_equals_ground_truth_on_exact_stationary_data():
+    """kinetic_fokker_planck.py:33-58 identity: E[loss] = E[loss gt] for exact OU data with
+    time-uniform 0T samples (checked through moments, no sampling noise)."""
+    d, T = 2, 2.0
+    F = nr.problem_constants(d)
+    cfg = nr.ou_configuration(F)
+    ts = (np.arange(4000) + 0.5) * T / 4000
+    M0 = np.mean([nr.ou_mean_cov(t, cfg)[1] for t in ts], 0)
+    PT = nr.ou_mean_cov(T, cfg)[1]
+
+    def mom(P):  # exact moments in the packed layout (mean 0)
+        m = P.shape[0]
+        return np.concatenate([[1.0], np.zeros(m), P[np.triu_indices(m)]])
+    rng = np.random.default_rng(3)
+    K, b = rng.standard_normal((d, d)), rng.standard_normal(d) * 0.1
+    loss, gt, *_ = nr.kfp_quadratic_from_moments(K, b, mom(cfg["P_0"]), mom(M0), mom(PT), F, 1.0, T)
+    assert abs(loss - gt) < 1e-5 * (1 + abs(gt))
+
+
+def test_gmm_analytic_adjoint_vs_finite_differences():
+    rng = np.random.default_rng(1)
+    d, K = 3, 4
+    mus_true, mus = nr.gmm_centres(d, 5), rng.standard_normal((K, d))
+    zi, zt, z0 = (1.5 * rng.standard_normal((m, 2 * d)) for m in (200, 150, 800))
+    G = nr.kfp_gmm_grad_analytic(mus, zi, zt, z0, mus_true, 0.5, 2.0)
+    g_fd = nr.fd_grad(lambda th: nr.kfp_gmm_loss(th, zi, zt, z0, mus_true, 0.5, 2.0)[0], mus)
+    assert np.allclose(G, g_fd, rtol=1e-6, atol=1e-7)
+
+
+def test_kmv_moment_form_equals_pairwise():
+    rng = np.random.default_rng(2)
+    d, n, n_t = 3, 120, 3
+    F = nr.problem_constants(d)
+    cfg = nr.ou_configuration(F)
+    x, v = rng.standard_normal((n, n_t, d)), rng.standard_normal((n, n_t, d))
+    tau = np.array([0.2, 0.9, 1.7])
+    K, b = 0.3 * rng.standard_normal((d, d)), 0.2 * rng.standard_normal(d)
+    l1, g1 = nr.kmv_pairwise_loss(K, b, x, v, tau, cfg)
+    l2, g2, gK, gb = nr.kmv_from_moments(K, b, x, v, tau, cfg)
+    assert abs(l1 - l2) < 1e-9 * (1 + abs(l1)) and abs(g1 - g2) < 1e-9 * (1 + abs(g1))
+    g_fd = nr.fd_grad(lambda th: nr.kmv_pairwise_loss(th[:9].reshape(3, 3), th[9:], x, v, tau, cfg)[0],
+                      np.concatenate([K.ravel(), b]))
+    assert np.allclose(np.concatenate([gK.ravel(), gb]), g_fd, rtol=1e-5, atol=1e-6)
+
+
+def test_partial_s_log_density_fd_kat():
+    """test_partial_s_log_density.py:241-311 (d = 10, s = 0.1, delta 1e-4 / 1e-3), asserted."""
+    g = np.load(os.path.join(GOLD, "dlogrho_d10.npz"))
+    cfg = nr.ou_configuration(g["F"], gamma=1.0)
+    x, s = g["x"], float(g["s"])
+    fd1 = (nr.log_density(s + 1e-4, x, cfg) - nr.log_density(s - 1e-4, x, cfg)) / 2e-4
+    fd2 = (nr.partial_s_log_density(s + 1e-3, x, cfg) - nr.partial_s_log_density(s - 1e-3, x, cfg)) / 2e-3
+    assert np.sqrt(np.mean(((g["ds"] - fd1) / fd1) ** 2)) < 1e-3
+    assert np.sqrt(np.mean(((g["ds2"] - fd2) / fd2) ** 2)) < 1e-3
+    assert np.allclose(nr.partial_s_log_density(s, x, cfg), g["ds"], rtol=1e-12)
+
+
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLD, "sde_*.npz"))))
+def test_oracle_reproduces_sde_golden(oracle_lib, path):
+    g = np.load(path)
+    F = g["params"]
+    grad = nr.grad_quadratic(F) if str(g["kind"]) == "quadratic" else nr.grad_gmm(F)
+    n = g["xi"].shape[0] - 1
+    last, traj, _ = nr.sde_scan(g["z0"], n, float(g["dt"]), float(g["gamma"]), grad, g["xi"], g["u"])
+    assert np.allclose(traj[g["keep"]], g["traj"], rtol=1e-12, atol=1e-12)
+    kind = str(g["kind"])
+    o = oracle_lib.sde_simulate(g["z0"], n, float(g["dt"]), float(g["gamma"]), kind, F, n_centers=F.shape[0] if kind == "gmm" else 0,
+                                noise=g["xi"], shift_u=g["u"])
+    assert np.array_equal(o["tau"], g["tau"])
+    scale = np.abs(g["traj"]).max() + 1
+    assert np.max(np.abs(o["traj"][g["keep"]] - g["traj"])) / scale < 2e-5
+
+
+def test_residual_goldens():
+    g = np.load(os.path.join(GOLD, "kfp_quadratic.npz"))
+    loss, gt, _ = nr.kfp_quadratic_samples(g["K"], g["b"], g["zi"], g["zt"], g["z0"], g["F"], 1.0, 2.0)
+    assert np.isclose(loss, g["loss"], rtol=1e-12) and np.isclose(gt, g["loss_gt"], rtol=1e-12)
+    g = np.load(os.path.join(GOLD, "kfp_gmm.npz"))
+    loss, gt, _ = nr.kfp_gmm_loss(g["mus"], g["zi"], g["zt"], g["z0"], g["mus_true"], 0.5, 2.0)
+    assert np.isclose(loss, g["loss"], rtol=1e-12)
+    G = nr.kfp_gmm_grad_analytic(g["mus"], g["zi"], g["zt"], g["z0"], g["mus_true"], 0.5, 2.0)
+    assert np.allclose(G, g["grad"], rtol=1e-5, atol=1e-7)
+    g = np.load(os.path.join(GOLD, "kmv_pairwise.npz"))
+    cfg = nr.ou_configuration(g["F"])
+    loss, gt, gK, gb = nr.kmv_from_moments(g["K"], g["b"], g["x"], g["v"], g["tau"], cfg)
+    assert np.isclose(loss, g["loss"], rtol=1e-10)
+    assert np.allclose(np.concatenate([gK.ravel(), gb]), g["grad"], rtol=1e-5, atol=1e-7)
+
+
+def test_constants_recipe():
+    g = np.load(os.path.join(GOLD, "constants.npz"))
+    from example_problems.kinetic_fokker_planck_example_OU import problem_matrix
+    for d in (2, 4, 8, 10):
+        assert np.array_equal(problem_matrix(d), g[f"tilde_F_d{d}"])
+        assert np.array_equal(nr.problem_constants(d), g[f"tilde_F_d{d}"])
