@@ -11,7 +11,6 @@
 // terminal = last) that the parametric-quadratic residual needs, so the KFP residual
 // (kinetic_fokker_planck.py:33-58) costs no second pass over the trajectory.
 #include <math.h>
-#include <stdlib.h>
 
 #include "common.h"
 
@@ -162,8 +161,8 @@ __device__ __forceinline__ float shift_u(const SdeArgs& a, uint32_t plo, uint32_
   return u32_unit(r.x);
 }
 
-template <int D, int POT, bool MOM, int STORE>
-__global__ __launch_bounds__(kBlock) void sde_simulate_kernel(SdeArgs a, const float* __restrict__ z0,
+template <int D, int POT, bool MOM, int STORE, int MINW = 1>
+__global__ __launch_bounds__(kBlock, MINW) void sde_simulate_kernel(SdeArgs a, const float* __restrict__ z0,
                                                               float* __restrict__ traj,
                                                               float* __restrict__ tau,
                                                               float* __restrict__ last,
@@ -387,21 +386,10 @@ extern "C" size_t pdeinv_sde_workspace_bytes(const pdeinv_sde_desc* d) {
   return (size_t)3 * moment_len(2 * d->dim) * sim_grid(d->n_particles) * sizeof(float);
 }
 
-// Experiment knob (A/B of the store forms on the D = 4 quadratic kernel): PDEINV_STORE_MODE.
-static int store_mode_env() {
-  const char* e = getenv("PDEINV_STORE_MODE");
-  return e ? atoi(e) : -1;
-}
-
 template <int D, int POT, bool MOM>
 static void launch_sim(const SdeArgs& a, const float* z0, float* traj, float* tau, float* last,
                        float* ws, hipStream_t st) {
   const dim3 g(sim_grid(a.N)), b(kBlock);
-  if constexpr (D == 4 && POT == PDEINV_POT_QUADRATIC) {
-    const int m = store_mode_env();
-    if (m == kStoreNT) { hipLaunchKernelGGL((sde_simulate_kernel<D, POT, MOM, kStoreNT>), g, b, 0, st, a, z0, traj, tau, last, ws); return; }
-    if (m == kStorePlain) { hipLaunchKernelGGL((sde_simulate_kernel<D, POT, MOM, kStorePlain>), g, b, 0, st, a, z0, traj, tau, last, ws); return; }
-  }
   hipLaunchKernelGGL((sde_simulate_kernel<D, POT, MOM, kStoreStaged>), g, b, 0, st, a, z0, traj, tau, last, ws);
 }
 
