@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Headline benchmark: particle-steps/s of the hot path on MI355X (BASELINE.json metric).
 
-Workload (BASELINE.json configs[1], "C2"): kinetic OU, d = 4, 2^21 particles per GPU,
+Default workload (BASELINE.json configs[1], "C2"): kinetic OU, d = 4, 2^21 particles per GPU,
 n = 100 Euler–Maruyama steps, T = 2, gamma = 1, Gaussian-init ensemble N(0, I_8), parametric
 drift recovery. One timed step = one pass of the hot path over one batch:
   1. the HIP simulator (all n+1 updates; trajectory [n,N,8], tau [n,N] and last [N,8] written to
@@ -11,9 +11,13 @@ drift recovery. One timed step = one pass of the hot path over one batch:
   3. the KFP residual value_and_grad for the current parameters (finalize kernel).
 value = particle-updates per second over all ranks = N_total * (n + 1) / step time (weak scaling).
 
-After the timed region (untimed): the drift tilde_F is recovered as the exact minimiser of the
+Other workloads (--config): C3 = kinetic FP with a GMM potential (d = 4, K = 8, 2^22 particles,
+simulate + fused GMM residual over init/0T/terminal); C4 = kinetic McKean–Vlasov (d = 8, 2^21
+particles per GPU, one all-reduced mean field per update, + the KMV residual).
+
+After the timed region (untimed, C2): the drift tilde_F is recovered as the exact minimiser of the
 residual from the moments of all timed steps, with Richardson extrapolation over n = 100 / 200
-to cancel the O(dt) Euler–Maruyama bias, and the CPU baseline — the NumPy
+to cancel the O(dt) Euler–Maruyama bias; the CPU baseline — the NumPy
 restatement of sampling_utils.py in oracle/ — is timed on a bounded sample on rank 0.
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; N > 1 under torch.distributed.run.
@@ -48,16 +52,16 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--particles", type=int, default=1 << 21, help="particles per GPU")
+    p.add_argument("--config", default="C2", choices=["C2", "C3", "C4"])
+    p.add_argument("--particles", type=int, default=0, help="particles per GPU (0 = the config's)")
     p.add_argument("--n-steps", type=int, default=100)
-    p.add_argument("--dim", type=int, default=4)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-recovery", action="store_true")
     p.add_argument("--cpu-particles", type=int, default=1 << 20)
     return p.parse_args()
 
 
-def algorithmic_bytes(N, n, d):
+def sim_bytes(N, n, d):
     """z0 read 8d + n (traj 8d + tau 4) + last 8d bytes per particle."""
     return N * (8 * d + n * (8 * d + 4) + 8 * d)
 
@@ -102,20 +106,53 @@ def cpu_model():
     return platform.processor() or "unknown"
 
 
-def main():
-    a = parse()
-    dist.init_from_env("nccl")
-    rank, world = dist.rank(), dist.world_size()
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    native.lib()
+def timed(step, K, W, dev):
+    """W untimed warmup steps, then K steps between barrier+synchronize; max over ranks.
+    step(record) records record[0]/record[1] around the dominant kernel's launch."""
+    for _ in range(W):
+        step(None)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(K):
+        step(evs[k])
+    torch.cuda.synchronize()
+    dist.barrier()
+    el = dist.allreduce_max_scalar(time.perf_counter() - t0, device=dev)
+    kern_ms = dist.allreduce_max_scalar(float(np.mean([s.elapsed_time(e) for s, e in evs])), device=dev)
+    return el * 1e3 / K, kern_ms
 
+
+def traffic_from_profiles(key):
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
+            return json.load(f).get(key)
+    except Exception:
+        return None
+
+
+def base_record(a, world, value, ms, config, kern_ms, bytes_launch, kernel, traffic=None):
+    achieved = bytes_launch / (kern_ms / 1e3) / 1e9
+    return {
+        "metric": METRIC, "value": value, "unit": "particle-steps/s", "n_gpus": world, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic: Philox Gaussian-init ensembles, fresh noise per step",
+        "config": config, "hbm_GBps": achieved,
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic, "kernel": kernel,
+                     "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": bytes_launch},
+    }
+
+
+# ------------------------------------------------------------------------------------------
+def run_c2(a, rank, world, dev):
     from example_problems.kinetic_fokker_planck_example_OU import problem_matrix
     from methods.consistency_instances.kinetic_fokker_planck import recover_quadratic_drift
 
-    d, n, N, T, gamma = a.dim, a.n_steps, a.particles, 2.0, 1.0
-    dt = T / n
+    d, n, T, gamma = 4, a.n_steps, 2.0, 1.0
+    N = a.particles or (1 << 21)
     F = problem_matrix(d)
     pot = dict(kind=native.POT_QUADRATIC, params=F)
     seed = 0x5EED_0001
@@ -128,63 +165,29 @@ def main():
             "moments": torch.empty((3, native.moment_len(2 * d)), device=dev, dtype=torch.float64)}
     mom_total = torch.zeros((3, native.moment_len(2 * d)), device=dev, dtype=torch.float64)
     counter = [0]
+    last_res = [None]
 
-    def step(n_steps=n, out=bufs, record=None):
+    def step(record):
         if record is not None:
             record[0].record()
-        r = native.sde_simulate(z0, n_steps, T / n_steps, gamma, pot, seed=seed, counter_offset=counter[0],
-                                particle_offset=poff, moments=True, out=out)
+        r = native.sde_simulate(z0, n, T / n, gamma, pot, seed=seed, counter_offset=counter[0],
+                                particle_offset=poff, moments=True, out=bufs)
         if record is not None:
             record[1].record()
-        counter[0] = (counter[0] + n_steps + 1) & 0xFFFFFFFF
+        counter[0] = (counter[0] + n + 1) & 0xFFFFFFFF
         mom = dist.allreduce_sum(r["moments"])
-        res = native.residual_kfp_quadratic(mom, theta, F, gamma, T)
-        return mom, res
+        last_res[0] = native.residual_kfp_quadratic(mom, theta, F, gamma, T)
+        mom_total.add_(mom)
 
-    for _ in range(a.warmup):
-        mom, _ = step()
-        mom_total += mom
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
-    dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(a.steps):
-        mom, res = step(record=evs[k])
-        mom_total += mom
-    torch.cuda.synchronize()
-    dist.barrier()
-    el = time.perf_counter() - t0
-    el = dist.allreduce_max_scalar(el, device=dev)
-    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in evs]))
-    kern_ms = dist.allreduce_max_scalar(kern_ms, device=dev)
-    ms_per_step = el * 1e3 / a.steps
-    total_updates = world * N * (n + 1)
-    value = total_updates / (ms_per_step / 1e3)
-    bytes_launch = algorithmic_bytes(N, n, d)
-    achieved = bytes_launch / (kern_ms / 1e3) / 1e9
-
-    out = {
-        "metric": METRIC, "value": value, "unit": "particle-steps/s", "n_gpus": world, "steps": a.steps,
-        "warmup": a.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "f32", "data": "synthetic: Philox N(0, I) initial ensembles, fresh noise per step",
-        "config": {"workload": "C2 kinetic OU d=4: EM simulate (traj+tau+last, fused moments) + KFP residual "
-                               "value_and_grad, per GPU 2^21 particles x 101 updates",
-                   "dim": d, "n_steps": n, "particles_per_gpu": N, "total_time": T, "gamma": gamma,
-                   "parallelism": f"dp{world}"},
-        "hbm_GBps": achieved,
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
-                     "kernel": "sde_simulate_kernel<4,QUADRATIC,MOM> (+ its slab reduce)",
-                     "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": bytes_launch},
-    }
-    traffic_file = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(traffic_file) and (d, n, N) == (4, 100, 1 << 21):
-        try:
-            with open(traffic_file) as f:
-                out["roofline"]["traffic"] = json.load(f).get("sde_simulate_C2_bytes_per_launch")
-        except Exception:
-            pass
-
+    ms, kern_ms = timed(step, a.steps, a.warmup, dev)
+    value = world * N * (n + 1) / (ms / 1e3)
+    cfg = {"workload": "C2 kinetic OU d=4: EM simulate (traj+tau+last, fused moments) + KFP residual "
+                       "value_and_grad", "dim": d, "n_steps": n, "particles_per_gpu": N, "total_time": T,
+           "gamma": gamma, "parallelism": f"dp{world}"}
+    out = base_record(a, world, value, ms, cfg, kern_ms, sim_bytes(N, n, d),
+                      "sde_simulate_kernel<4,QUADRATIC,moments,staged> (+ its slab reduce)",
+                      traffic_from_profiles("sde_simulate_C2_bytes_per_launch") if (N, n) == (1 << 21, 100) else None)
+    out["loss"] = float(last_res[0][0][0].item())
     if not a.no_recovery:
         S100, _ = recover_quadratic_drift(mom_total, gamma, T, d)
         mom2 = torch.zeros_like(mom_total)
@@ -199,9 +202,7 @@ def main():
         out["drift_err_l2"] = float(np.linalg.norm(S_rich - F) / np.linalg.norm(F))
         out["drift_err_em_n100"] = float(np.abs(S100 - F).max())
         out["drift_recovery"] = ("max |S - tilde_F|, S = K + K^T the exact residual minimiser, Richardson "
-                                 f"2*S(n=200) - S(n=100) over {(a.steps + a.warmup) * world * N} trajectories each")
-        out["loss"] = float(res[0][0].item())
-
+                                 f"2*S(n=200) - S(n=100), {(a.steps + a.warmup) * world * N} trajectories each")
     if rank == 0 and not a.no_cpu_baseline:
         ups, secs = cpu_baseline(F, d, n, T, gamma, a.cpu_particles)
         out["cpu_baseline"] = {"value": ups, "unit": "particle-steps/s", "cores": 1, "kind": "port",
@@ -209,6 +210,112 @@ def main():
                                          f"+ moment pass, fp32, d={d}, {a.cpu_particles} particles x {n + 1} updates, "
                                          f"{secs:.1f} s; host {cpu_model()}, os.cpu_count()={os.cpu_count()}"}
         out["gpu_over_cpu"] = value / ups
+    return out
+
+
+def run_c3(a, rank, world, dev):
+    from example_problems.kinetic_fokker_planck_example_GMM import gmm_means
+    from utils import prng
+
+    d, K, n, T, gamma = 4, 8, a.n_steps, 2.0, 0.5
+    N = a.particles or (1 << 22)
+    mus = gmm_means(d, K, prng.PRNGKey(2))
+    pot = dict(kind=native.POT_GMM, params=mus, n_centers=K, sigma=1.0)
+    seed = 0x5EED_0003
+    poff = rank * N
+    ch = torch.diag(torch.tensor([2.0] * d + [math.sqrt(0.1)] * d, device=dev))  # x0~N(0,4I), v0~N(0,0.1I)
+    z0 = native.gaussian_sample(N, torch.zeros(2 * d, device=dev), ch, seed=seed ^ 0xA5A5, row_offset=poff)
+    mus_model = torch.as_tensor(np.random.default_rng(0).standard_normal((K, d)), dtype=torch.float32, device=dev)
+    bufs = {"traj": torch.empty((n, N, 2 * d), device=dev), "tau": torch.empty((n, N), device=dev),
+            "last": torch.empty((N, 2 * d), device=dev)}
+    desc = native.kfp_gmm_desc(d, K, mus, gamma, T, N, N, N * n, world_scale=1.0 / world)
+    counter = [0]
+    res_ev = []
+
+    def step(record):
+        if record is not None:
+            record[0].record()
+        r = native.sde_simulate(z0, n, T / n, gamma, pot, seed=seed, counter_offset=counter[0],
+                                particle_offset=poff, out=bufs)
+        if record is not None:
+            record[1].record()
+        counter[0] = (counter[0] + n + 1) & 0xFFFFFFFF
+        acc = native.residual_kfp_gmm(desc, z0, r["last"], r["traj"].view(-1, 2 * d), mus_model)
+        if record is not None:
+            e2 = torch.cuda.Event(enable_timing=True)
+            e2.record()
+            res_ev.append((record[1], e2))
+        acc = dist.allreduce_sum(acc)
+        native.residual_kfp_gmm_finalize(desc, acc)
+
+    ms, kern_ms = timed(step, a.steps, a.warmup, dev)
+    value = world * N * (n + 1) / (ms / 1e3)
+    cfg = {"workload": "C3 kinetic FP, GMM potential K=8, d=4: EM simulate (traj+tau+last) + fused GMM "
+                       "residual value_and_grad over init/0T/terminal", "dim": d, "n_centers": K, "n_steps": n,
+           "particles_per_gpu": N, "total_time": T, "gamma": gamma, "parallelism": f"dp{world}"}
+    out = base_record(a, world, value, ms, cfg, kern_ms, sim_bytes(N, n, d), "sde_simulate_kernel<4,GMM,staged>")
+    r_ms = float(np.mean([s.elapsed_time(e) for s, e in res_ev]))
+    res_bytes = (N * (n + 2)) * 8 * d
+    out["residual"] = {"kernel": "kfp_gmm_kernel<4,8> + slab reduce", "ms": r_ms,
+                       "algorithmic_bytes": res_bytes, "GBps": res_bytes / (r_ms / 1e3) / 1e9}
+    return out
+
+
+def run_c4(a, rank, world, dev):
+    from example_problems.kinetic_fokker_planck_example_OU import initialize_configuration
+    from example_problems.kinetic_mckean_vlasov_example_quadratic import dlogrho_coefficients
+    from core.potential import MeanFieldQuadraticPotential
+    from utils.mean_field import simulate_mean_field
+    from utils import prng
+
+    d, n, T = 8, a.n_steps, 2.0
+    N = a.particles or (1 << 21)
+    ic = initialize_configuration(d)
+    gamma = ic["gamma_friction"]
+    A = ic["tilde_F"]
+    poff = rank * N
+    z0 = native.gaussian_sample(N, torch.zeros(2 * d, device=dev), torch.eye(2 * d, device=dev), seed=7,
+                                row_offset=poff)
+    theta = torch.zeros(d * d + d, device=dev)
+    key = prng.Key(0x5EED_0004)
+    counter = [0]
+    pot = MeanFieldQuadraticPotential(A)
+
+    def step(record):
+        if record is not None:
+            record[0].record()
+        r = simulate_mean_field(z0, n, T / n, key, pot, gamma, particle_offset=poff, counter_offset=counter[0])
+        if record is not None:
+            record[1].record()
+        counter[0] = (counter[0] + n + 1) & 0xFFFFFFFF
+        traj = r["traj"]
+        tau = r["tau"][:, 0].double().cpu().numpy()
+        mom = native.moments_batched(traj, n, N, 2 * d, N * 2 * d, 2 * d)
+        coef = torch.as_tensor(dlogrho_coefficients(tau, ic, d), dtype=torch.float32, device=dev)
+        wst, _ = native.kmv_weights(d, gamma, coef, traj, n, N, N * 2 * d, 2 * d)
+        both = dist.allreduce_sum(torch.cat([mom.reshape(-1), wst.reshape(-1)]))
+        native.residual_kmv(both[: mom.numel()].view_as(mom), both[mom.numel():].view_as(wst), theta, A, gamma)
+
+    ms, kern_ms = timed(step, a.steps, a.warmup, dev)
+    value = world * N * (n + 1) / (ms / 1e3)
+    cfg = {"workload": "C4 kinetic McKean-Vlasov quadratic interaction d=8: interacting-particle EM "
+                       "(one all-reduced mean field per update) + KMV residual value_and_grad",
+           "dim": d, "n_steps": n, "particles_per_gpu": N, "total_time": T, "gamma": gamma,
+           "parallelism": f"dp{world}"}
+    mf_bytes = N * (n + 1) * (16 * d) + N * n * 4  # each update reads and writes the state; tau
+    return base_record(a, world, value, ms, cfg, kern_ms, mf_bytes,
+                       "101 x (mf_step_kernel<8> + slab reduce + all-reduce): the whole simulator")
+
+
+def main():
+    a = parse()
+    dist.init_from_env("nccl")
+    rank, world = dist.rank(), dist.world_size()
+    local = dist.local_device()
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    native.lib()
+    out = {"C2": run_c2, "C3": run_c3, "C4": run_c4}[a.config](a, rank, world, dev)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist.is_distributed():

@@ -32,12 +32,19 @@ def init_from_env(backend: str = None) -> bool:
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     if ws <= 1 or dist.is_initialized():
         return dist.is_initialized()
+    backend = os.environ.get("PDEINV_DIST_BACKEND", backend)  # test override (e.g. gloo on one GPU)
     if backend is None:
         backend = "nccl" if torch.cuda.is_available() else "gloo"
-    if backend == "nccl":
-        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local_device())
     dist.init_process_group(backend=backend)
     return True
+
+
+def local_device() -> int:
+    """LOCAL_RANK modulo the visible devices (lets a test run several ranks on one GPU)."""
+    n = max(torch.cuda.device_count(), 1)
+    return int(os.environ.get("LOCAL_RANK", "0")) % n
 
 
 def shard(n_global: int, r: int = None, w: int = None):
