@@ -126,7 +126,7 @@ __global__ __launch_bounds__(kBlock) void kfp_quadratic_finalize_kernel(KfpQuadA
 // =========================================================================================
 struct GmmResArgs {
   int K, KT;
-  float s2, nh_s2_l2e, s2t, nh_s2t_l2e;  // 1/sigma^2 and -0.5/sigma^2*log2(e)
+  float s2, l2s, s2t, l2st;  // 1/sigma^2 and log2(e)/sigma^2
   int64_t n0, ni, nt, ld0, ldi, ldt;
   const float* z0T;
   const float* zi;
@@ -137,22 +137,24 @@ struct GmmResArgs {
 
 constexpr int kGmmGridCap = 1024;
 
-// softmax weights w_k of a_k = -|x - mu_k|^2 / (2 s^2); returns sum_k w_k mu_k in mbar.
+// softmax weights w_k of a_k = -|x - mu_k|^2 / (2 s^2) = (x.mu_k - |mu_k|^2/2)/s^2 + const(x)
+// (the |x|^2 term cancels in the softmax); returns w, mbar = sum_k w_k mu_k and t_k = x.mu_k.
+// l2s = log2(e)/s^2, nh[k] = -|mu_k|^2/2.
 template <int D, int KM>
-__device__ __forceinline__ void gmm_softmax(const float* x, const float (*mu)[D], int K, float nh,
-                                            float* w, float* mbar) {
+__device__ __forceinline__ void gmm_softmax(const float* x, const float (*mu)[D], const float* nh, int K,
+                                            float l2s, float* w, float* mbar, float* t) {
   float amax = -INFINITY;
 #pragma unroll
   for (int k = 0; k < KM; ++k) {
     if (k < K) {
-      float d2 = 0.f;
+      float dot = 0.f;
 #pragma unroll
-      for (int i = 0; i < D; ++i) {
-        const float t = x[i] - mu[k][i];
-        d2 = fmaf(t, t, d2);
-      }
-      w[k] = d2 * nh;
+      for (int i = 0; i < D; ++i) dot = fmaf(x[i], mu[k][i], dot);
+      t[k] = dot;
+      w[k] = (dot + nh[k]) * l2s;
       amax = fmaxf(amax, w[k]);
+    } else {
+      t[k] = 0.f;
     }
   }
   float den = 0.f;
@@ -165,7 +167,7 @@ __device__ __forceinline__ void gmm_softmax(const float* x, const float (*mu)[D]
       w[k] = 0.f;
     }
   }
-  const float inv = 1.f / den;
+  const float inv = __builtin_amdgcn_rcpf(den);
 #pragma unroll
   for (int i = 0; i < D; ++i) mbar[i] = 0.f;
 #pragma unroll
@@ -182,13 +184,20 @@ __global__ __launch_bounds__(kBlock) void kfp_gmm_kernel(GmmResArgs a, const flo
   constexpr int NS = PDEINV_GMM_NACC;
   float mu[KM][D];
   float mut[KM][D];
+  float nh[KM], nht[KM];
 #pragma unroll
-  for (int k = 0; k < KM; ++k)
+  for (int k = 0; k < KM; ++k) {
+    float n2 = 0.f, n2t = 0.f;
 #pragma unroll
     for (int i = 0; i < D; ++i) {
       mu[k][i] = (k < a.K) ? mus[k * D + i] : 0.f;
       mut[k][i] = (k < a.KT) ? a.mus_true[k * D + i] : 0.f;
+      n2 = fmaf(mu[k][i], mu[k][i], n2);
+      n2t = fmaf(mut[k][i], mut[k][i], n2t);
     }
+    nh[k] = -0.5f * n2;
+    nht[k] = -0.5f * n2t;
+  }
   float acc[NS + KM * D];
 #pragma unroll
   for (int c = 0; c < NS + KM * D; ++c) acc[c] = 0.f;
@@ -196,18 +205,35 @@ __global__ __launch_bounds__(kBlock) void kfp_gmm_kernel(GmmResArgs a, const flo
   const int64_t total = a.n0 + a.ni + a.nt;
   const int64_t stride = (int64_t)gridDim.x * kBlock;
   const float s2 = a.s2;
-  for (int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x; r < total; r += stride) {
-    int set;
-    const float* row;
-    if (r < a.n0) { set = 0; row = a.z0T + r * a.ld0; }
-    else if (r < a.n0 + a.ni) { set = 1; row = a.zi + (r - a.n0) * a.ldi; }
-    else { set = 2; row = a.zt + (r - a.n0 - a.ni) * a.ldt; }
+  auto row_of = [&](int64_t r, int& set) -> const float* {
+    if (r < a.n0) { set = 0; return a.z0T + r * a.ld0; }
+    if (r < a.n0 + a.ni) { set = 1; return a.zi + (r - a.n0) * a.ldi; }
+    set = 2;
+    return a.zt + (r - a.n0 - a.ni) * a.ldt;
+  };
+  // software pipeline: the next row is loaded before the current one is processed (only a few
+  // waves fit per SIMD at this register count, so the load latency must hide behind ALU work)
+  int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  int set_n = 0;
+  float xn[D], vn[D];
+  if (r < total) {
+    const float* row = row_of(r, set_n);
+#pragma unroll
+    for (int i = 0; i < D; ++i) { xn[i] = row[i]; vn[i] = row[D + i]; }
+  }
+  for (; r < total; r += stride) {
+    const int set = set_n;
     float x[D], v[D];
 #pragma unroll
-    for (int i = 0; i < D; ++i) { x[i] = row[i]; v[i] = row[D + i]; }
+    for (int i = 0; i < D; ++i) { x[i] = xn[i]; v[i] = vn[i]; }
+    if (r + stride < total) {
+      const float* row = row_of(r + stride, set_n);
+#pragma unroll
+      for (int i = 0; i < D; ++i) { xn[i] = row[i]; vn[i] = row[D + i]; }
+    }
 
-    float w[KM], mbar[D];
-    gmm_softmax<D, KM>(x, mu, a.K, a.nh_s2_l2e, w, mbar);
+    float w[KM], mbar[D], xm[KM];
+    gmm_softmax<D, KM>(x, mu, nh, a.K, a.l2s, w, mbar, xm);
     float e[D], g[D], T1 = 0.f, T3 = 0.f, vv = 0.f;
 #pragma unroll
     for (int i = 0; i < D; ++i) {
@@ -220,9 +246,9 @@ __global__ __launch_bounds__(kBlock) void kfp_gmm_kernel(GmmResArgs a, const flo
     float pk[KM], em[KM], pbar = 0.f, wp2 = 0.f;
 #pragma unroll
     for (int k = 0; k < KM; ++k) {
-      float p = 0.f, q = 0.f;
+      float p = 0.f, q = xm[k];  // e.mu_k = x.mu_k - mbar.mu_k
 #pragma unroll
-      for (int i = 0; i < D; ++i) { p = fmaf(mu[k][i], v[i], p); q = fmaf(mu[k][i], e[i], q); }
+      for (int i = 0; i < D; ++i) { p = fmaf(mu[k][i], v[i], p); q = fmaf(-mu[k][i], mbar[i], q); }
       pk[k] = p;
       em[k] = q;
       pbar = fmaf(w[k], p, pbar);
@@ -252,8 +278,8 @@ __global__ __launch_bounds__(kBlock) void kfp_gmm_kernel(GmmResArgs a, const flo
     }
     acc[PDEINV_GMM_ACC_LOSS] += c1 * T1 + c2 * T2 + c3 * T3;
     if (set == 0) {
-      float wt[KM], mbt[D];
-      gmm_softmax<D, KM>(x, mut, a.KT, a.nh_s2t_l2e, wt, mbt);
+      float wt[KM], mbt[D], xmt[KM];
+      gmm_softmax<D, KM>(x, mut, nht, a.KT, a.l2st, wt, mbt, xmt);
       float Tt = 0.f, Tgt = 0.f;
 #pragma unroll
       for (int i = 0; i < D; ++i) {
@@ -426,9 +452,9 @@ extern "C" int pdeinv_residual_kfp_gmm(const pdeinv_kfp_gmm_desc* d, const float
   a.K = d->n_centers;
   a.KT = d->n_centers_true;
   a.s2 = 1.f / (d->sigma * d->sigma);
-  a.nh_s2_l2e = -0.5f * a.s2 * 1.4426950408889634f;
+  a.l2s = a.s2 * 1.4426950408889634f;
   a.s2t = 1.f / (d->sigma_true * d->sigma_true);
-  a.nh_s2t_l2e = -0.5f * a.s2t * 1.4426950408889634f;
+  a.l2st = a.s2t * 1.4426950408889634f;
   a.n0 = n0; a.ni = ni; a.nt = nt;
   a.ld0 = ld0 ? ld0 : 2 * D; a.ldi = ldi ? ldi : 2 * D; a.ldt = ldt ? ldt : 2 * D;
   PDEINV_REQUIRE(a.ld0 >= 2 * D && a.ldi >= 2 * D && a.ldt >= 2 * D, PDEINV_ERR_INVALID,

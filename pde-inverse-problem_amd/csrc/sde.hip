@@ -23,7 +23,9 @@ struct SdeArgs {
   uint32_t k0, k1, ctr_off;
   const float* noise;
   const float* shift_u;
-  float params[PDEINV_MAX_PARAMS + PDEINV_MAX_DIM];
+  // QUADRATIC: A (d*d) then c (d). GMM (packed on the host at compile-time offsets):
+  // [kMaxGmmK*d scaled mu | kMaxGmmK constants | kMaxGmmK*d raw mu]
+  float params[2 * 16 * PDEINV_MAX_DIM + 16];
 };
 
 constexpr int kMaxGmmK = 16;
@@ -67,22 +69,26 @@ __device__ __forceinline__ void grad_quadratic(const SdeArgs& a, const float* q,
 
 // grad of U = -logsumexp_k(-|q-mu_k|^2/(2 s^2)) = (q - sum_k w_k mu_k) / s^2
 // (core/potential.py:32-37; the softmax form of the commented analytic gradient :39-43).
-// Centres are kernel arguments (scalar loads); exponents in log2 units for v_exp_f32.
+// Softmax logits are shift-invariant, so |q|^2 drops out: a_k = (q . mu_k - |mu_k|^2 / 2) / s^2,
+// one d-term dot per centre. The centres arrive in the kernel arguments pre-scaled to log2 units
+// (params[k*D+i] = mu_ki * log2e / s^2, params[K*D + k] = -|mu_k|^2 log2e / (2 s^2)) and raw
+// (params[K*D + K + k*D + i] = mu_ki) for the weighted mean.
 template <int D>
 __device__ __forceinline__ void grad_gmm(const SdeArgs& a, const float* q, float* g) {
+  const int K = a.K;
+  const float* mu_s = a.params;                      // compile-time offsets: the centres stay
+  const float* c = a.params + kMaxGmmK * D;          // scalar (SGPR) loads, not VGPR copies
+  const float* mu = a.params + kMaxGmmK * D + kMaxGmmK;
   float al[kMaxGmmK];
   float amax = -INFINITY;
 #pragma unroll
   for (int k = 0; k < kMaxGmmK; ++k) {
-    if (k < a.K) {
-      float d2 = 0.f;
+    if (k < K) {
+      float t = c[k];
 #pragma unroll
-      for (int i = 0; i < D; ++i) {
-        const float t = q[i] - a.params[k * D + i];
-        d2 = fmaf(t, t, d2);
-      }
-      al[k] = d2 * a.neg_half_inv_s2_log2e;
-      amax = fmaxf(amax, al[k]);
+      for (int i = 0; i < D; ++i) t = fmaf(q[i], mu_s[k * D + i], t);
+      al[k] = t;
+      amax = fmaxf(amax, t);
     }
   }
   float den = 0.f, acc[D];
@@ -90,16 +96,16 @@ __device__ __forceinline__ void grad_gmm(const SdeArgs& a, const float* q, float
   for (int i = 0; i < D; ++i) acc[i] = 0.f;
 #pragma unroll
   for (int k = 0; k < kMaxGmmK; ++k) {
-    if (k < a.K) {
+    if (k < K) {
       const float e = __builtin_amdgcn_exp2f(al[k] - amax);
       den += e;
 #pragma unroll
-      for (int i = 0; i < D; ++i) acc[i] = fmaf(e, a.params[k * D + i], acc[i]);
+      for (int i = 0; i < D; ++i) acc[i] = fmaf(e, mu[k * D + i], acc[i]);
     }
   }
-  const float inv = 1.0f / den;
+  const float inv = __builtin_amdgcn_rcpf(den);
 #pragma unroll
-  for (int i = 0; i < D; ++i) g[i] = a.inv_s2 * (q[i] - acc[i] * inv);
+  for (int i = 0; i < D; ++i) g[i] = a.inv_s2 * fmaf(-acc[i], inv, q[i]);
 }
 
 // Store modes for the per-step trajectory rows (M = 2d floats per particle):
@@ -355,10 +361,25 @@ static int build_args(const pdeinv_sde_desc* d, SdeArgs& a) {
                      PDEINV_ERR_UNSUPPORTED, "sde: GMM needs 1 <= n_centers <= 16");
       PDEINV_REQUIRE(std::isfinite(p.sigma) && p.sigma > 0.f, PDEINV_ERR_INVALID,
                      "sde: GMM sigma must be > 0");
+      PDEINV_REQUIRE(p.params != nullptr, PDEINV_ERR_INVALID, "sde: potential params are null");
       a.K = p.n_centers;
       a.inv_s2 = 1.0f / (p.sigma * p.sigma);
       a.neg_half_inv_s2_log2e = -0.5f * a.inv_s2 * 1.4426950408889634f;
-      n_params = p.n_centers * D;
+      {
+        const double sc = 1.4426950408889634 / ((double)p.sigma * (double)p.sigma);
+        const int K = p.n_centers;
+        for (int k = 0; k < K; ++k) {
+          double n2 = 0;
+          for (int i = 0; i < D; ++i) {
+            const double m = p.params[k * D + i];
+            a.params[k * D + i] = (float)(m * sc);
+            a.params[kMaxGmmK * D + kMaxGmmK + k * D + i] = (float)m;
+            n2 += m * m;
+          }
+          a.params[kMaxGmmK * D + k] = (float)(-0.5 * n2 * sc);
+        }
+      }
+      n_params = 0;  // packed above
       break;
     case PDEINV_POT_NONE:
       n_params = 0;  // quadratic with A = 0
