@@ -269,6 +269,39 @@ int pdeinv_residual_kmv(const pdeinv_kmv_desc* desc, const double* d_mom, const 
                         const float* d_theta, float* d_out, float* d_grad, void* stream);
 
 /* ---------------------------------------------------------------------------------------
+ * KFP residual for the non-parametric hypothesis V_hypothesis (core/model.py:32-62):
+ * V(x) = sum_o y_o^2, y = Dense_out(tanh(Dense_W(... tanh(Dense_W(x))))), out = 40.
+ * Fused value + d loss / d theta over the three sample sets (same loss and coefficients as the
+ * GMM residual): Taylor-mode forward streams, the grad_x reverse chain, its forward adjoint, the
+ * reverse sweep and the weight-gradient outer products, as dense GEMMs (rocBLAS sgemm, fp32) plus
+ * fused element-wise kernels, chunked over chunk_rows rows.
+ * d_params / d_grad: flat flax order [K_1 (d x W), b_1, K_2 (W x W), b_2, ..., K_o (W x out), b_o]
+ * (pdeinv_mlp_param_count floats). d_acc [PDEINV_GMM_NACC] and d_grad are ACCUMULATED (+=): zero
+ * them first. pdeinv_kfp_terms_finalize turns (acc, grad) into the PDEINV_KFP_* slots.
+ * --------------------------------------------------------------------------------------- */
+typedef struct {
+  int32_t dim;            /* d */
+  int32_t n_layers;       /* hidden layers L >= 1 (neural_network.layers) */
+  int32_t width;          /* hidden width W (neural_network.hidden_dim) */
+  int32_t out_features;   /* 40 in the reference */
+  int32_t true_kind;      /* PDEINV_POT_QUADRATIC (tilde_F, d*d) or PDEINV_POT_GMM (mus, K*d) */
+  int32_t n_centers_true;
+  float sigma_true;
+  const float* true_params; /* HOST */
+  float gamma;
+  float c_nabla, c_hess, c_fric, c_true, c_init, c_term;
+  int64_t chunk_rows;     /* rows per GEMM chunk (workspace grows with it); 0 => 2^18 */
+} pdeinv_kfp_mlp_desc;
+int64_t pdeinv_mlp_param_count(int32_t dim, int32_t n_layers, int32_t width, int32_t out_features);
+size_t pdeinv_residual_kfp_mlp_workspace_bytes(const pdeinv_kfp_mlp_desc* desc);
+int pdeinv_residual_kfp_mlp(const pdeinv_kfp_mlp_desc* desc, const float* d_init, int64_t n_init,
+                            int64_t ld_init, const float* d_term, int64_t n_term, int64_t ld_term,
+                            const float* d_0T, int64_t n_0T, int64_t ld_0T, const float* d_params,
+                            void* d_workspace, double* d_acc, float* d_grad, void* stream);
+int pdeinv_kfp_terms_finalize(const double* d_acc, const float* d_grad, int64_t n_grad, float gamma,
+                              float* d_out, void* stream);
+
+/* ---------------------------------------------------------------------------------------
  * GMM potential value and gradient over a batch — GMMPotential.value/.gradient
  * (core/potential.py:48-61; V_true_fn of …_GMM.py:94-102). Either output nullable.
  * --------------------------------------------------------------------------------------- */

@@ -495,3 +495,134 @@ def kmv_from_moments(K, b, x, v, tau, cfg):
     G += -2 * Mvv
     loss = nabla - 2 * hess + 2 * value + true
     return loss, gt, G + G.T, gb
+
+
+# --------------------------------------------------------------------------------------
+# non-parametric hypothesis V_hypothesis (core/model.py:32-62): Dense(W) x L, tanh, Dense(40), sum y^2
+# --------------------------------------------------------------------------------------
+def mlp_forward_terms(params, x, v):
+    """Per sample: V, g = grad_x V (reverse), Vd = grad V . v, Vdd = v^T Hess V v (Taylor mode).
+    params = [(K_1, b_1), ..., (K_L, b_L), (K_o, b_o)] with flax kernels [in, out]."""
+    x = np.asarray(x, np.float64); v = np.asarray(v, np.float64)
+    h, hd, hdd = x, v, np.zeros_like(x)
+    cache = []
+    for K, b in params[:-1]:
+        z, zd, zdd = h @ K + b, hd @ K, hdd @ K
+        h = np.tanh(z)
+        s1 = 1 - h * h
+        s2 = -2 * h * s1
+        hd, hdd = s1 * zd, s1 * zdd + s2 * zd * zd
+        cache.append(s1)
+    Ko, bo = params[-1]
+    y, yd, ydd = h @ Ko + bo, hd @ Ko, hdd @ Ko
+    V = np.sum(y * y, -1)
+    Vd = 2 * np.sum(y * yd, -1)
+    Vdd = 2 * np.sum(yd * yd + y * ydd, -1)
+    a = (2 * y) @ Ko.T
+    for (K, _), s1 in zip(reversed(params[:-1]), reversed(cache)):
+        a = (s1 * a) @ K.T
+    return V, a, Vd, Vdd
+
+
+def kfp_mlp_loss(params, z_init, z_term, z_0T, grad_true, gamma, T):
+    """loss_fn (kinetic_fokker_planck.py:33-50) / loss_ground_truth_fn (:52-58) for the MLP model;
+    grad_true(x) -> grad V*(x)."""
+    d = params[0][0].shape[0]
+    z_0T = np.asarray(z_0T, np.float64)
+    x0, v0 = z_0T[:, :d], z_0T[:, d:]
+    _, g, Vd, Vdd = mlp_forward_terms(params, x0, v0)
+    gt = grad_true(x0)
+    parts = dict(nabla=np.mean(np.sum(g * g, -1)), hessian=np.mean(Vdd), friction=gamma * np.mean(Vd),
+                 nabla_true=np.mean(np.sum(gt * gt, -1)))
+    for name, z in (("initial", z_init), ("terminal", z_term)):
+        z = np.asarray(z, np.float64)
+        parts[name] = np.mean(mlp_forward_terms(params, z[:, :d], z[:, d:])[2]) if len(z) else 0.0
+    loss = (parts["nabla"] - 2 * parts["hessian"] + 2 * parts["friction"] + parts["nabla_true"]
+            + (-2 * parts["initial"] + 2 * parts["terminal"]) / T)
+    return loss, np.mean(np.sum((gt - g) ** 2, -1)), parts
+
+
+def mlp_flat(params):
+    return np.concatenate([np.concatenate([K.ravel(), b.ravel()]) for K, b in params])
+
+
+def mlp_unflat(flat, dims):
+    """dims = [d, W_1, ..., W_L, out]."""
+    out, o = [], 0
+    for i in range(len(dims) - 1):
+        K = flat[o:o + dims[i] * dims[i + 1]].reshape(dims[i], dims[i + 1]); o += dims[i] * dims[i + 1]
+        b = flat[o:o + dims[i + 1]]; o += dims[i + 1]
+        out.append((K, b))
+    return out
+
+
+def kfp_mlp_grad_analytic(params, z_init, z_term, z_0T, gamma, T):
+    """d loss / d params for the MLP model by the adjoint mlp.hip implements: Taylor forward
+    (h, hd, hdd), the grad_x reverse chain (a, zeta), its forward-mode adjoint (abar, zetabar),
+    then reverse over the three forward streams; weight gradients are sums of outer products."""
+    d = params[0][0].shape[0]
+    L = len(params) - 1
+    rows, coefs = [], []
+    for z, c in ((z_0T, (1.0 / len(z_0T), -2.0 / len(z_0T), 2 * gamma / len(z_0T))),
+                 (z_init, (0.0, 0.0, -2.0 / (T * max(len(z_init), 1)))),
+                 (z_term, (0.0, 0.0, 2.0 / (T * max(len(z_term), 1))))):
+        z = np.asarray(z, np.float64)
+        if len(z):
+            rows.append(z)
+            coefs.append(np.tile(np.asarray(c)[None], (len(z), 1)))
+    Z = np.concatenate(rows)
+    C = np.concatenate(coefs)
+    c1, c2, c3 = C[:, :1], C[:, 1:2], C[:, 2:3]
+    x, v = Z[:, :d], Z[:, d:]
+    A = [(x, v, np.zeros_like(x))]          # (h, hd, hdd) per layer input
+    Zs, S = [], []
+    for K, b in params[:-1]:
+        h, hd, hdd = A[-1]
+        z, zd, zdd = h @ K + b, hd @ K, hdd @ K
+        hn = np.tanh(z)
+        s1 = 1 - hn * hn
+        s2 = -2 * hn * s1
+        s3 = -2 * s1 * s1 - 2 * hn * s2
+        A.append((hn, s1 * zd, s1 * zdd + s2 * zd * zd))
+        Zs.append((zd, zdd))
+        S.append((s1, s2, s3))
+    Ko, bo = params[-1]
+    hL, hdL, hddL = A[-1]
+    y, yd, ydd = hL @ Ko + bo, hdL @ Ko, hddL @ Ko
+    # grad_x chain
+    u = 2 * y
+    a_l = [None] * (L + 1)
+    zeta = [None] * (L + 1)
+    a = u @ Ko.T
+    for l in range(L, 0, -1):
+        a_l[l] = a
+        zeta[l] = S[l - 1][0] * a
+        a = zeta[l] @ params[l - 1][0].T
+    g = a
+    # forward-mode adjoint of the grad chain
+    abar = [None] * (L + 1)
+    zetabar = [None] * (L + 1)
+    abar[0] = 2 * c1 * g
+    for l in range(1, L + 1):
+        zetabar[l] = abar[l - 1] @ params[l - 1][0]
+        abar[l] = S[l - 1][0] * zetabar[l]
+    ubar = abar[L] @ Ko
+    ybar = 2 * c3 * yd + 2 * c2 * ydd + 2 * ubar
+    ydbar = 2 * c3 * y + 4 * c2 * yd
+    yddbar = 2 * c2 * y
+    grads = [None] * (L + 1)
+    gKo = hL.T @ ybar + hdL.T @ ydbar + hddL.T @ yddbar + abar[L].T @ u
+    grads[L] = (gKo, ybar.sum(0))
+    hb, hdb, hddb = ybar @ Ko.T, ydbar @ Ko.T, yddbar @ Ko.T
+    for l in range(L, 0, -1):
+        s1, s2, s3 = S[l - 1]
+        zd, zdd = Zs[l - 1]
+        zb = s1 * hb + s2 * zd * hdb + (s2 * zdd + s3 * zd * zd) * hddb + s2 * a_l[l] * zetabar[l]
+        zdb = s1 * hdb + 2 * s2 * zd * hddb
+        zddb = s1 * hddb
+        hp, hdp, hddp = A[l - 1]
+        K = params[l - 1][0]
+        gK = hp.T @ zb + hdp.T @ zdb + hddp.T @ zddb + abar[l - 1].T @ zeta[l]
+        grads[l - 1] = (gK, zb.sum(0))
+        hb, hdb, hddb = zb @ K.T, zdb @ K.T, zddb @ K.T
+    return grads

@@ -104,6 +104,23 @@ class V_hypothesis:  # noqa: N801 - reference name
         return {"params": {f"layers_{i}": _dense_params(rng, dims[i], dims[i + 1], 2.0, device)
                            for i in range(len(dims) - 1)}}
 
+    def dims(self, d: int):
+        return [d] + self.hidden_dims + [self.out_features]
+
+    def flat(self, params) -> torch.Tensor:
+        p = params["params"]
+        return torch.cat([t for i in range(len(p)) for t in (p[f"layers_{i}"]["kernel"].reshape(-1),
+                                                              p[f"layers_{i}"]["bias"])]).contiguous()
+
+    def unflat(self, flat: torch.Tensor, d: int):
+        dims = self.dims(d)
+        out, o = {}, 0
+        for i in range(len(dims) - 1):
+            k = flat[o:o + dims[i] * dims[i + 1]].view(dims[i], dims[i + 1]); o += dims[i] * dims[i + 1]
+            b = flat[o:o + dims[i + 1]]; o += dims[i + 1]
+            out[f"layers_{i}"] = {"kernel": k, "bias": b}
+        return {"params": out}
+
     def apply(self, params, y: torch.Tensor):
         h = y
         n = len(params["params"])

@@ -1,0 +1,488 @@
+// mlp.hip — KFP residual for the non-parametric hypothesis V_hypothesis (gfx950).
+//
+// V(x) = sum_o y_o^2, y = h_L K_o + b_o, h_l = tanh(h_{l-1} K_l + b_l), h_0 = x   (core/model.py:32-62)
+// Per sample the residual (kinetic_fokker_planck.py:33-58) needs g = grad_x V, V' = g.v and
+// V'' = v^T Hess V v, and the trainer needs d loss / d theta (jax.value_and_grad, :60-61).
+// Batched over samples this is a chain of dense GEMMs — [rows x W] x [W x W] — plus per-element
+// Taylor / adjoint algebra:
+//   F1  Taylor-mode forward, three streams (h, h', h'') through every layer        3P MACs / sample
+//   R1  reverse chain of grad_x V (a_l, zeta_l)                                     1P
+//   F2  forward-mode adjoint of that chain (abar_l, zetabar_l)                      1P
+//   R2  reverse over the three forward streams                                      3P
+//   G   weight gradients: sums of outer products over samples (4 stream pairs)      4P
+// (24P FLOP per sample). The GEMMs are plain library GEMMs (rocBLAS sgemm, fp32
+// on the MFMA f32 path); every element-wise step, the per-row loss terms and the reductions are
+// the kernels below. The derivation is oracle/numpy_ref.py kfp_mlp_grad_analytic, checked against
+// central finite differences.
+#include <rocblas/rocblas.h>
+
+#include <math.h>
+
+#include <mutex>
+
+#include "common.h"
+
+namespace pdeinv {
+
+// ---- rocBLAS plumbing ------------------------------------------------------------------------
+static rocblas_handle blas_handle(int device) {
+  static std::mutex mu;
+  static rocblas_handle handles[64] = {};
+  std::lock_guard<std::mutex> lock(mu);
+  if (device < 0 || device >= 64) return nullptr;
+  if (!handles[device]) {
+    if (rocblas_create_handle(&handles[device]) != rocblas_status_success) handles[device] = nullptr;
+  }
+  return handles[device];
+}
+
+struct Blas {
+  rocblas_handle h;
+  int status = 0;
+  // row-major C[R x n_out] = A[R x n_in] . K[n_in x n_out]
+  void fwd(const float* A, const float* K, float* C, int64_t R, int n_in, int n_out) {
+    const float one = 1.f, zero = 0.f;
+    if (rocblas_sgemm(h, rocblas_operation_none, rocblas_operation_none, n_out, (rocblas_int)R, n_in, &one, K,
+                      n_out, A, n_in, &zero, C, n_out) != rocblas_status_success)
+      status = 1;
+  }
+  // row-major C[R x n_in] = A[R x n_out] . K^T
+  void bwd(const float* A, const float* K, float* C, int64_t R, int n_in, int n_out) {
+    const float one = 1.f, zero = 0.f;
+    if (rocblas_sgemm(h, rocblas_operation_transpose, rocblas_operation_none, n_in, (rocblas_int)R, n_out, &one, K,
+                      n_out, A, n_out, &zero, C, n_in) != rocblas_status_success)
+      status = 1;
+  }
+  // Kbar[n_in x n_out] += A[R x n_in]^T . B[R x n_out]
+  void wgrad(const float* A, const float* B, float* Kbar, int64_t R, int n_in, int n_out) {
+    const float one = 1.f;
+    if (rocblas_sgemm(h, rocblas_operation_none, rocblas_operation_transpose, n_out, n_in, (rocblas_int)R, &one, B,
+                      n_out, A, n_in, &one, Kbar, n_out) != rocblas_status_success)
+      status = 1;
+  }
+  // bbar[n] += sum over the R rows of B[R x n]
+  void colsum(const float* B, const float* ones, float* bbar, int64_t R, int n) {
+    const float one = 1.f;
+    if (rocblas_sgemv(h, rocblas_operation_none, n, (rocblas_int)R, &one, B, n, ones, 1, &one, bbar, 1) !=
+        rocblas_status_success)
+      status = 1;
+  }
+};
+
+// ---- element-wise kernels --------------------------------------------------------------------
+__device__ __forceinline__ float fast_tanh(float z) {
+  // tanh(z) = 1 - 2 / (exp(2z) + 1); exp2 on the hardware unit, saturates cleanly at +-1
+  const float e = __builtin_amdgcn_exp2f(2.8853900817779268f * z);
+  return 1.f - 2.f * __builtin_amdgcn_rcpf(e + 1.f);
+}
+
+// F1: z (+bias), z', z'' -> h = tanh z, h' = s1 z', h'' = s1 z'' + s2 z'^2
+__global__ void mlp_act_fwd(const float* __restrict__ Z, float* __restrict__ A, const float* __restrict__ bias,
+                            int64_t R, int n) {
+  const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t S = R * n;
+  if (e >= S) return;
+  const int j = (int)(e % n);
+  const float z = Z[e] + bias[j], zd = Z[S + e], zdd = Z[2 * S + e];
+  const float h = fast_tanh(z);
+  const float s1 = 1.f - h * h, s2 = -2.f * h * s1;
+  A[e] = h;
+  A[S + e] = s1 * zd;
+  A[2 * S + e] = fmaf(s1, zdd, s2 * zd * zd);
+}
+
+// output layer: y (+bias) stored back; u = 2y (seed of the grad_x chain); V' = 2 y.y', V'' = 2(y'.y' + y.y'')
+__global__ void mlp_out(float* __restrict__ Y, const float* __restrict__ bias, float* __restrict__ YB,
+                        float2* __restrict__ terms, int64_t R, int O) {
+  const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (r >= R) return;
+  const int64_t S = R * O;
+  float vd = 0.f, vdd = 0.f;
+  for (int o = 0; o < O; ++o) {
+    const int64_t e = r * O + o;
+    const float y = Y[e] + bias[o], yd = Y[S + e], ydd = Y[2 * S + e];
+    Y[e] = y;
+    YB[3 * S + e] = 2.f * y;
+    vd = fmaf(y, yd, vd);
+    vdd = fmaf(yd, yd, fmaf(y, ydd, vdd));
+  }
+  terms[r] = make_float2(2.f * vd, 2.f * vdd);
+}
+
+// R1: zeta = tanh'(z) * a   (a = GEMM output, kept for R2)
+__global__ void mlp_gchain(const float* __restrict__ a, const float* __restrict__ h, float* __restrict__ zeta,
+                           int64_t S) {
+  const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (e >= S) return;
+  const float hv = h[e];
+  zeta[e] = (1.f - hv * hv) * a[e];
+}
+
+// F2: abar = tanh'(z) * zetabar
+__global__ void mlp_gadj(const float* __restrict__ zetabar, const float* __restrict__ h, float* __restrict__ abar,
+                         int64_t S) {
+  const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (e >= S) return;
+  const float hv = h[e];
+  abar[e] = (1.f - hv * hv) * zetabar[e];
+}
+
+struct MlpLossArgs {
+  int d, set, true_kind, KT;
+  float c1, c2, c3, c_true, inv_n;
+  float s2t, l2st;
+  float tp[PDEINV_MAX_PARAMS];  // tilde_F [d*d] or true GMM centres [K*d]
+};
+
+// per row: T1 = |g|^2, T2 = V'', T3 = V', true-potential terms (0T rows); seeds abar_0 = 2 c1 g;
+// block partial sums of the 8 accumulator slots of pdeinv.h (PDEINV_GMM_ACC_*).
+template <int D>
+__global__ __launch_bounds__(kBlock) void mlp_loss(MlpLossArgs a, const float* __restrict__ G,
+                                                   const float* __restrict__ X, int64_t ldx,
+                                                   const float2* __restrict__ terms, float* __restrict__ abar0,
+                                                   int64_t R, float* __restrict__ partials) {
+  float acc[PDEINV_GMM_NACC] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x; r < R; r += stride) {
+    float g[D], x[D], T1 = 0.f;
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      g[i] = G[r * D + i];
+      x[i] = X[r * ldx + i];
+      T1 = fmaf(g[i], g[i], T1);
+      abar0[r * D + i] = 2.f * a.c1 * g[i];
+    }
+    const float2 t = terms[r];
+    const float T2 = t.y, T3 = t.x;
+    acc[PDEINV_GMM_ACC_LOSS] += a.c1 * T1 + a.c2 * T2 + a.c3 * T3;
+    if (a.set == 0) {
+      float gt[D];
+      if (a.true_kind == PDEINV_POT_QUADRATIC) {
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+          float s = 0.f;
+#pragma unroll
+          for (int j = 0; j < D; ++j) s = fmaf(a.tp[i * D + j], x[j], s);
+          gt[i] = s;
+        }
+      } else {
+        float w[16], amax = -INFINITY;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          if (k < a.KT) {
+            float d2 = 0.f;
+#pragma unroll
+            for (int i = 0; i < D; ++i) {
+              const float u = x[i] - a.tp[k * D + i];
+              d2 = fmaf(u, u, d2);
+            }
+            w[k] = -0.5f * d2 * a.l2st;
+            amax = fmaxf(amax, w[k]);
+          }
+        }
+        float den = 0.f, m[D];
+#pragma unroll
+        for (int i = 0; i < D; ++i) m[i] = 0.f;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          if (k < a.KT) {
+            const float e = __builtin_amdgcn_exp2f(w[k] - amax);
+            den += e;
+#pragma unroll
+            for (int i = 0; i < D; ++i) m[i] = fmaf(e, a.tp[k * D + i], m[i]);
+          }
+        }
+        const float inv = 1.f / den;
+#pragma unroll
+        for (int i = 0; i < D; ++i) gt[i] = a.s2t * (x[i] - m[i] * inv);
+      }
+      float Tt = 0.f, Tgt = 0.f;
+#pragma unroll
+      for (int i = 0; i < D; ++i) {
+        Tt = fmaf(gt[i], gt[i], Tt);
+        Tgt = fmaf(gt[i] - g[i], gt[i] - g[i], Tgt);
+      }
+      acc[PDEINV_GMM_ACC_LOSS] += a.c_true * Tt;
+      acc[PDEINV_GMM_ACC_LOSS_GT] += a.c_true * Tgt;
+      acc[PDEINV_GMM_ACC_NABLA] += a.c_true * T1;
+      acc[PDEINV_GMM_ACC_HESSIAN] += a.c_true * T2;
+      acc[PDEINV_GMM_ACC_FRICTION] += a.c_true * T3;
+      acc[PDEINV_GMM_ACC_NABLA_TRUE] += a.c_true * Tt;
+    } else if (a.set == 1) {
+      acc[PDEINV_GMM_ACC_INITIAL] += a.inv_n * T3;
+    } else {
+      acc[PDEINV_GMM_ACC_TERMINAL] += a.inv_n * T3;
+    }
+  }
+  __shared__ float lds[kWavesPerBlock * PDEINV_GMM_NACC];
+  block_reduce_to_slab(acc, PDEINV_GMM_NACC, lds, partials, blockIdx.x, gridDim.x);
+}
+
+// seeds of the reverse sweep over the forward streams:
+//   ybar = 2 c3 y' + 2 c2 y'' + 2 ubar,  y'bar = 2 c3 y + 4 c2 y',  y''bar = 2 c2 y
+__global__ void mlp_seeds(const float* __restrict__ Y, const float* __restrict__ UB, float* __restrict__ YB,
+                          float c2, float c3, int64_t S) {
+  const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (e >= S) return;
+  const float y = Y[e], yd = Y[S + e], ydd = Y[2 * S + e];
+  YB[e] = 2.f * c3 * yd + 2.f * c2 * ydd + 2.f * UB[e];
+  YB[S + e] = 2.f * c3 * y + 4.f * c2 * yd;
+  YB[2 * S + e] = 2.f * c2 * y;
+}
+
+// R2 element-wise step through tanh (s1 = tanh', s2 = tanh'', s3 = tanh'''):
+//   zbar   = s1 hbar + s2 z' h'bar + (s2 z'' + s3 z'^2) h''bar + s2 a zetabar   (last: grad_x chain)
+//   z'bar  = s1 h'bar + 2 s2 z' h''bar ;   z''bar = s1 h''bar
+__global__ void mlp_act_bwd(const float* __restrict__ HB, const float* __restrict__ h, const float* __restrict__ Z,
+                            const float* __restrict__ aL, const float* __restrict__ zb, float* __restrict__ ZB,
+                            int64_t S) {
+  const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (e >= S) return;
+  const float hv = h[e];
+  const float s1 = 1.f - hv * hv, s2 = -2.f * hv * s1, s3 = -2.f * s1 * s1 - 2.f * hv * s2;
+  const float zd = Z[S + e], zdd = Z[2 * S + e];
+  const float hb = HB[e], hdb = HB[S + e], hddb = HB[2 * S + e];
+  ZB[e] = s1 * hb + s2 * zd * hdb + (s2 * zdd + s3 * zd * zd) * hddb + s2 * aL[e] * zb[e];
+  ZB[S + e] = s1 * hdb + 2.f * s2 * zd * hddb;
+  ZB[2 * S + e] = s1 * hddb;
+}
+
+// copy the (x, v) rows of a sample set into the stream-0 / stream-1 input planes of layer 1
+__global__ void mlp_load_rows(const float* __restrict__ z, int64_t ld, int d, float* __restrict__ A0, int64_t R) {
+  const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (e >= R * d) return;
+  const int64_t r = e / d;
+  const int i = (int)(e - r * d);
+  A0[e] = z[r * ld + i];
+  A0[R * d + e] = z[r * ld + d + i];
+}
+
+__global__ void fill_kernel(float* p, float v, int64_t n) {
+  const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (e < n) p[e] = v;
+}
+
+__global__ void slab_reduce_accum_kernel(const float* __restrict__ partials, int n_blocks,
+                                         double* __restrict__ out) {
+  const int c = blockIdx.x;
+  const float* col = partials + (int64_t)c * n_blocks;
+  double s = 0.0;
+  for (int b = threadIdx.x; b < n_blocks; b += kBlock) s += (double)col[b];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  __shared__ double w[kWavesPerBlock];
+  if ((threadIdx.x & 63) == 0) w[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) out[c] += w[0] + w[1] + w[2] + w[3];
+}
+
+__global__ void kfp_terms_finalize_kernel(const double* __restrict__ acc, const float* __restrict__ grad,
+                                          int64_t n_grad, float gamma, float* __restrict__ out) {
+  double s = 0.0;
+  for (int64_t k = threadIdx.x; k < n_grad; k += kBlock) s += (double)grad[k] * (double)grad[k];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  __shared__ double w[kWavesPerBlock];
+  if ((threadIdx.x & 63) == 0) w[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    out[PDEINV_KFP_LOSS] = (float)acc[PDEINV_GMM_ACC_LOSS];
+    out[PDEINV_KFP_LOSS_GT] = (float)acc[PDEINV_GMM_ACC_LOSS_GT];
+    out[PDEINV_KFP_GRAD_NORM] = (float)sqrt(w[0] + w[1] + w[2] + w[3]);
+    out[PDEINV_KFP_NABLA] = (float)acc[PDEINV_GMM_ACC_NABLA];
+    out[PDEINV_KFP_HESSIAN] = (float)acc[PDEINV_GMM_ACC_HESSIAN];
+    out[PDEINV_KFP_FRICTION] = (float)(gamma * acc[PDEINV_GMM_ACC_FRICTION]);
+    out[PDEINV_KFP_NABLA_TRUE] = (float)acc[PDEINV_GMM_ACC_NABLA_TRUE];
+    out[PDEINV_KFP_INITIAL] = (float)acc[PDEINV_GMM_ACC_INITIAL];
+    out[PDEINV_KFP_TERMINAL] = (float)acc[PDEINV_GMM_ACC_TERMINAL];
+  }
+}
+
+// ---- workspace plan -------------------------------------------------------------------------
+constexpr int kLossGrid = 512;
+
+struct MlpPlan {
+  int d, L, W, O;
+  int64_t Bc;
+  size_t off_A0, off_Y, off_YB, off_UB, off_G, off_ones, off_terms, off_part, total;
+  size_t off_layer0, layer_stride;  // per hidden layer: A(4) Z(3) ZB(4) HB(3) aL(1) zb(1) planes of Bc*W
+};
+
+static MlpPlan make_plan(const pdeinv_kfp_mlp_desc* d) {
+  MlpPlan p{};
+  p.d = d->dim; p.L = d->n_layers; p.W = d->width; p.O = d->out_features;
+  p.Bc = d->chunk_rows > 0 ? d->chunk_rows : (1 << 18);
+  size_t o = 0;
+  auto take = [&](size_t floats) { const size_t at = o; o += (floats + 63) & ~(size_t)63; return at; };
+  p.off_A0 = take(4 * p.Bc * p.d);
+  p.off_Y = take(3 * p.Bc * p.O);
+  p.off_YB = take(4 * p.Bc * p.O);
+  p.off_UB = take(p.Bc * p.O);
+  p.off_G = take(p.Bc * p.d);
+  p.off_ones = take(p.Bc);
+  p.off_terms = take(2 * p.Bc);
+  p.off_part = take((size_t)PDEINV_GMM_NACC * kLossGrid);
+  p.layer_stride = 16 * p.Bc * p.W;
+  p.off_layer0 = take(p.layer_stride * p.L);
+  p.total = o * sizeof(float);
+  return p;
+}
+
+}  // namespace pdeinv
+
+using namespace pdeinv;
+
+extern "C" size_t pdeinv_residual_kfp_mlp_workspace_bytes(const pdeinv_kfp_mlp_desc* d) {
+  if (!d || d->dim < 1 || d->n_layers < 1 || d->width < 1 || d->out_features < 1) return 0;
+  return make_plan(d).total;
+}
+
+extern "C" int64_t pdeinv_mlp_param_count(int32_t dim, int32_t n_layers, int32_t width, int32_t out_features) {
+  int64_t n = (int64_t)dim * width + width;
+  for (int l = 1; l < n_layers; ++l) n += (int64_t)width * width + width;
+  return n + (int64_t)width * out_features + out_features;
+}
+
+extern "C" int pdeinv_residual_kfp_mlp(const pdeinv_kfp_mlp_desc* d, const float* zi, int64_t ni, int64_t ldi,
+                                       const float* zt, int64_t nt, int64_t ldt, const float* z0, int64_t n0,
+                                       int64_t ld0, const float* params, void* ws, double* acc, float* grad,
+                                       void* stream) {
+  PDEINV_REQUIRE(d != nullptr, PDEINV_ERR_INVALID, "kfp_mlp: null descriptor");
+  const int D = d->dim;
+  PDEINV_REQUIRE(D >= 1 && D <= 16, PDEINV_ERR_UNSUPPORTED, "kfp_mlp: dim must be in [1, 16]");
+  PDEINV_REQUIRE(d->n_layers >= 1 && d->width >= 1 && d->out_features >= 1, PDEINV_ERR_INVALID,
+                 "kfp_mlp: need n_layers, width, out_features >= 1");
+  PDEINV_REQUIRE(d->true_kind == PDEINV_POT_QUADRATIC || d->true_kind == PDEINV_POT_GMM, PDEINV_ERR_UNSUPPORTED,
+                 "kfp_mlp: true potential must be QUADRATIC or GMM");
+  PDEINV_REQUIRE(d->true_params != nullptr, PDEINV_ERR_INVALID, "kfp_mlp: true_params is null");
+  PDEINV_REQUIRE(d->true_kind != PDEINV_POT_GMM || (d->n_centers_true >= 1 && d->n_centers_true <= 16 &&
+                                                   d->n_centers_true * D <= PDEINV_MAX_PARAMS && d->sigma_true > 0.f),
+                 PDEINV_ERR_UNSUPPORTED, "kfp_mlp: true GMM needs 1..16 centres");
+  PDEINV_REQUIRE(n0 >= 1 && ni >= 0 && nt >= 0, PDEINV_ERR_INVALID, "kfp_mlp: 0T set must be non-empty");
+  PDEINV_REQUIRE(params && ws && acc && grad && z0 && (ni == 0 || zi) && (nt == 0 || zt), PDEINV_ERR_INVALID,
+                 "kfp_mlp: null pointer");
+  const MlpPlan p = make_plan(d);
+  PDEINV_REQUIRE(p.Bc <= (1 << 26), PDEINV_ERR_INVALID, "kfp_mlp: chunk_rows too large");
+  hipStream_t st = (hipStream_t)stream;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return fail(PDEINV_ERR_HIP, "kfp_mlp: hipGetDevice failed");
+  Blas blas{blas_handle(dev)};
+  if (!blas.h) return fail(PDEINV_ERR_HIP, "kfp_mlp: rocblas_create_handle failed");
+  if (rocblas_set_stream(blas.h, st) != rocblas_status_success) return fail(PDEINV_ERR_HIP, "kfp_mlp: rocblas_set_stream");
+
+  float* w = (float*)ws;
+  const int W = p.W, O = p.O, L = p.L;
+  // parameter offsets (flax order: K_1, b_1, ..., K_L, b_L, K_o, b_o)
+  int64_t poff[18], boff[18];
+  int64_t o = 0;
+  for (int l = 0; l <= L; ++l) {
+    const int n_in = (l == 0) ? D : W, n_out = (l == L) ? O : W;
+    poff[l] = o; o += (int64_t)n_in * n_out;
+    boff[l] = o; o += n_out;
+  }
+  PDEINV_REQUIRE(L <= 16, PDEINV_ERR_UNSUPPORTED, "kfp_mlp: at most 16 hidden layers");
+  float* A0 = w + p.off_A0;
+  float* Y = w + p.off_Y;
+  float* YB = w + p.off_YB;
+  float* UB = w + p.off_UB;
+  float* G = w + p.off_G;
+  float* ones = w + p.off_ones;
+  float2* terms = (float2*)(w + p.off_terms);
+  float* part = w + p.off_part;
+  // planes per hidden layer l: A 0-3, Z 4-6, ZB 7-10, HB 11-13, aL 14, zb 15. Inside a chunk of R rows
+  // the planes are packed at stride R*W so that consecutive streams form one [k*R x W] GEMM operand.
+  int64_t R = 0;
+  auto layer = [&](int l, int plane) { return w + p.off_layer0 + p.layer_stride * (l - 1) + (size_t)plane * R * W; };
+  hipLaunchKernelGGL(fill_kernel, dim3(grid_for(p.Bc)), dim3(kBlock), 0, st, ones, 1.f, p.Bc);
+
+  MlpLossArgs la{};
+  la.d = D;
+  la.true_kind = d->true_kind;
+  la.KT = d->n_centers_true;
+  la.s2t = d->sigma_true > 0.f ? 1.f / (d->sigma_true * d->sigma_true) : 1.f;
+  la.l2st = la.s2t * 1.4426950408889634f;
+  const int ntp = d->true_kind == PDEINV_POT_QUADRATIC ? D * D : d->n_centers_true * D;
+  for (int k = 0; k < ntp; ++k) la.tp[k] = d->true_params[k];
+
+  struct Set { const float* z; int64_t n, ld; int id; float c1, c2, c3; } sets[3] = {
+      {z0, n0, ld0 ? ld0 : 2 * D, 0, d->c_nabla, d->c_hess, d->c_fric},
+      {zi, ni, ldi ? ldi : 2 * D, 1, 0.f, 0.f, d->c_init},
+      {zt, nt, ldt ? ldt : 2 * D, 2, 0.f, 0.f, d->c_term}};
+  for (const Set& s : sets) {
+    PDEINV_REQUIRE(s.n == 0 || s.ld >= 2 * D, PDEINV_ERR_INVALID, "kfp_mlp: row stride < 2*dim");
+    for (int64_t r0 = 0; r0 < s.n; r0 += p.Bc) {
+      R = (s.n - r0) < p.Bc ? (s.n - r0) : p.Bc;
+      const float* zr = s.z + r0 * s.ld;
+      const int64_t SD = R * D, SW = R * W, SO = R * O;
+      // ---- F1: Taylor-mode forward --------------------------------------------------------
+      hipLaunchKernelGGL(mlp_load_rows, dim3(grid_for(SD)), dim3(kBlock), 0, st, zr, s.ld, D, A0, R);
+      if (hipMemsetAsync(A0 + 2 * SD, 0, sizeof(float) * SD, st) != hipSuccess) return fail(PDEINV_ERR_HIP, "memset");
+      // A planes are [4][R][n] within a chunk buffer sized for Bc rows: streams packed at stride R*n
+      for (int l = 1; l <= L; ++l) {
+        const int n_in = (l == 1) ? D : W;
+        const float* Ain = (l == 1) ? A0 : layer(l - 1, 0);
+        float* Z = layer(l, 4);
+        // three streams packed contiguously: one GEMM with 3R rows
+        blas.fwd(Ain, params + poff[l - 1], Z, 3 * R, n_in, W);
+        hipLaunchKernelGGL(mlp_act_fwd, dim3(grid_for(SW)), dim3(kBlock), 0, st, Z, layer(l, 0), params + boff[l - 1],
+                           R, W);
+      }
+      blas.fwd(layer(L, 0), params + poff[L], Y, 3 * R, W, O);
+      hipLaunchKernelGGL(mlp_out, dim3(grid_for(R)), dim3(kBlock), 0, st, Y, params + boff[L], YB, terms, R, O);
+      // ---- R1: grad_x chain ---------------------------------------------------------------
+      blas.bwd(YB + 3 * SO, params + poff[L], layer(L, 14), R, W, O);  // a_L = u K_o^T
+      for (int l = L; l >= 1; --l) {
+        hipLaunchKernelGGL(mlp_gchain, dim3(grid_for(SW)), dim3(kBlock), 0, st, layer(l, 14), layer(l, 0),
+                           layer(l, 10), SW);  // zeta_l -> ZB plane 3
+        if (l > 1) blas.bwd(layer(l, 10), params + poff[l - 1], layer(l - 1, 14), R, W, W);
+        else blas.bwd(layer(1, 10), params + poff[0], G, R, D, W);  // g = zeta_1 K_1^T
+      }
+      // ---- loss terms, seed abar_0 = 2 c1 g ------------------------------------------------
+      la.set = s.id; la.c1 = s.c1; la.c2 = s.c2; la.c3 = s.c3; la.c_true = d->c_true;
+      la.inv_n = 1.f / (float)s.n;
+      const int lg = grid_for(R) < kLossGrid ? grid_for(R) : kLossGrid;
+      switch (D) {
+#define CASE(DD) case DD: hipLaunchKernelGGL(mlp_loss<DD>, dim3(lg), dim3(kBlock), 0, st, la, G, zr, s.ld, terms, A0 + 3 * SD, R, part); break;
+        CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) CASE(10) CASE(12) CASE(16)
+#undef CASE
+        default:
+          return fail(PDEINV_ERR_UNSUPPORTED, "kfp_mlp: dim must be one of 1-8, 10, 12, 16");
+      }
+      hipLaunchKernelGGL(slab_reduce_accum_kernel, dim3(PDEINV_GMM_NACC), dim3(kBlock), 0, st, part, lg, acc);
+      // ---- F2: forward-mode adjoint of the grad_x chain --------------------------------------
+      for (int l = 1; l <= L; ++l) {
+        const float* abar_prev = (l == 1) ? A0 + 3 * SD : layer(l - 1, 3);
+        blas.fwd(abar_prev, params + poff[l - 1], layer(l, 15), R, (l == 1) ? D : W, W);  // zetabar_l
+        hipLaunchKernelGGL(mlp_gadj, dim3(grid_for(SW)), dim3(kBlock), 0, st, layer(l, 15), layer(l, 0),
+                           layer(l, 3), SW);  // abar_l -> A plane 3
+      }
+      blas.fwd(layer(L, 3), params + poff[L], UB, R, W, O);  // ubar = abar_L K_o
+      hipLaunchKernelGGL(mlp_seeds, dim3(grid_for(SO)), dim3(kBlock), 0, st, Y, UB, YB, s.c2, s.c3, SO);
+      // ---- R2 + G: reverse over the three forward streams, weight gradients ---------------------
+      blas.wgrad(layer(L, 0), YB, grad + poff[L], 4 * R, W, O);  // K_o += [h;h';h'';abar]^T [ybar;..;u]
+      blas.colsum(YB, ones, grad + boff[L], R, O);
+      blas.bwd(YB, params + poff[L], layer(L, 11), 3 * R, W, O);  // hbar streams of layer L
+      for (int l = L; l >= 1; --l) {
+        hipLaunchKernelGGL(mlp_act_bwd, dim3(grid_for(SW)), dim3(kBlock), 0, st, layer(l, 11), layer(l, 0),
+                           layer(l, 4), layer(l, 14), layer(l, 15), layer(l, 7), SW);
+        const int n_in = (l == 1) ? D : W;
+        const float* Ain = (l == 1) ? A0 : layer(l - 1, 0);
+        blas.wgrad(Ain, layer(l, 7), grad + poff[l - 1], 4 * R, n_in, W);
+        blas.colsum(layer(l, 7), ones, grad + boff[l - 1], R, W);
+        if (l > 1) blas.bwd(layer(l, 7), params + poff[l - 1], layer(l - 1, 11), 3 * R, W, W);
+      }
+      if (blas.status) return fail(PDEINV_ERR_HIP, "kfp_mlp: rocBLAS call failed");
+      int rc = check_launch("kfp_mlp kernels");
+      if (rc) return rc;
+    }
+  }
+  return PDEINV_OK;
+}
+
+extern "C" int pdeinv_kfp_terms_finalize(const double* acc, const float* grad, int64_t n_grad, float gamma,
+                                         float* out, void* stream) {
+  PDEINV_REQUIRE(acc && grad && out && n_grad >= 0, PDEINV_ERR_INVALID, "kfp_terms_finalize: bad arguments");
+  hipLaunchKernelGGL(kfp_terms_finalize_kernel, dim3(1), dim3(kBlock), 0, (hipStream_t)stream, acc, grad, n_grad,
+                     gamma, out);
+  return check_launch("kfp_terms_finalize_kernel");
+}

@@ -69,8 +69,22 @@ def value_and_grad_fn(forward_fn, params, data, rng, pde_instance):
             acc[native.GMM_NACC - 2:native.GMM_NACC] /= dist.world_size()
         out, grad = native.residual_kfp_gmm_finalize(desc, acc)
         return _result(out, {"params": {"mus": grad}})
-    raise NotImplementedError(f"no native KFP residual for model kind '{model.residual_kind}' yet "
-                              "(MLP hypothesis: SURVEY.md §8 a11, scheduled next)")
+    if model.residual_kind == "mlp":
+        d = pde_instance.dim
+        if "tilde_F" in ic:
+            true_kind, true_params, sigma_true = native.POT_QUADRATIC, ic["tilde_F"], 1.0
+        else:
+            true_kind, true_params, sigma_true = native.POT_GMM, pde_instance.potential.mus, pde_instance.potential.sigma
+        acc, grad = native.residual_kfp_mlp(model.dims(d), model.flat(params), data["initial"], data["terminal"],
+                                            data["0T"], true_kind=true_kind, true_params=true_params, gamma=gamma,
+                                            total_time=T, sigma_true=sigma_true, world_scale=1.0 / dist.world_size())
+        if dist.world_size() > 1:
+            both = dist.allreduce_sum(torch.cat([acc, grad.double()]))
+            acc, grad = both[: acc.numel()], both[acc.numel():].float()
+            acc[native.GMM_NACC - 2:native.GMM_NACC] /= dist.world_size()
+        out = native.kfp_terms_finalize(acc, grad, gamma)
+        return _result(out, model.unflat(grad, d))
+    raise NotImplementedError(f"no native KFP residual for model kind '{model.residual_kind}'")
 
 
 def recover_quadratic_drift(moments3, gamma: float, T: float, d: int):

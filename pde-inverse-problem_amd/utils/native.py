@@ -44,6 +44,8 @@ EXPORTED_SYMBOLS = (
     "pdeinv_philox_fill", "pdeinv_gather_subsample", "pdeinv_abi_version", "pdeinv_last_error",
     "pdeinv_runtime_version", "pdeinv_moments_batched_workspace_bytes", "pdeinv_moments_batched",
     "pdeinv_kmv_weights_workspace_bytes", "pdeinv_kmv_weights", "pdeinv_residual_kmv",
+    "pdeinv_mlp_param_count", "pdeinv_residual_kfp_mlp_workspace_bytes", "pdeinv_residual_kfp_mlp",
+    "pdeinv_kfp_terms_finalize",
 )
 
 
@@ -70,6 +72,15 @@ class KfpQuadDesc(ctypes.Structure):
 class KmvDesc(ctypes.Structure):
     _fields_ = [("dim", ctypes.c_int32), ("n_sets", ctypes.c_int32), ("gamma", ctypes.c_float),
                 ("tilde_F", ctypes.c_void_p)]
+
+
+class KfpMlpDesc(ctypes.Structure):
+    _fields_ = [("dim", ctypes.c_int32), ("n_layers", ctypes.c_int32), ("width", ctypes.c_int32),
+                ("out_features", ctypes.c_int32), ("true_kind", ctypes.c_int32), ("n_centers_true", ctypes.c_int32),
+                ("sigma_true", ctypes.c_float), ("true_params", ctypes.c_void_p), ("gamma", ctypes.c_float),
+                ("c_nabla", ctypes.c_float), ("c_hess", ctypes.c_float), ("c_fric", ctypes.c_float),
+                ("c_true", ctypes.c_float), ("c_init", ctypes.c_float), ("c_term", ctypes.c_float),
+                ("chunk_rows", ctypes.c_int64)]
 
 
 class KfpGmmDesc(ctypes.Structure):
@@ -128,6 +139,10 @@ def lib():
         "pdeinv_kmv_weights_workspace_bytes": (ctypes.c_size_t, [i64, i64, i32]),
         "pdeinv_kmv_weights": (i32, [i32, f32, P, P, i64, i64, i64, i64, P, P, P, P]),
         "pdeinv_residual_kmv": (i32, [P, P, P, P, P, P, P]),
+        "pdeinv_mlp_param_count": (i64, [i32, i32, i32, i32]),
+        "pdeinv_residual_kfp_mlp_workspace_bytes": (ctypes.c_size_t, [P]),
+        "pdeinv_residual_kfp_mlp": (i32, [P, P, i64, i64, P, i64, i64, P, i64, i64, P, P, P, P, P]),
+        "pdeinv_kfp_terms_finalize": (i32, [P, P, i64, f32, P, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -516,3 +531,48 @@ def mf_desc(N: int, d: int, n_steps: int, dt: float, gamma: float, A, *, seed: i
 def mf_workspace(desc: SdeDesc, device) -> torch.Tensor:
     nbytes = lib().pdeinv_mf_workspace_bytes(ctypes.byref(desc))
     return torch.empty(max(nbytes // 4, 1), device=device, dtype=torch.float32)
+
+
+# -----------------------------------------------------------------------------------------
+# non-parametric (MLP) KFP residual
+# -----------------------------------------------------------------------------------------
+def residual_kfp_mlp(dims, params_flat: torch.Tensor, z_init: torch.Tensor, z_term: torch.Tensor,
+                     z_0T: torch.Tensor, *, true_kind: int, true_params, gamma: float, total_time: float,
+                     sigma_true: float = 1.0, world_scale: float = 1.0, chunk_rows: int = 1 << 18):
+    """kinetic_fokker_planck.py:11-69 for V_hypothesis. dims = [d, W, ..., W, out] (equal hidden widths).
+    Returns (acc fp64 [8], grad fp32 [P]) — sums with the reference's loss weights."""
+    _require_gpu()
+    d, W, O = dims[0], dims[1], dims[-1]
+    L = len(dims) - 2
+    if L < 1 or any(w != W for w in dims[1:-1]):
+        raise NotImplementedError("MLP residual: hidden layers must share one width (V_hypothesis)")
+    P = lib().pdeinv_mlp_param_count(d, L, W, O)
+    if params_flat.numel() != P or not params_flat.is_contiguous():
+        raise ValueError(f"MLP residual: params must be a contiguous flat vector of {P} floats")
+    m = 2 * d
+    pi, ni, ldi = _rows(z_init, "initial", m) if z_init.shape[0] else (None, 0, m)
+    pt, nt, ldt = _rows(z_term, "terminal", m) if z_term.shape[0] else (None, 0, m)
+    p0, n0, ld0 = _rows(z_0T, "0T", m)
+    tp = _host_f32(true_params)
+    M = float(n0)
+    c = dict(c_nabla=1.0 / M, c_hess=-2.0 / M, c_fric=2.0 * gamma / M, c_true=1.0 / M,
+             c_init=(-2.0 / (total_time * ni)) if ni else 0.0, c_term=(2.0 / (total_time * nt)) if nt else 0.0)
+    c = {k: v * world_scale for k, v in c.items()}
+    desc = KfpMlpDesc(d, L, W, O, int(true_kind), int(tp.size // d) if true_kind == POT_GMM else 0,
+                      float(sigma_true), tp.ctypes.data_as(ctypes.c_void_p), float(gamma), c["c_nabla"],
+                      c["c_hess"], c["c_fric"], c["c_true"], c["c_init"], c["c_term"], int(chunk_rows))
+    nbytes = lib().pdeinv_residual_kfp_mlp_workspace_bytes(ctypes.byref(desc))
+    ws = torch.empty(nbytes // 4, device=z_0T.device, dtype=torch.float32)
+    acc = torch.zeros(GMM_NACC, device=z_0T.device, dtype=torch.float64)
+    grad = torch.zeros(P, device=z_0T.device, dtype=torch.float32)
+    _check(lib().pdeinv_residual_kfp_mlp(ctypes.byref(desc), pi, ni, ldi, pt, nt, ldt, p0, n0, ld0,
+                                         _dev(params_flat, "params"), _dev(ws, "ws"), _dev(acc, "acc", torch.float64),
+                                         _dev(grad, "grad"), stream_handle()), "pdeinv_residual_kfp_mlp")
+    return acc, grad
+
+
+def kfp_terms_finalize(acc: torch.Tensor, grad: torch.Tensor, gamma: float) -> torch.Tensor:
+    out = torch.empty(KFP_NOUT, device=acc.device, dtype=torch.float32)
+    _check(lib().pdeinv_kfp_terms_finalize(_dev(acc, "acc", torch.float64), _dev(grad, "grad"), grad.numel(),
+                                           float(gamma), _dev(out, "out"), stream_handle()), "pdeinv_kfp_terms_finalize")
+    return out

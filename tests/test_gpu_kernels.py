@@ -244,3 +244,33 @@ def test_sde_edge_cases(native):
                             dict(kind=native.POT_QUADRATIC, params=np.eye(11)), seed=1)
     with pytest.raises(ValueError):
         native.sde_simulate(_t(np.ones((3, 4))), 0, 0.1, 1.0, pot, seed=1)
+
+
+@pytest.mark.parametrize("dims,true_kind,chunk", [([2, 16, 16, 5], "gmm", 1000), ([4, 32, 32, 40], "quad", 1 << 18),
+                                                   ([8, 64, 64, 64, 40], "gmm", 777)])
+def test_residual_mlp_vs_restatement(native, dims, true_kind, chunk):
+    """V_hypothesis residual (value + d loss/d theta) vs the fp64 restatement whose adjoint is
+    FD-checked in tests/test_oracle.py. Multi-chunk paths exercised (chunk < rows)."""
+    rng = np.random.default_rng(len(dims) + dims[1])
+    d = dims[0]
+    flat = np.concatenate([np.concatenate([rng.standard_normal((dims[i], dims[i + 1])).ravel() * np.sqrt(1.0 / dims[i]),
+                                           0.1 * rng.standard_normal(dims[i + 1])]) for i in range(len(dims) - 1)])
+    P = nr.mlp_unflat(flat, dims)
+    zi, zt, z0 = (rng.standard_normal((m, 2 * d)).astype(np.float32) for m in (900, 700, 2500))
+    if true_kind == "gmm":
+        mus = nr.gmm_centres(d, 3)
+        kind, tp, gt = native.POT_GMM, mus, nr.grad_gmm(mus)
+    else:
+        F = nr.problem_constants(d)
+        kind, tp, gt = native.POT_QUADRATIC, F, nr.grad_quadratic(F)
+    acc, grad = native.residual_kfp_mlp(dims, _t(flat), _t(zi), _t(zt), _t(z0), true_kind=kind, true_params=tp,
+                                        gamma=0.5, total_time=2.0, chunk_rows=chunk)
+    out = native.kfp_terms_finalize(acc, grad, 0.5).cpu().numpy()
+    loss, loss_gt, parts = nr.kfp_mlp_loss(P, zi, zt, z0, gt, 0.5, 2.0)
+    g_ref = nr.mlp_flat(nr.kfp_mlp_grad_analytic(P, zi, zt, z0, 0.5, 2.0))
+    assert abs(out[0] - loss) < 1e-3 * (1 + abs(loss)), (out[0], loss)
+    assert abs(out[1] - loss_gt) < 1e-3 * (1 + abs(loss_gt))
+    assert abs(out[4] - parts["hessian"]) < 1e-3 * (1 + abs(parts["hessian"]))
+    g = grad.cpu().numpy()
+    assert np.max(np.abs(g - g_ref)) < 2e-3 * (1 + np.abs(g_ref).max()), np.max(np.abs(g - g_ref))
+    assert abs(out[2] - np.linalg.norm(g_ref)) < 2e-3 * (1 + np.linalg.norm(g_ref))

@@ -111,7 +111,7 @@ def test_adam_matches_optax_semantics():
 
 def _header_functions():
     txt = open(os.path.join(ROOT, "include", "pdeinv.h")).read()
-    return set(re.findall(r"^(?:int|size_t|const char\*)\s+(pdeinv_\w+)\(", txt, flags=re.M))
+    return set(re.findall(r"^(?:int|int64_t|size_t|const char\*)\s+(pdeinv_\w+)\(", txt, flags=re.M))
 
 
 def test_header_and_binding_agree():

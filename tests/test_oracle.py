@@ -208,3 +208,23 @@ def test_constants_recipe():
     for d in (2, 4, 8, 10):
         assert np.array_equal(problem_matrix(d), g[f"tilde_F_d{d}"])
         assert np.array_equal(nr.problem_constants(d), g[f"tilde_F_d{d}"])
+
+
+def test_mlp_taylor_terms_and_adjoint_vs_finite_differences():
+    """The MLP residual's per-sample terms (grad, V', V'') and the analytic parameter adjoint that
+    mlp.hip implements, against central differences (tiny net, fp64)."""
+    rng = np.random.default_rng(1)
+    dims = [2, 5, 4, 3]
+    flat = rng.standard_normal(sum(dims[i] * dims[i + 1] + dims[i + 1] for i in range(3))) * 0.6
+    P = nr.mlp_unflat(flat, dims)
+    x, v = rng.standard_normal((7, 2)), rng.standard_normal((7, 2))
+    V, g, Vd, Vdd = nr.mlp_forward_terms(P, x, v)
+    e = 1e-5
+    Vp, Vm = nr.mlp_forward_terms(P, x + e * v, v)[0], nr.mlp_forward_terms(P, x - e * v, v)[0]
+    assert np.allclose((Vp - Vm) / (2 * e), Vd, atol=1e-7)
+    assert np.allclose((Vp - 2 * V + Vm) / e ** 2, Vdd, atol=1e-3)
+    zi, zt, z0 = (rng.standard_normal((m, 4)) for m in (20, 15, 60))
+    gt = nr.grad_gmm(nr.gmm_centres(2, 3))
+    f = lambda fl: nr.kfp_mlp_loss(nr.mlp_unflat(fl, dims), zi, zt, z0, gt, 0.5, 2.0)[0]
+    ga = nr.mlp_flat(nr.kfp_mlp_grad_analytic(P, zi, zt, z0, 0.5, 2.0))
+    assert np.allclose(ga, nr.fd_grad(f, flat, eps=1e-6), rtol=1e-6, atol=1e-8)
