@@ -330,6 +330,11 @@ int pdeinv_gather_subsample(const float* d_traj, int64_t n_particles, int32_t n_
                             const int32_t* d_time_idx, int32_t n_time_sel, float* d_out,
                             void* stream);
 
+/* One uniformly drawn step per particle (Philox stream ctr.w = 0x20000000): out[p] =
+ * traj_tm[t_p, p], optional t_out[p] = t_p. The per-particle 0T batch of BASELINE config 5. */
+int pdeinv_gather_random_step(const float* d_traj, int64_t n_particles, int32_t n_steps, int32_t m,
+                              uint64_t seed, uint32_t ctr, float* d_out, int32_t* d_t_out, void* stream);
+
 int pdeinv_abi_version(void);
 const char* pdeinv_last_error(void);
 /* HIP runtime version the library is running against (detects a second HIP runtime). */

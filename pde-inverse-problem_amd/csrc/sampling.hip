@@ -72,9 +72,35 @@ __global__ void gather_kernel(const float* __restrict__ traj, int64_t N, int n_s
   for (int k = 0; k < m; ++k) dst[k] = src[k];
 }
 
+// One uniformly drawn trajectory row per particle: out[p] = traj[t_p, p], t_p = Philox(seed;
+// p, ctr) mod n_steps (the C5 residual batch). Coalesced: consecutive particles
+// read consecutive rows of their (different) time slabs.
+__global__ void gather_random_step_kernel(const float* __restrict__ traj, int64_t N, int n_steps, int m,
+                                          uint32_t k0, uint32_t k1, uint32_t ctr, float* __restrict__ out,
+                                          int32_t* __restrict__ t_out) {
+  const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (p >= N) return;
+  const uint4 b = philox4x32_10(make_uint4((uint32_t)p, (uint32_t)((uint64_t)p >> 32), ctr, 0x20000000u), k0, k1);
+  const int t = (int)(((uint64_t)b.x * (uint64_t)n_steps) >> 32);  // unbiased-enough range reduction
+  if (t_out) t_out[p] = t;
+  const float* src = traj + ((int64_t)t * N + p) * m;
+  float* dst = out + p * m;
+  for (int k = 0; k < m; ++k) dst[k] = src[k];
+}
+
 }  // namespace pdeinv
 
 using namespace pdeinv;
+
+extern "C" int pdeinv_gather_random_step(const float* traj, int64_t N, int32_t n_steps, int32_t m, uint64_t seed,
+                                         uint32_t ctr, float* out, int32_t* t_out, void* stream) {
+  PDEINV_REQUIRE(N >= 0 && n_steps >= 1 && m >= 1, PDEINV_ERR_INVALID, "gather_random_step: bad sizes");
+  if (N == 0) return PDEINV_OK;
+  PDEINV_REQUIRE(traj && out, PDEINV_ERR_INVALID, "gather_random_step: null pointer");
+  hipLaunchKernelGGL(gather_random_step_kernel, dim3(grid_for(N)), dim3(kBlock), 0, (hipStream_t)stream, traj, N,
+                     n_steps, m, (uint32_t)seed, (uint32_t)(seed >> 32), ctr, out, t_out);
+  return check_launch("gather_random_step_kernel");
+}
 
 extern "C" int pdeinv_gaussian_sample(int64_t n, int32_t m, uint64_t seed, uint32_t ctr,
                                       int64_t row_off, const float* mean, const float* ch,

@@ -45,7 +45,7 @@ EXPORTED_SYMBOLS = (
     "pdeinv_runtime_version", "pdeinv_moments_batched_workspace_bytes", "pdeinv_moments_batched",
     "pdeinv_kmv_weights_workspace_bytes", "pdeinv_kmv_weights", "pdeinv_residual_kmv",
     "pdeinv_mlp_param_count", "pdeinv_residual_kfp_mlp_workspace_bytes", "pdeinv_residual_kfp_mlp",
-    "pdeinv_kfp_terms_finalize",
+    "pdeinv_kfp_terms_finalize", "pdeinv_gather_random_step",
 )
 
 
@@ -143,6 +143,7 @@ def lib():
         "pdeinv_residual_kfp_mlp_workspace_bytes": (ctypes.c_size_t, [P]),
         "pdeinv_residual_kfp_mlp": (i32, [P, P, i64, i64, P, i64, i64, P, i64, i64, P, P, P, P, P]),
         "pdeinv_kfp_terms_finalize": (i32, [P, P, i64, f32, P, P]),
+        "pdeinv_gather_random_step": (i32, [P, i64, i32, i32, u64, u32, P, P, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -576,3 +577,17 @@ def kfp_terms_finalize(acc: torch.Tensor, grad: torch.Tensor, gamma: float) -> t
     _check(lib().pdeinv_kfp_terms_finalize(_dev(acc, "acc", torch.float64), _dev(grad, "grad"), grad.numel(),
                                            float(gamma), _dev(out, "out"), stream_handle()), "pdeinv_kfp_terms_finalize")
     return out
+
+
+def gather_random_step(traj_tm: torch.Tensor, *, seed: int, ctr: int = 0, return_t: bool = False):
+    """One uniformly drawn step per particle from a time-major trajectory [n, N, m] -> [N, m]."""
+    _require_gpu()
+    n, N, m = traj_tm.shape
+    if not traj_tm.is_contiguous():
+        raise ValueError("trajectory must be contiguous time-major [n, N, m]")
+    out = torch.empty((N, m), device=traj_tm.device, dtype=torch.float32)
+    t = torch.empty(N, device=traj_tm.device, dtype=torch.int32) if return_t else None
+    _check(lib().pdeinv_gather_random_step(_dev(traj_tm, "traj"), N, n, m, int(seed) & 0xFFFFFFFFFFFFFFFF,
+                                           int(ctr) & 0xFFFFFFFF, _dev(out, "out"), _dev(t, "t", torch.int32),
+                                           stream_handle()), "pdeinv_gather_random_step")
+    return (out, t) if return_t else out

@@ -274,3 +274,18 @@ def test_residual_mlp_vs_restatement(native, dims, true_kind, chunk):
     g = grad.cpu().numpy()
     assert np.max(np.abs(g - g_ref)) < 2e-3 * (1 + np.abs(g_ref).max()), np.max(np.abs(g - g_ref))
     assert abs(out[2] - np.linalg.norm(g_ref)) < 2e-3 * (1 + np.linalg.norm(g_ref))
+
+
+def test_gather_random_step(native):
+    rng = np.random.default_rng(3)
+    n, N, m = 37, 5000, 8
+    traj = _t(rng.standard_normal((n, N, m)))
+    out, t = native.gather_random_step(traj, seed=5, ctr=2, return_t=True)
+    t = t.cpu().numpy()
+    assert t.min() >= 0 and t.max() < n and len(np.unique(t)) == n
+    ref = traj.cpu().numpy()[t, np.arange(N)]
+    assert np.array_equal(out.cpu().numpy(), ref)
+    # uniform over steps (chi-square, 36 dof)
+    cnt = np.bincount(t, minlength=n)
+    chi2 = np.sum((cnt - N / n) ** 2 / (N / n))
+    assert chi2 < 80
