@@ -36,8 +36,39 @@ static rocblas_handle blas_handle(int device) {
   return handles[device];
 }
 
+// K-split factor of the weight-gradient GEMMs: the reduction runs over 4 x chunk rows while the
+// output is only n_in x n_out (<= 256 x 256), so one GEMM launches a few dozen workgroups. Slicing
+// the rows into up to kMaxKSplit batched GEMMs (>= kMinKSlice rows each) fills the chip; the fp32
+// partial slabs are summed in a fixed order (deterministic, no atomics).
+constexpr int kMaxKSplit = 256;
+constexpr int64_t kMinKSlice = 4096;
+constexpr int kColsumBlocks = 512;
+
+__global__ void sum_slices_kernel(const float* __restrict__ part, int S, int64_t n, float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  float s = 0.f;
+  for (int k = 0; k < S; ++k) s += part[(int64_t)k * n + i];
+  out[i] += s;
+}
+
+// partial column sums of B[R x n] (row-major): block b sums rows [b*rpb, (b+1)*rpb) for the
+// columns blockIdx.y*kBlock + tid. Consecutive lanes read consecutive floats of a row.
+__global__ __launch_bounds__(kBlock) void colsum_partial_kernel(const float* __restrict__ B, int64_t R, int n,
+                                                                int64_t rpb, float* __restrict__ part) {
+  const int c = blockIdx.y * kBlock + threadIdx.x;
+  if (c >= n) return;
+  const int64_t r0 = (int64_t)blockIdx.x * rpb;
+  const int64_t r1 = r0 + rpb < R ? r0 + rpb : R;
+  float s = 0.f;
+  for (int64_t r = r0; r < r1; ++r) s += B[r * n + c];
+  part[(int64_t)blockIdx.x * n + c] = s;
+}
+
 struct Blas {
   rocblas_handle h;
+  hipStream_t st;
+  float* part;  // >= kMaxKSplit * max(n_in * n_out) floats (also holds the colsum partials)
   int status = 0;
   // row-major C[R x n_out] = A[R x n_in] . K[n_in x n_out]
   void fwd(const float* A, const float* K, float* C, int64_t R, int n_in, int n_out) {
@@ -53,19 +84,30 @@ struct Blas {
                       n_out, A, n_out, &zero, C, n_in) != rocblas_status_success)
       status = 1;
   }
-  // Kbar[n_in x n_out] += A[R x n_in]^T . B[R x n_out]
+  // Kbar[n_in x n_out] += A[R x n_in]^T . B[R x n_out]  (K-split into S batched slices + slab sum)
   void wgrad(const float* A, const float* B, float* Kbar, int64_t R, int n_in, int n_out) {
-    const float one = 1.f;
-    if (rocblas_sgemm(h, rocblas_operation_none, rocblas_operation_transpose, n_out, n_in, (rocblas_int)R, &one, B,
-                      n_out, A, n_in, &one, Kbar, n_out) != rocblas_status_success)
+    const float one = 1.f, zero = 0.f;
+    int64_t S = R / kMinKSlice;
+    S = S < 1 ? 1 : (S > kMaxKSplit ? kMaxKSplit : S);
+    const int64_t Ks = R / S, rem = R - S * Ks;
+    const int64_t nout = (int64_t)n_in * n_out;
+    if (rocblas_sgemm_strided_batched(h, rocblas_operation_none, rocblas_operation_transpose, n_out, n_in,
+                                      (rocblas_int)Ks, &one, B, n_out, Ks * n_out, A, n_in, Ks * n_in, &zero, part,
+                                      n_out, nout, (rocblas_int)S) != rocblas_status_success)
+      status = 1;
+    hipLaunchKernelGGL(sum_slices_kernel, dim3(grid_for(nout)), dim3(kBlock), 0, st, part, (int)S, nout, Kbar);
+    if (rem > 0 && rocblas_sgemm(h, rocblas_operation_none, rocblas_operation_transpose, n_out, n_in,
+                                 (rocblas_int)rem, &one, B + S * Ks * n_out, n_out, A + S * Ks * n_in, n_in, &one,
+                                 Kbar, n_out) != rocblas_status_success)
       status = 1;
   }
   // bbar[n] += sum over the R rows of B[R x n]
-  void colsum(const float* B, const float* ones, float* bbar, int64_t R, int n) {
-    const float one = 1.f;
-    if (rocblas_sgemv(h, rocblas_operation_none, n, (rocblas_int)R, &one, B, n, ones, 1, &one, bbar, 1) !=
-        rocblas_status_success)
-      status = 1;
+  void colsum(const float* B, float* bbar, int64_t R, int n) {
+    const int64_t rpb = (R + kColsumBlocks - 1) / kColsumBlocks;
+    const int nb = (int)((R + rpb - 1) / rpb);
+    hipLaunchKernelGGL(colsum_partial_kernel, dim3(nb, (n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, B, R, n,
+                       rpb, part);
+    hipLaunchKernelGGL(sum_slices_kernel, dim3(grid_for(n)), dim3(kBlock), 0, st, part, nb, (int64_t)n, bbar);
   }
 };
 
@@ -92,21 +134,34 @@ __global__ void mlp_act_fwd(const float* __restrict__ Z, float* __restrict__ A, 
 }
 
 // output layer: y (+bias) stored back; u = 2y (seed of the grad_x chain); V' = 2 y.y', V'' = 2(y'.y' + y.y'')
-__global__ void mlp_out(float* __restrict__ Y, const float* __restrict__ bias, float* __restrict__ YB,
-                        float2* __restrict__ terms, int64_t R, int O) {
-  const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (r >= R) return;
+// A block owns rb consecutive rows = rb*O consecutive elements of each plane: phase 1 is
+// element-wise and coalesced, the per-element products go to LDS, phase 2 sums them per row.
+__global__ __launch_bounds__(kBlock) void mlp_out(float* __restrict__ Y, const float* __restrict__ bias,
+                                                  float* __restrict__ YB, float2* __restrict__ terms, int64_t R,
+                                                  int O, int rb) {
+  extern __shared__ float prod[];  // [2][rb*O]
   const int64_t S = R * O;
-  float vd = 0.f, vdd = 0.f;
-  for (int o = 0; o < O; ++o) {
-    const int64_t e = r * O + o;
-    const float y = Y[e] + bias[o], yd = Y[S + e], ydd = Y[2 * S + e];
+  const int64_t r0 = (int64_t)blockIdx.x * rb;
+  const int nr = (int)((R - r0) < rb ? (R - r0) : rb);
+  const int ne = nr * O;
+  const int64_t e0 = r0 * O;
+  for (int k = threadIdx.x; k < ne; k += kBlock) {
+    const int64_t e = e0 + k;
+    const float y = Y[e] + bias[k % O], yd = Y[S + e], ydd = Y[2 * S + e];
     Y[e] = y;
     YB[3 * S + e] = 2.f * y;
-    vd = fmaf(y, yd, vd);
-    vdd = fmaf(yd, yd, fmaf(y, ydd, vdd));
+    prod[k] = y * yd;
+    prod[rb * O + k] = fmaf(yd, yd, y * ydd);
   }
-  terms[r] = make_float2(2.f * vd, 2.f * vdd);
+  __syncthreads();
+  for (int r = threadIdx.x; r < nr; r += kBlock) {
+    float vd = 0.f, vdd = 0.f;
+    for (int o = 0; o < O; ++o) {
+      vd += prod[r * O + o];
+      vdd += prod[rb * O + r * O + o];
+    }
+    terms[r0 + r] = make_float2(2.f * vd, 2.f * vdd);
+  }
 }
 
 // R1: zeta = tanh'(z) * a   (a = GEMM output, kept for R2)
@@ -257,11 +312,6 @@ __global__ void mlp_load_rows(const float* __restrict__ z, int64_t ld, int d, fl
   A0[R * d + e] = z[r * ld + d + i];
 }
 
-__global__ void fill_kernel(float* p, float v, int64_t n) {
-  const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (e < n) p[e] = v;
-}
-
 __global__ void slab_reduce_accum_kernel(const float* __restrict__ partials, int n_blocks,
                                          double* __restrict__ out) {
   const int c = blockIdx.x;
@@ -304,7 +354,7 @@ constexpr int kLossGrid = 512;
 struct MlpPlan {
   int d, L, W, O;
   int64_t Bc;
-  size_t off_A0, off_Y, off_YB, off_UB, off_G, off_ones, off_terms, off_part, total;
+  size_t off_A0, off_Y, off_YB, off_UB, off_G, off_kpart, off_terms, off_part, total;
   size_t off_layer0, layer_stride;  // per hidden layer: A(4) Z(3) ZB(4) HB(3) aL(1) zb(1) planes of Bc*W
 };
 
@@ -319,7 +369,9 @@ static MlpPlan make_plan(const pdeinv_kfp_mlp_desc* d) {
   p.off_YB = take(4 * p.Bc * p.O);
   p.off_UB = take(p.Bc * p.O);
   p.off_G = take(p.Bc * p.d);
-  p.off_ones = take(p.Bc);
+  const int64_t wmax = (int64_t)p.W * (p.W > p.d ? (p.W > p.O ? p.W : p.O) : p.d);
+  const int64_t cmax = (int64_t)kColsumBlocks * (p.W > p.O ? p.W : p.O);
+  p.off_kpart = take((size_t)(kMaxKSplit * wmax > cmax ? kMaxKSplit * wmax : cmax));
   p.off_terms = take(2 * p.Bc);
   p.off_part = take((size_t)PDEINV_GMM_NACC * kLossGrid);
   p.layer_stride = 16 * p.Bc * p.W;
@@ -366,11 +418,11 @@ extern "C" int pdeinv_residual_kfp_mlp(const pdeinv_kfp_mlp_desc* d, const float
   hipStream_t st = (hipStream_t)stream;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return fail(PDEINV_ERR_HIP, "kfp_mlp: hipGetDevice failed");
-  Blas blas{blas_handle(dev)};
+  float* w = (float*)ws;
+  Blas blas{blas_handle(dev), st, w + p.off_kpart};
   if (!blas.h) return fail(PDEINV_ERR_HIP, "kfp_mlp: rocblas_create_handle failed");
   if (rocblas_set_stream(blas.h, st) != rocblas_status_success) return fail(PDEINV_ERR_HIP, "kfp_mlp: rocblas_set_stream");
 
-  float* w = (float*)ws;
   const int W = p.W, O = p.O, L = p.L;
   // parameter offsets (flax order: K_1, b_1, ..., K_L, b_L, K_o, b_o)
   int64_t poff[18], boff[18];
@@ -386,14 +438,12 @@ extern "C" int pdeinv_residual_kfp_mlp(const pdeinv_kfp_mlp_desc* d, const float
   float* YB = w + p.off_YB;
   float* UB = w + p.off_UB;
   float* G = w + p.off_G;
-  float* ones = w + p.off_ones;
   float2* terms = (float2*)(w + p.off_terms);
   float* part = w + p.off_part;
   // planes per hidden layer l: A 0-3, Z 4-6, ZB 7-10, HB 11-13, aL 14, zb 15. Inside a chunk of R rows
   // the planes are packed at stride R*W so that consecutive streams form one [k*R x W] GEMM operand.
   int64_t R = 0;
   auto layer = [&](int l, int plane) { return w + p.off_layer0 + p.layer_stride * (l - 1) + (size_t)plane * R * W; };
-  hipLaunchKernelGGL(fill_kernel, dim3(grid_for(p.Bc)), dim3(kBlock), 0, st, ones, 1.f, p.Bc);
 
   MlpLossArgs la{};
   la.d = D;
@@ -428,7 +478,11 @@ extern "C" int pdeinv_residual_kfp_mlp(const pdeinv_kfp_mlp_desc* d, const float
                            R, W);
       }
       blas.fwd(layer(L, 0), params + poff[L], Y, 3 * R, W, O);
-      hipLaunchKernelGGL(mlp_out, dim3(grid_for(R)), dim3(kBlock), 0, st, Y, params + boff[L], YB, terms, R, O);
+      {
+        const int rb = O >= 2048 ? 1 : 2048 / O;  // 16 KB of LDS products per block
+        hipLaunchKernelGGL(mlp_out, dim3((unsigned)((R + rb - 1) / rb)), dim3(kBlock), 2 * rb * O * sizeof(float), st,
+                           Y, params + boff[L], YB, terms, R, O, rb);
+      }
       // ---- R1: grad_x chain ---------------------------------------------------------------
       blas.bwd(YB + 3 * SO, params + poff[L], layer(L, 14), R, W, O);  // a_L = u K_o^T
       for (int l = L; l >= 1; --l) {
@@ -460,7 +514,7 @@ extern "C" int pdeinv_residual_kfp_mlp(const pdeinv_kfp_mlp_desc* d, const float
       hipLaunchKernelGGL(mlp_seeds, dim3(grid_for(SO)), dim3(kBlock), 0, st, Y, UB, YB, s.c2, s.c3, SO);
       // ---- R2 + G: reverse over the three forward streams, weight gradients ---------------------
       blas.wgrad(layer(L, 0), YB, grad + poff[L], 4 * R, W, O);  // K_o += [h;h';h'';abar]^T [ybar;..;u]
-      blas.colsum(YB, ones, grad + boff[L], R, O);
+      blas.colsum(YB, grad + boff[L], R, O);
       blas.bwd(YB, params + poff[L], layer(L, 11), 3 * R, W, O);  // hbar streams of layer L
       for (int l = L; l >= 1; --l) {
         hipLaunchKernelGGL(mlp_act_bwd, dim3(grid_for(SW)), dim3(kBlock), 0, st, layer(l, 11), layer(l, 0),
@@ -468,7 +522,7 @@ extern "C" int pdeinv_residual_kfp_mlp(const pdeinv_kfp_mlp_desc* d, const float
         const int n_in = (l == 1) ? D : W;
         const float* Ain = (l == 1) ? A0 : layer(l - 1, 0);
         blas.wgrad(Ain, layer(l, 7), grad + poff[l - 1], 4 * R, n_in, W);
-        blas.colsum(layer(l, 7), ones, grad + boff[l - 1], R, W);
+        blas.colsum(layer(l, 7), grad + boff[l - 1], R, W);
         if (l > 1) blas.bwd(layer(l, 7), params + poff[l - 1], layer(l - 1, 11), 3 * R, W, W);
       }
       if (blas.status) return fail(PDEINV_ERR_HIP, "kfp_mlp: rocBLAS call failed");
