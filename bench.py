@@ -368,7 +368,10 @@ def run_c5(a, rank, world, dev):
         "dtype": "f32", "data": "synthetic: Philox Gaussian-init ensembles, fresh noise per step", "config": cfg,
         "residual_samples_per_s": world * rows / (kern_ms / 1e3),
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": 157.3, "unit": "TFLOP/s", "frac": achieved / 157.3,
-                     "traffic": None, "kernel": "MLP residual (rocBLAS sgemm chain + fused element-wise kernels)",
+                     "traffic": None,
+                     "kernel": ("MLP residual, fused fp32-MFMA path (hand-written GEMMs with fused prologues/epilogues)"
+                                if native.mlp_fused_supported(dims) else
+                                "MLP residual, library path (rocBLAS sgemm + element-wise kernels)"),
                      "kernel_ms": kern_ms, "algorithmic_flops_per_launch": flops},
         "simulate_ms": sim_ms, "simulate_GBps": sim_bytes(N, n, d) / (sim_ms / 1e3) / 1e9,
     }

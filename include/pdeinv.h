@@ -274,7 +274,12 @@ int pdeinv_residual_kmv(const pdeinv_kmv_desc* desc, const double* d_mom, const 
  * Fused value + d loss / d theta over the three sample sets (same loss and coefficients as the
  * GMM residual): Taylor-mode forward streams, the grad_x reverse chain, its forward adjoint, the
  * reverse sweep and the weight-gradient outer products, as dense GEMMs (rocBLAS sgemm, fp32) plus
- * fused element-wise kernels, chunked over chunk_rows rows.
+ * fused element-wise kernels, chunked over chunk_rows rows. impl selects the implementation:
+ * PDEINV_MLP_IMPL_AUTO picks the fused path when the shape allows it (L >= 2, W % 128 == 0,
+ * W <= 512, out <= 64, d in {2, 4, 8, 16}): hand-written fp32 MFMA GEMMs whose prologues and
+ * epilogues carry all of the element-wise algebra (layer 1 is recomputed from the rows, never
+ * stored). PDEINV_MLP_IMPL_LIBRARY forces the rocBLAS + element-wise-kernel path (any shape);
+ * PDEINV_MLP_IMPL_FUSED forces the fused path (PDEINV_ERR_UNSUPPORTED if the shape is not).
  * d_params / d_grad: flat flax order [K_1 (d x W), b_1, K_2 (W x W), b_2, ..., K_o (W x out), b_o]
  * (pdeinv_mlp_param_count floats). d_acc [PDEINV_GMM_NACC] and d_grad are ACCUMULATED (+=): zero
  * them first. pdeinv_kfp_terms_finalize turns (acc, grad) into the PDEINV_KFP_* slots.
@@ -291,7 +296,12 @@ typedef struct {
   float gamma;
   float c_nabla, c_hess, c_fric, c_true, c_init, c_term;
   int64_t chunk_rows;     /* rows per GEMM chunk (workspace grows with it); 0 => 2^18 */
+  int32_t impl;           /* PDEINV_MLP_IMPL_* */
 } pdeinv_kfp_mlp_desc;
+#define PDEINV_MLP_IMPL_AUTO 0
+#define PDEINV_MLP_IMPL_LIBRARY 1
+#define PDEINV_MLP_IMPL_FUSED 2
+int pdeinv_mlp_fused_supported(int32_t dim, int32_t n_layers, int32_t width, int32_t out_features);
 int64_t pdeinv_mlp_param_count(int32_t dim, int32_t n_layers, int32_t width, int32_t out_features);
 size_t pdeinv_residual_kfp_mlp_workspace_bytes(const pdeinv_kfp_mlp_desc* desc);
 int pdeinv_residual_kfp_mlp(const pdeinv_kfp_mlp_desc* desc, const float* d_init, int64_t n_init,
@@ -334,6 +344,12 @@ int pdeinv_gather_subsample(const float* d_traj, int64_t n_particles, int32_t n_
  * traj_tm[t_p, p], optional t_out[p] = t_p. The per-particle 0T batch of BASELINE config 5. */
 int pdeinv_gather_random_step(const float* d_traj, int64_t n_particles, int32_t n_steps, int32_t m,
                               uint64_t seed, uint32_t ctr, float* d_out, int32_t* d_t_out, void* stream);
+
+/* Fused optimizer step of the trainer (core/trainer.py:85-86 + main.py:11-29):
+ * optax.chain(add_decayed_weights(weight_decay), adam(lr, b1, b2, eps)) then apply_updates, in
+ * place over a flat parameter vector; count = the step number after increment (>= 1). */
+int pdeinv_adam_update(float* d_params, const float* d_grad, float* d_mu, float* d_nu, int64_t n, float lr,
+                       float b1, float b2, float eps, float weight_decay, int32_t count, void* stream);
 
 int pdeinv_abi_version(void);
 const char* pdeinv_last_error(void);

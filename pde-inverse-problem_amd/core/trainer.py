@@ -6,8 +6,9 @@ drivers are unchanged. Differences of mechanism, not of behaviour:
     value_and_grad_fn all-reduces its fp64 sums, which is the reference's pmap +
     jnp.mean(axis=0) (trainer.py:44-53);
   * the optimizer is optax's add_decayed_weights -> adam(b1=0.9, eps=1e-4) with a constant or
-    cosine(20000, alpha=1e-3) learning rate (main.py:11-29), applied to the parameter pytree on
-    the device; the EMA branch (trainer.py:87-103) is kept;
+    cosine(20000, alpha=1e-3) learning rate (main.py:11-29); on the device it is one fused HIP
+    launch per parameter leaf (pdeinv_adam_update, in place); the EMA branch (trainer.py:87-103)
+    is kept;
   * metrics go to a local JSONL log (wandb is optional and not installed here).
 """
 from __future__ import annotations
@@ -39,6 +40,14 @@ class Adam:
         count = state["count"] + 1
         lr = self.lr(state["count"])
         b1, b2, eps, wd = self.b1, self.b2, self.eps, self.wd
+        leaves = tree_leaves(params)
+        if leaves and all(t.is_cuda for t in leaves):
+            # device path: one fused HIP launch per leaf, parameters and moments updated in place
+            from utils import native
+            for p, g, m, v in zip(leaves, tree_leaves(grads), tree_leaves(state["mu"]), tree_leaves(state["nu"])):
+                native.adam_update(p, g.contiguous(), m, v, lr=lr, b1=b1, b2=b2, eps=eps, weight_decay=wd,
+                                   count=count)
+            return params, {"count": count, "mu": state["mu"], "nu": state["nu"]}
         g_all = tree_map(lambda g, p: g + wd * p, grads, params)
         mu = tree_map(lambda m, g: b1 * m + (1 - b1) * g, state["mu"], g_all)
         nu = tree_map(lambda v, g: b2 * v + (1 - b2) * g * g, state["nu"], g_all)

@@ -21,6 +21,7 @@
 #include <mutex>
 
 #include "common.h"
+#include "mlp_fused.h"
 
 namespace pdeinv {
 
@@ -384,10 +385,45 @@ static MlpPlan make_plan(const pdeinv_kfp_mlp_desc* d) {
 
 using namespace pdeinv;
 
+static bool use_fused(const pdeinv_kfp_mlp_desc* d) {
+  if (d->impl == PDEINV_MLP_IMPL_LIBRARY) return false;
+  return mlpf::supported(d->dim, d->n_layers, d->width, d->out_features);
+}
+
+static int64_t chunk_rows_of(const pdeinv_kfp_mlp_desc* d) { return d->chunk_rows > 0 ? d->chunk_rows : (1 << 18); }
+
 extern "C" size_t pdeinv_residual_kfp_mlp_workspace_bytes(const pdeinv_kfp_mlp_desc* d) {
   if (!d || d->dim < 1 || d->n_layers < 1 || d->width < 1 || d->out_features < 1) return 0;
+  if (use_fused(d))
+    return (mlpf::workspace_floats(d->dim, d->n_layers, d->width, d->out_features, chunk_rows_of(d)) +
+            (size_t)PDEINV_GMM_NACC * kLossGrid) * sizeof(float);
   return make_plan(d).total;
 }
+
+namespace pdeinv {
+struct LossCtx {
+  MlpLossArgs la;
+  const float* zr;
+  int64_t ld;
+  float* part;
+  double* acc;
+  int D;
+};
+
+static int fused_loss_hook(void* p, const float* G, const float2* terms, float* abar0, int64_t R, hipStream_t st) {
+  LossCtx* c = (LossCtx*)p;
+  const int lg = grid_for(R) < kLossGrid ? grid_for(R) : kLossGrid;
+  switch (c->D) {
+#define CASE(DD) case DD: hipLaunchKernelGGL(mlp_loss<DD>, dim3(lg), dim3(kBlock), 0, st, c->la, G, c->zr, c->ld, terms, abar0, R, c->part); break;
+    CASE(2) CASE(4) CASE(8) CASE(16)
+#undef CASE
+    default:
+      return fail(PDEINV_ERR_UNSUPPORTED, "kfp_mlp fused: dim must be 2, 4, 8 or 16");
+  }
+  hipLaunchKernelGGL(slab_reduce_accum_kernel, dim3(PDEINV_GMM_NACC), dim3(kBlock), 0, st, c->part, lg, c->acc);
+  return check_launch("kfp_mlp fused loss");
+}
+}  // namespace pdeinv
 
 extern "C" int64_t pdeinv_mlp_param_count(int32_t dim, int32_t n_layers, int32_t width, int32_t out_features) {
   int64_t n = (int64_t)dim * width + width;
@@ -419,11 +455,8 @@ extern "C" int pdeinv_residual_kfp_mlp(const pdeinv_kfp_mlp_desc* d, const float
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return fail(PDEINV_ERR_HIP, "kfp_mlp: hipGetDevice failed");
   float* w = (float*)ws;
-  Blas blas{blas_handle(dev), st, w + p.off_kpart};
-  if (!blas.h) return fail(PDEINV_ERR_HIP, "kfp_mlp: rocblas_create_handle failed");
-  if (rocblas_set_stream(blas.h, st) != rocblas_status_success) return fail(PDEINV_ERR_HIP, "kfp_mlp: rocblas_set_stream");
-
   const int W = p.W, O = p.O, L = p.L;
+  PDEINV_REQUIRE(L <= 16, PDEINV_ERR_UNSUPPORTED, "kfp_mlp: at most 16 hidden layers");
   // parameter offsets (flax order: K_1, b_1, ..., K_L, b_L, K_o, b_o)
   int64_t poff[18], boff[18];
   int64_t o = 0;
@@ -432,7 +465,6 @@ extern "C" int pdeinv_residual_kfp_mlp(const pdeinv_kfp_mlp_desc* d, const float
     poff[l] = o; o += (int64_t)n_in * n_out;
     boff[l] = o; o += n_out;
   }
-  PDEINV_REQUIRE(L <= 16, PDEINV_ERR_UNSUPPORTED, "kfp_mlp: at most 16 hidden layers");
   float* A0 = w + p.off_A0;
   float* Y = w + p.off_Y;
   float* YB = w + p.off_YB;
@@ -458,6 +490,40 @@ extern "C" int pdeinv_residual_kfp_mlp(const pdeinv_kfp_mlp_desc* d, const float
       {z0, n0, ld0 ? ld0 : 2 * D, 0, d->c_nabla, d->c_hess, d->c_fric},
       {zi, ni, ldi ? ldi : 2 * D, 1, 0.f, 0.f, d->c_init},
       {zt, nt, ldt ? ldt : 2 * D, 2, 0.f, 0.f, d->c_term}};
+  if (use_fused(d)) {
+    const int64_t Bc = chunk_rows_of(d);
+    const size_t fl = mlpf::workspace_floats(D, L, p.W, p.O, Bc);
+    LossCtx lc{};
+    lc.la = la;
+    lc.part = (float*)ws + fl;
+    lc.acc = acc;
+    lc.D = D;
+    for (const Set& s : sets) {
+      PDEINV_REQUIRE(s.n == 0 || s.ld >= 2 * D, PDEINV_ERR_INVALID, "kfp_mlp: row stride < 2*dim");
+      lc.la.set = s.id; lc.la.c1 = s.c1; lc.la.c2 = s.c2; lc.la.c3 = s.c3; lc.la.c_true = d->c_true;
+      lc.la.inv_n = s.n ? 1.f / (float)s.n : 0.f;
+      for (int64_t r0 = 0; r0 < s.n; r0 += Bc) {
+        mlpf::Chunk c{};
+        c.d = D; c.L = L; c.W = p.W; c.O = p.O;
+        c.R = (s.n - r0) < Bc ? (s.n - r0) : Bc;
+        c.z = s.z + r0 * s.ld;
+        c.ldz = s.ld;
+        c.params = params; c.grad = grad; c.poff = poff; c.boff = boff;
+        c.c2 = s.c2; c.c3 = s.c3;
+        c.ws = (float*)ws; c.Bc = Bc;
+        lc.zr = c.z;
+        lc.ld = s.ld;
+        const int rc = mlpf::run_chunk(c, mlpf::LossHook{fused_loss_hook, &lc}, st);
+        if (rc) return rc;
+      }
+    }
+    return PDEINV_OK;
+  }
+  PDEINV_REQUIRE(d->impl != PDEINV_MLP_IMPL_FUSED, PDEINV_ERR_UNSUPPORTED,
+                 "kfp_mlp: fused path needs L >= 2, W in {128, 256, 512}, out <= 64, d in {2, 4, 8, 16}");
+  Blas blas{blas_handle(dev), st, w + p.off_kpart};
+  if (!blas.h) return fail(PDEINV_ERR_HIP, "kfp_mlp: rocblas_create_handle failed");
+  if (rocblas_set_stream(blas.h, st) != rocblas_status_success) return fail(PDEINV_ERR_HIP, "kfp_mlp: rocblas_set_stream");
   for (const Set& s : sets) {
     PDEINV_REQUIRE(s.n == 0 || s.ld >= 2 * D, PDEINV_ERR_INVALID, "kfp_mlp: row stride < 2*dim");
     for (int64_t r0 = 0; r0 < s.n; r0 += p.Bc) {

@@ -1,0 +1,38 @@
+// mlp_fused.h — fused fp32-MFMA path of the V_hypothesis KFP residual (internal interface).
+#pragma once
+#include "common.h"
+
+namespace pdeinv {
+namespace mlpf {
+
+// Shapes the fused path handles (else the rocBLAS path runs).
+bool supported(int d, int L, int W, int O);
+
+// Workspace (floats) for chunks of Bc rows.
+size_t workspace_floats(int d, int L, int W, int O, int64_t Bc);
+
+// Per-set loss hook: the orchestrator computes g [R x d] and the per-row terms (V', V''), then
+// calls this to accumulate the loss slots and write abar0 = 2 c1 g [R x d] (mlp.hip's loss kernel).
+struct LossHook {
+  int (*fn)(void* ctx, const float* g, const float2* terms, float* abar0, int64_t R, hipStream_t st);
+  void* ctx;
+};
+
+struct Chunk {
+  int d, L, W, O;
+  int64_t R;                 // rows in this chunk
+  const float* z;            // rows [x | v], stride ldz
+  int64_t ldz;
+  const float* params;       // flat flax order
+  float* grad;               // accumulated (+=)
+  const int64_t* poff;       // kernel offsets per layer (0..L)
+  const int64_t* boff;       // bias offsets per layer (0..L)
+  float c2, c3;              // loss weights of V'' and V' for this set
+  float* ws;                 // workspace_floats(..., Bc >= R)
+  int64_t Bc;
+};
+
+int run_chunk(const Chunk& c, const LossHook& loss, hipStream_t st);
+
+}  // namespace mlpf
+}  // namespace pdeinv

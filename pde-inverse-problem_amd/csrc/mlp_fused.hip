@@ -1,0 +1,960 @@
+// mlp_fused.hip — the V_hypothesis KFP residual on hand-written fp32 MFMA kernels (gfx950).
+//
+// Same algebra as mlp.hip's library path (oracle/numpy_ref.py kfp_mlp_grad_analytic), but the
+// element-wise steps ride in GEMM prologues (building the A operand in LDS) or epilogues (on the
+// accumulators). The first hidden layer has K = d (<= 16) inputs, so its streams come from small
+// VALU kernels over the sample rows (h1 planes, abar1, g, and the layer-1 parameter gradient).
+//
+// Row GEMMs (samples x features):  C_s[BM x BN] = A_s[BM x K] . B[K x BN], s < S streams sharing
+// one weight tile. v_mfma_f32_32x32x2_f32 (exact fp32, 64 cycles / SIMD, 16 acc regs); 4 waves
+// in a WGM x WGN grid; A and B staged k-major in LDS (As[s][k][m], Bs[k][n]) so both MFMA operand
+// reads are 32 consecutive floats per half-wave. Workgroups loop over row blocks (persistent grid)
+// so the epilogues that reduce over rows (bias gradients) keep register partials and write one
+// slab row per workgroup; slabs are summed in a fixed order (deterministic). The next k-tile's
+// global loads are issued before the current tile's MFMAs (register prefetch).
+//
+// Weight gradients (sum over samples of 4 stream-pair outer products): C[n_in x n_out] =
+// sum_p A_p^T B_p, rows split into slices (one partial slab each); the 4 pairs of a 16-row block
+// are staged together so every source plane is read once per tile.
+//
+// Per chunk (L = 2; deeper nets add the "middle" steps):
+//   L1f   h1, h1', h1'' planes                 VALU over [x | v] rows
+//   FWD   z2 streams = [h1, h1', h1''] K2                               E: tanh -> h2, z2', z2''
+//   OUT   y streams  = [h2, h2', h2''] Ko      A: h', h'' from planes   E: +bo, V' and V'' per row
+//   R1    a2 = (2y) Ko^T                                                E: store
+//   R1    a1 = (s1(h2) a2) K2^T                                         E: store
+//   g     g = (s1(z1) a1) K1^T                 VALU, one wave per row (layer-1 recompute)
+//   loss  (mlp.hip)  per-row terms, abar0 = 2 c1 g
+//   L1a   abar1 = s1(z1) (abar0 K1)             VALU
+//   F2    zetabar2 = abar1 K2                                            E: store
+//   UB    ubar = (s1(h2) zetabar2) Ko                                   E: seeds ybar.., bo grad
+//   R2    hbar2 streams = ybar streams Ko^T                             E: act_bwd -> zbar2, b2 grad
+//   R2    hbar1 streams = zbar2 streams K2^T                            E: store
+//   L1    layer-1 act_bwd + K1 / b1 gradient   VALU, columns per thread, rows looped
+//   G     Ko += [h2..abar2]^T [ybar..u];  K2 += [h1..abar1]^T [zbar2..zeta2]
+#include <math.h>
+
+#include <algorithm>
+
+#include "mlp_fused.h"
+
+namespace pdeinv {
+namespace mlpf {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int BK = 32;   // feature k-step of the row GEMMs
+constexpr int BKG = 16;  // rows per weight-gradient step (4 pairs staged together)
+constexpr int kT = 256;
+
+__device__ __forceinline__ float ftanh(float z) {
+  const float e = __builtin_amdgcn_exp2f(2.8853900817779268f * z);
+  return 1.f - 2.f * __builtin_amdgcn_rcpf(e + 1.f);
+}
+
+enum { A_RAW1 = 0, A_FWD, A_S1MUL, A_U, A_S3 };
+enum { B_NN = 0, B_NT };
+enum { E_ACT_FWD = 0, E_OUT, E_STORE, E_STORE3, E_SEEDS, E_ACT_BWD };
+
+struct GemmArgs {
+  int64_t R;
+  int K, N;
+  int n_mblocks;
+  const float *pa0, *pa1, *pa2;           // A-source planes, ld K
+  const float* Bw;                        // [K x N] (B_NN) or [N x K] (B_NT), row-major
+  const float* bias;                      // [N], stream 0 (E_ACT_FWD, E_OUT)
+  float *po0, *po1, *po2;                 // outputs, ld N
+  const float *pe0, *pe1, *pe2, *pe3, *pe4;  // epilogue inputs, ld N
+  float2* terms;
+  float c2, c3;
+  float* part;
+};
+
+// ---- operand staging: global -> registers (issued one k-block ahead, in flight under the
+//      MFMAs of the current block) -> prologue math -> LDS (k-major) ----------------------
+template <int BM, int AM>
+struct ARegs {
+  static constexpr int NE = BM * BK / kT;  // elements per thread
+  static constexpr int NV = (AM == A_FWD || AM == A_S3) ? 3 : (AM == A_S1MUL ? 2 : 1);
+  float v[NE][NV > 0 ? NV : 1];
+};
+
+template <int BM, int AM>
+__device__ __forceinline__ void load_a(const GemmArgs& a, ARegs<BM, AM>& ra, int64_t r0, int k0) {
+  if constexpr (ARegs<BM, AM>::NV > 0) {
+#pragma unroll
+    for (int j = 0; j < ARegs<BM, AM>::NE; ++j) {
+      const int e = threadIdx.x + j * kT;
+      const int m = e / BK, kk = e - m * BK;
+      const int64_t r = r0 + m;
+      const int k = k0 + kk;
+      const bool ok = r < a.R && k < a.K;
+      const int64_t o = ok ? r * a.K + k : 0;
+      ra.v[j][0] = ok ? a.pa0[o] : 0.f;
+      if constexpr (ARegs<BM, AM>::NV > 1) ra.v[j][1] = ok ? a.pa1[o] : 0.f;
+      if constexpr (ARegs<BM, AM>::NV > 2) ra.v[j][2] = ok ? a.pa2[o] : 0.f;
+    }
+  }
+}
+
+template <int S, int BM, int AM>
+__device__ __forceinline__ void store_a(const ARegs<BM, AM>& ra, float* As) {
+  constexpr int LDA = BM + 4;
+#pragma unroll
+  for (int j = 0; j < ARegs<BM, AM>::NE; ++j) {
+    const int e = threadIdx.x + j * kT;
+    const int m = e / BK, kk = e - m * BK;
+    float v0 = 0.f, v1 = 0.f, v2 = 0.f;
+    if constexpr (AM == A_FWD) {
+      const float h = ra.v[j][0], zd = ra.v[j][1], zdd = ra.v[j][2];
+      const float s1 = 1.f - h * h, s2 = -2.f * h * s1;
+      v0 = h;
+      v1 = s1 * zd;
+      v2 = fmaf(s1, zdd, s2 * zd * zd);
+    } else if constexpr (AM == A_S1MUL) {
+      const float h = ra.v[j][0];
+      v0 = (1.f - h * h) * ra.v[j][1];
+    } else if constexpr (AM == A_U) {
+      v0 = 2.f * ra.v[j][0];
+    } else if constexpr (AM == A_RAW1) {
+      v0 = ra.v[j][0];
+    } else {  // A_S3
+      v0 = ra.v[j][0];
+      v1 = ra.v[j][1];
+      v2 = ra.v[j][2];
+    }
+    As[kk * LDA + m] = v0;
+    if constexpr (S > 1) As[(BK + kk) * LDA + m] = v1;
+    if constexpr (S > 2) As[(2 * BK + kk) * LDA + m] = v2;
+  }
+}
+
+template <int BN, int BMD>
+__device__ __forceinline__ void load_b(const GemmArgs& a, float (&rb)[BK * BN / kT], int k0, int n0) {
+#pragma unroll
+  for (int j = 0; j < BK * BN / kT; ++j) {
+    const int e = threadIdx.x + j * kT;
+    if constexpr (BMD == B_NN) {
+      const int kk = e / BN, nn = e - kk * BN;
+      const int k = k0 + kk, n = n0 + nn;
+      rb[j] = (k < a.K && n < a.N) ? a.Bw[(int64_t)k * a.N + n] : 0.f;
+    } else {
+      const int nn = e / BK, kk = e - nn * BK;
+      const int k = k0 + kk, n = n0 + nn;
+      rb[j] = (k < a.K && n < a.N) ? a.Bw[(int64_t)n * a.K + k] : 0.f;
+    }
+  }
+}
+
+template <int BN, int BMD>
+__device__ __forceinline__ void store_b(const float (&rb)[BK * BN / kT], float* Bs) {
+  constexpr int LDB = BN + 4;
+#pragma unroll
+  for (int j = 0; j < BK * BN / kT; ++j) {
+    const int e = threadIdx.x + j * kT;
+    if constexpr (BMD == B_NN) {
+      const int kk = e / BN, nn = e - kk * BN;
+      Bs[kk * LDB + nn] = rb[j];
+    } else {
+      const int nn = e / BK, kk = e - nn * BK;
+      Bs[kk * LDB + nn] = rb[j];
+    }
+  }
+}
+
+template <int S, int BM, int BN, int WGM, int AM, int BMD, int EM>
+__global__ __launch_bounds__(kT) void fgemm(GemmArgs a) {
+  constexpr int WGN = 4 / WGM;
+  constexpr int WM = BM / WGM, WN = BN / WGN, MI = WM / 32, NI = WN / 32;
+  static_assert(MI >= 1 && NI >= 1 && MI * 32 == WM && NI * 32 == WN, "wave tile must be 32-multiples");
+  static_assert(EM != E_OUT || WGN == 1, "E_OUT reduces each row inside one wave");
+  constexpr int LDA = BM + 4, LDB = BN + 4;
+  constexpr int NP = (EM == E_SEEDS || EM == E_ACT_BWD) ? 1 : 0;
+  extern __shared__ float lds[];
+  float* As = lds;                  // [S][BK][LDA]
+  float* Bs = As + S * BK * LDA;    // [BK][LDB]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WGN, wn = wave - (wave / WGN) * WGN, l31 = lane & 31, hi = lane >> 5;
+  const int n0 = blockIdx.y * BN;
+  [[maybe_unused]] float pacc[NI];
+#pragma unroll
+  for (int ni = 0; ni < NI; ++ni) pacc[ni] = 0.f;
+
+  for (int mb = blockIdx.x; mb < a.n_mblocks; mb += gridDim.x) {
+    const int64_t r0 = (int64_t)mb * BM;
+    f32x16 acc[S][MI][NI];
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+          for (int q = 0; q < 16; ++q) acc[s][mi][ni][q] = 0.f;
+
+    ARegs<BM, AM> ra;
+    float rb[BK * BN / kT];
+    load_a<BM, AM>(a, ra, r0, 0);
+    load_b<BN, BMD>(a, rb, 0, n0);
+    for (int k0 = 0; k0 < a.K; k0 += BK) {
+      __syncthreads();  // every wave is done reading the previous tile
+      store_a<S, BM, AM>(ra, As);
+      store_b<BN, BMD>(rb, Bs);
+      __syncthreads();
+      if (k0 + BK < a.K) {  // next tile's global loads fly under this tile's MFMAs
+        load_a<BM, AM>(a, ra, r0, k0 + BK);
+        load_b<BN, BMD>(a, rb, k0 + BK, n0);
+      }
+#pragma unroll
+      for (int kk = 0; kk < BK; kk += 2) {
+        float bv[NI];
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni) bv[ni] = Bs[(kk + hi) * LDB + wn * WN + ni * 32 + l31];
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+#pragma unroll
+          for (int mi = 0; mi < MI; ++mi) {
+            const float av = As[(s * BK + kk + hi) * LDA + wm * WM + mi * 32 + l31];
+#pragma unroll
+            for (int ni = 0; ni < NI; ++ni)
+              acc[s][mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv[ni], acc[s][mi][ni], 0, 0, 0);
+          }
+      }
+    }
+
+    // ---- epilogue: acc register q of tile (mi, ni) is C[row][col] with
+    //      row = (q & 3) + 8 (q >> 2) + 4 (lane >> 5), col = lane & 31 (32x32 C/D map)
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi) {
+      [[maybe_unused]] float t1[16], t2[16];
+      if constexpr (EM == E_OUT) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) t1[q] = t2[q] = 0.f;
+      }
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) {
+        const int n = n0 + wn * WN + ni * 32 + l31;
+        const bool nv = n < a.N;
+        [[maybe_unused]] float bn = 0.f;
+        if constexpr (EM == E_ACT_FWD || EM == E_OUT) bn = nv ? a.bias[n] : 0.f;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int64_t r = r0 + wm * WM + mi * 32 + (q & 3) + 8 * (q >> 2) + 4 * hi;
+          const bool ok = nv && r < a.R;
+          const int64_t o = r * a.N + n;
+          if constexpr (EM == E_ACT_FWD) {
+            if (ok) {
+              a.po0[o] = ftanh(acc[0][mi][ni][q] + bn);
+              a.po1[o] = acc[1][mi][ni][q];
+              a.po2[o] = acc[2][mi][ni][q];
+            }
+          } else if constexpr (EM == E_STORE) {
+            if (ok) a.po0[o] = acc[0][mi][ni][q];
+          } else if constexpr (EM == E_STORE3) {
+            if (ok) {
+              a.po0[o] = acc[0][mi][ni][q];
+              a.po1[o] = acc[1][mi][ni][q];
+              a.po2[o] = acc[2][mi][ni][q];
+            }
+          } else if constexpr (EM == E_OUT) {
+            if (ok) {
+              const float y = acc[0][mi][ni][q] + bn, yd = acc[1][mi][ni][q], ydd = acc[2][mi][ni][q];
+              a.po0[o] = y;
+              a.po1[o] = yd;
+              a.po2[o] = ydd;
+              t1[q] = fmaf(y, yd, t1[q]);
+              t2[q] = fmaf(yd, yd, fmaf(y, ydd, t2[q]));
+            }
+          } else if constexpr (EM == E_SEEDS) {
+            if (ok) {
+              const float ub = acc[0][mi][ni][q];
+              const float y = a.pe0[o], yd = a.pe1[o], ydd = a.pe2[o];
+              const float yb = 2.f * a.c3 * yd + 2.f * a.c2 * ydd + 2.f * ub;
+              a.po0[o] = yb;
+              a.po1[o] = 2.f * a.c3 * y + 4.f * a.c2 * yd;
+              a.po2[o] = 2.f * a.c2 * y;
+              pacc[ni] += yb;
+            }
+          } else if constexpr (EM == E_ACT_BWD) {
+            if (ok) {
+              const float hb = acc[0][mi][ni][q], hdb = acc[1][mi][ni][q], hddb = acc[2][mi][ni][q];
+              const float h = a.pe0[o], zd = a.pe1[o], zdd = a.pe2[o], aL = a.pe3[o], zb = a.pe4[o];
+              const float s1 = 1.f - h * h, s2 = -2.f * h * s1, s3 = -2.f * s1 * s1 - 2.f * h * s2;
+              const float zbar = s1 * hb + s2 * zd * hdb + (s2 * zdd + s3 * zd * zd) * hddb + s2 * aL * zb;
+              a.po0[o] = zbar;
+              a.po1[o] = s1 * hdb + 2.f * s2 * zd * hddb;
+              a.po2[o] = s1 * hddb;
+              pacc[ni] += zbar;
+            }
+          }
+        }
+      }
+      if constexpr (EM == E_OUT) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          float p1 = t1[q], p2 = t2[q];
+#pragma unroll
+          for (int off = 16; off > 0; off >>= 1) {
+            p1 += __shfl_xor(p1, off, 64);
+            p2 += __shfl_xor(p2, off, 64);
+          }
+          const int64_t r = r0 + wm * WM + mi * 32 + (q & 3) + 8 * (q >> 2) + 4 * hi;
+          if (l31 == 0 && r < a.R) a.terms[r] = make_float2(2.f * p1, 2.f * p2);
+        }
+      }
+    }
+  }
+
+  if constexpr (NP > 0) {
+    __syncthreads();
+    float* red = lds;  // [WGM][BN]
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) {
+      const float v = pacc[ni] + __shfl_xor(pacc[ni], 32, 64);
+      if (hi == 0) red[wm * BN + wn * WN + ni * 32 + l31] = v;
+    }
+    __syncthreads();
+    for (int c = tid; c < BN; c += kT) {
+      float s = 0.f;
+#pragma unroll
+      for (int w = 0; w < WGM; ++w) s += red[w * BN + c];
+      if (n0 + c < a.N) a.part[(int64_t)blockIdx.x * a.N + n0 + c] = s;
+    }
+  }
+}
+
+// ---- layer-1 kernels (VALU; K1 is d x W, d <= 16) ------------------------------------------
+// g = zeta1 K1^T with zeta1 = s1(z1) a1, z1 = x K1 + b1: one wave per row, lane owns columns
+// lane + 64 j; the d partial sums are wave-reduced.
+template <int D, int CPL>
+__global__ __launch_bounds__(kT) void l1_g_kernel(const float* __restrict__ a1, const float* __restrict__ z,
+                                                  int64_t ldz, const float* __restrict__ K1,
+                                                  const float* __restrict__ b1, int64_t R, float* __restrict__ G) {
+  constexpr int W = 64 * CPL;
+  const int lane = threadIdx.x & 63;
+  float k1[CPL][D], bb[CPL];
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    bb[j] = b1[lane + 64 * j];
+#pragma unroll
+    for (int i = 0; i < D; ++i) k1[j][i] = K1[i * W + lane + 64 * j];
+  }
+  const int64_t nw = (int64_t)gridDim.x * (kT / 64);
+  for (int64_t r = (int64_t)blockIdx.x * (kT / 64) + (threadIdx.x >> 6); r < R; r += nw) {
+    float x[D], g[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      x[i] = z[r * ldz + i];
+      g[i] = 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) {
+      float zz = bb[j];
+#pragma unroll
+      for (int i = 0; i < D; ++i) zz = fmaf(x[i], k1[j][i], zz);
+      const float h = ftanh(zz);
+      const float zeta = (1.f - h * h) * a1[r * W + lane + 64 * j];
+#pragma unroll
+      for (int i = 0; i < D; ++i) g[i] = fmaf(zeta, k1[j][i], g[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < D; ++i) g[i] = wave_sum(g[i]);
+    if (lane == 0) {
+#pragma unroll
+      for (int i = 0; i < D; ++i) G[r * D + i] = g[i];
+    }
+  }
+}
+
+// Layer-1 reverse step and its parameter gradient, from hbar1 streams (R2 final GEMM) and a1:
+//   zbar1 = s1 hb + s2 z1' h'b + s3 z1'^2 h''b + s2 a1 zetabar1,  z'bar1 = s1 h'b + 2 s2 z1' h''b,
+//   zeta1 = s1 a1;  K1[i][k] += x_i zbar1 + v_i z'bar1 + abar0_i zeta1,  b1[k] += zbar1
+// (the third input stream h0'' = 0 carries nothing). Thread owns columns, loops rows; per-block
+// partial slab [(D + 1) x W] (K1 rows then b1 = the flat parameter order).
+constexpr int kL1Rows = 64;  // rows staged in LDS per step
+
+template <int D, int W>
+__global__ __launch_bounds__(kT) void l1_grad_kernel(const float* __restrict__ hb0, const float* __restrict__ hb1,
+                                                     const float* __restrict__ hb2, const float* __restrict__ a1,
+                                                     const float* __restrict__ z, int64_t ldz,
+                                                     const float* __restrict__ abar0, const float* __restrict__ K1,
+                                                     const float* __restrict__ b1, int64_t R, int64_t rpb,
+                                                     float* __restrict__ part) {
+  constexpr int CW = W < kT ? W : kT;       // columns covered per pass
+  constexpr int CPT = W / CW;               // columns per thread
+  constexpr int RPH = kT / CW;              // row phases
+  __shared__ float xs[kL1Rows * 3 * D];
+  __shared__ float red[(RPH > 1 ? RPH : 1) * W];
+  const int tid = threadIdx.x, c0 = tid % CW, ph = tid / CW;
+  float k1[CPT][D], bb[CPT], pacc[CPT][D + 1];
+#pragma unroll
+  for (int j = 0; j < CPT; ++j) {
+    bb[j] = b1[c0 + CW * j];
+#pragma unroll
+    for (int i = 0; i < D; ++i) k1[j][i] = K1[i * W + c0 + CW * j];
+#pragma unroll
+    for (int i = 0; i <= D; ++i) pacc[j][i] = 0.f;
+  }
+  const int64_t rs = (int64_t)blockIdx.x * rpb;
+  const int64_t re = rs + rpb < R ? rs + rpb : R;
+  for (int64_t rb = rs; rb < re; rb += kL1Rows) {
+    __syncthreads();
+    for (int e = tid; e < kL1Rows * 3 * D; e += kT) {
+      const int m = e / (3 * D), c = e - m * (3 * D);
+      const int64_t r = rb + m;
+      xs[e] = r < re ? (c < 2 * D ? z[r * ldz + c] : abar0[r * D + c - 2 * D]) : 0.f;
+    }
+    __syncthreads();
+    const int nr = (int)(re - rb < kL1Rows ? re - rb : kL1Rows);
+    for (int m = ph; m < nr; m += RPH) {
+      const float* x = xs + m * 3 * D;
+      const int64_t rowo = (rb + m) * W;
+#pragma unroll
+      for (int j = 0; j < CPT; ++j) {
+        const int64_t o = rowo + c0 + CW * j;
+        const float hb = hb0[o], hdb = hb1[o], hddb = hb2[o], aL = a1[o];
+        float zz = bb[j], zd = 0.f, zb = 0.f;
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+          zz = fmaf(x[i], k1[j][i], zz);
+          zd = fmaf(x[D + i], k1[j][i], zd);
+          zb = fmaf(x[2 * D + i], k1[j][i], zb);
+        }
+        const float h = ftanh(zz);
+        const float s1 = 1.f - h * h, s2 = -2.f * h * s1, s3 = -2.f * s1 * s1 - 2.f * h * s2;
+        const float zbar = s1 * hb + s2 * zd * hdb + s3 * zd * zd * hddb + s2 * aL * zb;
+        const float zdbar = s1 * hdb + 2.f * s2 * zd * hddb;
+        const float zeta = s1 * aL;
+#pragma unroll
+        for (int i = 0; i < D; ++i)
+          pacc[j][i] = fmaf(x[i], zbar, fmaf(x[D + i], zdbar, fmaf(x[2 * D + i], zeta, pacc[j][i])));
+        pacc[j][D] += zbar;
+      }
+    }
+  }
+  float* out = part + (int64_t)blockIdx.x * (D + 1) * W;
+#pragma unroll
+  for (int i = 0; i <= D; ++i) {
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < CPT; ++j) red[ph * W + c0 + CW * j] = pacc[j][i];
+    __syncthreads();
+    for (int c = tid; c < W; c += kT) {
+      float s = 0.f;
+#pragma unroll
+      for (int p = 0; p < RPH; ++p) s += red[p * W + c];
+      out[i * W + c] = s;
+    }
+  }
+}
+
+// ---- weight gradients -------------------------------------------------------------------
+enum { GA_RAW4 = 0, GA_PL };  // A streams: 4 stored planes | h, s1 z', s1 z'' + s2 z'^2, s1 zetabar
+enum { GB_PL = 0, GB_SM };    // B streams: zbar0..2, s1(h) a | ybar0..2, 2 y
+
+struct WgradArgs {
+  int64_t R;
+  int n_in, n_out;
+  int64_t rows_per_slice;
+  const float *pa0, *pa1, *pa2, *pa3;        // A planes (ld n_in)
+  const float *pb0, *pb1, *pb2, *pb3, *pb4;  // B planes (ld n_out): ZB0..2, H, A  |  YB0..2, Y0
+  float* part;                               // [slices][n_in][n_out]
+};
+
+// Offsets inside one chunk's planes fit in 32 bits (run_chunk checks Bc * W < 2^31), so the
+// loads use a uniform base + 32-bit lane offset.
+template <int BM, int BN, int GA, int GB>
+__global__ __launch_bounds__(kT) void fwgrad(WgradArgs a) {
+  constexpr int WM = BM / 2, WN = BN / 2, MI = WM / 32, NI = WN / 32;
+  static_assert(MI >= 1 && NI >= 1, "tile");
+  constexpr int LDA = BM + 4, LDB = BN + 4;
+  constexpr int NEA = BKG * BM / kT, NEB = BKG * BN / kT;
+  constexpr int NVB = GB == GB_PL ? 5 : 4;
+  extern __shared__ float lds[];
+  float* As = lds;                  // [4][BKG][LDA]  (k = sample row)
+  float* Bs = As + 4 * BKG * LDA;   // [4][BKG][LDB]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1, l31 = lane & 31, hi = lane >> 5;
+  const int tiles_n = (a.n_out + BN - 1) / BN;
+  const int i0 = (blockIdx.x / tiles_n) * BM, n0 = (blockIdx.x % tiles_n) * BN;
+  const int rs0 = (int)((int64_t)blockIdx.y * a.rows_per_slice);
+  const int rs1 = (int)(rs0 + a.rows_per_slice < a.R ? rs0 + a.rows_per_slice : a.R);
+  f32x16 acc[MI][NI];
+#pragma unroll
+  for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[mi][ni][q] = 0.f;
+
+  float ra[NEA][4], rb[NEB][NVB];
+  auto load = [&](int rb0) {
+#pragma unroll
+    for (int j = 0; j < NEA; ++j) {
+      const int e = tid + j * kT, rr = e / BM, ii = e - rr * BM;
+      const int r = rb0 + rr, i = i0 + ii;
+      const bool ok = r < rs1 && i < a.n_in;
+      const int o = ok ? r * a.n_in + i : 0;
+      ra[j][0] = ok ? a.pa0[o] : 0.f;
+      ra[j][1] = ok ? a.pa1[o] : 0.f;
+      ra[j][2] = ok ? a.pa2[o] : 0.f;
+      ra[j][3] = ok ? a.pa3[o] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < NEB; ++j) {
+      const int e = tid + j * kT, rr = e / BN, nn = e - rr * BN;
+      const int r = rb0 + rr, n = n0 + nn;
+      const bool ok = r < rs1 && n < a.n_out;
+      const int o = ok ? r * a.n_out + n : 0;
+      rb[j][0] = ok ? a.pb0[o] : 0.f;
+      rb[j][1] = ok ? a.pb1[o] : 0.f;
+      rb[j][2] = ok ? a.pb2[o] : 0.f;
+      rb[j][3] = ok ? a.pb3[o] : 0.f;
+      if constexpr (NVB > 4) rb[j][4] = ok ? a.pb4[o] : 0.f;
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int j = 0; j < NEA; ++j) {
+      const int e = tid + j * kT, rr = e / BM, ii = e - rr * BM;
+      float v0 = ra[j][0], v1 = ra[j][1], v2 = ra[j][2], v3 = ra[j][3];
+      if constexpr (GA == GA_PL) {
+        const float h = v0, zd = v1, zdd = v2, zeb = v3;
+        const float s1 = 1.f - h * h, s2 = -2.f * h * s1;
+        v1 = s1 * zd;
+        v2 = fmaf(s1, zdd, s2 * zd * zd);
+        v3 = s1 * zeb;
+      }
+      As[(0 * BKG + rr) * LDA + ii] = v0;
+      As[(1 * BKG + rr) * LDA + ii] = v1;
+      As[(2 * BKG + rr) * LDA + ii] = v2;
+      As[(3 * BKG + rr) * LDA + ii] = v3;
+    }
+#pragma unroll
+    for (int j = 0; j < NEB; ++j) {
+      const int e = tid + j * kT, rr = e / BN, nn = e - rr * BN;
+      float v3;
+      if constexpr (GB == GB_PL) {
+        const float h = rb[j][3];
+        v3 = (1.f - h * h) * rb[j][4];
+      } else {
+        v3 = 2.f * rb[j][3];
+      }
+      Bs[(0 * BKG + rr) * LDB + nn] = rb[j][0];
+      Bs[(1 * BKG + rr) * LDB + nn] = rb[j][1];
+      Bs[(2 * BKG + rr) * LDB + nn] = rb[j][2];
+      Bs[(3 * BKG + rr) * LDB + nn] = v3;
+    }
+  };
+
+  if (rs0 < rs1) load(rs0);
+  for (int rb0 = rs0; rb0 < rs1; rb0 += BKG) {
+    __syncthreads();
+    store();
+    __syncthreads();
+    if (rb0 + BKG < rs1) load(rb0 + BKG);  // in flight under this block's MFMAs
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+      for (int kk = 0; kk < BKG; kk += 2) {
+        float bv[NI];
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni) bv[ni] = Bs[(p * BKG + kk + hi) * LDB + wn * WN + ni * 32 + l31];
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi) {
+          const float av = As[(p * BKG + kk + hi) * LDA + wm * WM + mi * 32 + l31];
+#pragma unroll
+          for (int ni = 0; ni < NI; ++ni)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv[ni], acc[mi][ni], 0, 0, 0);
+        }
+      }
+  }
+  float* out = a.part + (int64_t)blockIdx.y * a.n_in * a.n_out;
+#pragma unroll
+  for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) {
+      const int n = n0 + wn * WN + ni * 32 + l31;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int i = i0 + wm * WM + mi * 32 + (q & 3) + 8 * (q >> 2) + 4 * hi;
+        if (i < a.n_in && n < a.n_out) out[(int64_t)i * a.n_out + n] = acc[mi][ni][q];
+      }
+    }
+}
+
+// ---- layer-1 streams stored once (VALU): thread owns columns, rows staged in LDS ------------
+//   fwd:  h1 = tanh(x K1 + b1), h1' = s1 (v K1), h1'' = s2 (v K1)^2      (the FWD A operand)
+//   adj:  abar1 = (1 - h1^2) (abar0 K1)                                  (the F2 A operand)
+template <int D, int W, bool ADJ>
+__global__ __launch_bounds__(kT) void l1_planes_kernel(const float* __restrict__ z, int64_t ldz,
+                                                       const float* __restrict__ abar0,
+                                                       const float* __restrict__ K1, const float* __restrict__ b1,
+                                                       int64_t R, int64_t rpb, float* __restrict__ o0,
+                                                       float* __restrict__ o1, float* __restrict__ o2) {
+  constexpr int CW = W < kT ? W : kT, CPT = W / CW, RPH = kT / CW;
+  constexpr int XW = ADJ ? D : 2 * D;
+  __shared__ float xs[kL1Rows * XW];
+  const int tid = threadIdx.x, c0 = tid % CW, ph = tid / CW;
+  float k1[CPT][D], bb[CPT];
+#pragma unroll
+  for (int j = 0; j < CPT; ++j) {
+    bb[j] = b1[c0 + CW * j];
+#pragma unroll
+    for (int i = 0; i < D; ++i) k1[j][i] = K1[i * W + c0 + CW * j];
+  }
+  const int64_t rs = (int64_t)blockIdx.x * rpb;
+  const int64_t re = rs + rpb < R ? rs + rpb : R;
+  for (int64_t rb = rs; rb < re; rb += kL1Rows) {
+    __syncthreads();
+    for (int e = tid; e < kL1Rows * XW; e += kT) {
+      const int m = e / XW, c = e - m * XW;
+      const int64_t r = rb + m;
+      xs[e] = r < re ? (ADJ ? abar0[r * D + c] : z[r * ldz + c]) : 0.f;
+    }
+    __syncthreads();
+    const int nr = (int)(re - rb < kL1Rows ? re - rb : kL1Rows);
+    for (int m = ph; m < nr; m += RPH) {
+      const float* x = xs + m * XW;
+      const int64_t rowo = (rb + m) * W;
+#pragma unroll
+      for (int j = 0; j < CPT; ++j) {
+        const int64_t o = rowo + c0 + CW * j;
+        if constexpr (ADJ) {
+          float zb = 0.f;
+#pragma unroll
+          for (int i = 0; i < D; ++i) zb = fmaf(x[i], k1[j][i], zb);
+          const float h = o1[o];  // h1 plane (read), abar1 -> o0
+          o0[o] = (1.f - h * h) * zb;
+        } else {
+          float zz = bb[j], zd = 0.f;
+#pragma unroll
+          for (int i = 0; i < D; ++i) {
+            zz = fmaf(x[i], k1[j][i], zz);
+            zd = fmaf(x[D + i], k1[j][i], zd);
+          }
+          const float h = ftanh(zz), s1 = 1.f - h * h;
+          o0[o] = h;
+          o1[o] = s1 * zd;
+          o2[o] = -2.f * h * s1 * zd * zd;
+        }
+      }
+    }
+  }
+}
+
+// Fixed-order slab sums: out[i] += sum_s part[s][i]. Many slabs are first folded in groups of
+// kFold (more parallelism, same order every run), then the group sums are added.
+constexpr int kFold = 16;
+
+__global__ void fold_slabs_kernel(const float* __restrict__ part, int S, int64_t n, float* __restrict__ out2) {
+  const int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x;
+  if (i >= n) return;
+  const int s0 = blockIdx.y * kFold, s1 = s0 + kFold < S ? s0 + kFold : S;
+  float s = 0.f;
+  for (int k = s0; k < s1; ++k) s += part[(int64_t)k * n + i];
+  out2[(int64_t)blockIdx.y * n + i] = s;
+}
+
+__global__ void sum_slabs_kernel(const float* __restrict__ part, int S, int64_t n, float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x;
+  if (i >= n) return;
+  float s = 0.f;
+  for (int k = 0; k < S; ++k) s += part[(int64_t)k * n + i];
+  out[i] += s;
+}
+
+// ---- host side ------------------------------------------------------------------------
+constexpr int kMaxWgradSlices = 256;
+constexpr int kRowGridCap = 1024;  // workgroups per row GEMM launch (persistent over row blocks)
+
+static int mblocks(int64_t R, int BM) { return (int)((R + BM - 1) / BM); }
+
+static int sum_slabs(const float* part, int S, int64_t n, float* out, float* scratch, hipStream_t st) {
+  const unsigned gx = (unsigned)((n + kT - 1) / kT);
+  if (S > 2 * kFold) {
+    const int G = (S + kFold - 1) / kFold;
+    hipLaunchKernelGGL(fold_slabs_kernel, dim3(gx, G), dim3(kT), 0, st, part, S, n, scratch);
+    part = scratch;
+    S = G;
+  }
+  hipLaunchKernelGGL(sum_slabs_kernel, dim3(gx), dim3(kT), 0, st, part, S, n, out);
+  return check_launch("kfp_mlp fused slab sum");
+}
+
+template <int S, int BM, int BN, int WGM, int AM, int BMD, int EM>
+static int launch_gemm(GemmArgs a, hipStream_t st, int* grid_x_out = nullptr) {
+  const size_t bytes = ((size_t)S * BK * (BM + 4) + (size_t)BK * (BN + 4)) * sizeof(float);
+  auto kern = fgemm<S, BM, BN, WGM, AM, BMD, EM>;
+  if (bytes > 64 * 1024)
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  a.n_mblocks = mblocks(a.R, BM);
+  const int gy = (a.N + BN - 1) / BN;
+  const int gx = std::max(1, std::min(a.n_mblocks, kRowGridCap / gy));
+  if (grid_x_out) *grid_x_out = gx;
+  hipLaunchKernelGGL(kern, dim3(gx, gy), dim3(kT), bytes, st, a);
+  return check_launch("kfp_mlp fused row GEMM");
+}
+
+// single-stream GEMM over N = W: full-width 256-column tiles when W allows (A built once per row)
+template <int AM, int BMD>
+static int launch_gemm1(GemmArgs a, hipStream_t st) {
+  if (a.N % 256 == 0) return launch_gemm<1, 64, 256, 2, AM, BMD, E_STORE>(a, st);
+  return launch_gemm<1, 64, 128, 2, AM, BMD, E_STORE>(a, st);
+}
+
+template <int BM, int BN, int GA, int GB>
+static int launch_wgrad(WgradArgs a, float* grad_out, float* scratch, hipStream_t st) {
+  const size_t bytes = ((size_t)4 * BKG * (BM + 4) + (size_t)4 * BKG * (BN + 4)) * sizeof(float);
+  auto kern = fwgrad<BM, BN, GA, GB>;
+  if (bytes > 64 * 1024)
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  const int tiles = ((a.n_in + BM - 1) / BM) * ((a.n_out + BN - 1) / BN);
+  int slices = std::max(1, std::min(kMaxWgradSlices, 1024 / tiles));
+  int64_t rps = (a.R + slices - 1) / slices;
+  rps = ((rps + BKG - 1) / BKG) * BKG;
+  slices = (int)((a.R + rps - 1) / rps);
+  a.rows_per_slice = rps;
+  hipLaunchKernelGGL(kern, dim3(tiles, slices), dim3(kT), bytes, st, a);
+  int rc = check_launch("kfp_mlp fused weight gradient");
+  if (rc) return rc;
+  return sum_slabs(a.part, slices, (int64_t)a.n_in * a.n_out, grad_out, scratch, st);
+}
+
+bool supported(int d, int L, int W, int O) {
+  return (d == 2 || d == 4 || d == 8 || d == 16) && L >= 2 && L <= 16 && (W == 128 || W == 256 || W == 512) &&
+         O >= 1 && O <= 64;
+}
+
+// workspace layout (floats), chunk of Bc rows
+struct Layout {
+  size_t layer0, layer_stride, h1, abar1, a1, hb1, ys, yb, terms, g, abar0, part, part2, total;
+};
+enum { P_H = 0, P_ZD, P_ZDD, P_A, P_ZETABAR, P_ZB0, P_ZB1, P_ZB2, kPlanes };
+
+static size_t part_floats(int d, int W, int O) {
+  size_t m = (size_t)kRowGridCap * (d + 1) * W;                  // layer-1 gradient slabs
+  m = std::max(m, (size_t)kRowGridCap * std::max(W, O));         // bias slabs
+  m = std::max(m, (size_t)kMaxWgradSlices * W * std::max(W, O)); // weight-gradient slabs
+  return m;
+}
+
+static Layout layout(int d, int L, int W, int O, int64_t Bc) {
+  Layout y{};
+  size_t o = 0;
+  auto take = [&](size_t n) { const size_t at = o; o += (n + 63) & ~(size_t)63; return at; };
+  const size_t plane = ((size_t)Bc * W + 63) & ~(size_t)63;
+  y.layer_stride = plane * kPlanes;
+  y.layer0 = take(y.layer_stride * (L - 1));
+  y.h1 = take(3 * plane);
+  y.abar1 = take(plane);
+  y.a1 = take(plane);
+  y.hb1 = take(3 * plane);
+  y.ys = take((size_t)3 * Bc * O);
+  y.yb = take((size_t)3 * Bc * O);
+  y.terms = take((size_t)2 * Bc);
+  y.g = take((size_t)Bc * d);
+  y.abar0 = take((size_t)Bc * d);
+  y.part = take(part_floats(d, W, O));
+  y.part2 = take(part_floats(d, W, O) / kFold + 64);
+  y.total = o;
+  return y;
+}
+
+size_t workspace_floats(int d, int L, int W, int O, int64_t Bc) { return layout(d, L, W, O, Bc).total; }
+
+template <int D, int WB>
+static int run_chunk_t(const Chunk& c, const LossHook& loss, hipStream_t st) {
+  const int L = c.L, W = c.W, O = c.O;
+  const int64_t R = c.R;
+  const Layout y = layout(D, L, W, O, c.Bc);
+  float* ws = c.ws;
+  const size_t plane = ((size_t)c.Bc * W + 63) & ~(size_t)63;
+  auto P = [&](int l, int k) { return ws + y.layer0 + y.layer_stride * (size_t)(l - 2) + plane * k; };
+  float* H1[3] = {ws + y.h1, ws + y.h1 + plane, ws + y.h1 + 2 * plane};
+  float* ABAR1 = ws + y.abar1;
+  float* A1 = ws + y.a1;
+  float* HB1[3] = {ws + y.hb1, ws + y.hb1 + plane, ws + y.hb1 + 2 * plane};
+  float* Ys[3] = {ws + y.ys, ws + y.ys + (size_t)c.Bc * O, ws + y.ys + 2 * (size_t)c.Bc * O};
+  float* YB[3] = {ws + y.yb, ws + y.yb + (size_t)c.Bc * O, ws + y.yb + 2 * (size_t)c.Bc * O};
+  float2* terms = (float2*)(ws + y.terms);
+  float* G = ws + y.g;
+  float* abar0 = ws + y.abar0;
+  float* part = ws + y.part;
+  float* part2 = ws + y.part2;
+  const float* prm = c.params;
+  auto Kw = [&](int l) { return prm + c.poff[l - 1]; };  // hidden layer l (1-based) kernel
+  auto Bw = [&](int l) { return prm + c.boff[l - 1]; };
+  const float* Ko = prm + c.poff[L];
+  const float* bo = prm + c.boff[L];
+
+  GemmArgs base{};
+  base.R = R;
+  base.c2 = c.c2;
+  base.c3 = c.c3;
+  base.part = part;
+  int rc = 0;
+#define RC(x)          \
+  do {                 \
+    rc = (x);          \
+    if (rc) return rc; \
+  } while (0)
+
+  const int l1_blocks = (int)std::min<int64_t>((R + kL1Rows - 1) / kL1Rows, kRowGridCap);
+  const int64_t l1_rpb = (R + l1_blocks - 1) / l1_blocks;
+  // ---- F1 -------------------------------------------------------------------------------
+  hipLaunchKernelGGL((l1_planes_kernel<D, WB, false>), dim3(l1_blocks), dim3(kT), 0, st, c.z, c.ldz, nullptr, Kw(1),
+                     Bw(1), R, l1_rpb, H1[0], H1[1], H1[2]);
+  RC(check_launch("kfp_mlp fused layer-1 streams"));
+  {
+    GemmArgs a = base;
+    a.K = W; a.N = W; a.Bw = Kw(2); a.bias = Bw(2);
+    a.pa0 = H1[0]; a.pa1 = H1[1]; a.pa2 = H1[2];
+    a.po0 = P(2, P_H); a.po1 = P(2, P_ZD); a.po2 = P(2, P_ZDD);
+    RC((launch_gemm<3, 64, 128, 2, A_S3, B_NN, E_ACT_FWD>(a, st)));
+  }
+  for (int l = 3; l <= L; ++l) {
+    GemmArgs a = base;
+    a.K = W; a.N = W; a.Bw = Kw(l); a.bias = Bw(l);
+    a.pa0 = P(l - 1, P_H); a.pa1 = P(l - 1, P_ZD); a.pa2 = P(l - 1, P_ZDD);
+    a.po0 = P(l, P_H); a.po1 = P(l, P_ZD); a.po2 = P(l, P_ZDD);
+    RC((launch_gemm<3, 64, 128, 2, A_FWD, B_NN, E_ACT_FWD>(a, st)));
+  }
+  {
+    GemmArgs a = base;
+    a.K = W; a.N = O; a.Bw = Ko; a.bias = bo;
+    a.pa0 = P(L, P_H); a.pa1 = P(L, P_ZD); a.pa2 = P(L, P_ZDD);
+    a.po0 = Ys[0]; a.po1 = Ys[1]; a.po2 = Ys[2]; a.terms = terms;
+    RC((launch_gemm<3, 128, 64, 4, A_FWD, B_NN, E_OUT>(a, st)));
+  }
+  // ---- R1: grad_x chain -------------------------------------------------------------------
+  {
+    GemmArgs a = base;
+    a.K = O; a.N = W; a.Bw = Ko; a.pa0 = Ys[0]; a.po0 = P(L, P_A);
+    RC((launch_gemm1<A_U, B_NT>(a, st)));
+  }
+  for (int l = L; l >= 2; --l) {
+    GemmArgs a = base;
+    a.K = W; a.N = W; a.Bw = Kw(l); a.pa0 = P(l, P_H); a.pa1 = P(l, P_A);
+    a.po0 = l > 2 ? P(l - 1, P_A) : A1;
+    RC((launch_gemm1<A_S1MUL, B_NT>(a, st)));
+  }
+  {
+    const int blocks = (int)std::min<int64_t>((R + 3) / 4, 2048);
+    hipLaunchKernelGGL((l1_g_kernel<D, WB / 64>), dim3(blocks), dim3(kT), 0, st, A1, c.z, c.ldz, Kw(1), Bw(1), R, G);
+    RC(check_launch("kfp_mlp fused g"));
+  }
+  RC(loss.fn(loss.ctx, G, terms, abar0, R, st));
+  // ---- F2: forward adjoint ----------------------------------------------------------------
+  hipLaunchKernelGGL((l1_planes_kernel<D, WB, true>), dim3(l1_blocks), dim3(kT), 0, st, c.z, c.ldz, abar0, Kw(1),
+                     Bw(1), R, l1_rpb, ABAR1, H1[0], nullptr);
+  RC(check_launch("kfp_mlp fused layer-1 adjoint"));
+  {
+    GemmArgs a = base;
+    a.K = W; a.N = W; a.Bw = Kw(2); a.pa0 = ABAR1; a.po0 = P(2, P_ZETABAR);
+    RC((launch_gemm1<A_RAW1, B_NN>(a, st)));
+  }
+  for (int l = 3; l <= L; ++l) {
+    GemmArgs a = base;
+    a.K = W; a.N = W; a.Bw = Kw(l); a.pa0 = P(l - 1, P_H); a.pa1 = P(l - 1, P_ZETABAR);
+    a.po0 = P(l, P_ZETABAR);
+    RC((launch_gemm1<A_S1MUL, B_NN>(a, st)));
+  }
+  {
+    GemmArgs a = base;
+    a.K = W; a.N = O; a.Bw = Ko; a.pa0 = P(L, P_H); a.pa1 = P(L, P_ZETABAR);
+    a.pe0 = Ys[0]; a.pe1 = Ys[1]; a.pe2 = Ys[2];
+    a.po0 = YB[0]; a.po1 = YB[1]; a.po2 = YB[2];
+    int gx = 0;
+    RC((launch_gemm<1, 128, 64, 4, A_S1MUL, B_NN, E_SEEDS>(a, st, &gx)));
+    RC(sum_slabs(part, gx, O, c.grad + c.boff[L], part2, st));
+  }
+  // ---- R2: reverse over the forward streams -------------------------------------------------
+  {
+    GemmArgs a = base;
+    a.K = O; a.N = W; a.Bw = Ko;
+    a.pa0 = YB[0]; a.pa1 = YB[1]; a.pa2 = YB[2];
+    a.pe0 = P(L, P_H); a.pe1 = P(L, P_ZD); a.pe2 = P(L, P_ZDD); a.pe3 = P(L, P_A); a.pe4 = P(L, P_ZETABAR);
+    a.po0 = P(L, P_ZB0); a.po1 = P(L, P_ZB1); a.po2 = P(L, P_ZB2);
+    int gx = 0;
+    RC((launch_gemm<3, 64, 128, 2, A_S3, B_NT, E_ACT_BWD>(a, st, &gx)));
+    RC(sum_slabs(part, gx, W, c.grad + c.boff[L - 1], part2, st));
+  }
+  for (int l = L; l >= 3; --l) {
+    GemmArgs a = base;
+    a.K = W; a.N = W; a.Bw = Kw(l);
+    a.pa0 = P(l, P_ZB0); a.pa1 = P(l, P_ZB1); a.pa2 = P(l, P_ZB2);
+    a.pe0 = P(l - 1, P_H); a.pe1 = P(l - 1, P_ZD); a.pe2 = P(l - 1, P_ZDD); a.pe3 = P(l - 1, P_A);
+    a.pe4 = P(l - 1, P_ZETABAR);
+    a.po0 = P(l - 1, P_ZB0); a.po1 = P(l - 1, P_ZB1); a.po2 = P(l - 1, P_ZB2);
+    int gx = 0;
+    RC((launch_gemm<3, 64, 128, 2, A_S3, B_NT, E_ACT_BWD>(a, st, &gx)));
+    RC(sum_slabs(part, gx, W, c.grad + c.boff[l - 2], part2, st));
+  }
+  {
+    GemmArgs a = base;
+    a.K = W; a.N = W; a.Bw = Kw(2);
+    a.pa0 = P(2, P_ZB0); a.pa1 = P(2, P_ZB1); a.pa2 = P(2, P_ZB2);
+    a.po0 = HB1[0]; a.po1 = HB1[1]; a.po2 = HB1[2];
+    RC((launch_gemm<3, 64, 128, 2, A_S3, B_NT, E_STORE3>(a, st)));
+    hipLaunchKernelGGL((l1_grad_kernel<D, WB>), dim3(l1_blocks), dim3(kT), 0, st, HB1[0], HB1[1], HB1[2], A1, c.z,
+                       c.ldz, abar0, Kw(1), Bw(1), R, l1_rpb, part);
+    RC(check_launch("kfp_mlp fused layer-1 gradient"));
+    RC(sum_slabs(part, l1_blocks, (int64_t)(D + 1) * W, c.grad + c.poff[0], part2, st));  // K1 then b1
+  }
+  // ---- G: weight gradients ------------------------------------------------------------------
+  {
+    WgradArgs g{};
+    g.R = R; g.n_in = W; g.n_out = O; g.part = part;
+    g.pa0 = P(L, P_H); g.pa1 = P(L, P_ZD); g.pa2 = P(L, P_ZDD); g.pa3 = P(L, P_ZETABAR);
+    g.pb0 = YB[0]; g.pb1 = YB[1]; g.pb2 = YB[2]; g.pb3 = Ys[0];
+    RC((launch_wgrad<128, 64, GA_PL, GB_SM>(g, c.grad + c.poff[L], part2, st)));
+  }
+  for (int l = L; l >= 3; --l) {
+    WgradArgs g{};
+    g.R = R; g.n_in = W; g.n_out = W; g.part = part;
+    g.pa0 = P(l - 1, P_H); g.pa1 = P(l - 1, P_ZD); g.pa2 = P(l - 1, P_ZDD); g.pa3 = P(l - 1, P_ZETABAR);
+    g.pb0 = P(l, P_ZB0); g.pb1 = P(l, P_ZB1); g.pb2 = P(l, P_ZB2); g.pb3 = P(l, P_H); g.pb4 = P(l, P_A);
+    RC((launch_wgrad<128, 128, GA_PL, GB_PL>(g, c.grad + c.poff[l - 1], part2, st)));
+  }
+  {
+    WgradArgs g{};
+    g.R = R; g.n_in = W; g.n_out = W; g.part = part;
+    g.pa0 = H1[0]; g.pa1 = H1[1]; g.pa2 = H1[2]; g.pa3 = ABAR1;
+    g.pb0 = P(2, P_ZB0); g.pb1 = P(2, P_ZB1); g.pb2 = P(2, P_ZB2); g.pb3 = P(2, P_H); g.pb4 = P(2, P_A);
+    RC((launch_wgrad<128, 128, GA_RAW4, GB_PL>(g, c.grad + c.poff[1], part2, st)));
+  }
+#undef RC
+  return 0;
+}
+
+template <int D>
+static int run_chunk_d(const Chunk& c, const LossHook& loss, hipStream_t st) {
+  switch (c.W) {
+    case 128: return run_chunk_t<D, 128>(c, loss, st);
+    case 256: return run_chunk_t<D, 256>(c, loss, st);
+    case 512: return run_chunk_t<D, 512>(c, loss, st);
+    default: return fail(PDEINV_ERR_UNSUPPORTED, "kfp_mlp fused: width must be 128, 256 or 512");
+  }
+}
+
+int run_chunk(const Chunk& c, const LossHook& loss, hipStream_t st) {
+  if (!supported(c.d, c.L, c.W, c.O)) return fail(PDEINV_ERR_UNSUPPORTED, "kfp_mlp fused: unsupported shape");
+  if (c.Bc * (int64_t)c.W >= ((int64_t)1 << 31))
+    return fail(PDEINV_ERR_INVALID, "kfp_mlp fused: chunk_rows * width must stay below 2^31");
+  if (c.R <= 0) return 0;
+  switch (c.d) {
+    case 2: return run_chunk_d<2>(c, loss, st);
+    case 4: return run_chunk_d<4>(c, loss, st);
+    case 8: return run_chunk_d<8>(c, loss, st);
+    case 16: return run_chunk_d<16>(c, loss, st);
+    default: return fail(PDEINV_ERR_UNSUPPORTED, "kfp_mlp fused: dim must be 2, 4, 8 or 16");
+  }
+}
+
+}  // namespace mlpf
+}  // namespace pdeinv
+
+extern "C" int pdeinv_mlp_fused_supported(int32_t dim, int32_t n_layers, int32_t width, int32_t out_features) {
+  return pdeinv::mlpf::supported(dim, n_layers, width, out_features) ? 1 : 0;
+}

@@ -45,7 +45,8 @@ EXPORTED_SYMBOLS = (
     "pdeinv_runtime_version", "pdeinv_moments_batched_workspace_bytes", "pdeinv_moments_batched",
     "pdeinv_kmv_weights_workspace_bytes", "pdeinv_kmv_weights", "pdeinv_residual_kmv",
     "pdeinv_mlp_param_count", "pdeinv_residual_kfp_mlp_workspace_bytes", "pdeinv_residual_kfp_mlp",
-    "pdeinv_kfp_terms_finalize", "pdeinv_gather_random_step",
+    "pdeinv_kfp_terms_finalize", "pdeinv_gather_random_step", "pdeinv_mlp_fused_supported",
+    "pdeinv_adam_update",
 )
 
 
@@ -80,7 +81,10 @@ class KfpMlpDesc(ctypes.Structure):
                 ("sigma_true", ctypes.c_float), ("true_params", ctypes.c_void_p), ("gamma", ctypes.c_float),
                 ("c_nabla", ctypes.c_float), ("c_hess", ctypes.c_float), ("c_fric", ctypes.c_float),
                 ("c_true", ctypes.c_float), ("c_init", ctypes.c_float), ("c_term", ctypes.c_float),
-                ("chunk_rows", ctypes.c_int64)]
+                ("chunk_rows", ctypes.c_int64), ("impl", ctypes.c_int32)]
+
+
+MLP_IMPL_AUTO, MLP_IMPL_LIBRARY, MLP_IMPL_FUSED = 0, 1, 2
 
 
 class KfpGmmDesc(ctypes.Structure):
@@ -140,6 +144,8 @@ def lib():
         "pdeinv_kmv_weights": (i32, [i32, f32, P, P, i64, i64, i64, i64, P, P, P, P]),
         "pdeinv_residual_kmv": (i32, [P, P, P, P, P, P, P]),
         "pdeinv_mlp_param_count": (i64, [i32, i32, i32, i32]),
+        "pdeinv_mlp_fused_supported": (i32, [i32, i32, i32, i32]),
+        "pdeinv_adam_update": (i32, [P, P, P, P, i64, f32, f32, f32, f32, f32, i32, P]),
         "pdeinv_residual_kfp_mlp_workspace_bytes": (ctypes.c_size_t, [P]),
         "pdeinv_residual_kfp_mlp": (i32, [P, P, i64, i64, P, i64, i64, P, i64, i64, P, P, P, P, P]),
         "pdeinv_kfp_terms_finalize": (i32, [P, P, i64, f32, P, P]),
@@ -539,7 +545,8 @@ def mf_workspace(desc: SdeDesc, device) -> torch.Tensor:
 # -----------------------------------------------------------------------------------------
 def residual_kfp_mlp(dims, params_flat: torch.Tensor, z_init: torch.Tensor, z_term: torch.Tensor,
                      z_0T: torch.Tensor, *, true_kind: int, true_params, gamma: float, total_time: float,
-                     sigma_true: float = 1.0, world_scale: float = 1.0, chunk_rows: int = 1 << 18):
+                     sigma_true: float = 1.0, world_scale: float = 1.0, chunk_rows: int = 1 << 18,
+                     impl: int = MLP_IMPL_AUTO):
     """kinetic_fokker_planck.py:11-69 for V_hypothesis. dims = [d, W, ..., W, out] (equal hidden widths).
     Returns (acc fp64 [8], grad fp32 [P]) — sums with the reference's loss weights."""
     _require_gpu()
@@ -561,7 +568,8 @@ def residual_kfp_mlp(dims, params_flat: torch.Tensor, z_init: torch.Tensor, z_te
     c = {k: v * world_scale for k, v in c.items()}
     desc = KfpMlpDesc(d, L, W, O, int(true_kind), int(tp.size // d) if true_kind == POT_GMM else 0,
                       float(sigma_true), tp.ctypes.data_as(ctypes.c_void_p), float(gamma), c["c_nabla"],
-                      c["c_hess"], c["c_fric"], c["c_true"], c["c_init"], c["c_term"], int(chunk_rows))
+                      c["c_hess"], c["c_fric"], c["c_true"], c["c_init"], c["c_term"], int(chunk_rows),
+                      int(impl))
     nbytes = lib().pdeinv_residual_kfp_mlp_workspace_bytes(ctypes.byref(desc))
     ws = torch.empty(nbytes // 4, device=z_0T.device, dtype=torch.float32)
     acc = torch.zeros(GMM_NACC, device=z_0T.device, dtype=torch.float64)
@@ -570,6 +578,24 @@ def residual_kfp_mlp(dims, params_flat: torch.Tensor, z_init: torch.Tensor, z_te
                                          _dev(params_flat, "params"), _dev(ws, "ws"), _dev(acc, "acc", torch.float64),
                                          _dev(grad, "grad"), stream_handle()), "pdeinv_residual_kfp_mlp")
     return acc, grad
+
+
+def adam_update(params: torch.Tensor, grad: torch.Tensor, mu: torch.Tensor, nu: torch.Tensor, *, lr: float,
+                b1: float, b2: float, eps: float, weight_decay: float, count: int) -> None:
+    """In-place fused add_decayed_weights + adam + apply_updates on contiguous fp32 device tensors."""
+    _require_gpu()
+    n = params.numel()
+    for t, name in ((params, "params"), (grad, "grad"), (mu, "mu"), (nu, "nu")):
+        if t.numel() != n or not t.is_contiguous():
+            raise ValueError(f"adam_update: {name} must be contiguous with {n} elements")
+    _check(lib().pdeinv_adam_update(_dev(params, "params"), _dev(grad, "grad"), _dev(mu, "mu"), _dev(nu, "nu"), n,
+                                    float(lr), float(b1), float(b2), float(eps), float(weight_decay), int(count),
+                                    stream_handle()), "pdeinv_adam_update")
+
+
+def mlp_fused_supported(dims) -> bool:
+    """True when residual_kfp_mlp runs the fused MFMA path for this V_hypothesis shape."""
+    return bool(lib().pdeinv_mlp_fused_supported(dims[0], len(dims) - 2, dims[1], dims[-1]))
 
 
 def kfp_terms_finalize(acc: torch.Tensor, grad: torch.Tensor, gamma: float) -> torch.Tensor:

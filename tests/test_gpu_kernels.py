@@ -246,11 +246,19 @@ def test_sde_edge_cases(native):
         native.sde_simulate(_t(np.ones((3, 4))), 0, 0.1, 1.0, pot, seed=1)
 
 
-@pytest.mark.parametrize("dims,true_kind,chunk", [([2, 16, 16, 5], "gmm", 1000), ([4, 32, 32, 40], "quad", 1 << 18),
-                                                   ([8, 64, 64, 64, 40], "gmm", 777)])
-def test_residual_mlp_vs_restatement(native, dims, true_kind, chunk):
+LIB, FUSED = 1, 2  # native.MLP_IMPL_LIBRARY / MLP_IMPL_FUSED
+
+
+@pytest.mark.parametrize("dims,true_kind,chunk,impl", [
+    ([2, 16, 16, 5], "gmm", 1000, LIB), ([4, 32, 32, 40], "quad", 1 << 18, LIB),
+    ([8, 64, 64, 64, 40], "gmm", 777, LIB), ([8, 256, 256, 40], "gmm", 1 << 18, LIB),
+    ([2, 128, 128, 5], "gmm", 1000, FUSED), ([4, 128, 128, 40], "quad", 1 << 18, FUSED),
+    ([8, 256, 256, 40], "gmm", 777, FUSED), ([16, 128, 128, 128, 64], "quad", 1500, FUSED),
+    ([8, 512, 512, 512, 40], "gmm", 3000, FUSED)])
+def test_residual_mlp_vs_restatement(native, dims, true_kind, chunk, impl):
     """V_hypothesis residual (value + d loss/d theta) vs the fp64 restatement whose adjoint is
-    FD-checked in tests/test_oracle.py. Multi-chunk paths exercised (chunk < rows)."""
+    FD-checked in tests/test_oracle.py, on both implementations (rocBLAS library path and the
+    fused MFMA path). Multi-chunk paths exercised (chunk < rows); L = 3 covers the middle layers."""
     rng = np.random.default_rng(len(dims) + dims[1])
     d = dims[0]
     flat = np.concatenate([np.concatenate([rng.standard_normal((dims[i], dims[i + 1])).ravel() * np.sqrt(1.0 / dims[i]),
@@ -264,7 +272,8 @@ def test_residual_mlp_vs_restatement(native, dims, true_kind, chunk):
         F = nr.problem_constants(d)
         kind, tp, gt = native.POT_QUADRATIC, F, nr.grad_quadratic(F)
     acc, grad = native.residual_kfp_mlp(dims, _t(flat), _t(zi), _t(zt), _t(z0), true_kind=kind, true_params=tp,
-                                        gamma=0.5, total_time=2.0, chunk_rows=chunk)
+                                        gamma=0.5, total_time=2.0, chunk_rows=chunk, impl=impl)
+    assert impl != FUSED or native.mlp_fused_supported(dims)
     out = native.kfp_terms_finalize(acc, grad, 0.5).cpu().numpy()
     loss, loss_gt, parts = nr.kfp_mlp_loss(P, zi, zt, z0, gt, 0.5, 2.0)
     g_ref = nr.mlp_flat(nr.kfp_mlp_grad_analytic(P, zi, zt, z0, 0.5, 2.0))
@@ -274,6 +283,26 @@ def test_residual_mlp_vs_restatement(native, dims, true_kind, chunk):
     g = grad.cpu().numpy()
     assert np.max(np.abs(g - g_ref)) < 2e-3 * (1 + np.abs(g_ref).max()), np.max(np.abs(g - g_ref))
     assert abs(out[2] - np.linalg.norm(g_ref)) < 2e-3 * (1 + np.linalg.norm(g_ref))
+
+
+def test_residual_mlp_fused_matches_library(native):
+    """The two implementations agree to fp32 reassociation level on the C5 shape, and the fused
+    path is deterministic run to run (fixed-order slab sums, no atomics)."""
+    dims = [8, 256, 256, 40]
+    rng = np.random.default_rng(11)
+    flat = np.concatenate([np.concatenate([rng.standard_normal((dims[i], dims[i + 1])).ravel() * np.sqrt(2.0 / dims[i]),
+                                           np.zeros(dims[i + 1])]) for i in range(len(dims) - 1)])
+    zi, zt, z0 = (_t(rng.standard_normal((m, 16)) * 2) for m in (3000, 3000, 40000))
+    mus = nr.gmm_centres(8, 8)
+    kw = dict(true_kind=native.POT_GMM, true_params=mus, gamma=0.5, total_time=2.0, chunk_rows=16384)
+    a_l, g_l = native.residual_kfp_mlp(dims, _t(flat), zi, zt, z0, impl=LIB, **kw)
+    a_f, g_f = native.residual_kfp_mlp(dims, _t(flat), zi, zt, z0, impl=FUSED, **kw)
+    a_f2, g_f2 = native.residual_kfp_mlp(dims, _t(flat), zi, zt, z0, impl=FUSED, **kw)
+    assert torch.equal(a_f, a_f2) and torch.equal(g_f, g_f2)
+    a_l, a_f = a_l.cpu().numpy(), a_f.cpu().numpy()
+    assert np.allclose(a_f, a_l, rtol=2e-4, atol=1e-5 * np.abs(a_l).max()), (a_f, a_l)
+    g_l, g_f = g_l.cpu().numpy(), g_f.cpu().numpy()
+    assert np.max(np.abs(g_f - g_l)) < 2e-4 * np.abs(g_l).max(), np.max(np.abs(g_f - g_l))
 
 
 def test_gather_random_step(native):
@@ -289,3 +318,25 @@ def test_gather_random_step(native):
     cnt = np.bincount(t, minlength=n)
     chi2 = np.sum((cnt - N / n) ** 2 / (N / n))
     assert chi2 < 80
+
+
+def test_adam_update_matches_optax_formula(native):
+    """pdeinv_adam_update == optax.chain(add_decayed_weights(wd), adam(lr, b1, b2, eps)) + apply_updates
+    (core/trainer.py:85-86, main.py:11-29), evaluated in fp64 on the host, over several steps."""
+    rng = np.random.default_rng(4)
+    n, lr, b1, b2, eps, wd = 78376, 1e-3, 0.9, 0.999, 1e-4, 1e-2
+    p = rng.standard_normal(n)
+    mu, nu = np.zeros(n), np.zeros(n)
+    dp, dmu, dnu = _t(p), _t(mu), _t(nu)
+    for t in range(1, 5):
+        g = rng.standard_normal(n)
+        native.adam_update(dp, _t(g), dmu, dnu, lr=lr, b1=b1, b2=b2, eps=eps, weight_decay=wd, count=t)
+        g = g + wd * p
+        mu = b1 * mu + (1 - b1) * g
+        nu = b2 * nu + (1 - b2) * g * g
+        p = p - lr * (mu / (1 - b1 ** t)) / (np.sqrt(nu / (1 - b2 ** t)) + eps)
+    assert np.allclose(dp.cpu().numpy(), p, rtol=0, atol=2e-6)
+    assert np.allclose(dmu.cpu().numpy(), mu, rtol=1e-5, atol=1e-6)
+    assert np.allclose(dnu.cpu().numpy(), nu, rtol=1e-5, atol=1e-7)
+    with pytest.raises(ValueError):
+        native.adam_update(dp, _t(np.zeros(3)), dmu, dnu, lr=lr, b1=b1, b2=b2, eps=eps, weight_decay=wd, count=1)
