@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define PDEINV_ABI_VERSION 1
+#define PDEINV_ABI_VERSION 2
 #define PDEINV_MAX_DIM 16          /* d (configuration-space dimension) */
 #define PDEINV_MAX_PARAMS 256      /* floats of potential parameters passed by value */
 
@@ -265,8 +265,9 @@ typedef struct {
   float gamma;
   const float* tilde_F;  /* HOST [d*d]: Phi* = 0.5 y^T tilde_F y (…_quadratic.py:193-203) */
 } pdeinv_kmv_desc;
+size_t pdeinv_residual_kmv_workspace_bytes(const pdeinv_kmv_desc* desc);
 int pdeinv_residual_kmv(const pdeinv_kmv_desc* desc, const double* d_mom, const double* d_wstats,
-                        const float* d_theta, float* d_out, float* d_grad, void* stream);
+                        const float* d_theta, void* d_workspace, float* d_out, float* d_grad, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * KFP residual for the non-parametric hypothesis V_hypothesis (core/model.py:32-62):

@@ -109,84 +109,122 @@ struct KmvArgs {
 //   value = (1/N) sum_t [ 1/2 tr(S Wxx_t) - xbar_t^T S Wx_t + 1/2 W_t tr(S M_t) + b.(Wx_t - W_t xbar_t) ]
 //   true  = (1/N) sum_t n_t tr(F C_t F)              gt = (1/N) sum_t n_t tr(D C_t D^T) + b.b, D = F - S
 //   loss  = nabla - 2 hess + 2 value + true
-__global__ __launch_bounds__(kBlock) void kmv_finalize_kernel(KmvArgs a, const double* __restrict__ mom,
-                                                              const double* __restrict__ wst,
-                                                              const float* __restrict__ theta,
-                                                              float* __restrict__ out,
-                                                              float* __restrict__ grad) {
-  const int d = a.d, m = 2 * d, Lz = moment_len(m), Lw = moment_len(d);
-  auto S = [&](int i, int j) { return (double)theta[i * d + j] + (double)theta[j * d + i]; };
-  auto b = [&](int i) { return (double)theta[d * d + i]; };
-  auto F = [&](int i, int j) { return (double)a.F[i * d + j]; };
-  auto tri = [](int i, int j, int mm) {
-    if (i > j) { const int t = i; i = j; j = t; }
-    return i * mm - i * (i - 1) / 2 + (j - i);
-  };
-  // global counts and E[v v^T]
-  double Ntot = 0;
-  for (int t = 0; t < a.n_sets; ++t) Ntot += mom[(int64_t)t * Lz];
-  const double invN = Ntot > 0 ? 1.0 / Ntot : 0.0;
-  auto xbar = [&](int t, int i) {
-    const double* v = mom + (int64_t)t * Lz;
-    return v[0] > 0 ? v[1 + i] / v[0] : 0.0;
-  };
-  auto Mx = [&](int t, int i, int j) {  // E_t[x_i x_j]
-    const double* v = mom + (int64_t)t * Lz;
-    return v[0] > 0 ? v[1 + m + tri(i, j, m)] / v[0] : 0.0;
-  };
-  auto Cx = [&](int t, int i, int j) { return Mx(t, i, j) - xbar(t, i) * xbar(t, j); };
-  auto Mvv = [&](int i, int j) {
-    double s = 0;
-    for (int t = 0; t < a.n_sets; ++t) s += mom[(int64_t)t * Lz + 1 + m + tri(d + i, d + j, m)];
-    return s * invN;
-  };
-  auto W = [&](int t) { return wst[(int64_t)t * Lw]; };
-  auto Wx = [&](int t, int i) { return wst[(int64_t)t * Lw + 1 + i]; };
-  auto Wxx = [&](int t, int i, int j) { return wst[(int64_t)t * Lw + 1 + d + tri(i, j, d)]; };
+// Two launches: one block per time stamp (C_t, S, F staged in LDS, thread per (i, j)) writes the
+// per-t terms to a slab; one block sums the slab in a fixed order and assembles loss and grad.
+constexpr int kKmvScalars = 4;  // nabla, value, true, gt (per-t contributions)
 
-  double acc[7] = {0, 0, 0, 0, 0, 0, 0};  // nabla, hess, value, true, gt, |grad|^2, spare
-  const int tid = threadIdx.x;
+__host__ __device__ inline int kmv_slots(int d) { return d * d + d + kKmvScalars; }
+
+__device__ __forceinline__ int tri_idx(int i, int j, int mm) {
+  if (i > j) { const int t = i; i = j; j = t; }
+  return i * mm - i * (i - 1) / 2 + (j - i);
+}
+
+__global__ __launch_bounds__(kBlock) void kmv_terms_kernel(KmvArgs a, const double* __restrict__ mom,
+                                                           const double* __restrict__ wst,
+                                                           const float* __restrict__ theta,
+                                                           double* __restrict__ slab) {
+  const int d = a.d, m = 2 * d, Lz = moment_len(m), Lw = moment_len(d), t = blockIdx.x, tid = threadIdx.x;
+  __shared__ double sS[PDEINV_MAX_DIM * PDEINV_MAX_DIM], sF[PDEINV_MAX_DIM * PDEINV_MAX_DIM];
+  __shared__ double sM[PDEINV_MAX_DIM * PDEINV_MAX_DIM], sC[PDEINV_MAX_DIM * PDEINV_MAX_DIM];
+  __shared__ double sxb[PDEINV_MAX_DIM], sWx[PDEINV_MAX_DIM];
+  __shared__ double red[kWavesPerBlock][kKmvScalars];
+  const double* v = mom + (int64_t)t * Lz;
+  const double* w = wst + (int64_t)t * Lw;
+  double Ntot = 0;
+  for (int u = 0; u < a.n_sets; ++u) Ntot += mom[(int64_t)u * Lz];
+  const double invN = Ntot > 0 ? 1.0 / Ntot : 0.0;
+  const double cnt = v[0], inv_c = cnt > 0 ? 1.0 / cnt : 0.0;
+  if (tid < d) {
+    sxb[tid] = v[1 + tid] * inv_c;
+    sWx[tid] = w[1 + tid];
+  }
   if (tid < d * d) {
     const int i = tid / d, j = tid % d;
-    double Gij = 0, Gji = 0;
-    for (int t = 0; t < a.n_sets; ++t) {
-      const double nt = mom[(int64_t)t * Lz] * invN;
-      double SC_ij = 0, CS_ij = 0, SC_ji = 0, CS_ji = 0, FC = 0, DC = 0;
-      for (int k = 0; k < d; ++k) {
-        SC_ij += S(i, k) * Cx(t, k, j);
-        CS_ij += Cx(t, i, k) * S(k, j);
-        SC_ji += S(j, k) * Cx(t, k, i);
-        CS_ji += Cx(t, j, k) * S(k, i);
-        FC += F(i, k) * Cx(t, k, j);
-        DC += (F(i, k) - S(i, k)) * Cx(t, k, j);
-      }
-      acc[0] += nt * SC_ij * S(j, i);                 // tr(S C S)
-      acc[3] += nt * FC * F(i, j);                    // tr(F C F^T)
-      acc[4] += nt * DC * (F(i, j) - S(i, j));        // tr(D C D^T)
-      // value: 1/2 tr(S Wxx) - xbar^T S Wx + 1/2 W tr(S M)
-      acc[2] += invN * (0.5 * S(i, j) * Wxx(t, j, i) - xbar(t, i) * S(i, j) * Wx(t, j) +
-                        0.5 * W(t) * S(i, j) * Mx(t, j, i));
-      Gij += nt * (SC_ij + CS_ij) + 2 * invN * (0.5 * Wxx(t, i, j) - xbar(t, i) * Wx(t, j) + 0.5 * W(t) * Mx(t, i, j));
-      Gji += nt * (SC_ji + CS_ji) + 2 * invN * (0.5 * Wxx(t, j, i) - xbar(t, j) * Wx(t, i) + 0.5 * W(t) * Mx(t, j, i));
+    sS[tid] = (double)theta[i * d + j] + (double)theta[j * d + i];
+    sF[tid] = (double)a.F[tid];
+    sM[tid] = v[1 + m + tri_idx(i, j, m)] * inv_c;
+  }
+  __syncthreads();
+  if (tid < d * d) sC[tid] = sM[tid] - sxb[tid / d] * sxb[tid % d];
+  __syncthreads();
+  double c[kKmvScalars] = {0, 0, 0, 0};
+  double* out = slab + (int64_t)t * kmv_slots(d);
+  if (tid < d * d) {
+    const int i = tid / d, j = tid % d;
+    const double nt = cnt * invN;
+    double SC_ij = 0, CS_ij = 0, FC = 0, DC = 0;
+    for (int k = 0; k < d; ++k) {
+      const double ckj = sC[k * d + j];
+      SC_ij += sS[i * d + k] * ckj;
+      CS_ij += sC[i * d + k] * sS[k * d + j];
+      FC += sF[i * d + k] * ckj;
+      DC += (sF[i * d + k] - sS[i * d + k]) * ckj;
     }
-    const double mvv_ij = Mvv(i, j);
-    acc[1] = S(i, j) * mvv_ij;
-    Gij += -2 * mvv_ij;
-    Gji += -2 * mvv_ij;
-    const double gk = Gij + Gji;
+    const double Wt = w[0], Wxx_ji = w[1 + d + tri_idx(j, i, d)];
+    c[0] = nt * SC_ij * sS[j * d + i];                                    // tr(S C S)
+    c[2] = nt * FC * sF[i * d + j];                                       // tr(F C F^T)
+    c[3] = nt * DC * (sF[i * d + j] - sS[i * d + j]);                     // tr(D C D^T)
+    c[1] = invN * (0.5 * sS[i * d + j] * Wxx_ji - sxb[i] * sS[i * d + j] * sWx[j] +
+                   0.5 * Wt * sS[i * d + j] * sM[j * d + i]);              // value
+    // d/dK_ij of the t terms (the (j, i) transpose is added in the combine)
+    out[tid] = nt * (SC_ij + CS_ij) +
+               2 * invN * (0.5 * Wxx_ji - sxb[i] * sWx[j] + 0.5 * Wt * sM[i * d + j]);
+  }
+  if (tid < d) out[d * d + tid] = sWx[tid] - w[0] * sxb[tid];  // bias weights (Wx_t - W_t xbar_t)
+#pragma unroll
+  for (int q = 0; q < kKmvScalars; ++q) {
+    double x = c[q];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+    if ((tid & 63) == 0) red[tid >> 6][q] = x;
+  }
+  __syncthreads();
+  if (tid < kKmvScalars) out[d * d + d + tid] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
+}
+
+__global__ __launch_bounds__(kBlock) void kmv_combine_kernel(KmvArgs a, const double* __restrict__ mom,
+                                                             const double* __restrict__ slab,
+                                                             const float* __restrict__ theta,
+                                                             float* __restrict__ out, float* __restrict__ grad) {
+  const int d = a.d, m = 2 * d, Lz = moment_len(m), ns = kmv_slots(d), tid = threadIdx.x;
+  __shared__ double tot[PDEINV_MAX_DIM * PDEINV_MAX_DIM + PDEINV_MAX_DIM + kKmvScalars];
+  double Ntot = 0;
+  for (int u = 0; u < a.n_sets; ++u) Ntot += mom[(int64_t)u * Lz];
+  const double invN = Ntot > 0 ? 1.0 / Ntot : 0.0;
+  for (int q = tid; q < ns; q += kBlock) {
+    double s = 0;
+    for (int t = 0; t < a.n_sets; ++t) s += slab[(int64_t)t * ns + q];  // fixed order
+    tot[q] = s;
+  }
+  __syncthreads();
+  auto S = [&](int i, int j) { return (double)theta[i * d + j] + (double)theta[j * d + i]; };
+  double acc[7] = {0, 0, 0, 0, 0, 0, 0};  // nabla, hess, value, true, gt, |grad|^2
+  if (tid < d * d) {
+    const int i = tid / d, j = tid % d;
+    double mvv = 0;
+    for (int t = 0; t < a.n_sets; ++t) mvv += mom[(int64_t)t * Lz + 1 + m + tri_idx(d + i, d + j, m)];
+    mvv *= invN;
+    acc[1] = S(i, j) * mvv;
+    const double gk = tot[i * d + j] + tot[j * d + i] - 4 * mvv;
     grad[i * d + j] = (float)gk;
     acc[5] = gk * gk;
   }
   if (tid < d) {
-    const int i = tid;
-    double wsum = 0;
-    for (int t = 0; t < a.n_sets; ++t) wsum += Wx(t, i) - W(t) * xbar(t, i);
-    acc[0] += b(i) * b(i);
-    acc[4] += b(i) * b(i);
-    acc[2] += invN * b(i) * wsum;
-    const double gb = 2 * b(i) + 2 * invN * wsum;
-    grad[d * d + i] = (float)gb;
+    const double b = (double)theta[d * d + tid], wsum = tot[d * d + tid];
+    acc[0] += b * b;
+    acc[4] += b * b;
+    acc[2] += invN * b * wsum;
+    const double gb = 2 * b + 2 * invN * wsum;
+    grad[d * d + tid] = (float)gb;
     acc[5] += gb * gb;
+  }
+  if (tid == 0) {
+    const double* sc = tot + d * d + d;
+    acc[0] += sc[0];
+    acc[2] += sc[1];
+    acc[3] += sc[2];
+    acc[4] += sc[3];
   }
   __shared__ double red[kWavesPerBlock][7];
 #pragma unroll
@@ -277,18 +315,28 @@ extern "C" int pdeinv_kmv_weights(int32_t D, float gamma, const float* coef, con
   return check_launch("slab_reduce_kernel");
 }
 
+extern "C" size_t pdeinv_residual_kmv_workspace_bytes(const pdeinv_kmv_desc* d) {
+  if (!d || d->dim < 1 || d->dim > 8 || d->n_sets < 1) return 0;
+  return (size_t)d->n_sets * kmv_slots(d->dim) * sizeof(double);
+}
+
 extern "C" int pdeinv_residual_kmv(const pdeinv_kmv_desc* d, const double* mom, const double* wst,
-                                   const float* theta, float* out, float* grad, void* stream) {
+                                   const float* theta, void* ws, float* out, float* grad, void* stream) {
   PDEINV_REQUIRE(d != nullptr, PDEINV_ERR_INVALID, "residual_kmv: null descriptor");
   PDEINV_REQUIRE(d->dim >= 1 && d->dim <= 8, PDEINV_ERR_UNSUPPORTED, "residual_kmv: dim must be in [1, 8]");
-  PDEINV_REQUIRE(d->n_sets >= 1, PDEINV_ERR_INVALID, "residual_kmv: n_sets must be >= 1");
-  PDEINV_REQUIRE(mom && wst && theta && out && grad && d->tilde_F, PDEINV_ERR_INVALID, "residual_kmv: null pointer");
+  PDEINV_REQUIRE(d->n_sets >= 1 && d->n_sets <= 65535, PDEINV_ERR_INVALID, "residual_kmv: need 1 <= n_sets <= 65535");
+  PDEINV_REQUIRE(mom && wst && theta && ws && out && grad && d->tilde_F, PDEINV_ERR_INVALID,
+                 "residual_kmv: null pointer");
   KmvArgs a{};
   a.d = d->dim;
   a.n_sets = d->n_sets;
   a.gamma = d->gamma;
   for (int k = 0; k < d->dim * d->dim; ++k) a.F[k] = d->tilde_F[k];
-  hipLaunchKernelGGL(kmv_finalize_kernel, dim3(1), dim3(kBlock), 0, (hipStream_t)stream, a, mom, wst, theta, out,
-                     grad);
-  return check_launch("kmv_finalize_kernel");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(kmv_terms_kernel, dim3((unsigned)d->n_sets), dim3(kBlock), 0, st, a, mom, wst, theta,
+                     (double*)ws);
+  int rc = check_launch("kmv_terms_kernel");
+  if (rc) return rc;
+  hipLaunchKernelGGL(kmv_combine_kernel, dim3(1), dim3(kBlock), 0, st, a, mom, (const double*)ws, theta, out, grad);
+  return check_launch("kmv_combine_kernel");
 }

@@ -156,6 +156,31 @@ __device__ __forceinline__ void store_rows_staged(float* wave_dst, const float* 
   __builtin_amdgcn_wave_barrier();
 }
 
+// The mirror image: 16-byte chunks of the wave's 64 consecutive rows -> LDS (coalesced), then
+// each lane reads its own row. Rows at or beyond n_valid read as zero.
+template <int D>
+__device__ __forceinline__ void load_rows_staged(const float* wave_src, float* z, float* slot, int lane,
+                                                 int n_valid) {
+  constexpr int M = 2 * D;
+  static_assert(M % 4 == 0, "staged loads need 2d % 4 == 0");
+#pragma unroll
+  for (int k = 0; k < M / 4; ++k) {
+    const int c = k * 64 + lane;
+    const f32x4 v = (4 * c < n_valid * M) ? *reinterpret_cast<const f32x4*>(wave_src + 4 * c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    *reinterpret_cast<f32x4*>(slot + 4 * c) = v;
+  }
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int k = 0; k < M; k += 4) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(slot + lane * M + k);
+    z[k] = v[0];
+    z[k + 1] = v[1];
+    z[k + 2] = v[2];
+    z[k + 3] = v[3];
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
 __device__ __forceinline__ float tau_value(float tau0, int s, float dt) {
 #pragma clang fp contract(off)
   return tau0 + (float)s * dt;  // tau_0 + arange(n)*dt, two roundings (sampling_utils.py:48)
@@ -270,13 +295,23 @@ __global__ __launch_bounds__(kBlock) void mf_step_kernel(SdeArgs a, int s, float
                                                          const double* __restrict__ xbar_sum,
                                                          float* __restrict__ partials) {
   constexpr int M = 2 * D;
+  constexpr bool kStaged = (M % 4 == 0);
   const int64_t i_raw = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool active = i_raw < a.N;
   const int64_t i = active ? i_raw : a.N - 1;
   const uint64_t gid = (uint64_t)(a.poff + i);
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t wave_row0 = i_raw - lane;
+  const int n_valid = (int)((a.N - wave_row0) < kWave ? (a.N - wave_row0) : kWave);
+  __shared__ float stage[kStaged ? kBlock * M : 1];
+  float* slot = stage + (threadIdx.x - lane) * M;
   float z[M];
+  if constexpr (kStaged) {
+    if (n_valid > 0) load_rows_staged<D>(zin + wave_row0 * M, z, slot, lane, n_valid);
+  } else {
 #pragma unroll
-  for (int k = 0; k < M; ++k) z[k] = zin[i * M + k];
+    for (int k = 0; k < M; ++k) z[k] = zin[i * M + k];
+  }
   const double cnt = xbar_sum[0];
   float y[D];
 #pragma unroll
@@ -301,10 +336,12 @@ __global__ __launch_bounds__(kBlock) void mf_step_kernel(SdeArgs a, int s, float
     z[D + k] = pn;
     z[k] = fmaf(h, pn, z[k]);
   }
-  if (active) {
+  if constexpr (kStaged) {
+    if (n_valid > 0) store_rows_staged<D>(zout + wave_row0 * M, z, slot, lane, n_valid);
+  } else if (active) {
     store_row<D, kStoreNT>(zout + i * M, z);
-    if (tau_row) tau_row[i] = tau_value(tau0, s, a.dt);
   }
+  if (active && tau_row) tau_row[i] = tau_value(tau0, s, a.dt);
   float v[1 + D];
   v[0] = active ? 1.f : 0.f;
 #pragma unroll

@@ -21,33 +21,51 @@ from utils import native, prng
 from utils.prng import Key
 
 
+def _mean_cov_stamps(s, configuration):
+    """(m(s_k), P(s_k)) at every stamp: the closed form of OU_process (…_OU.py:73-93) with the
+    matrix exponentials of all stamps taken in one batched call."""
+    from scipy.linalg import expm
+
+    s = np.atleast_1d(np.asarray(s, dtype=np.float64))
+    F, L, m0, P0 = (configuration[k] for k in ("F", "L", "m_0", "P_0"))
+    n = F.shape[0]
+    blk = np.zeros((2 * n, 2 * n))
+    blk[:n, :n] = -F
+    blk[:n, n:] = L
+    blk[n:, n:] = F.T
+    E = expm(F[None] * s[:, None, None])
+    V = expm(blk[None] * s[:, None, None])
+    P = E @ P0 @ E.transpose(0, 2, 1) + V[:, n:, n:].transpose(0, 2, 1) @ V[:, :n, n:]
+    return E @ m0, 0.5 * (P + P.transpose(0, 2, 1))
+
+
 def dlogrho_coefficients(s_values, configuration, dim: int) -> np.ndarray:
     """Coefficient rows [m1, a1, beta1, Gamma1, a2, beta2, Gamma2] (include/pdeinv.h) such that
     ds log rho = a1 + beta1.r + r^T Gamma1 r and ds2 log rho = a2 + beta2.r + r^T Gamma2 r, r = m1 - x,
-    restating partial_s_log_density_fn (:51-69) and partial_s2_log_density_fn (:120-177)."""
-    from example_problems.kinetic_fokker_planck_example_OU import get_mean_cov
+    restating partial_s_log_density_fn (:51-69) and partial_s2_log_density_fn (:120-177), batched
+    over the time stamps."""
     F, L = configuration["F"], configuration["L"]
     d = dim
-    rows = []
-    for s in np.atleast_1d(np.asarray(s_values, dtype=np.float64)):
-        mean, cov = get_mean_cov(float(s), configuration)
-        m1, P11 = mean[:d], cov[:d, :d]
-        Pinv = np.linalg.inv(P11)
-        dm = F @ mean
-        d2m = F @ dm
-        dP = F @ cov + cov @ F.T + L
-        d2P = F @ dP + dP @ F.T
-        dm1, d2m1, dP11, d2P11 = dm[:d], d2m[:d], dP[:d, :d], d2P[:d, :d]
-        dPinv = -Pinv @ dP11 @ Pinv
-        d2Pinv = -Pinv @ d2P11 @ Pinv + 2 * Pinv @ dP11 @ Pinv @ dP11 @ Pinv
-        a1 = -0.5 * np.trace(dP11 @ Pinv)
-        beta1 = -Pinv @ dm1
-        G1 = -0.5 * dPinv
-        a2 = -dm1 @ Pinv @ dm1 + 0.5 * np.trace(Pinv @ dP11 @ Pinv @ dP11) - 0.5 * np.trace(Pinv @ d2P11)
-        beta2 = -Pinv @ d2m1 - (dPinv + dPinv.T) @ dm1
-        G2 = -0.5 * d2Pinv
-        rows.append(np.concatenate([m1, [a1], beta1, G1.ravel(), [a2], beta2, G2.ravel()]))
-    return np.stack(rows)
+    mean, cov = _mean_cov_stamps(s_values, configuration)
+    K = mean.shape[0]
+    m1, P11 = mean[:, :d], cov[:, :d, :d]
+    Pinv = np.linalg.inv(P11)
+    dm = mean @ F.T
+    d2m = dm @ F.T
+    dP = F @ cov + cov @ F.T + L
+    d2P = F @ dP + dP @ F.T
+    dm1, d2m1, dP11, d2P11 = dm[:, :d], d2m[:, :d], dP[:, :d, :d], d2P[:, :d, :d]
+    PdP = Pinv @ dP11
+    dPinv = -PdP @ Pinv
+    d2Pinv = -Pinv @ d2P11 @ Pinv + 2 * PdP @ PdP @ Pinv
+    tr = lambda X: np.einsum("kii->k", X)
+    a1 = -0.5 * tr(dP11 @ Pinv)
+    beta1 = -np.einsum("kij,kj->ki", Pinv, dm1)
+    G1 = -0.5 * dPinv
+    a2 = -np.einsum("ki,kij,kj->k", dm1, Pinv, dm1) + 0.5 * tr(PdP @ PdP) - 0.5 * tr(Pinv @ d2P11)
+    beta2 = -np.einsum("kij,kj->ki", Pinv, d2m1) - np.einsum("kij,kj->ki", dPinv + dPinv.transpose(0, 2, 1), dm1)
+    G2 = -0.5 * d2Pinv
+    return np.concatenate([m1, a1[:, None], beta1, G1.reshape(K, -1), a2[:, None], beta2, G2.reshape(K, -1)], axis=1)
 
 
 class KineticMcKeanVlasov(KineticFokkerPlanck):

@@ -12,11 +12,28 @@ from __future__ import annotations
 import math
 from typing import Optional
 
+import numpy as np
 import torch
 
 from utils import distributed as dist
 from utils import native
 from utils.prng import Key
+
+
+def stamp_times(seed: int, counter_offset: int, n_steps: int, dt: float, random_shift: bool = True) -> np.ndarray:
+    """The shared-clock time stamps tau_k = tau0 + k dt (fp32, bit-identical to the simulator's
+    tau rows) computed on the host: tau0 = u dt with u from Philox4x32-10 at counter
+    (UINT64_MAX, counter_offset, 0x80000000) (include/pdeinv.h stream layout). Lets callers build
+    the per-stamp coefficient rows without waiting for the device."""
+    from utils.prng import philox4x32_10
+    dt32 = np.float32(dt)
+    if random_shift:
+        c0 = philox4x32_10((0xFFFFFFFF, 0xFFFFFFFF, counter_offset, 0x80000000), (seed, seed >> 32))[0]
+        tau0 = np.float32(np.float32(c0 >> 8) * np.float32(2.0 ** -24)) * dt32
+    else:
+        tau0 = np.float32(0.0)
+    k = np.arange(n_steps, dtype=np.float32)
+    return (np.float32(tau0) + (k * dt32).astype(np.float32)).astype(np.float32)
 
 
 def simulate_mean_field(q0_p0: torch.Tensor, n_steps: int, dt: float, key: Key, potential, gamma: float, *,

@@ -34,6 +34,8 @@ KFP_SLOTS = ("loss", "loss ground truth", "grad_norm", "loss_nabla", "loss_Hessi
 GMM_NACC = 8
 SQRT2 = math.sqrt(2.0)
 
+ABI_VERSION = 2  # PDEINV_ABI_VERSION of include/pdeinv.h this binding was written against
+
 # Every exported symbol of include/pdeinv.h (tests check the library exports all of them).
 EXPORTED_SYMBOLS = (
     "pdeinv_moment_len", "pdeinv_sde_workspace_bytes", "pdeinv_sde_simulate",
@@ -44,6 +46,7 @@ EXPORTED_SYMBOLS = (
     "pdeinv_philox_fill", "pdeinv_gather_subsample", "pdeinv_abi_version", "pdeinv_last_error",
     "pdeinv_runtime_version", "pdeinv_moments_batched_workspace_bytes", "pdeinv_moments_batched",
     "pdeinv_kmv_weights_workspace_bytes", "pdeinv_kmv_weights", "pdeinv_residual_kmv",
+    "pdeinv_residual_kmv_workspace_bytes",
     "pdeinv_mlp_param_count", "pdeinv_residual_kfp_mlp_workspace_bytes", "pdeinv_residual_kfp_mlp",
     "pdeinv_kfp_terms_finalize", "pdeinv_gather_random_step", "pdeinv_mlp_fused_supported",
     "pdeinv_adam_update",
@@ -142,7 +145,8 @@ def lib():
         "pdeinv_moments_batched": (i32, [P, i64, i64, i32, i64, i64, P, P, P]),
         "pdeinv_kmv_weights_workspace_bytes": (ctypes.c_size_t, [i64, i64, i32]),
         "pdeinv_kmv_weights": (i32, [i32, f32, P, P, i64, i64, i64, i64, P, P, P, P]),
-        "pdeinv_residual_kmv": (i32, [P, P, P, P, P, P, P]),
+        "pdeinv_residual_kmv_workspace_bytes": (ctypes.c_size_t, [P]),
+        "pdeinv_residual_kmv": (i32, [P, P, P, P, P, P, P, P]),
         "pdeinv_mlp_param_count": (i64, [i32, i32, i32, i32]),
         "pdeinv_mlp_fused_supported": (i32, [i32, i32, i32, i32]),
         "pdeinv_adam_update": (i32, [P, P, P, P, i64, f32, f32, f32, f32, f32, i32, P]),
@@ -155,7 +159,7 @@ def lib():
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
-    if L.pdeinv_abi_version() != 1:
+    if L.pdeinv_abi_version() != ABI_VERSION:
         raise RuntimeError("libpdeinv ABI version mismatch")
     _lib = L
     return _lib
@@ -505,9 +509,12 @@ def residual_kmv(mom: torch.Tensor, wst: torch.Tensor, theta_flat: torch.Tensor,
     desc = KmvDesc(d, n_sets, float(gamma), F.ctypes.data_as(ctypes.c_void_p))
     out = torch.empty(KFP_NOUT, device=mom.device, dtype=torch.float32)
     grad = torch.empty_like(theta_flat)
+    ws = torch.empty(max(1, lib().pdeinv_residual_kmv_workspace_bytes(ctypes.byref(desc)) // 8), device=mom.device,
+                     dtype=torch.float64)
     _check(lib().pdeinv_residual_kmv(ctypes.byref(desc), _dev(mom.contiguous(), "mom", torch.float64),
                                      _dev(wst.contiguous(), "wst", torch.float64), _dev(theta_flat.contiguous(), "theta"),
-                                     _dev(out, "out"), _dev(grad, "grad"), stream_handle()), "pdeinv_residual_kmv")
+                                     _dev(ws, "ws", torch.float64), _dev(out, "out"), _dev(grad, "grad"),
+                                     stream_handle()), "pdeinv_residual_kmv")
     return out, grad
 
 

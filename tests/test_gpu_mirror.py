@@ -88,6 +88,8 @@ def test_mean_field_simulator_vs_c_oracle(native, oracle_lib):
     r = simulate_mean_field(_t(z0), n, 0.02, key, MeanFieldQuadraticPotential(A), 1.0, counter_offset=5)
     o = oracle_lib.sde_simulate(z0, n, 0.02, 1.0, "meanfield", A, seed=key.seed, counter_offset=5)
     assert np.array_equal(r["tau"].cpu().numpy(), o["tau"])
+    from utils.mean_field import stamp_times
+    assert np.array_equal(r["tau"][:, 0].cpu().numpy(), stamp_times(key.seed, 5, n, 0.02))
     assert np.max(np.abs(r["traj"].cpu().numpy() - o["traj"])) < 2e-4
     assert np.max(np.abs(r["last"].cpu().numpy() - o["last"])) < 2e-4
 
