@@ -346,6 +346,47 @@ int pdeinv_gather_subsample(const float* d_traj, int64_t n_particles, int32_t n_
 int pdeinv_gather_random_step(const float* d_traj, int64_t n_particles, int32_t n_steps, int32_t m,
                               uint64_t seed, uint32_t ctr, float* d_out, int32_t* d_t_out, void* stream);
 
+/* ---------------------------------------------------------------------------------------
+ * Time-conditioned RealNVP log-density (core/normalizing_flow.py:8-229, the model built by
+ * core/log_density_estimation.py:103-114): log p_t(x) = log p0(T_t^{-1}(x)) + sum ldj, the
+ * coupling layers applied in reverse order (MNF.__call__(reverse=True), :205-217).
+ * Each CouplingLayer (:115-163): xt = [x * mask, temb(t)] (or [x * mask, t], or x * mask),
+ * s = scale_net(xt), tr = translate_net(xt) (BasicMLP: Dense 8, act, Dense 16, act, Dense 16,
+ * act, Dense dim), [soft_init == 0: s, tr *= t], sf = exp(scaling_factor), s = tanh(s / sf) sf,
+ * s, tr *= (1 - mask); x = (x + tr) exp(s), ldj += sum s.
+ * temb (TimeEmbedding, :8-22): Dense_E(act(Dense_E(SinusoidalEmbedding_E(t)))).
+ * Flat parameter layout (d_params, fp32, flax kernels [in, out] row-major):
+ *   [E > 0] temb: W1 [E x E], b1 [E], W2 [E x E], b2 [E]
+ *   per layer l (forward order): scaling_factor [dim]; scale_net: W0 [in x 8], b0, W1 [8 x 16], b1,
+ *   W2 [16 x 16], b2, W3 [16 x dim], b3; translate_net: the same; in = dim + (E > 0 ? E : 1)
+ *   (dim only when ignore_time). pdeinv_realnvp_param_count gives the total.
+ * --------------------------------------------------------------------------------------- */
+#define PDEINV_ACT_CELU 0
+#define PDEINV_ACT_RELU 1
+#define PDEINV_ACT_TANH 2
+#define PDEINV_ACT_ELU 3
+#define PDEINV_ACT_SILU 4
+#define PDEINV_ACT_SOFTPLUS 5
+#define PDEINV_ACT_GELU 6 /* tanh approximation (flax nn.gelu default) */
+#define PDEINV_REALNVP_MAX_LAYERS 64
+typedef struct {
+  int32_t dim;             /* 1..8 */
+  int32_t n_layers;        /* coupling layers, <= PDEINV_REALNVP_MAX_LAYERS */
+  int32_t embed_time_dim;  /* E: 0 => the raw t is appended; even, <= 16 */
+  int32_t ignore_time;
+  float soft_init;         /* 0 => hard parameterisation (s, tr scaled by t) */
+  int32_t activation;      /* PDEINV_ACT_* */
+  const float* masks;      /* HOST [n_layers * dim], 1 = keep */
+  const float* base_mean;  /* HOST [dim]: log p0 = -1/2 (log_det + (x - m)^T inv_cov (x - m)) */
+  const float* base_inv_cov; /* HOST [dim * dim] */
+  float base_log_det;      /* log det(2 pi cov) (distribution.py:60) */
+} pdeinv_realnvp_desc;
+int64_t pdeinv_realnvp_param_count(const pdeinv_realnvp_desc* desc);
+/* out[i] = log p_{t_i}(x_i); t_stride 0 broadcasts d_t[0]. */
+int pdeinv_realnvp_logdensity(const pdeinv_realnvp_desc* desc, const float* d_params, const float* d_t,
+                              int64_t t_stride, const float* d_x, int64_t n, int64_t ld_x, float* d_out,
+                              void* stream);
+
 /* Fused optimizer step of the trainer (core/trainer.py:85-86 + main.py:11-29):
  * optax.chain(add_decayed_weights(weight_decay), adam(lr, b1, b2, eps)) then apply_updates, in
  * place over a flat parameter vector; count = the step number after increment (>= 1). */

@@ -626,3 +626,173 @@ def kfp_mlp_grad_analytic(params, z_init, z_term, z_0T, gamma, T):
         grads[l - 1] = (gK, zb.sum(0))
         hb, hdb, hddb = zb @ K.T, zdb @ K.T, zddb @ K.T
     return grads
+
+
+# --------------------------------------------------------------------------------------
+# RealNVP log-density (core/normalizing_flow.py:8-229; core/log_density_estimation.py:103-114)
+# --------------------------------------------------------------------------------------
+def _nvp_act(name, x):
+    if name == "celu":
+        return np.where(x > 0, x, np.expm1(np.minimum(x, 0)))
+    if name == "relu":
+        return np.maximum(x, 0)
+    if name == "tanh":
+        return np.tanh(x)
+    if name == "elu":
+        return np.where(x > 0, x, np.expm1(np.minimum(x, 0)))
+    if name == "silu":
+        return x / (1 + np.exp(-x))
+    if name == "softplus":
+        return np.logaddexp(x, 0)
+    if name == "gelu":  # flax nn.gelu(approximate=True)
+        return 0.5 * x * (1 + np.tanh(np.sqrt(2 / np.pi) * (x + 0.044715 * x ** 3)))
+    raise ValueError(name)
+
+
+def nvp_masks(dim, couple_mul, mask_type):
+    """MNF.setup (:174-199): 'loop' zeroes one coordinate per layer; 'random' draws Bernoulli(1/2)
+    masks from RandomState(888), rejecting all-0 / all-1 and repeats of the previous mask."""
+    if mask_type == "loop":
+        out = []
+        for i in range(dim * couple_mul):
+            m = np.ones(dim)
+            m[i % dim] = 0
+            out.append(m)
+        return np.stack(out)
+    rng = np.random.RandomState(seed=888)
+    prev = np.zeros(dim, dtype=int)
+    out = []
+    for _ in range(couple_mul):
+        while True:
+            m = rng.binomial(1, p=0.5, size=[dim])
+            if not (m.sum() in [0, dim] or (m == prev).all()):
+                prev = m
+                break
+        out.append(m.astype(np.float64))
+    return np.stack(out)
+
+
+def nvp_in_dim(dim, E, ignore_time):
+    return dim if ignore_time else dim + (E if E > 0 else 1)
+
+
+def nvp_param_count(dim, n_layers, E, ignore_time):
+    i = nvp_in_dim(dim, E, ignore_time)
+    mlp = i * 8 + 8 + 8 * 16 + 16 + 16 * 16 + 16 + 16 * dim + dim
+    Et = 0 if ignore_time else E
+    return (2 * (Et * Et + Et) if Et > 0 else 0) + n_layers * (dim + 2 * mlp)
+
+
+def nvp_unflat(flat, dim, n_layers, E, ignore_time):
+    """The flat layout of include/pdeinv.h (pdeinv_realnvp_desc) -> nested lists."""
+    flat = np.asarray(flat, dtype=np.float64)
+    o = [0]
+
+    def take(*shape):
+        n = int(np.prod(shape))
+        v = flat[o[0]:o[0] + n].reshape(shape)
+        o[0] += n
+        return v
+
+    Et = 0 if ignore_time else E
+    temb = [(take(Et, Et), take(Et)), (take(Et, Et), take(Et))] if Et > 0 else None
+    i = nvp_in_dim(dim, E, ignore_time)
+    layers = []
+    for _ in range(n_layers):
+        sf = take(dim)
+        nets = []
+        for _ in range(2):
+            nets.append([(take(i, 8), take(8)), (take(8, 16), take(16)), (take(16, 16), take(16)), (take(16, dim), take(dim))])
+        layers.append((sf, nets[0], nets[1]))
+    assert o[0] == flat.size
+    return temb, layers
+
+
+def nvp_time_embedding(temb, t, E, act):
+    half = E // 2
+    emb = np.exp(np.arange(half) * -(np.log(10000) / (half - 1)))   # SinusoidalEmbedding (:24-38)
+    e = np.asarray(t)[..., None] * emb
+    se = np.concatenate([np.sin(e), np.cos(e)], -1)
+    (W1, b1), (W2, b2) = temb
+    return _nvp_act(act, se @ W1 + b1) @ W2 + b2                      # TimeEmbedding (:8-22)
+
+
+def _nvp_mlp(net, x, act):
+    h = x
+    for k, (W, b) in enumerate(net):
+        h = h @ W + b
+        if k < 3:
+            h = _nvp_act(act, h)
+    return h
+
+
+def realnvp_apply(flat, t, x, *, dim, masks, E=10, ignore_time=False, soft_init=1.0, act="celu", reverse=True):
+    """MNF.__call__ (:205-217) over a batch: returns (x_out, ldj). reverse=True is the likelihood
+    direction (layers reversed, x <- (x + tr) e^s)."""
+    n_layers = masks.shape[0]
+    temb, layers = nvp_unflat(flat, dim, n_layers, E, ignore_time)
+    x = np.asarray(x, dtype=np.float64).copy()
+    t = np.broadcast_to(np.asarray(t, dtype=np.float64), x.shape[:1])
+    if ignore_time:
+        tcat = np.zeros((x.shape[0], 0))
+    elif E > 0:
+        tcat = nvp_time_embedding(temb, t, E, act)
+    else:
+        tcat = t[:, None]
+    ldj = np.zeros(x.shape[0])
+    order = range(n_layers - 1, -1, -1) if reverse else range(n_layers)
+    for l in order:
+        m = masks[l]
+        sf, snet, tnet = layers[l]
+        xt = np.concatenate([x * m, tcat], -1)                         # CouplingLayer (:133-163)
+        s, tr = _nvp_mlp(snet, xt, act), _nvp_mlp(tnet, xt, act)
+        if not ignore_time and soft_init == 0.0:
+            s, tr = t[:, None] * s, t[:, None] * tr
+        f = np.exp(sf)
+        s = np.tanh(s / f) * f * (1 - m)
+        tr = tr * (1 - m)
+        if reverse:
+            x = (x + tr) * np.exp(s)
+            ldj += s.sum(-1)
+        else:
+            x = x * np.exp(-s) - tr
+            ldj -= s.sum(-1)
+    return x, ldj
+
+
+def realnvp_logdensity(flat, t, x, *, dim, masks, base_mean, base_cov, **kw):
+    """RealNVP.__call__ (:223-229): log p0(T^{-1}(x)) + ldj with p0 = Gaussian (distribution.py:52-81)."""
+    x0, ldj = realnvp_apply(flat, t, x, dim=dim, masks=masks, reverse=True, **kw)
+    off = x0 - base_mean
+    quad = np.einsum("ni,ij,nj->n", off, np.linalg.inv(base_cov), off)
+    log_det = np.log(np.linalg.det(base_cov * 2 * np.pi))
+    return -0.5 * (log_det + quad) + ldj
+
+
+def nvp_init(dim, n_layers, E, ignore_time, seed=0, scale=1.0, perturb=False):
+    """Flax defaults (lecun_normal kernels, zero biases, zero scaling factors). perturb=True adds
+    random biases and scaling factors (and `scale` multiplies the kernels) so tests see a
+    non-trivial flow (a fresh init is close to the identity map)."""
+    rng = np.random.default_rng(seed)
+    parts = []
+    Et = 0 if ignore_time else E
+
+    def dense(i, o):
+        k = rng.standard_normal((i, o))
+        k = np.clip(k, -2, 2) / 0.87962566103423978 * np.sqrt(1.0 / i) * scale
+        parts.extend([k.ravel(), 0.3 * rng.standard_normal(o) if perturb else np.zeros(o)])
+
+    if Et > 0:
+        dense(Et, Et)
+        dense(Et, Et)
+    i = nvp_in_dim(dim, E, ignore_time)
+    for _ in range(n_layers):
+        parts.append(-1.0 + 0.2 * rng.standard_normal(dim) if perturb else np.zeros(dim))
+        for _ in range(2):
+            dense(i, 8)
+            dense(8, 16)
+            dense(16, 16)
+            dense(16, dim)
+    flat = np.concatenate(parts)
+    assert flat.size == nvp_param_count(dim, n_layers, E, ignore_time)
+    return flat

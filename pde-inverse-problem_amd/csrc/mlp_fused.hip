@@ -35,6 +35,7 @@
 #include <math.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "mlp_fused.h"
 
@@ -50,6 +51,14 @@ constexpr int kT = 256;
 __device__ __forceinline__ float ftanh(float z) {
   const float e = __builtin_amdgcn_exp2f(2.8853900817779268f * z);
   return 1.f - 2.f * __builtin_amdgcn_rcpf(e + 1.f);
+}
+
+// 32-bit byte offsets from a uniform base (saddr addressing): a chunk's planes stay below 2^29 floats
+__device__ __forceinline__ float ldo(const float* base, uint32_t idx) {
+  return *reinterpret_cast<const float*>(reinterpret_cast<const char*>(base) + (idx << 2));
+}
+__device__ __forceinline__ void sto(float* base, uint32_t idx, float v) {
+  *reinterpret_cast<float*>(reinterpret_cast<char*>(base) + (idx << 2)) = v;
 }
 
 enum { A_RAW1 = 0, A_FWD, A_S1MUL, A_U, A_S3 };
@@ -79,20 +88,26 @@ struct ARegs {
   float v[NE][NV > 0 ? NV : 1];
 };
 
+// Loads are unconditional from a clamped 32-bit offset (a chunk's planes stay below 2^31 floats)
+// and zeroed by a select: no per-element exec-mask branches, uniform base + lane offset addressing.
 template <int BM, int AM>
-__device__ __forceinline__ void load_a(const GemmArgs& a, ARegs<BM, AM>& ra, int64_t r0, int k0) {
-  if constexpr (ARegs<BM, AM>::NV > 0) {
+__device__ __forceinline__ void load_a(const GemmArgs& a, ARegs<BM, AM>& ra, int r0, int k0) {
 #pragma unroll
-    for (int j = 0; j < ARegs<BM, AM>::NE; ++j) {
-      const int e = threadIdx.x + j * kT;
-      const int m = e / BK, kk = e - m * BK;
-      const int64_t r = r0 + m;
-      const int k = k0 + kk;
-      const bool ok = r < a.R && k < a.K;
-      const int64_t o = ok ? r * a.K + k : 0;
-      ra.v[j][0] = ok ? a.pa0[o] : 0.f;
-      if constexpr (ARegs<BM, AM>::NV > 1) ra.v[j][1] = ok ? a.pa1[o] : 0.f;
-      if constexpr (ARegs<BM, AM>::NV > 2) ra.v[j][2] = ok ? a.pa2[o] : 0.f;
+  for (int j = 0; j < ARegs<BM, AM>::NE; ++j) {
+    const int e = threadIdx.x + j * kT;
+    const int m = e / BK, kk = e - m * BK;
+    const int r = r0 + m, k = k0 + kk;
+    const bool ok = r < a.R && k < a.K;
+    const uint32_t o = ok ? (uint32_t)(r * a.K + k) : 0u;
+    const float t0 = ldo(a.pa0, o);
+    ra.v[j][0] = ok ? t0 : 0.f;
+    if constexpr (ARegs<BM, AM>::NV > 1) {
+      const float t1 = ldo(a.pa1, o);
+      ra.v[j][1] = ok ? t1 : 0.f;
+    }
+    if constexpr (ARegs<BM, AM>::NV > 2) {
+      const float t2 = ldo(a.pa2, o);
+      ra.v[j][2] = ok ? t2 : 0.f;
     }
   }
 }
@@ -134,15 +149,19 @@ __device__ __forceinline__ void load_b(const GemmArgs& a, float (&rb)[BK * BN / 
 #pragma unroll
   for (int j = 0; j < BK * BN / kT; ++j) {
     const int e = threadIdx.x + j * kT;
+    int kk, nn;
     if constexpr (BMD == B_NN) {
-      const int kk = e / BN, nn = e - kk * BN;
-      const int k = k0 + kk, n = n0 + nn;
-      rb[j] = (k < a.K && n < a.N) ? a.Bw[(int64_t)k * a.N + n] : 0.f;
+      kk = e / BN;
+      nn = e - kk * BN;
     } else {
-      const int nn = e / BK, kk = e - nn * BK;
-      const int k = k0 + kk, n = n0 + nn;
-      rb[j] = (k < a.K && n < a.N) ? a.Bw[(int64_t)n * a.K + k] : 0.f;
+      nn = e / BK;
+      kk = e - nn * BK;
     }
+    const int k = k0 + kk, n = n0 + nn;
+    const bool ok = k < a.K && n < a.N;
+    const uint32_t o = ok ? (uint32_t)(BMD == B_NN ? k * a.N + n : n * a.K + k) : 0u;
+    const float t = ldo(a.Bw, o);
+    rb[j] = ok ? t : 0.f;
   }
 }
 
@@ -181,7 +200,7 @@ __global__ __launch_bounds__(kT) void fgemm(GemmArgs a) {
   for (int ni = 0; ni < NI; ++ni) pacc[ni] = 0.f;
 
   for (int mb = blockIdx.x; mb < a.n_mblocks; mb += gridDim.x) {
-    const int64_t r0 = (int64_t)mb * BM;
+    const int r0 = mb * BM;
     f32x16 acc[S][MI][NI];
 #pragma unroll
     for (int s = 0; s < S; ++s)
@@ -224,85 +243,91 @@ __global__ __launch_bounds__(kT) void fgemm(GemmArgs a) {
 
     // ---- epilogue: acc register q of tile (mi, ni) is C[row][col] with
     //      row = (q & 3) + 8 (q >> 2) + 4 (lane >> 5), col = lane & 31 (32x32 C/D map)
-#pragma unroll
-    for (int mi = 0; mi < MI; ++mi) {
-      [[maybe_unused]] float t1[16], t2[16];
-      if constexpr (EM == E_OUT) {
-#pragma unroll
-        for (int q = 0; q < 16; ++q) t1[q] = t2[q] = 0.f;
-      }
-#pragma unroll
-      for (int ni = 0; ni < NI; ++ni) {
-        const int n = n0 + wn * WN + ni * 32 + l31;
-        const bool nv = n < a.N;
-        [[maybe_unused]] float bn = 0.f;
-        if constexpr (EM == E_ACT_FWD || EM == E_OUT) bn = nv ? a.bias[n] : 0.f;
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          const int64_t r = r0 + wm * WM + mi * 32 + (q & 3) + 8 * (q >> 2) + 4 * hi;
-          const bool ok = nv && r < a.R;
-          const int64_t o = r * a.N + n;
-          if constexpr (EM == E_ACT_FWD) {
-            if (ok) {
-              a.po0[o] = ftanh(acc[0][mi][ni][q] + bn);
-              a.po1[o] = acc[1][mi][ni][q];
-              a.po2[o] = acc[2][mi][ni][q];
-            }
-          } else if constexpr (EM == E_STORE) {
-            if (ok) a.po0[o] = acc[0][mi][ni][q];
-          } else if constexpr (EM == E_STORE3) {
-            if (ok) {
-              a.po0[o] = acc[0][mi][ni][q];
-              a.po1[o] = acc[1][mi][ni][q];
-              a.po2[o] = acc[2][mi][ni][q];
-            }
-          } else if constexpr (EM == E_OUT) {
-            if (ok) {
-              const float y = acc[0][mi][ni][q] + bn, yd = acc[1][mi][ni][q], ydd = acc[2][mi][ni][q];
-              a.po0[o] = y;
-              a.po1[o] = yd;
-              a.po2[o] = ydd;
-              t1[q] = fmaf(y, yd, t1[q]);
-              t2[q] = fmaf(yd, yd, fmaf(y, ydd, t2[q]));
-            }
-          } else if constexpr (EM == E_SEEDS) {
-            if (ok) {
-              const float ub = acc[0][mi][ni][q];
-              const float y = a.pe0[o], yd = a.pe1[o], ydd = a.pe2[o];
-              const float yb = 2.f * a.c3 * yd + 2.f * a.c2 * ydd + 2.f * ub;
-              a.po0[o] = yb;
-              a.po1[o] = 2.f * a.c3 * y + 4.f * a.c2 * yd;
-              a.po2[o] = 2.f * a.c2 * y;
-              pacc[ni] += yb;
-            }
-          } else if constexpr (EM == E_ACT_BWD) {
-            if (ok) {
-              const float hb = acc[0][mi][ni][q], hdb = acc[1][mi][ni][q], hddb = acc[2][mi][ni][q];
-              const float h = a.pe0[o], zd = a.pe1[o], zdd = a.pe2[o], aL = a.pe3[o], zb = a.pe4[o];
-              const float s1 = 1.f - h * h, s2 = -2.f * h * s1, s3 = -2.f * s1 * s1 - 2.f * h * s2;
-              const float zbar = s1 * hb + s2 * zd * hdb + (s2 * zdd + s3 * zd * zd) * hddb + s2 * aL * zb;
-              a.po0[o] = zbar;
-              a.po1[o] = s1 * hdb + 2.f * s2 * zd * hddb;
-              a.po2[o] = s1 * hddb;
-              pacc[ni] += zbar;
+    const bool full = r0 + BM <= a.R && n0 + BN <= a.N;  // interior tile: guard-free copy
+    auto epilogue = [&](auto check) {
+      constexpr bool CHECK = decltype(check)::value;
+  #pragma unroll
+      for (int mi = 0; mi < MI; ++mi) {
+        [[maybe_unused]] float t1[16], t2[16];
+        if constexpr (EM == E_OUT) {
+  #pragma unroll
+          for (int q = 0; q < 16; ++q) t1[q] = t2[q] = 0.f;
+        }
+  #pragma unroll
+        for (int ni = 0; ni < NI; ++ni) {
+          const int n = n0 + wn * WN + ni * 32 + l31;
+          const bool nv = n < a.N;
+          [[maybe_unused]] float bn = 0.f;
+          if constexpr (EM == E_ACT_FWD || EM == E_OUT) bn = a.bias[nv ? n : 0];
+  #pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            const int r = r0 + wm * WM + mi * 32 + (q & 3) + 8 * (q >> 2) + 4 * hi;
+            const bool ok = !CHECK || (nv && r < a.R);
+            const uint32_t o = (uint32_t)(r * a.N + n);
+            if constexpr (EM == E_ACT_FWD) {
+              if (ok) {
+                sto(a.po0, o, ftanh(acc[0][mi][ni][q] + bn));
+                sto(a.po1, o, acc[1][mi][ni][q]);
+                sto(a.po2, o, acc[2][mi][ni][q]);
+              }
+            } else if constexpr (EM == E_STORE) {
+              if (ok) sto(a.po0, o, acc[0][mi][ni][q]);
+            } else if constexpr (EM == E_STORE3) {
+              if (ok) {
+                sto(a.po0, o, acc[0][mi][ni][q]);
+                sto(a.po1, o, acc[1][mi][ni][q]);
+                sto(a.po2, o, acc[2][mi][ni][q]);
+              }
+            } else if constexpr (EM == E_OUT) {
+              if (ok) {
+                const float y = acc[0][mi][ni][q] + bn, yd = acc[1][mi][ni][q], ydd = acc[2][mi][ni][q];
+                sto(a.po0, o, y);
+                sto(a.po1, o, yd);
+                sto(a.po2, o, ydd);
+                t1[q] = fmaf(y, yd, t1[q]);
+                t2[q] = fmaf(yd, yd, fmaf(y, ydd, t2[q]));
+              }
+            } else if constexpr (EM == E_SEEDS) {
+              if (ok) {
+                const float ub = acc[0][mi][ni][q];
+                const float y = ldo(a.pe0, o), yd = ldo(a.pe1, o), ydd = ldo(a.pe2, o);
+                const float yb = 2.f * a.c3 * yd + 2.f * a.c2 * ydd + 2.f * ub;
+                sto(a.po0, o, yb);
+                sto(a.po1, o, 2.f * a.c3 * y + 4.f * a.c2 * yd);
+                sto(a.po2, o, 2.f * a.c2 * y);
+                pacc[ni] += yb;
+              }
+            } else if constexpr (EM == E_ACT_BWD) {
+              if (ok) {
+                const float hb = acc[0][mi][ni][q], hdb = acc[1][mi][ni][q], hddb = acc[2][mi][ni][q];
+                const float h = ldo(a.pe0, o), zd = ldo(a.pe1, o), zdd = ldo(a.pe2, o), aL = ldo(a.pe3, o), zb = ldo(a.pe4, o);
+                const float s1 = 1.f - h * h, s2 = -2.f * h * s1, s3 = -2.f * s1 * s1 - 2.f * h * s2;
+                const float zbar = s1 * hb + s2 * zd * hdb + (s2 * zdd + s3 * zd * zd) * hddb + s2 * aL * zb;
+                sto(a.po0, o, zbar);
+                sto(a.po1, o, s1 * hdb + 2.f * s2 * zd * hddb);
+                sto(a.po2, o, s1 * hddb);
+                pacc[ni] += zbar;
+              }
             }
           }
         }
-      }
-      if constexpr (EM == E_OUT) {
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          float p1 = t1[q], p2 = t2[q];
-#pragma unroll
-          for (int off = 16; off > 0; off >>= 1) {
-            p1 += __shfl_xor(p1, off, 64);
-            p2 += __shfl_xor(p2, off, 64);
+        if constexpr (EM == E_OUT) {
+  #pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            float p1 = t1[q], p2 = t2[q];
+  #pragma unroll
+            for (int off = 16; off > 0; off >>= 1) {
+              p1 += __shfl_xor(p1, off, 64);
+              p2 += __shfl_xor(p2, off, 64);
+            }
+            const int r = r0 + wm * WM + mi * 32 + (q & 3) + 8 * (q >> 2) + 4 * hi;
+            if (l31 == 0 && r < a.R) a.terms[r] = make_float2(2.f * p1, 2.f * p2);
           }
-          const int64_t r = r0 + wm * WM + mi * 32 + (q & 3) + 8 * (q >> 2) + 4 * hi;
-          if (l31 == 0 && r < a.R) a.terms[r] = make_float2(2.f * p1, 2.f * p2);
         }
       }
-    }
+    };
+    if (full) epilogue(std::false_type{});
+    else epilogue(std::true_type{});
   }
 
   if constexpr (NP > 0) {
@@ -494,23 +519,28 @@ __global__ __launch_bounds__(kT) void fwgrad(WgradArgs a) {
       const int e = tid + j * kT, rr = e / BM, ii = e - rr * BM;
       const int r = rb0 + rr, i = i0 + ii;
       const bool ok = r < rs1 && i < a.n_in;
-      const int o = ok ? r * a.n_in + i : 0;
-      ra[j][0] = ok ? a.pa0[o] : 0.f;
-      ra[j][1] = ok ? a.pa1[o] : 0.f;
-      ra[j][2] = ok ? a.pa2[o] : 0.f;
-      ra[j][3] = ok ? a.pa3[o] : 0.f;
+      const uint32_t o = ok ? (uint32_t)(r * a.n_in + i) : 0u;
+      const float t0 = ldo(a.pa0, o), t1 = ldo(a.pa1, o), t2 = ldo(a.pa2, o), t3 = ldo(a.pa3, o);
+      ra[j][0] = ok ? t0 : 0.f;
+      ra[j][1] = ok ? t1 : 0.f;
+      ra[j][2] = ok ? t2 : 0.f;
+      ra[j][3] = ok ? t3 : 0.f;
     }
 #pragma unroll
     for (int j = 0; j < NEB; ++j) {
       const int e = tid + j * kT, rr = e / BN, nn = e - rr * BN;
       const int r = rb0 + rr, n = n0 + nn;
       const bool ok = r < rs1 && n < a.n_out;
-      const int o = ok ? r * a.n_out + n : 0;
-      rb[j][0] = ok ? a.pb0[o] : 0.f;
-      rb[j][1] = ok ? a.pb1[o] : 0.f;
-      rb[j][2] = ok ? a.pb2[o] : 0.f;
-      rb[j][3] = ok ? a.pb3[o] : 0.f;
-      if constexpr (NVB > 4) rb[j][4] = ok ? a.pb4[o] : 0.f;
+      const uint32_t o = ok ? (uint32_t)(r * a.n_out + n) : 0u;
+      const float t0 = ldo(a.pb0, o), t1 = ldo(a.pb1, o), t2 = ldo(a.pb2, o), t3 = ldo(a.pb3, o);
+      rb[j][0] = ok ? t0 : 0.f;
+      rb[j][1] = ok ? t1 : 0.f;
+      rb[j][2] = ok ? t2 : 0.f;
+      rb[j][3] = ok ? t3 : 0.f;
+      if constexpr (NVB > 4) {
+        const float t4 = ldo(a.pb4, o);
+        rb[j][4] = ok ? t4 : 0.f;
+      }
     }
   };
   auto store = [&]() {

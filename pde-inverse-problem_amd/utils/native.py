@@ -49,7 +49,7 @@ EXPORTED_SYMBOLS = (
     "pdeinv_residual_kmv_workspace_bytes",
     "pdeinv_mlp_param_count", "pdeinv_residual_kfp_mlp_workspace_bytes", "pdeinv_residual_kfp_mlp",
     "pdeinv_kfp_terms_finalize", "pdeinv_gather_random_step", "pdeinv_mlp_fused_supported",
-    "pdeinv_adam_update",
+    "pdeinv_adam_update", "pdeinv_realnvp_param_count", "pdeinv_realnvp_logdensity",
 )
 
 
@@ -88,6 +88,15 @@ class KfpMlpDesc(ctypes.Structure):
 
 
 MLP_IMPL_AUTO, MLP_IMPL_LIBRARY, MLP_IMPL_FUSED = 0, 1, 2
+
+ACTIVATIONS = {"celu": 0, "relu": 1, "tanh": 2, "elu": 3, "silu": 4, "softplus": 5, "gelu": 6}
+
+
+class RealNvpDesc(ctypes.Structure):
+    _fields_ = [("dim", ctypes.c_int32), ("n_layers", ctypes.c_int32), ("embed_time_dim", ctypes.c_int32),
+                ("ignore_time", ctypes.c_int32), ("soft_init", ctypes.c_float), ("activation", ctypes.c_int32),
+                ("masks", ctypes.c_void_p), ("base_mean", ctypes.c_void_p), ("base_inv_cov", ctypes.c_void_p),
+                ("base_log_det", ctypes.c_float)]
 
 
 class KfpGmmDesc(ctypes.Structure):
@@ -150,6 +159,8 @@ def lib():
         "pdeinv_mlp_param_count": (i64, [i32, i32, i32, i32]),
         "pdeinv_mlp_fused_supported": (i32, [i32, i32, i32, i32]),
         "pdeinv_adam_update": (i32, [P, P, P, P, i64, f32, f32, f32, f32, f32, i32, P]),
+        "pdeinv_realnvp_param_count": (i64, [P]),
+        "pdeinv_realnvp_logdensity": (i32, [P, P, P, i64, P, i64, i64, P, P]),
         "pdeinv_residual_kfp_mlp_workspace_bytes": (ctypes.c_size_t, [P]),
         "pdeinv_residual_kfp_mlp": (i32, [P, P, i64, i64, P, i64, i64, P, i64, i64, P, P, P, P, P]),
         "pdeinv_kfp_terms_finalize": (i32, [P, P, i64, f32, P, P]),
@@ -598,6 +609,44 @@ def adam_update(params: torch.Tensor, grad: torch.Tensor, mu: torch.Tensor, nu: 
     _check(lib().pdeinv_adam_update(_dev(params, "params"), _dev(grad, "grad"), _dev(mu, "mu"), _dev(nu, "nu"), n,
                                     float(lr), float(b1), float(b2), float(eps), float(weight_decay), int(count),
                                     stream_handle()), "pdeinv_adam_update")
+
+
+def realnvp_desc(dim: int, masks, embed_time_dim: int, ignore_time: bool, soft_init: float, activation: str,
+                 base_mean, base_inv_cov, base_log_det: float):
+    """(descriptor, keep-alive host arrays) for pdeinv_realnvp_* ."""
+    if activation not in ACTIVATIONS:
+        raise NotImplementedError(f"RealNVP activation '{activation}' (prelu has parameters; not supported)")
+    m = _host_f32(masks)
+    mu = _host_f32(base_mean)
+    ic = _host_f32(base_inv_cov)
+    desc = RealNvpDesc(int(dim), int(m.size // dim), int(embed_time_dim), int(bool(ignore_time)), float(soft_init),
+                       ACTIVATIONS[activation], m.ctypes.data_as(ctypes.c_void_p), mu.ctypes.data_as(ctypes.c_void_p),
+                       ic.ctypes.data_as(ctypes.c_void_p), float(base_log_det))
+    return desc, (m, mu, ic)
+
+
+def realnvp_param_count(desc) -> int:
+    n = lib().pdeinv_realnvp_param_count(ctypes.byref(desc))
+    if n < 0:
+        raise ValueError("RealNVP: bad descriptor")
+    return int(n)
+
+
+def realnvp_logdensity(desc, params: torch.Tensor, t: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+    """log p_t(x) for rows x [n, dim] and times t [n] (or a 0-d / [1] t broadcast)."""
+    _require_gpu()
+    n = x.shape[0]
+    if params.numel() != realnvp_param_count(desc) or not params.is_contiguous():
+        raise ValueError("RealNVP: params must be a contiguous flat vector of pdeinv_realnvp_param_count floats")
+    t = t.reshape(-1)
+    if t.numel() not in (1, n):
+        raise ValueError("RealNVP: t must have one entry per row or a single entry")
+    px, _, ld = _rows(x, "x", desc.dim)
+    out = torch.empty(n, device=x.device, dtype=torch.float32)
+    _check(lib().pdeinv_realnvp_logdensity(ctypes.byref(desc), _dev(params, "params"), _dev(t.contiguous(), "t"),
+                                           0 if t.numel() == 1 else 1, px, n, ld, _dev(out, "out"),
+                                           stream_handle()), "pdeinv_realnvp_logdensity")
+    return out
 
 
 def mlp_fused_supported(dims) -> bool:

@@ -340,3 +340,36 @@ def test_adam_update_matches_optax_formula(native):
     assert np.allclose(dnu.cpu().numpy(), nu, rtol=1e-5, atol=1e-7)
     with pytest.raises(ValueError):
         native.adam_update(dp, _t(np.zeros(3)), dmu, dnu, lr=lr, b1=b1, b2=b2, eps=eps, weight_decay=wd, count=1)
+
+
+@pytest.mark.parametrize("dim,mask_type,E,soft_init,ignore_time,act", [
+    (2, "loop", 10, 1.0, False, "celu"), (4, "random", 0, 0.0, False, "tanh"), (8, "loop", 10, 1.0, False, "silu"),
+    (3, "random", 6, 1.0, True, "softplus"), (1, "loop", 4, 0.0, False, "gelu")])
+def test_realnvp_logdensity_vs_restatement(native, dim, mask_type, E, soft_init, ignore_time, act):
+    """pdeinv_realnvp_logdensity (normalizing_flow.py:115-229) vs the fp64 restatement that
+    tests/test_oracle.py pins by invertibility and normalisation; fp32 tolerance."""
+    from core.distribution import Gaussian
+    from core.normalizing_flow import MNF, RealNVP
+    couple = 4 if mask_type == "loop" else 3
+    mnf = MNF(dim, couple, mask_type, soft_init, ignore_time, act, E)
+    rng = np.random.default_rng(dim)
+    mean = rng.standard_normal(dim) * 0.3
+    Lc = rng.standard_normal((dim, dim)) * 0.3
+    cov = Lc @ Lc.T + np.eye(dim)
+    flow = RealNVP(mnf, Gaussian(mean, cov).logdensity)
+    flat = nr.nvp_init(dim, mnf.n_layers, E, ignore_time, seed=dim + 1, scale=1.3, perturb=True)
+    assert flat.size == mnf.param_count() == native.realnvp_param_count(flow._desc)
+    x = rng.standard_normal((5000, dim)) * 1.5
+    t = rng.uniform(0, 2, 5000)
+    got = flow.apply({"params": _t(flat)}, _t(t), _t(x)).cpu().numpy()
+    ref = nr.realnvp_logdensity(flat, t, x, dim=dim, masks=mnf.masks, base_mean=mean, base_cov=cov, E=E,
+                                ignore_time=ignore_time, soft_init=soft_init, act=act)
+    assert np.max(np.abs(got - ref)) < 2e-4 * (1 + np.abs(ref).max()), np.max(np.abs(got - ref))
+    one = flow.apply({"params": _t(flat)}, float(t[0]), _t(x[0])).item()   # unbatched call
+    assert abs(one - ref[0]) < 2e-4 * (1 + abs(ref[0]))
+    # the reference's model (log_density_estimation.py:103-114) at its fresh init
+    from core.log_density_estimation import create_normalizing_flow_fn
+    from utils import prng
+    f2 = create_normalizing_flow_fn(Gaussian(np.zeros(2), np.eye(2)).logdensity, 2)
+    p2 = f2.init(prng.PRNGKey(0), 0.0, np.zeros(2))
+    assert torch.isfinite(f2.apply(p2, _t(t[:10]), _t(x[:10, :2] if dim >= 2 else np.zeros((10, 2))))).all()

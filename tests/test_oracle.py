@@ -242,3 +242,28 @@ def test_shared_clock_stamp_times_match_c_oracle(oracle_lib):
     for seed, ctr in ((0xABCDEF, 5), (0x5EED_0004, 101 * 7), (2**40 + 3, 0)):
         o = oracle_lib.sde_simulate(z0, 30, 0.02, 1.0, "meanfield", A, seed=seed, counter_offset=ctr)
         assert np.array_equal(o["tau"][:, 0], stamp_times(seed, ctr, 30, 0.02))
+
+
+@pytest.mark.parametrize("dim,mask_type,E,soft_init,act", [(1, "loop", 10, 1.0, "celu"), (2, "loop", 10, 1.0, "celu"),
+                                                           (2, "random", 0, 0.0, "tanh"), (2, "loop", 6, 1.0, "silu")])
+def test_realnvp_restatement_is_a_normalised_invertible_density(dim, mask_type, E, soft_init, act):
+    """Pins the RealNVP restatement (normalizing_flow.py:115-229) without JAX: the sampling direction
+    inverts the likelihood direction (x -> x0 -> x) with opposite log-det-Jacobians, and exp(log p_t)
+    integrates to 1 over x (change of variables; 1-D and 2-D quadrature)."""
+    couple = 4 if mask_type == "loop" else 3
+    masks = nr.nvp_masks(dim, couple, mask_type)
+    flat = nr.nvp_init(dim, masks.shape[0], E, False, seed=dim, scale=1.5, perturb=True)
+    kw = dict(dim=dim, masks=masks, E=E, soft_init=soft_init, act=act)
+    rng = np.random.default_rng(0)
+    x = rng.standard_normal((200, dim))
+    t = rng.uniform(0, 2, 200)
+    x0, ldj_r = nr.realnvp_apply(flat, t, x, reverse=True, **kw)
+    x1, ldj_f = nr.realnvp_apply(flat, t, x0, reverse=False, **kw)
+    assert np.max(np.abs(x1 - x)) < 1e-10 and np.max(np.abs(ldj_r + ldj_f)) < 1e-10
+    mean, cov = np.full(dim, 0.3), np.eye(dim) * 1.7
+    g = np.linspace(-60, 60, 12001) if dim == 1 else np.linspace(-60, 60, 801)
+    pts = g[:, None] if dim == 1 else np.stack(np.meshgrid(g, g, indexing="ij"), -1).reshape(-1, 2)
+    for tt in (0.0, 0.7):
+        p = np.exp(nr.realnvp_logdensity(flat, tt, pts, base_mean=mean, base_cov=cov, **kw))
+        integral = p.sum() * (g[1] - g[0]) ** dim
+        assert abs(integral - 1.0) < 2e-3, integral
