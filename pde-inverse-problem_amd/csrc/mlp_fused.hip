@@ -88,8 +88,9 @@ struct ARegs {
   float v[NE][NV > 0 ? NV : 1];
 };
 
-// Loads are unconditional from a clamped 32-bit offset (a chunk's planes stay below 2^31 floats)
-// and zeroed by a select: no per-element exec-mask branches, uniform base + lane offset addressing.
+// Loads are unconditional from a clamped 32-bit offset (a chunk's planes stay below 2^31 floats):
+// no per-element exec-mask branches. The zeroing select of out-of-range elements happens in the
+// store phase, after the MFMAs, so the loads stay in flight under the current tile's math.
 template <int BM, int AM>
 __device__ __forceinline__ void load_a(const GemmArgs& a, ARegs<BM, AM>& ra, int r0, int k0) {
 #pragma unroll
@@ -99,26 +100,21 @@ __device__ __forceinline__ void load_a(const GemmArgs& a, ARegs<BM, AM>& ra, int
     const int r = r0 + m, k = k0 + kk;
     const bool ok = r < a.R && k < a.K;
     const uint32_t o = ok ? (uint32_t)(r * a.K + k) : 0u;
-    const float t0 = ldo(a.pa0, o);
-    ra.v[j][0] = ok ? t0 : 0.f;
-    if constexpr (ARegs<BM, AM>::NV > 1) {
-      const float t1 = ldo(a.pa1, o);
-      ra.v[j][1] = ok ? t1 : 0.f;
-    }
-    if constexpr (ARegs<BM, AM>::NV > 2) {
-      const float t2 = ldo(a.pa2, o);
-      ra.v[j][2] = ok ? t2 : 0.f;
-    }
+    ra.v[j][0] = ldo(a.pa0, o);
+    if constexpr (ARegs<BM, AM>::NV > 1) ra.v[j][1] = ldo(a.pa1, o);
+    if constexpr (ARegs<BM, AM>::NV > 2) ra.v[j][2] = ldo(a.pa2, o);
   }
 }
 
 template <int S, int BM, int AM>
-__device__ __forceinline__ void store_a(const ARegs<BM, AM>& ra, float* As) {
+__device__ __forceinline__ void store_a(const GemmArgs& a, const ARegs<BM, AM>& ra, float* As, int r0, int k0,
+                                        bool full) {
   constexpr int LDA = BM + 4;
 #pragma unroll
   for (int j = 0; j < ARegs<BM, AM>::NE; ++j) {
     const int e = threadIdx.x + j * kT;
     const int m = e / BK, kk = e - m * BK;
+    const bool ok = full || (r0 + m < a.R && k0 + kk < a.K);
     float v0 = 0.f, v1 = 0.f, v2 = 0.f;
     if constexpr (AM == A_FWD) {
       const float h = ra.v[j][0], zd = ra.v[j][1], zdd = ra.v[j][2];
@@ -138,9 +134,20 @@ __device__ __forceinline__ void store_a(const ARegs<BM, AM>& ra, float* As) {
       v1 = ra.v[j][1];
       v2 = ra.v[j][2];
     }
-    As[kk * LDA + m] = v0;
-    if constexpr (S > 1) As[(BK + kk) * LDA + m] = v1;
-    if constexpr (S > 2) As[(2 * BK + kk) * LDA + m] = v2;
+    As[kk * LDA + m] = ok ? v0 : 0.f;
+    if constexpr (S > 1) As[(BK + kk) * LDA + m] = ok ? v1 : 0.f;
+    if constexpr (S > 2) As[(2 * BK + kk) * LDA + m] = ok ? v2 : 0.f;
+  }
+}
+
+template <int BN, int BMD>
+__device__ __forceinline__ void b_coords(int e, int& kk, int& nn) {
+  if constexpr (BMD == B_NN) {
+    kk = e / BN;
+    nn = e - kk * BN;
+  } else {
+    nn = e / BK;
+    kk = e - nn * BK;
   }
 }
 
@@ -148,36 +155,25 @@ template <int BN, int BMD>
 __device__ __forceinline__ void load_b(const GemmArgs& a, float (&rb)[BK * BN / kT], int k0, int n0) {
 #pragma unroll
   for (int j = 0; j < BK * BN / kT; ++j) {
-    const int e = threadIdx.x + j * kT;
     int kk, nn;
-    if constexpr (BMD == B_NN) {
-      kk = e / BN;
-      nn = e - kk * BN;
-    } else {
-      nn = e / BK;
-      kk = e - nn * BK;
-    }
+    b_coords<BN, BMD>(threadIdx.x + j * kT, kk, nn);
     const int k = k0 + kk, n = n0 + nn;
     const bool ok = k < a.K && n < a.N;
     const uint32_t o = ok ? (uint32_t)(BMD == B_NN ? k * a.N + n : n * a.K + k) : 0u;
-    const float t = ldo(a.Bw, o);
-    rb[j] = ok ? t : 0.f;
+    rb[j] = ldo(a.Bw, o);
   }
 }
 
 template <int BN, int BMD>
-__device__ __forceinline__ void store_b(const float (&rb)[BK * BN / kT], float* Bs) {
+__device__ __forceinline__ void store_b(const GemmArgs& a, const float (&rb)[BK * BN / kT], float* Bs, int k0, int n0,
+                                        bool full) {
   constexpr int LDB = BN + 4;
 #pragma unroll
   for (int j = 0; j < BK * BN / kT; ++j) {
-    const int e = threadIdx.x + j * kT;
-    if constexpr (BMD == B_NN) {
-      const int kk = e / BN, nn = e - kk * BN;
-      Bs[kk * LDB + nn] = rb[j];
-    } else {
-      const int nn = e / BK, kk = e - nn * BK;
-      Bs[kk * LDB + nn] = rb[j];
-    }
+    int kk, nn;
+    b_coords<BN, BMD>(threadIdx.x + j * kT, kk, nn);
+    const bool ok = full || (k0 + kk < a.K && n0 + nn < a.N);
+    Bs[kk * LDB + nn] = ok ? rb[j] : 0.f;
   }
 }
 
@@ -217,8 +213,8 @@ __global__ __launch_bounds__(kT) void fgemm(GemmArgs a) {
     load_b<BN, BMD>(a, rb, 0, n0);
     for (int k0 = 0; k0 < a.K; k0 += BK) {
       __syncthreads();  // every wave is done reading the previous tile
-      store_a<S, BM, AM>(ra, As);
-      store_b<BN, BMD>(rb, Bs);
+      store_a<S, BM, AM>(a, ra, As, r0, k0, r0 + BM <= a.R && k0 + BK <= a.K);
+      store_b<BN, BMD>(a, rb, Bs, k0, n0, k0 + BK <= a.K && n0 + BN <= a.N);
       __syncthreads();
       if (k0 + BK < a.K) {  // next tile's global loads fly under this tile's MFMAs
         load_a<BM, AM>(a, ra, r0, k0 + BK);
@@ -520,11 +516,10 @@ __global__ __launch_bounds__(kT) void fwgrad(WgradArgs a) {
       const int r = rb0 + rr, i = i0 + ii;
       const bool ok = r < rs1 && i < a.n_in;
       const uint32_t o = ok ? (uint32_t)(r * a.n_in + i) : 0u;
-      const float t0 = ldo(a.pa0, o), t1 = ldo(a.pa1, o), t2 = ldo(a.pa2, o), t3 = ldo(a.pa3, o);
-      ra[j][0] = ok ? t0 : 0.f;
-      ra[j][1] = ok ? t1 : 0.f;
-      ra[j][2] = ok ? t2 : 0.f;
-      ra[j][3] = ok ? t3 : 0.f;
+      ra[j][0] = ldo(a.pa0, o);
+      ra[j][1] = ldo(a.pa1, o);
+      ra[j][2] = ldo(a.pa2, o);
+      ra[j][3] = ldo(a.pa3, o);
     }
 #pragma unroll
     for (int j = 0; j < NEB; ++j) {
@@ -532,21 +527,19 @@ __global__ __launch_bounds__(kT) void fwgrad(WgradArgs a) {
       const int r = rb0 + rr, n = n0 + nn;
       const bool ok = r < rs1 && n < a.n_out;
       const uint32_t o = ok ? (uint32_t)(r * a.n_out + n) : 0u;
-      const float t0 = ldo(a.pb0, o), t1 = ldo(a.pb1, o), t2 = ldo(a.pb2, o), t3 = ldo(a.pb3, o);
-      rb[j][0] = ok ? t0 : 0.f;
-      rb[j][1] = ok ? t1 : 0.f;
-      rb[j][2] = ok ? t2 : 0.f;
-      rb[j][3] = ok ? t3 : 0.f;
-      if constexpr (NVB > 4) {
-        const float t4 = ldo(a.pb4, o);
-        rb[j][4] = ok ? t4 : 0.f;
-      }
+      rb[j][0] = ldo(a.pb0, o);
+      rb[j][1] = ldo(a.pb1, o);
+      rb[j][2] = ldo(a.pb2, o);
+      rb[j][3] = ldo(a.pb3, o);
+      if constexpr (NVB > 4) rb[j][4] = ldo(a.pb4, o);
     }
   };
-  auto store = [&]() {
+  auto store = [&](int rb0) {
+    const bool rows_full = rb0 + BKG <= rs1;
 #pragma unroll
     for (int j = 0; j < NEA; ++j) {
       const int e = tid + j * kT, rr = e / BM, ii = e - rr * BM;
+      const bool ok = (rows_full || rb0 + rr < rs1) && i0 + ii < a.n_in;
       float v0 = ra[j][0], v1 = ra[j][1], v2 = ra[j][2], v3 = ra[j][3];
       if constexpr (GA == GA_PL) {
         const float h = v0, zd = v1, zdd = v2, zeb = v3;
@@ -555,14 +548,15 @@ __global__ __launch_bounds__(kT) void fwgrad(WgradArgs a) {
         v2 = fmaf(s1, zdd, s2 * zd * zd);
         v3 = s1 * zeb;
       }
-      As[(0 * BKG + rr) * LDA + ii] = v0;
-      As[(1 * BKG + rr) * LDA + ii] = v1;
-      As[(2 * BKG + rr) * LDA + ii] = v2;
-      As[(3 * BKG + rr) * LDA + ii] = v3;
+      As[(0 * BKG + rr) * LDA + ii] = ok ? v0 : 0.f;
+      As[(1 * BKG + rr) * LDA + ii] = ok ? v1 : 0.f;
+      As[(2 * BKG + rr) * LDA + ii] = ok ? v2 : 0.f;
+      As[(3 * BKG + rr) * LDA + ii] = ok ? v3 : 0.f;
     }
 #pragma unroll
     for (int j = 0; j < NEB; ++j) {
       const int e = tid + j * kT, rr = e / BN, nn = e - rr * BN;
+      const bool ok = (rows_full || rb0 + rr < rs1) && n0 + nn < a.n_out;
       float v3;
       if constexpr (GB == GB_PL) {
         const float h = rb[j][3];
@@ -570,17 +564,17 @@ __global__ __launch_bounds__(kT) void fwgrad(WgradArgs a) {
       } else {
         v3 = 2.f * rb[j][3];
       }
-      Bs[(0 * BKG + rr) * LDB + nn] = rb[j][0];
-      Bs[(1 * BKG + rr) * LDB + nn] = rb[j][1];
-      Bs[(2 * BKG + rr) * LDB + nn] = rb[j][2];
-      Bs[(3 * BKG + rr) * LDB + nn] = v3;
+      Bs[(0 * BKG + rr) * LDB + nn] = ok ? rb[j][0] : 0.f;
+      Bs[(1 * BKG + rr) * LDB + nn] = ok ? rb[j][1] : 0.f;
+      Bs[(2 * BKG + rr) * LDB + nn] = ok ? rb[j][2] : 0.f;
+      Bs[(3 * BKG + rr) * LDB + nn] = ok ? v3 : 0.f;
     }
   };
 
   if (rs0 < rs1) load(rs0);
   for (int rb0 = rs0; rb0 < rs1; rb0 += BKG) {
     __syncthreads();
-    store();
+    store(rb0);
     __syncthreads();
     if (rb0 + BKG < rs1) load(rb0 + BKG);  // in flight under this block's MFMAs
 #pragma unroll
