@@ -141,31 +141,24 @@ constexpr int kGmmGridCap = 1024;
 // (the |x|^2 term cancels in the softmax); returns w, mbar = sum_k w_k mu_k and t_k = x.mu_k.
 // l2s = log2(e)/s^2, nh[k] = -|mu_k|^2/2.
 template <int D, int KM>
-__device__ __forceinline__ void gmm_softmax(const float* x, const float (*mu)[D], const float* nh, int K,
-                                            float l2s, float* w, float* mbar, float* t) {
+__device__ __forceinline__ void gmm_softmax(const float* x, const float (*mu)[D], const float* nh, float l2s,
+                                            float* w, float* mbar, float* t) {
+  // unused centre slots carry nh = -inf: weight exactly 0, no per-centre branches
   float amax = -INFINITY;
 #pragma unroll
   for (int k = 0; k < KM; ++k) {
-    if (k < K) {
-      float dot = 0.f;
+    float dot = 0.f;
 #pragma unroll
-      for (int i = 0; i < D; ++i) dot = fmaf(x[i], mu[k][i], dot);
-      t[k] = dot;
-      w[k] = (dot + nh[k]) * l2s;
-      amax = fmaxf(amax, w[k]);
-    } else {
-      t[k] = 0.f;
-    }
+    for (int i = 0; i < D; ++i) dot = fmaf(x[i], mu[k][i], dot);
+    t[k] = dot;
+    w[k] = (dot + nh[k]) * l2s;
+    amax = fmaxf(amax, w[k]);
   }
   float den = 0.f;
 #pragma unroll
   for (int k = 0; k < KM; ++k) {
-    if (k < K) {
-      w[k] = __builtin_amdgcn_exp2f(w[k] - amax);
-      den += w[k];
-    } else {
-      w[k] = 0.f;
-    }
+    w[k] = __builtin_amdgcn_exp2f(w[k] - amax);
+    den += w[k];
   }
   const float inv = __builtin_amdgcn_rcpf(den);
 #pragma unroll
@@ -182,6 +175,11 @@ template <int D, int KM>
 __global__ __launch_bounds__(kBlock) void kfp_gmm_kernel(GmmResArgs a, const float* __restrict__ mus,
                                                          float* __restrict__ partials) {
   constexpr int NS = PDEINV_GMM_NACC;
+  // model and true centres pinned in VGPRs (as uniform SGPR values they overflow the scalar file
+  // and every use costs a v_readlane); empty slots: nh = -inf (softmax weight 0)
+  // Empty centre slots: nh = -inf (softmax weight exactly 0, no per-centre branches). Pinning the
+  // centres in VGPRs (as in the simulator) does not pay here: the K*d gradient accumulators already
+  // fill the register file (measured: occupancy 2 -> 1).
   float mu[KM][D];
   float mut[KM][D];
   float nh[KM], nht[KM];
@@ -195,8 +193,8 @@ __global__ __launch_bounds__(kBlock) void kfp_gmm_kernel(GmmResArgs a, const flo
       n2 = fmaf(mu[k][i], mu[k][i], n2);
       n2t = fmaf(mut[k][i], mut[k][i], n2t);
     }
-    nh[k] = -0.5f * n2;
-    nht[k] = -0.5f * n2t;
+    nh[k] = (k < a.K) ? -0.5f * n2 : -INFINITY;
+    nht[k] = (k < a.KT) ? -0.5f * n2t : -INFINITY;
   }
   float acc[NS + KM * D];
 #pragma unroll
@@ -233,7 +231,7 @@ __global__ __launch_bounds__(kBlock) void kfp_gmm_kernel(GmmResArgs a, const flo
     }
 
     float w[KM], mbar[D], xm[KM];
-    gmm_softmax<D, KM>(x, mu, nh, a.K, a.l2s, w, mbar, xm);
+    gmm_softmax<D, KM>(x, mu, nh, a.l2s, w, mbar, xm);
     float e[D], g[D], T1 = 0.f, T3 = 0.f, vv = 0.f;
 #pragma unroll
     for (int i = 0; i < D; ++i) {
@@ -279,7 +277,7 @@ __global__ __launch_bounds__(kBlock) void kfp_gmm_kernel(GmmResArgs a, const flo
     acc[PDEINV_GMM_ACC_LOSS] += c1 * T1 + c2 * T2 + c3 * T3;
     if (set == 0) {
       float wt[KM], mbt[D], xmt[KM];
-      gmm_softmax<D, KM>(x, mut, nht, a.KT, a.l2st, wt, mbt, xmt);
+      gmm_softmax<D, KM>(x, mut, nht, a.l2st, wt, mbt, xmt);
       float Tt = 0.f, Tgt = 0.f;
 #pragma unroll
       for (int i = 0; i < D; ++i) {

@@ -19,12 +19,12 @@ namespace pdeinv {
 struct SdeArgs {
   int64_t N, poff, ld_z0;
   int32_t n_steps, random_shift, K, has_center;
-  float dt, gamma, ns, neg_half_inv_s2_log2e, inv_s2;
+  float dt, gamma, ns, neg_half_inv_s2_log2e, inv_s2, l2s;
   uint32_t k0, k1, ctr_off;
   const float* noise;
   const float* shift_u;
   // QUADRATIC: A (d*d) then c (d). GMM (packed on the host at compile-time offsets):
-  // [kMaxGmmK*d scaled mu | kMaxGmmK constants | kMaxGmmK*d raw mu]
+  // GMM: [kMaxGmmK*d raw mu | kMaxGmmK constants c_k = -|mu_k|^2 log2e / (2 s^2)]
   float params[2 * 16 * PDEINV_MAX_DIM + 16];
 };
 
@@ -69,39 +69,50 @@ __device__ __forceinline__ void grad_quadratic(const SdeArgs& a, const float* q,
 
 // grad of U = -logsumexp_k(-|q-mu_k|^2/(2 s^2)) = (q - sum_k w_k mu_k) / s^2
 // (core/potential.py:32-37; the softmax form of the commented analytic gradient :39-43).
-// Softmax logits are shift-invariant, so |q|^2 drops out: a_k = (q . mu_k - |mu_k|^2 / 2) / s^2,
-// one d-term dot per centre. The centres arrive in the kernel arguments pre-scaled to log2 units
-// (params[k*D+i] = mu_ki * log2e / s^2, params[K*D + k] = -|mu_k|^2 log2e / (2 s^2)) and raw
-// (params[K*D + K + k*D + i] = mu_ki) for the weighted mean.
-template <int D>
-__device__ __forceinline__ void grad_gmm(const SdeArgs& a, const float* q, float* g) {
-  const int K = a.K;
-  const float* mu_s = a.params;                      // compile-time offsets: the centres stay
-  const float* c = a.params + kMaxGmmK * D;          // scalar (SGPR) loads, not VGPR copies
-  const float* mu = a.params + kMaxGmmK * D + kMaxGmmK;
-  float al[kMaxGmmK];
+// Softmax logits are shift-invariant, so |q|^2 drops out: in log2 units
+// a_k = l2s (q . mu_k) + c_k, l2s = log2e / s^2, c_k = -l2s |mu_k|^2 / 2 — one d-term dot per
+// centre. The KM centres live in VGPRs for the whole kernel (pinned once: kept as kernel-argument
+// SGPRs they overflow the scalar file and every use costs a v_readlane); unused slots carry
+// c_k = -inf, so the softmax needs no per-centre branches.
+template <int D, int KM>
+struct GmmCentres {
+  float mu[KM][D];
+  float c[KM];
+  __device__ __forceinline__ void load(const SdeArgs& a) {
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+#pragma unroll
+      for (int i = 0; i < D; ++i) {
+        mu[k][i] = k < a.K ? a.params[k * D + i] : 0.f;
+        asm volatile("" : "+v"(mu[k][i]));
+      }
+      c[k] = k < a.K ? a.params[kMaxGmmK * D + k] : -INFINITY;
+      asm volatile("" : "+v"(c[k]));
+    }
+  }
+};
+
+template <int D, int KM>
+__device__ __forceinline__ void grad_gmm(const SdeArgs& a, const GmmCentres<D, KM>& C, const float* q, float* g) {
+  float al[KM];
   float amax = -INFINITY;
 #pragma unroll
-  for (int k = 0; k < kMaxGmmK; ++k) {
-    if (k < K) {
-      float t = c[k];
+  for (int k = 0; k < KM; ++k) {
+    float t = 0.f;
 #pragma unroll
-      for (int i = 0; i < D; ++i) t = fmaf(q[i], mu_s[k * D + i], t);
-      al[k] = t;
-      amax = fmaxf(amax, t);
-    }
+    for (int i = 0; i < D; ++i) t = fmaf(q[i], C.mu[k][i], t);
+    al[k] = fmaf(a.l2s, t, C.c[k]);
+    amax = fmaxf(amax, al[k]);
   }
   float den = 0.f, acc[D];
 #pragma unroll
   for (int i = 0; i < D; ++i) acc[i] = 0.f;
 #pragma unroll
-  for (int k = 0; k < kMaxGmmK; ++k) {
-    if (k < K) {
-      const float e = __builtin_amdgcn_exp2f(al[k] - amax);
-      den += e;
+  for (int k = 0; k < KM; ++k) {
+    const float e = __builtin_amdgcn_exp2f(al[k] - amax);
+    den += e;
 #pragma unroll
-      for (int i = 0; i < D; ++i) acc[i] = fmaf(e, mu[k * D + i], acc[i]);
-    }
+    for (int i = 0; i < D; ++i) acc[i] = fmaf(e, C.mu[k][i], acc[i]);
   }
   const float inv = __builtin_amdgcn_rcpf(den);
 #pragma unroll
@@ -192,7 +203,7 @@ __device__ __forceinline__ float shift_u(const SdeArgs& a, uint32_t plo, uint32_
   return u32_unit(r.x);
 }
 
-template <int D, int POT, bool MOM, int STORE, int MINW = 1>
+template <int D, int POT, bool MOM, int STORE, int KM = 1, int MINW = 1>
 __global__ __launch_bounds__(kBlock, MINW) void sde_simulate_kernel(SdeArgs a, const float* __restrict__ z0,
                                                               float* __restrict__ traj,
                                                               float* __restrict__ tau,
@@ -209,6 +220,8 @@ __global__ __launch_bounds__(kBlock, MINW) void sde_simulate_kernel(SdeArgs a, c
   float z[M];
 #pragma unroll
   for (int k = 0; k < M; ++k) z[k] = z0[i * a.ld_z0 + k];
+  [[maybe_unused]] GmmCentres<D, KM> centres;
+  if constexpr (POT == PDEINV_POT_GMM) centres.load(a);
 
   __shared__ float lds[kWavesPerBlock * moment_len(M > 16 ? 2 : M)];
   const int nb = gridDim.x;
@@ -242,7 +255,7 @@ __global__ __launch_bounds__(kBlock, MINW) void sde_simulate_kernel(SdeArgs a, c
 
   auto update = [&](float h, float sh, uint32_t s) {
     float g[D], xi[D];
-    if constexpr (POT == PDEINV_POT_GMM) grad_gmm<D>(a, z, g);
+    if constexpr (POT == PDEINV_POT_GMM) grad_gmm<D, KM>(a, centres, z, g);
     else grad_quadratic<D>(a, z, g);
     gen_normals<D>(a, plo, phi, s, i, xi);
     const float gh = a.gamma * h;
@@ -402,6 +415,7 @@ static int build_args(const pdeinv_sde_desc* d, SdeArgs& a) {
       a.K = p.n_centers;
       a.inv_s2 = 1.0f / (p.sigma * p.sigma);
       a.neg_half_inv_s2_log2e = -0.5f * a.inv_s2 * 1.4426950408889634f;
+      a.l2s = (float)(1.4426950408889634 / ((double)p.sigma * (double)p.sigma));
       {
         const double sc = 1.4426950408889634 / ((double)p.sigma * (double)p.sigma);
         const int K = p.n_centers;
@@ -409,8 +423,7 @@ static int build_args(const pdeinv_sde_desc* d, SdeArgs& a) {
           double n2 = 0;
           for (int i = 0; i < D; ++i) {
             const double m = p.params[k * D + i];
-            a.params[k * D + i] = (float)(m * sc);
-            a.params[kMaxGmmK * D + kMaxGmmK + k * D + i] = (float)m;
+            a.params[k * D + i] = (float)m;
             n2 += m * m;
           }
           a.params[kMaxGmmK * D + k] = (float)(-0.5 * n2 * sc);
@@ -444,11 +457,19 @@ extern "C" size_t pdeinv_sde_workspace_bytes(const pdeinv_sde_desc* d) {
   return (size_t)3 * moment_len(2 * d->dim) * sim_grid(d->n_particles) * sizeof(float);
 }
 
-template <int D, int POT, bool MOM>
+template <int D, int POT, bool MOM, int KM = 1>
 static void launch_sim(const SdeArgs& a, const float* z0, float* traj, float* tau, float* last,
                        float* ws, hipStream_t st) {
   const dim3 g(sim_grid(a.N)), b(kBlock);
-  hipLaunchKernelGGL((sde_simulate_kernel<D, POT, MOM, kStoreStaged>), g, b, 0, st, a, z0, traj, tau, last, ws);
+  hipLaunchKernelGGL((sde_simulate_kernel<D, POT, MOM, kStoreStaged, KM>), g, b, 0, st, a, z0, traj, tau, last, ws);
+}
+
+template <int D, bool MOM>
+static void launch_gmm_sim(const SdeArgs& a, const float* z0, float* traj, float* tau, float* last, float* ws,
+                           hipStream_t st) {
+  if (a.K <= 4) launch_sim<D, PDEINV_POT_GMM, MOM, 4>(a, z0, traj, tau, last, ws, st);
+  else if (a.K <= 8) launch_sim<D, PDEINV_POT_GMM, MOM, 8>(a, z0, traj, tau, last, ws, st);
+  else launch_sim<D, PDEINV_POT_GMM, MOM, 16>(a, z0, traj, tau, last, ws, st);
 }
 
 template <int D>
@@ -456,9 +477,9 @@ static int dispatch_sim(const SdeArgs& a, int pot, bool mom, const float* z0, fl
                         float* tau, float* last, float* ws, hipStream_t st) {
   if (pot == PDEINV_POT_GMM) {
     if constexpr (D <= 8) {
-      if (mom) { launch_sim<D, PDEINV_POT_GMM, true>(a, z0, traj, tau, last, ws, st); return 0; }
+      if (mom) { launch_gmm_sim<D, true>(a, z0, traj, tau, last, ws, st); return 0; }
     }
-    launch_sim<D, PDEINV_POT_GMM, false>(a, z0, traj, tau, last, ws, st);
+    launch_gmm_sim<D, false>(a, z0, traj, tau, last, ws, st);
   } else {
     if constexpr (D <= 8) {
       if (mom) { launch_sim<D, PDEINV_POT_QUADRATIC, true>(a, z0, traj, tau, last, ws, st); return 0; }
