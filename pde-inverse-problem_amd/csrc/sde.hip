@@ -31,10 +31,13 @@ struct SdeArgs {
 constexpr int kMaxGmmK = 16;
 
 // d standard normals for update s of particle (plo, phi) — stream layout of include/pdeinv.h.
-template <int D>
+// EXPLICIT (the explicit-noise parity mode) is a compile-time choice: a global load left on the
+// Philox path of the step loop makes the compiler wait vmcnt(0) at the join, and on gfx950 vmcnt
+// also counts the previous steps' trajectory stores — every step would wait for them to retire.
+template <int D, bool EXPLICIT = false>
 __device__ __forceinline__ void gen_normals(const SdeArgs& a, uint32_t plo, uint32_t phi,
                                             uint32_t s, int64_t i, float* xi) {
-  if (a.noise) {
+  if constexpr (EXPLICIT) {
     const float* src = a.noise + ((int64_t)s * a.N + i) * D;
 #pragma unroll
     for (int k = 0; k < D; ++k) xi[k] = src[k];
@@ -203,7 +206,7 @@ __device__ __forceinline__ float shift_u(const SdeArgs& a, uint32_t plo, uint32_
   return u32_unit(r.x);
 }
 
-template <int D, int POT, bool MOM, int STORE, int KM = 1, int MINW = 1>
+template <int D, int POT, bool MOM, int STORE, int KM = 1, bool NOISE = false, int MINW = 1>
 __global__ __launch_bounds__(kBlock, MINW) void sde_simulate_kernel(SdeArgs a, const float* __restrict__ z0,
                                                               float* __restrict__ traj,
                                                               float* __restrict__ tau,
@@ -257,7 +260,7 @@ __global__ __launch_bounds__(kBlock, MINW) void sde_simulate_kernel(SdeArgs a, c
     float g[D], xi[D];
     if constexpr (POT == PDEINV_POT_GMM) grad_gmm<D, KM>(a, centres, z, g);
     else grad_quadratic<D>(a, z, g);
-    gen_normals<D>(a, plo, phi, s, i, xi);
+    gen_normals<D, NOISE>(a, plo, phi, s, i, xi);
     const float gh = a.gamma * h;
 #pragma unroll
     for (int k = 0; k < D; ++k) {
@@ -338,7 +341,8 @@ __global__ __launch_bounds__(kBlock) void mf_step_kernel(SdeArgs a, int s, float
     g[r] = acc;
   }
   float xi[D];
-  gen_normals<D>(a, (uint32_t)gid, (uint32_t)(gid >> 32), (uint32_t)s, i, xi);
+  if (a.noise) gen_normals<D, true>(a, (uint32_t)gid, (uint32_t)(gid >> 32), (uint32_t)s, i, xi);
+  else gen_normals<D, false>(a, (uint32_t)gid, (uint32_t)(gid >> 32), (uint32_t)s, i, xi);
   const float h = (s == 0) ? tau0 : ((s == a.n_steps) ? a.dt - tau0 : a.dt);
   const float sh = sqrtf(h) * a.ns;
   const float gh = a.gamma * h;
@@ -461,7 +465,12 @@ template <int D, int POT, bool MOM, int KM = 1>
 static void launch_sim(const SdeArgs& a, const float* z0, float* traj, float* tau, float* last,
                        float* ws, hipStream_t st) {
   const dim3 g(sim_grid(a.N)), b(kBlock);
-  hipLaunchKernelGGL((sde_simulate_kernel<D, POT, MOM, kStoreStaged, KM>), g, b, 0, st, a, z0, traj, tau, last, ws);
+  if (a.noise)
+    hipLaunchKernelGGL((sde_simulate_kernel<D, POT, MOM, kStoreStaged, KM, true>), g, b, 0, st, a, z0, traj, tau,
+                       last, ws);
+  else
+    hipLaunchKernelGGL((sde_simulate_kernel<D, POT, MOM, kStoreStaged, KM, false>), g, b, 0, st, a, z0, traj, tau,
+                       last, ws);
 }
 
 template <int D, bool MOM>
