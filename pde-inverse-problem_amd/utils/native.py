@@ -124,10 +124,11 @@ def lib():
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
-        raise RuntimeError(f"pdeinv native library missing at {LIB_PATH}; run __graft_entry__.build() "
+    path = os.environ.get("PDEINV_LIBRARY", LIB_PATH)  # A/B timing of alternative builds (tools/)
+    if not os.path.exists(path):
+        raise RuntimeError(f"pdeinv native library missing at {path}; run __graft_entry__.build() "
                            "(the hot path has no CPU fallback)")
-    L = ctypes.CDLL(LIB_PATH)
+    L = ctypes.CDLL(path)
     P, i32, i64, u32, u64, f32 = (ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32,
                                   ctypes.c_uint64, ctypes.c_float)
     sig = {
