@@ -60,7 +60,7 @@ template <int D>
 __device__ __forceinline__ void grad_quadratic(const SdeArgs& a, const float* q, float* g) {
   float y[D];
 #pragma unroll
-  for (int k = 0; k < D; ++k) y[k] = a.has_center ? q[k] - a.params[D * D + k] : q[k];
+  for (int k = 0; k < D; ++k) y[k] = q[k] - a.params[D * D + k];  // c = 0 (exact) without a centre
 #pragma unroll
   for (int r = 0; r < D; ++r) {
     float acc = 0.f;
@@ -161,11 +161,19 @@ __device__ __forceinline__ void store_rows_staged(float* wave_dst, const float* 
   for (int k = 0; k < M; k += 4)
     *reinterpret_cast<f32x4*>(slot + lane * M + k) = f32x4{z[k], z[k + 1], z[k + 2], z[k + 3]};
   __builtin_amdgcn_wave_barrier();
+  f32x4 v[M / 4];
 #pragma unroll
-  for (int k = 0; k < M / 4; ++k) {
-    const int c = k * 64 + lane;  // 16-byte chunk within the wave's 64*M floats
-    const f32x4 v = *reinterpret_cast<const f32x4*>(slot + 4 * c);
-    if (4 * c < n_valid * M) __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(wave_dst + 4 * c));
+  for (int k = 0; k < M / 4; ++k) v[k] = *reinterpret_cast<const f32x4*>(slot + 4 * (k * 64 + lane));
+  if (n_valid == kWave) {  // wave-uniform: every full wave stores unguarded (one lgkmcnt wait)
+#pragma unroll
+    for (int k = 0; k < M / 4; ++k)
+      __builtin_nontemporal_store(v[k], reinterpret_cast<f32x4*>(wave_dst + 4 * (k * 64 + lane)));
+  } else {
+#pragma unroll
+    for (int k = 0; k < M / 4; ++k) {
+      const int c = k * 64 + lane;  // 16-byte chunk within the wave's 64*M floats
+      if (4 * c < n_valid * M) __builtin_nontemporal_store(v[k], reinterpret_cast<f32x4*>(wave_dst + 4 * c));
+    }
   }
   __builtin_amdgcn_wave_barrier();
 }
@@ -206,6 +214,62 @@ __device__ __forceinline__ float shift_u(const SdeArgs& a, uint32_t plo, uint32_
   return u32_unit(r.x);
 }
 
+// Step-loop moment accumulator: sum z and the Gram sum z z^T of one particle's rows, laid out so
+// that every packed FMA (v_pk_fma_f32) multiplies an ALIGNED register pair (z[2p], z[2p+1]) by a
+// broadcast z[i]: row i keeps pairs p = i/2 .. M/2-1 (for odd i the first pair's low lane
+// duplicates entry (i-1, i) and is dropped). No register shuffles on the hot loop; finish() maps
+// the pairs onto the MomentAcc triangle (count, sums, i <= j) and applies the 0/1 lane weight.
+template <int M>
+struct PairGram {
+  static constexpr int P = M / 2;
+  static constexpr int npairs() {
+    int n = 0;
+    for (int i = 0; i < M; ++i) n += P - i / 2;
+    return n;
+  }
+  f32x2 s[P];
+  f32x2 g[npairs()];
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int p = 0; p < P; ++p) s[p] = f32x2{0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < npairs(); ++k) g[k] = f32x2{0.f, 0.f};
+  }
+  __device__ __forceinline__ void add(const float* z) {
+    f32x2 zp[P];
+#pragma unroll
+    for (int p = 0; p < P; ++p) zp[p] = f32x2{z[2 * p], z[2 * p + 1]};
+#pragma unroll
+    for (int p = 0; p < P; ++p) s[p] += zp[p];
+    int k = 0;
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      const f32x2 zi = f32x2{z[i], z[i]};
+#pragma unroll
+      for (int p = i / 2; p < P; ++p) {
+        g[k] = zi * zp[p] + g[k];
+        ++k;
+      }
+    }
+  }
+  __device__ __forceinline__ void finish(float rows, float w, float* v) const {
+    v[0] = rows * w;
+#pragma unroll
+    for (int i = 0; i < M; ++i) v[1 + i] = w * s[i / 2][i % 2];
+    int o = 1 + M, k = 0;
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+#pragma unroll
+      for (int p = i / 2; p < P; ++p) {
+#pragma unroll
+        for (int l = 0; l < 2; ++l)
+          if (2 * p + l >= i) v[o++] = w * g[k][l];
+        ++k;
+      }
+    }
+  }
+};
+
 template <int D, int POT, bool MOM, int STORE, int KM = 1, bool NOISE = false, int MINW = 1>
 __global__ __launch_bounds__(kBlock, MINW) void sde_simulate_kernel(SdeArgs a, const float* __restrict__ z0,
                                                               float* __restrict__ traj,
@@ -239,13 +303,14 @@ __global__ __launch_bounds__(kBlock, MINW) void sde_simulate_kernel(SdeArgs a, c
   const float tau0 = a.random_shift ? shift_u(a, plo, phi, i) * a.dt : 0.f;
   const float h_last = a.dt - tau0;
 
-  MomentAcc<(MOM ? M : 2)> acc;
+  PairGram<(MOM ? M : 2)> acc;
   acc.zero();
 
   constexpr bool kStaged = (STORE == kStoreStaged) && (M % 4 == 0);
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t wave_row0 = i_raw - lane;
-  const int n_valid = (int)((a.N - wave_row0) < kWave ? (a.N - wave_row0) : kWave);
+  // wave-uniform by construction; readfirstlane lets the compiler branch on it with SALU
+  const int n_valid = __builtin_amdgcn_readfirstlane((int)((a.N - wave_row0) < kWave ? (a.N - wave_row0) : kWave));
   __shared__ float stage[kStaged ? kBlock * M : 1];
   float* slot = stage + (threadIdx.x - lane) * M;
   float* tr = traj ? traj + (kStaged ? wave_row0 : i) * M : nullptr;
@@ -276,14 +341,14 @@ __global__ __launch_bounds__(kBlock, MINW) void sde_simulate_kernel(SdeArgs a, c
   update(tau0, sqrtf(tau0) * a.ns, 0u);
   if (tr) put(tr);
   if (active && ta) __builtin_nontemporal_store(tau_value(tau0, 0, a.dt), ta);
-  if constexpr (MOM) acc.add(z, w);
+  if constexpr (MOM) acc.add(z);
 
   const float sh_dt = sqrtf(a.dt) * a.ns;
   for (int s = 1; s < a.n_steps; ++s) {
     update(a.dt, sh_dt, (uint32_t)s);
     if (tr) put(tr + (int64_t)s * tr_stride);
     if (active && ta) __builtin_nontemporal_store(tau_value(tau0, s, a.dt), ta + (int64_t)s * a.N);
-    if constexpr (MOM) acc.add(z, w);
+    if constexpr (MOM) acc.add(z);
   }
 
   // final update: h = dt - tau0, lands exactly at T = n*dt (sampling_utils.py:44-46)
@@ -291,7 +356,9 @@ __global__ __launch_bounds__(kBlock, MINW) void sde_simulate_kernel(SdeArgs a, c
   if (active && last) store_row<D, kStoreNT>(last + i * M, z);
 
   if constexpr (MOM) {
-    block_reduce_to_slab(acc.v, L, lds, partials + (int64_t)L * nb, blockIdx.x, nb);
+    float mv[L];
+    acc.finish((float)a.n_steps, w, mv);
+    block_reduce_to_slab(mv, L, lds, partials + (int64_t)L * nb, blockIdx.x, nb);
     MomentAcc<M> term;
     term.zero();
     term.add(z, w);
