@@ -58,41 +58,13 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-recovery", action="store_true")
     p.add_argument("--cpu-particles", type=int, default=1 << 20)
+    p.add_argument("--cpu-procs", type=int, default=16, help="CPU-baseline shard processes (the box's CPU share)")
     return p.parse_args()
 
 
 def sim_bytes(N, n, d):
     """z0 read 8d + n (traj 8d + tau 4) + last 8d bytes per particle."""
     return N * (8 * d + n * (8 * d + 4) + 8 * d)
-
-
-def cpu_baseline(F, d, n, T, gamma, N):
-    """NumPy restatement of sampling_utils.py:6-52 (+ the moment pass), single thread."""
-    from oracle import numpy_ref as nr
-    try:
-        from threadpoolctl import threadpool_limits
-        limiter = threadpool_limits(1)
-    except Exception:  # pragma: no cover
-        limiter = None
-    rng = np.random.default_rng(0)
-    dt = np.float32(T / n)
-    F32 = F.astype(np.float32)
-    z0 = rng.standard_normal((N, 2 * d), dtype=np.float32)
-    t0 = time.perf_counter()
-    q, p = z0[:, :d].copy(), z0[:, d:].copy()
-    tau0 = rng.random(N, dtype=np.float32) * dt
-    acc = np.zeros((2 * d, 2 * d))
-    for s in range(n + 1):
-        h = tau0[:, None] if s == 0 else ((dt - tau0)[:, None] if s == n else dt)
-        xi = rng.standard_normal((N, d), dtype=np.float32)
-        q, p = nr.update_step(q, p, h, nr.grad_quadratic(F32), np.float32(gamma), xi, np.float32(math.sqrt(2)))
-        if s < n:
-            z = np.concatenate([q, p], 1)
-            acc += z.T.astype(np.float64) @ z.astype(np.float64)
-    el = time.perf_counter() - t0
-    if limiter is not None:
-        limiter.unregister()
-    return N * (n + 1) / el, el
 
 
 def cpu_model():
@@ -204,12 +176,20 @@ def run_c2(a, rank, world, dev):
         out["drift_recovery"] = ("max |S - tilde_F|, S = K + K^T the exact residual minimiser, Richardson "
                                  f"2*S(n=200) - S(n=100), {(a.steps + a.warmup) * world * N} trajectories each")
     if rank == 0 and not a.no_cpu_baseline:
-        ups, secs = cpu_baseline(F, d, n, T, gamma, a.cpu_particles)
-        out["cpu_baseline"] = {"value": ups, "unit": "particle-steps/s", "cores": 1, "kind": "port",
-                               "sample": f"NumPy restatement of sampling_utils.py (oracle/numpy_ref.py update_step) "
-                                         f"+ moment pass, fp32, d={d}, {a.cpu_particles} particles x {n + 1} updates, "
-                                         f"{secs:.1f} s; host {cpu_model()}, os.cpu_count()={os.cpu_count()}"}
-        out["gpu_over_cpu"] = value / ups
+        from oracle import cpu_baseline as cb
+        ups1, secs1 = cb.single(F, d, n, T, gamma, a.cpu_particles)
+        P = max(1, min(a.cpu_procs, os.cpu_count() or 1))
+        n_per = max(1, a.cpu_particles // 4)
+        upsP, secsP = cb.multi(F, d, n, T, gamma, n_per, P)
+        what = (f"NumPy restatement of sampling_utils.py (oracle/cpu_baseline.py: update_step + moment pass), fp32, "
+                f"d={d}, {n + 1} updates")
+        host = f"host {cpu_model()}, os.cpu_count()={os.cpu_count()}"
+        out["cpu_baseline"] = {"value": upsP, "unit": "particle-steps/s", "cores": P, "kind": "port",
+                               "sample": f"{what}; {P} processes x {n_per} particles started together, "
+                                         f"{secsP:.1f} s wall; {host}"}
+        out["cpu_baseline_1core"] = {"value": ups1, "unit": "particle-steps/s", "cores": 1, "kind": "port",
+                                     "sample": f"{what}; one process, {a.cpu_particles} particles, {secs1:.1f} s"}
+        out["gpu_over_cpu"] = value / upsP
     return out
 
 
