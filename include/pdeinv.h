@@ -328,6 +328,13 @@ int pdeinv_gmm_potential(int32_t dim, int32_t n_centers, float sigma, const floa
 int pdeinv_gaussian_sample(int64_t n, int32_t m, uint64_t seed, uint32_t counter_offset,
                            int64_t row_offset, const float* d_mean, const float* d_cov_half,
                            float* d_out, void* stream);
+/* Grouped form — the KOU exact sampler (…_OU.py:140-190: one Gaussian N(m(t_g), P(t_g)) per
+ * random time, `sample_per_time` rows each) in one launch: rows [g*rows_per_group, (g+1)*...)
+ * use d_means[g] ([n_groups, m]) and d_cov_halves[g] ([n_groups, m, m]). Same row stream as
+ * pdeinv_gaussian_sample (global row = row_offset + r). */
+int pdeinv_gaussian_sample_grouped(int64_t n_groups, int64_t rows_per_group, int32_t m, uint64_t seed,
+                                   uint32_t counter_offset, int64_t row_offset, const float* d_means,
+                                   const float* d_cov_halves, float* d_out, void* stream);
 
 /* Raw Philox4x32-10 blocks for the KAT / stream tests: block i uses
  * ctr = {lo32(i), hi32(i), ctr_z, ctr_w}; out [n_blocks, 4] u32. */

@@ -9,7 +9,12 @@ drivers are unchanged. Differences of mechanism, not of behaviour:
     cosine(20000, alpha=1e-3) learning rate (main.py:11-29); on the device it is one fused HIP
     launch per parameter leaf (pdeinv_adam_update, in place); the EMA branch (trainer.py:87-103)
     is kept;
-  * metrics go to a local JSONL log (wandb is optional and not installed here).
+  * metrics go to a local JSONL log (wandb is optional and not installed here);
+  * the iteration is device-resident: the per-iteration scalars (loss, grad_norm, loss ground
+    truth, params_norm) stay on the GPU and are fetched in one transfer every `test.frequency`
+    iterations (and at the end), instead of one blocking sync per iteration (trainer.py:112).
+    The host therefore launches iteration k+1 while the GPU still runs iteration k; the NaN
+    assertion (:113) fires at the next flush, naming the first NaN iteration.
 """
 from __future__ import annotations
 
@@ -103,6 +108,24 @@ class JaxTrainer:
         ema = None
         test_freq = int(cfg.test.frequency)
         verbose = bool(cfg.test.get("verbose", False))
+        pending = []  # (epoch, names, device scalars) of iterations not yet fetched
+
+        def flush():
+            if not pending:
+                return
+            vals = torch.stack([torch.stack([v.reshape(()).float() if torch.is_tensor(v) else
+                                             torch.tensor(float(v), device=v_dev) for v in vs])
+                                for _, _, vs in pending]).cpu().numpy()
+            for (ep, names, _), row in zip(pending, vals):
+                record = dict(zip(names, (float(x) for x in row)))
+                assert not math.isnan(record["loss"]), f"loss is NaN at iteration {ep}"
+                record["step"] = ep
+                record.update(tests.pop(ep, {}))
+                self._log(record)
+            pending.clear()
+
+        tests = {}
+        v_dev = None
         t0 = time.perf_counter()
         for epoch in range(n_iter):
             rng = prng.fold_in(self.rng, epoch)  # trainer.py:80-83 (one key per iteration)
@@ -118,14 +141,17 @@ class JaxTrainer:
                 self.params = tree_map(lambda e: e / c, ema["ema"])
             v_g_etc.pop("grad")
             v_g_etc["params_norm"] = compute_pytree_norm(self.params)
-            record = {k: float(v) for k, v in v_g_etc.items()}  # one host sync per iteration (:112)
-            assert not math.isnan(record["loss"])
-            record["step"] = epoch
+            names = list(v_g_etc.keys())
+            v_dev = v_dev or next((v.device for v in v_g_etc.values() if torch.is_tensor(v)), None)
+            pending.append((epoch, names, [v_g_etc[k] for k in names]))
             if (epoch % test_freq == 0) or epoch >= n_iter - 3:
-                record.update({k: float(v) for k, v in self.method.test_fn(self.forward_fn, self.params, rng_test).items()})
+                tests[epoch] = {k: float(v) for k, v in
+                                self.method.test_fn(self.forward_fn, self.params, rng_test).items()}
+                flush()
                 if verbose and dist.rank() == 0:
-                    print(f"In epoch {epoch + 1: 5d}, " + ", ".join(f"{k} is {v: .3e}" for k, v in record.items()))
-            self._log(record)
+                    rec = self.history[-1]
+                    print(f"In epoch {epoch + 1: 5d}, " + ", ".join(f"{k} is {v: .3e}" for k, v in rec.items()))
+        flush()
         self.elapsed = time.perf_counter() - t0
         return self.params
 

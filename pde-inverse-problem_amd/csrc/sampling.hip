@@ -4,14 +4,22 @@
 namespace pdeinv {
 
 // core/distribution.py:64-65  Gaussian.sample: z = C^{1/2} xi + mu (one row per thread).
+// Grouped form (the exact sampler of …_OU.py:140-190, one Gaussian per random time): row r
+// uses mean[g], ch[g] with g = r / rows_per_group; one group is the plain sampler.
 template <int M>
 __global__ __launch_bounds__(kBlock) void gaussian_sample_kernel(int64_t n, uint32_t k0, uint32_t k1,
                                                                  uint32_t ctr_z, int64_t row_off,
                                                                  const float* __restrict__ mean,
                                                                  const float* __restrict__ ch,
-                                                                 float* __restrict__ out) {
+                                                                 float* __restrict__ out,
+                                                                 int64_t rows_per_group) {
   const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (r >= n) return;
+  if (rows_per_group < n) {
+    const int64_t g = r / rows_per_group;
+    mean += g * M;
+    ch += g * M * M;
+  }
   const uint64_t gid = (uint64_t)(row_off + r);
   float xi[M];
 #pragma unroll
@@ -102,12 +110,14 @@ extern "C" int pdeinv_gather_random_step(const float* traj, int64_t N, int32_t n
   return check_launch("gather_random_step_kernel");
 }
 
-extern "C" int pdeinv_gaussian_sample(int64_t n, int32_t m, uint64_t seed, uint32_t ctr,
-                                      int64_t row_off, const float* mean, const float* ch,
-                                      float* out, void* stream) {
+extern "C" int pdeinv_gaussian_sample_grouped(int64_t n_groups, int64_t rows_per_group, int32_t m, uint64_t seed,
+                                              uint32_t ctr, int64_t row_off, const float* mean, const float* ch,
+                                              float* out, void* stream) {
   PDEINV_REQUIRE(m >= 1 && m <= 2 * PDEINV_MAX_DIM, PDEINV_ERR_UNSUPPORTED,
                  "gaussian_sample: dim must be in [1, 32]");
-  PDEINV_REQUIRE(n >= 0 && row_off >= 0, PDEINV_ERR_INVALID, "gaussian_sample: n / row_offset < 0");
+  PDEINV_REQUIRE(n_groups >= 0 && rows_per_group >= 0 && row_off >= 0, PDEINV_ERR_INVALID,
+                 "gaussian_sample: n_groups / rows_per_group / row_offset < 0");
+  const int64_t n = n_groups * rows_per_group;
   if (n == 0) return PDEINV_OK;
   PDEINV_REQUIRE(mean && ch && out, PDEINV_ERR_INVALID, "gaussian_sample: null pointer");
   PDEINV_REQUIRE(m % 4 != 0 || ((uintptr_t)out % 16) == 0, PDEINV_ERR_INVALID,
@@ -116,7 +126,7 @@ extern "C" int pdeinv_gaussian_sample(int64_t n, int32_t m, uint64_t seed, uint3
   const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
   const dim3 g(grid_for(n));
   switch (m) {
-#define CASE(MM) case MM: hipLaunchKernelGGL(gaussian_sample_kernel<MM>, g, dim3(kBlock), 0, st, n, k0, k1, ctr, row_off, mean, ch, out); break;
+#define CASE(MM) case MM: hipLaunchKernelGGL(gaussian_sample_kernel<MM>, g, dim3(kBlock), 0, st, n, k0, k1, ctr, row_off, mean, ch, out, rows_per_group); break;
     CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) CASE(9) CASE(10) CASE(11)
     CASE(12) CASE(13) CASE(14) CASE(15) CASE(16) CASE(18) CASE(20) CASE(24) CASE(32)
 #undef CASE
@@ -124,6 +134,13 @@ extern "C" int pdeinv_gaussian_sample(int64_t n, int32_t m, uint64_t seed, uint3
       return fail(PDEINV_ERR_UNSUPPORTED, "gaussian_sample: dim must be 1-16, 18, 20, 24 or 32");
   }
   return check_launch("gaussian_sample_kernel");
+}
+
+extern "C" int pdeinv_gaussian_sample(int64_t n, int32_t m, uint64_t seed, uint32_t ctr,
+                                      int64_t row_off, const float* mean, const float* ch,
+                                      float* out, void* stream) {
+  PDEINV_REQUIRE(n >= 0, PDEINV_ERR_INVALID, "gaussian_sample: n / row_offset < 0");
+  return pdeinv_gaussian_sample_grouped(n ? 1 : 0, n, m, seed, ctr, row_off, mean, ch, out, stream);
 }
 
 extern "C" int pdeinv_philox_fill(uint64_t seed, uint32_t cz, uint32_t cw, int64_t n, uint32_t* out,

@@ -79,6 +79,46 @@ def OU_process(t_space, configuration):  # noqa: N802 - reference name
     return np.stack(ms), np.stack(Ps)
 
 
+def ou_moments_batched(ts, configuration):
+    """(m(t_g), P(t_g)) for a batch of times in one vectorised pass — the same Van Loan block
+    exponential as OU_process, exp(B t) with B = [[-F, L], [0, F^T]], evaluated for every t_g at
+    once: the powers B^k (k <= 18) are shared by the batch, so exp(B t_g / 2^s) is one contraction
+    of the Taylor coefficients (t_g / 2^s)^k / k! with them, followed by s batched squarings
+    (s makes |B| t_max / 2^s <= 1, truncation < 1e-16). Replaces one odeint / expm per random time
+    of the reference's exact sampler (…_OU.py:140-156)."""
+    ts = np.atleast_1d(np.asarray(ts, dtype=np.float64))
+    F, L, m0, P0 = (configuration[k] for k in ("F", "L", "m_0", "P_0"))
+    n = F.shape[0]
+    B = np.zeros((2 * n, 2 * n))
+    B[:n, :n] = -F
+    B[:n, n:] = L
+    B[n:, n:] = F.T
+    tmax = float(np.max(np.abs(ts))) if ts.size else 0.0
+    nrm = np.abs(B).sum(axis=0).max() * tmax
+    s = max(0, int(np.ceil(np.log2(nrm)))) if nrm > 1.0 else 0
+    K = 18
+    pw = np.empty((K + 1, 2 * n, 2 * n))
+    pw[0] = np.eye(2 * n)
+    for k in range(1, K + 1):
+        pw[k] = pw[k - 1] @ B
+    tau = ts / (2.0 ** s)
+    coef = np.ones((ts.size, K + 1))
+    for k in range(1, K + 1):
+        coef[:, k] = coef[:, k - 1] * tau / k  # tau^k / k!
+    X = np.einsum("gk,kij->gij", coef, pw)
+    for _ in range(s):
+        X = X @ X
+    E = np.transpose(X[:, n:, n:], (0, 2, 1))  # e^{F t}
+    P = E @ P0 @ np.transpose(E, (0, 2, 1)) + np.transpose(X[:, n:, n:], (0, 2, 1)) @ X[:, :n, n:]
+    return E @ m0, 0.5 * (P + np.transpose(P, (0, 2, 1)))
+
+
+def sym_sqrt_batched(C):
+    """U diag(sqrt S) U^T per matrix — Gaussian.__init__'s SVD square root (distribution.py:59-61)."""
+    U, S, _ = np.linalg.svd(C)
+    return (U * np.sqrt(S)[:, None, :]) @ np.transpose(U, (0, 2, 1))
+
+
 def get_mean_cov(t, configuration):
     """…_OU.py:96-106."""
     t = np.asarray(t, dtype=np.float64)
@@ -137,13 +177,14 @@ class KineticFokkerPlanck(ProblemInstance):
             sample_per_time = 100
             assert batch_size >= sample_per_time * 2
             n_random_time = batch_size // sample_per_time
-            keys = prng.split(rng, n_random_time)
-            out = []
-            for k in keys:
-                k_t, k_x = prng.split(k)
-                t = float(self.distribution_time.sample(1, k_t)[0])
-                out.append(Gaussian(*self.get_mean_cov(t)).sample(sample_per_time, k_x))
-            return torch.cat(out, 0)
+            k_t, k_x = prng.split(rng)
+            # all random times at once; their moments in one batched pass; one grouped launch
+            t = np.asarray(self.distribution_time.sample(n_random_time, k_t), dtype=np.float64).reshape(-1)
+            means, covs = ou_moments_batched(t, self.initial_configuration)
+            f32 = lambda a: torch.as_tensor(a, dtype=torch.float32, device="cuda")
+            from utils import native
+            return native.gaussian_sample_grouped(sample_per_time, f32(means), f32(sym_sqrt_batched(covs)),
+                                                  seed=k_x.seed)
         k_shift, k = prng.split(rng)
         n_time_stamps, sample_per_time = batch_size
         assert n_time_stamps == 1  # …_OU.py:176 (the reference's grid mode is single-stamp)

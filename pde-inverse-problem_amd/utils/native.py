@@ -43,6 +43,7 @@ EXPORTED_SYMBOLS = (
     "pdeinv_moments_workspace_bytes", "pdeinv_moments", "pdeinv_residual_kfp_quadratic",
     "pdeinv_residual_kfp_gmm_workspace_bytes", "pdeinv_residual_kfp_gmm",
     "pdeinv_residual_kfp_gmm_finalize", "pdeinv_gmm_potential", "pdeinv_gaussian_sample",
+    "pdeinv_gaussian_sample_grouped",
     "pdeinv_philox_fill", "pdeinv_gather_subsample", "pdeinv_abi_version", "pdeinv_last_error",
     "pdeinv_runtime_version", "pdeinv_moments_batched_workspace_bytes", "pdeinv_moments_batched",
     "pdeinv_kmv_weights_workspace_bytes", "pdeinv_kmv_weights", "pdeinv_residual_kmv",
@@ -146,6 +147,7 @@ def lib():
         "pdeinv_residual_kfp_gmm_finalize": (i32, [P, P, P, P, P]),
         "pdeinv_gmm_potential": (i32, [i32, i32, f32, P, P, i64, i64, P, P, P]),
         "pdeinv_gaussian_sample": (i32, [i64, i32, u64, u32, i64, P, P, P, P]),
+        "pdeinv_gaussian_sample_grouped": (i32, [i64, i64, i32, u64, u32, i64, P, P, P, P]),
         "pdeinv_philox_fill": (i32, [u64, u32, u32, i64, P, P]),
         "pdeinv_gather_subsample": (i32, [P, i64, i32, i32, P, i64, P, i32, P, P]),
         "pdeinv_abi_version": (i32, []),
@@ -435,6 +437,22 @@ def gaussian_sample(n: int, mean: torch.Tensor, cov_half: torch.Tensor, *, seed:
                                         int(counter_offset) & 0xFFFFFFFF, int(row_offset),
                                         _dev(mean.contiguous(), "mean"), _dev(cov_half.contiguous(), "cov_half"),
                                         _dev(out, "out"), stream_handle()), "pdeinv_gaussian_sample")
+    return out
+
+
+def gaussian_sample_grouped(rows_per_group: int, means: torch.Tensor, cov_halves: torch.Tensor, *, seed: int,
+                            counter_offset: int = 0, row_offset: int = 0) -> torch.Tensor:
+    """[G * rows_per_group, m]: rows of group g drawn from N(means[g], cov_halves[g] cov_halves[g]^T)."""
+    _require_gpu()
+    G, m = means.shape
+    if cov_halves.shape != (G, m, m):
+        raise ValueError(f"cov_halves must be [{G}, {m}, {m}], got {tuple(cov_halves.shape)}")
+    out = torch.empty((G * int(rows_per_group), m), device=means.device, dtype=torch.float32)
+    _check(lib().pdeinv_gaussian_sample_grouped(int(G), int(rows_per_group), int(m), int(seed) & 0xFFFFFFFFFFFFFFFF,
+                                                int(counter_offset) & 0xFFFFFFFF, int(row_offset),
+                                                _dev(means.contiguous(), "means"),
+                                                _dev(cov_halves.contiguous(), "cov_halves"), _dev(out, "out"),
+                                                stream_handle()), "pdeinv_gaussian_sample_grouped")
     return out
 
 

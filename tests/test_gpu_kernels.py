@@ -221,6 +221,40 @@ def test_gaussian_sample_vs_oracle(native, oracle_lib, m):
     assert np.max(np.abs(g - o)) < 2e-5 * (1 + np.abs(o).max())
 
 
+def test_gaussian_sample_grouped_is_the_row_stream(native):
+    """Grouped launch == per-group plain launches at the same global rows (bit-exact), and the
+    KOU random-time sampler built on it reproduces each group's Gaussian."""
+    rng = np.random.default_rng(7)
+    G, R, m = 5, 300, 8
+    means = rng.standard_normal((G, m)).astype(np.float32)
+    chs = np.stack([np.linalg.cholesky(a @ a.T + np.eye(m)) for a in rng.standard_normal((G, m, m))]).astype(np.float32)
+    out = native.gaussian_sample_grouped(R, _t(means), _t(chs), seed=9, counter_offset=2, row_offset=64).cpu().numpy()
+    for g in range(G):
+        ref = native.gaussian_sample(R, _t(means[g]), _t(chs[g]), seed=9, counter_offset=2,
+                                     row_offset=64 + g * R).cpu().numpy()
+        assert np.array_equal(out[g * R:(g + 1) * R], ref)
+    with pytest.raises(ValueError):
+        native.gaussian_sample_grouped(R, _t(means), _t(chs[:-1]), seed=9)
+
+
+def test_kou_exact_random_time_sampler(native):
+    """sample_ground_truth(rng, int) (…_OU.py:141-156): groups of 100 rows, each N(m(t_g), P(t_g))."""
+    import registry
+    from utils import config as config_lib, prng
+    cfg = config_lib.compose("config", ["pde_instance=kinetic_fokker_planck", "pde_instance.domain_dim=2"])
+    pi = registry.get_pde_instance(cfg)(cfg=cfg, rng=prng.PRNGKey(0))
+    z = pi.sample_ground_truth(prng.PRNGKey(3), 20000).cpu().numpy()
+    assert z.shape == (20000, 4) and np.isfinite(z).all()
+    # pooled second moment = mean over groups of P(t_g) + m m^T; t_g ~ U(1e-4, T): compare with the
+    # time-averaged continuous OU covariance (5 sigma of the 20000-sample estimate)
+    cfg_o = nr.ou_configuration(pi.initial_configuration["tilde_F"])
+    ts = np.linspace(1e-4, 2.0, 401)
+    Pbar = np.mean([nr.ou_mean_cov(t, cfg_o)[1] for t in ts], 0)
+    emp = z.T @ z / z.shape[0]
+    sd = np.sqrt((np.diag(Pbar)[:, None] * np.diag(Pbar)[None, :] + Pbar ** 2) / (z.shape[0] / 100))
+    assert np.all(np.abs(emp - Pbar) < 5 * sd + 1e-3)
+
+
 def test_gather_subsample_exact(native):
     rng = np.random.default_rng(1)
     n, N, m = 40, 300, 8

@@ -93,6 +93,26 @@ def test_drift_recovery_is_exact_on_continuous_moments():
     assert np.abs(S - F).max() < 1e-5 and np.abs(b).max() < 1e-9
 
 
+def test_ou_moments_batched_match_oracle():
+    """The batched exact-sampler moments (one vectorised Van Loan pass) vs the oracle's
+    per-time closed form of the reference's odeint ODE (…_OU.py:73-106)."""
+    from example_problems.kinetic_fokker_planck_example_OU import (initialize_configuration, ou_moments_batched,
+                                                                   sym_sqrt_batched)
+    from oracle import numpy_ref as nr
+    for d in (2, 4, 8):
+        ic = initialize_configuration(d)
+        cfg = nr.ou_configuration(ic["tilde_F"])
+        ts = np.concatenate([[0.0, 1e-4], np.random.default_rng(d).uniform(0, 2, 50), [2.0, 5.0]])
+        m, P = ou_moments_batched(ts, ic)
+        for g, t in enumerate(ts):
+            mr, Pr = nr.ou_mean_cov(t, cfg) if t > 0 else (cfg["m_0"], cfg["P_0"])
+            assert np.abs(m[g] - mr).max() < 1e-10
+            assert np.abs(P[g] - Pr).max() < 1e-9 * (1 + np.abs(Pr).max())
+        C = sym_sqrt_batched(P)
+        assert np.abs(C @ C - P).max() < 1e-9 * (1 + np.abs(P).max())
+        assert np.allclose(C, np.transpose(C, (0, 2, 1)))
+
+
 def test_adam_matches_optax_semantics():
     import torch
     from core.trainer import Adam, cosine_decay_schedule
