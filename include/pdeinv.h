@@ -276,8 +276,8 @@ int pdeinv_residual_kmv(const pdeinv_kmv_desc* desc, const double* d_mom, const 
  * GMM residual): Taylor-mode forward streams, the grad_x reverse chain, its forward adjoint, the
  * reverse sweep and the weight-gradient outer products, as dense GEMMs (rocBLAS sgemm, fp32) plus
  * fused element-wise kernels, chunked over chunk_rows rows. impl selects the implementation:
- * PDEINV_MLP_IMPL_AUTO picks the fused path when the shape allows it (L >= 2, W % 128 == 0,
- * W <= 512, out <= 64, d in {2, 4, 8, 16}): hand-written fp32 MFMA GEMMs whose prologues and
+ * PDEINV_MLP_IMPL_AUTO picks the fused path when the shape allows it (L >= 2,
+ * W in {32, 64, 128, 256, 512}, out <= 64, d in {2, 4, 8, 16}): hand-written fp32 MFMA GEMMs whose prologues and
  * epilogues carry all of the element-wise algebra (layer 1 is recomputed from the rows, never
  * stored). PDEINV_MLP_IMPL_LIBRARY forces the rocBLAS + element-wise-kernel path (any shape);
  * PDEINV_MLP_IMPL_FUSED forces the fused path (PDEINV_ERR_UNSUPPORTED if the shape is not).

@@ -45,25 +45,59 @@ constexpr int kMaxKSplit = 256;
 constexpr int64_t kMinKSlice = 4096;
 constexpr int kColsumBlocks = 512;
 
-__global__ void sum_slices_kernel(const float* __restrict__ part, int S, int64_t n, float* __restrict__ out) {
-  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (i >= n) return;
+// out[i] += sum_k part[k * n + i]. A block owns kSumCols outputs; its kBlock / kSumCols thread
+// groups each sum a strided subset of the S slices (independent loads in flight), then the group
+// partials are added in a fixed order through LDS — deterministic, and fast for the small n
+// (a few thousand weights) and large S of the weight / bias gradients.
+constexpr int kSumCols = 32;
+__global__ __launch_bounds__(kBlock) void sum_slices_kernel(const float* __restrict__ part, int S, int64_t n,
+                                                            float* __restrict__ out) {
+  constexpr int G = kBlock / kSumCols;
+  __shared__ float red[G][kSumCols];
+  const int c = threadIdx.x % kSumCols, g = threadIdx.x / kSumCols;
+  const int64_t i = (int64_t)blockIdx.x * kSumCols + c;
   float s = 0.f;
-  for (int k = 0; k < S; ++k) s += part[(int64_t)k * n + i];
-  out[i] += s;
+  if (i < n)
+    for (int k = g; k < S; k += G) s += part[(int64_t)k * n + i];
+  red[g][c] = s;
+  __syncthreads();
+  if (g == 0 && i < n) {
+    float t = 0.f;
+#pragma unroll
+    for (int q = 0; q < G; ++q) t += red[q][c];
+    out[i] += t;
+  }
 }
 
-// partial column sums of B[R x n] (row-major): block b sums rows [b*rpb, (b+1)*rpb) for the
-// columns blockIdx.y*kBlock + tid. Consecutive lanes read consecutive floats of a row.
+// partial column sums of B[R x n] (row-major): block b sums rows [b*rpb, (b+1)*rpb). For n < kBlock
+// the block's threads cover kBlock / n rows at a time (lane t: column t % n, row offset t / n), so
+// every thread is busy and a wave reads contiguous bytes; the row-lanes are combined in a fixed
+// order through LDS. Wider outputs use blockIdx.y column tiles of kBlock.
 __global__ __launch_bounds__(kBlock) void colsum_partial_kernel(const float* __restrict__ B, int64_t R, int n,
                                                                 int64_t rpb, float* __restrict__ part) {
-  const int c = blockIdx.y * kBlock + threadIdx.x;
-  if (c >= n) return;
+  __shared__ float red[kBlock];
   const int64_t r0 = (int64_t)blockIdx.x * rpb;
   const int64_t r1 = r0 + rpb < R ? r0 + rpb : R;
+  if (n >= kBlock) {
+    const int c = blockIdx.y * kBlock + threadIdx.x;
+    if (c >= n) return;
+    float s = 0.f;
+    for (int64_t r = r0; r < r1; ++r) s += B[r * n + c];
+    part[(int64_t)blockIdx.x * n + c] = s;
+    return;
+  }
+  const int lanes = kBlock / n;  // row-lanes (>= 1)
+  const int c = threadIdx.x % n, q = threadIdx.x / n;
   float s = 0.f;
-  for (int64_t r = r0; r < r1; ++r) s += B[r * n + c];
-  part[(int64_t)blockIdx.x * n + c] = s;
+  if (q < lanes)
+    for (int64_t r = r0 + q; r < r1; r += lanes) s += B[r * n + c];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  if (q == 0) {
+    float t = 0.f;
+    for (int k = 0; k < lanes; ++k) t += red[k * n + c];
+    part[(int64_t)blockIdx.x * n + c] = t;
+  }
 }
 
 struct Blas {
@@ -96,7 +130,7 @@ struct Blas {
                                       (rocblas_int)Ks, &one, B, n_out, Ks * n_out, A, n_in, Ks * n_in, &zero, part,
                                       n_out, nout, (rocblas_int)S) != rocblas_status_success)
       status = 1;
-    hipLaunchKernelGGL(sum_slices_kernel, dim3(grid_for(nout)), dim3(kBlock), 0, st, part, (int)S, nout, Kbar);
+    hipLaunchKernelGGL(sum_slices_kernel, dim3(grid_for(nout, kSumCols)), dim3(kBlock), 0, st, part, (int)S, nout, Kbar);
     if (rem > 0 && rocblas_sgemm(h, rocblas_operation_none, rocblas_operation_transpose, n_out, n_in,
                                  (rocblas_int)rem, &one, B + S * Ks * n_out, n_out, A + S * Ks * n_in, n_in, &one,
                                  Kbar, n_out) != rocblas_status_success)
@@ -106,9 +140,9 @@ struct Blas {
   void colsum(const float* B, float* bbar, int64_t R, int n) {
     const int64_t rpb = (R + kColsumBlocks - 1) / kColsumBlocks;
     const int nb = (int)((R + rpb - 1) / rpb);
-    hipLaunchKernelGGL(colsum_partial_kernel, dim3(nb, (n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, B, R, n,
-                       rpb, part);
-    hipLaunchKernelGGL(sum_slices_kernel, dim3(grid_for(n)), dim3(kBlock), 0, st, part, nb, (int64_t)n, bbar);
+    hipLaunchKernelGGL(colsum_partial_kernel, dim3(nb, n >= kBlock ? (n + kBlock - 1) / kBlock : 1), dim3(kBlock), 0,
+                       st, B, R, n, rpb, part);
+    hipLaunchKernelGGL(sum_slices_kernel, dim3(grid_for(n, kSumCols)), dim3(kBlock), 0, st, part, nb, (int64_t)n, bbar);
   }
 };
 
@@ -520,7 +554,7 @@ extern "C" int pdeinv_residual_kfp_mlp(const pdeinv_kfp_mlp_desc* d, const float
     return PDEINV_OK;
   }
   PDEINV_REQUIRE(d->impl != PDEINV_MLP_IMPL_FUSED, PDEINV_ERR_UNSUPPORTED,
-                 "kfp_mlp: fused path needs L >= 2, W in {128, 256, 512}, out <= 64, d in {2, 4, 8, 16}");
+                 "kfp_mlp: fused path needs L >= 2, W in {32, 64, 128, 256, 512}, out <= 64, d in {2, 4, 8, 16}");
   Blas blas{blas_handle(dev), st, w + p.off_kpart};
   if (!blas.h) return fail(PDEINV_ERR_HIP, "kfp_mlp: rocblas_create_handle failed");
   if (rocblas_set_stream(blas.h, st) != rocblas_status_success) return fail(PDEINV_ERR_HIP, "kfp_mlp: rocblas_set_stream");

@@ -347,18 +347,20 @@ __global__ __launch_bounds__(kT) void fgemm(GemmArgs a) {
 // ---- layer-1 kernels (VALU; K1 is d x W, d <= 16) ------------------------------------------
 // g = zeta1 K1^T with zeta1 = s1(z1) a1, z1 = x K1 + b1: one wave per row, lane owns columns
 // lane + 64 j; the d partial sums are wave-reduced.
-template <int D, int CPL>
+template <int D, int W>
 __global__ __launch_bounds__(kT) void l1_g_kernel(const float* __restrict__ a1, const float* __restrict__ z,
                                                   int64_t ldz, const float* __restrict__ K1,
                                                   const float* __restrict__ b1, int64_t R, float* __restrict__ G) {
-  constexpr int W = 64 * CPL;
+  constexpr int CPL = W >= 64 ? W / 64 : 1;  // W < 64: lanes >= W carry zero weights
   const int lane = threadIdx.x & 63;
+  const bool cv = W >= 64 || lane < W;
+  const int lc = cv ? lane : 0;
   float k1[CPL][D], bb[CPL];
 #pragma unroll
   for (int j = 0; j < CPL; ++j) {
-    bb[j] = b1[lane + 64 * j];
+    bb[j] = cv ? b1[lc + 64 * j] : 0.f;
 #pragma unroll
-    for (int i = 0; i < D; ++i) k1[j][i] = K1[i * W + lane + 64 * j];
+    for (int i = 0; i < D; ++i) k1[j][i] = cv ? K1[i * W + lc + 64 * j] : 0.f;
   }
   const int64_t nw = (int64_t)gridDim.x * (kT / 64);
   for (int64_t r = (int64_t)blockIdx.x * (kT / 64) + (threadIdx.x >> 6); r < R; r += nw) {
@@ -374,7 +376,7 @@ __global__ __launch_bounds__(kT) void l1_g_kernel(const float* __restrict__ a1, 
 #pragma unroll
       for (int i = 0; i < D; ++i) zz = fmaf(x[i], k1[j][i], zz);
       const float h = ftanh(zz);
-      const float zeta = (1.f - h * h) * a1[r * W + lane + 64 * j];
+      const float zeta = cv ? (1.f - h * h) * a1[r * W + lc + 64 * j] : 0.f;
 #pragma unroll
       for (int i = 0; i < D; ++i) g[i] = fmaf(zeta, k1[j][i], g[i]);
     }
@@ -724,7 +726,9 @@ static int launch_gemm(GemmArgs a, hipStream_t st, int* grid_x_out = nullptr) {
 template <int AM, int BMD>
 static int launch_gemm1(GemmArgs a, hipStream_t st) {
   if (a.N % 256 == 0) return launch_gemm<1, 64, 256, 2, AM, BMD, E_STORE>(a, st);
-  return launch_gemm<1, 64, 128, 2, AM, BMD, E_STORE>(a, st);
+  if (a.N > 64) return launch_gemm<1, 64, 128, 2, AM, BMD, E_STORE>(a, st);
+  if (a.N > 32) return launch_gemm<1, 64, 64, 2, AM, BMD, E_STORE>(a, st);
+  return launch_gemm<1, 128, 32, 4, AM, BMD, E_STORE>(a, st);
 }
 
 template <int BM, int BN, int GA, int GB>
@@ -746,8 +750,8 @@ static int launch_wgrad(WgradArgs a, float* grad_out, float* scratch, hipStream_
 }
 
 bool supported(int d, int L, int W, int O) {
-  return (d == 2 || d == 4 || d == 8 || d == 16) && L >= 2 && L <= 16 && (W == 128 || W == 256 || W == 512) &&
-         O >= 1 && O <= 64;
+  return (d == 2 || d == 4 || d == 8 || d == 16) && L >= 2 && L <= 16 &&
+         (W == 32 || W == 64 || W == 128 || W == 256 || W == 512) && O >= 1 && O <= 64;
 }
 
 // workspace layout (floats), chunk of Bc rows
@@ -789,6 +793,13 @@ size_t workspace_floats(int d, int L, int W, int O, int64_t Bc) { return layout(
 
 template <int D, int WB>
 static int run_chunk_t(const Chunk& c, const LossHook& loss, hipStream_t st) {
+  // hidden-width row-GEMM tiles: 64 x 128 (2 x 2 waves) for W >= 128; narrow nets get tiles no
+  // wider than W (64: 64 x 64, 2 x 2 waves; 32: 128 x 32, 4 x 1 waves) so no MFMA column is padding
+  constexpr int TN = WB < 128 ? WB : 128;
+  constexpr int TM = TN == 32 ? 128 : 64;
+  constexpr int TG = TN == 32 ? 4 : 2;
+  // weight-gradient tiles (>= 64 per side: 2 x 2 waves of 32-multiples)
+  constexpr int GW = WB < 128 ? 64 : 128;
   const int L = c.L, W = c.W, O = c.O;
   const int64_t R = c.R;
   const Layout y = layout(D, L, W, O, c.Bc);
@@ -835,14 +846,14 @@ static int run_chunk_t(const Chunk& c, const LossHook& loss, hipStream_t st) {
     a.K = W; a.N = W; a.Bw = Kw(2); a.bias = Bw(2);
     a.pa0 = H1[0]; a.pa1 = H1[1]; a.pa2 = H1[2];
     a.po0 = P(2, P_H); a.po1 = P(2, P_ZD); a.po2 = P(2, P_ZDD);
-    RC((launch_gemm<3, 64, 128, 2, A_S3, B_NN, E_ACT_FWD>(a, st)));
+    RC((launch_gemm<3, TM, TN, TG, A_S3, B_NN, E_ACT_FWD>(a, st)));
   }
   for (int l = 3; l <= L; ++l) {
     GemmArgs a = base;
     a.K = W; a.N = W; a.Bw = Kw(l); a.bias = Bw(l);
     a.pa0 = P(l - 1, P_H); a.pa1 = P(l - 1, P_ZD); a.pa2 = P(l - 1, P_ZDD);
     a.po0 = P(l, P_H); a.po1 = P(l, P_ZD); a.po2 = P(l, P_ZDD);
-    RC((launch_gemm<3, 64, 128, 2, A_FWD, B_NN, E_ACT_FWD>(a, st)));
+    RC((launch_gemm<3, TM, TN, TG, A_FWD, B_NN, E_ACT_FWD>(a, st)));
   }
   {
     GemmArgs a = base;
@@ -865,7 +876,7 @@ static int run_chunk_t(const Chunk& c, const LossHook& loss, hipStream_t st) {
   }
   {
     const int blocks = (int)std::min<int64_t>((R + 3) / 4, 2048);
-    hipLaunchKernelGGL((l1_g_kernel<D, WB / 64>), dim3(blocks), dim3(kT), 0, st, A1, c.z, c.ldz, Kw(1), Bw(1), R, G);
+    hipLaunchKernelGGL((l1_g_kernel<D, WB>), dim3(blocks), dim3(kT), 0, st, A1, c.z, c.ldz, Kw(1), Bw(1), R, G);
     RC(check_launch("kfp_mlp fused g"));
   }
   RC(loss.fn(loss.ctx, G, terms, abar0, R, st));
@@ -901,7 +912,7 @@ static int run_chunk_t(const Chunk& c, const LossHook& loss, hipStream_t st) {
     a.pe0 = P(L, P_H); a.pe1 = P(L, P_ZD); a.pe2 = P(L, P_ZDD); a.pe3 = P(L, P_A); a.pe4 = P(L, P_ZETABAR);
     a.po0 = P(L, P_ZB0); a.po1 = P(L, P_ZB1); a.po2 = P(L, P_ZB2);
     int gx = 0;
-    RC((launch_gemm<3, 64, 128, 2, A_S3, B_NT, E_ACT_BWD>(a, st, &gx)));
+    RC((launch_gemm<3, TM, TN, TG, A_S3, B_NT, E_ACT_BWD>(a, st, &gx)));
     RC(sum_slabs(part, gx, W, c.grad + c.boff[L - 1], part2, st));
   }
   for (int l = L; l >= 3; --l) {
@@ -912,7 +923,7 @@ static int run_chunk_t(const Chunk& c, const LossHook& loss, hipStream_t st) {
     a.pe4 = P(l - 1, P_ZETABAR);
     a.po0 = P(l - 1, P_ZB0); a.po1 = P(l - 1, P_ZB1); a.po2 = P(l - 1, P_ZB2);
     int gx = 0;
-    RC((launch_gemm<3, 64, 128, 2, A_S3, B_NT, E_ACT_BWD>(a, st, &gx)));
+    RC((launch_gemm<3, TM, TN, TG, A_S3, B_NT, E_ACT_BWD>(a, st, &gx)));
     RC(sum_slabs(part, gx, W, c.grad + c.boff[l - 2], part2, st));
   }
   {
@@ -920,7 +931,7 @@ static int run_chunk_t(const Chunk& c, const LossHook& loss, hipStream_t st) {
     a.K = W; a.N = W; a.Bw = Kw(2);
     a.pa0 = P(2, P_ZB0); a.pa1 = P(2, P_ZB1); a.pa2 = P(2, P_ZB2);
     a.po0 = HB1[0]; a.po1 = HB1[1]; a.po2 = HB1[2];
-    RC((launch_gemm<3, 64, 128, 2, A_S3, B_NT, E_STORE3>(a, st)));
+    RC((launch_gemm<3, TM, TN, TG, A_S3, B_NT, E_STORE3>(a, st)));
     hipLaunchKernelGGL((l1_grad_kernel<D, WB>), dim3(l1_blocks), dim3(kT), 0, st, HB1[0], HB1[1], HB1[2], A1, c.z,
                        c.ldz, abar0, Kw(1), Bw(1), R, l1_rpb, part);
     RC(check_launch("kfp_mlp fused layer-1 gradient"));
@@ -932,21 +943,21 @@ static int run_chunk_t(const Chunk& c, const LossHook& loss, hipStream_t st) {
     g.R = R; g.n_in = W; g.n_out = O; g.part = part;
     g.pa0 = P(L, P_H); g.pa1 = P(L, P_ZD); g.pa2 = P(L, P_ZDD); g.pa3 = P(L, P_ZETABAR);
     g.pb0 = YB[0]; g.pb1 = YB[1]; g.pb2 = YB[2]; g.pb3 = Ys[0];
-    RC((launch_wgrad<128, 64, GA_PL, GB_SM>(g, c.grad + c.poff[L], part2, st)));
+    RC((launch_wgrad<GW, 64, GA_PL, GB_SM>(g, c.grad + c.poff[L], part2, st)));
   }
   for (int l = L; l >= 3; --l) {
     WgradArgs g{};
     g.R = R; g.n_in = W; g.n_out = W; g.part = part;
     g.pa0 = P(l - 1, P_H); g.pa1 = P(l - 1, P_ZD); g.pa2 = P(l - 1, P_ZDD); g.pa3 = P(l - 1, P_ZETABAR);
     g.pb0 = P(l, P_ZB0); g.pb1 = P(l, P_ZB1); g.pb2 = P(l, P_ZB2); g.pb3 = P(l, P_H); g.pb4 = P(l, P_A);
-    RC((launch_wgrad<128, 128, GA_PL, GB_PL>(g, c.grad + c.poff[l - 1], part2, st)));
+    RC((launch_wgrad<GW, GW, GA_PL, GB_PL>(g, c.grad + c.poff[l - 1], part2, st)));
   }
   {
     WgradArgs g{};
     g.R = R; g.n_in = W; g.n_out = W; g.part = part;
     g.pa0 = H1[0]; g.pa1 = H1[1]; g.pa2 = H1[2]; g.pa3 = ABAR1;
     g.pb0 = P(2, P_ZB0); g.pb1 = P(2, P_ZB1); g.pb2 = P(2, P_ZB2); g.pb3 = P(2, P_H); g.pb4 = P(2, P_A);
-    RC((launch_wgrad<128, 128, GA_RAW4, GB_PL>(g, c.grad + c.poff[1], part2, st)));
+    RC((launch_wgrad<GW, GW, GA_RAW4, GB_PL>(g, c.grad + c.poff[1], part2, st)));
   }
 #undef RC
   return 0;
@@ -955,10 +966,12 @@ static int run_chunk_t(const Chunk& c, const LossHook& loss, hipStream_t st) {
 template <int D>
 static int run_chunk_d(const Chunk& c, const LossHook& loss, hipStream_t st) {
   switch (c.W) {
+    case 32: return run_chunk_t<D, 32>(c, loss, st);
+    case 64: return run_chunk_t<D, 64>(c, loss, st);
     case 128: return run_chunk_t<D, 128>(c, loss, st);
     case 256: return run_chunk_t<D, 256>(c, loss, st);
     case 512: return run_chunk_t<D, 512>(c, loss, st);
-    default: return fail(PDEINV_ERR_UNSUPPORTED, "kfp_mlp fused: width must be 128, 256 or 512");
+    default: return fail(PDEINV_ERR_UNSUPPORTED, "kfp_mlp fused: width must be 32, 64, 128, 256 or 512");
   }
 }
 

@@ -288,7 +288,8 @@ LIB, FUSED = 1, 2  # native.MLP_IMPL_LIBRARY / MLP_IMPL_FUSED
     ([8, 64, 64, 64, 40], "gmm", 777, LIB), ([8, 256, 256, 40], "gmm", 1 << 18, LIB),
     ([2, 128, 128, 5], "gmm", 1000, FUSED), ([4, 128, 128, 40], "quad", 1 << 18, FUSED),
     ([8, 256, 256, 40], "gmm", 777, FUSED), ([16, 128, 128, 128, 64], "quad", 1500, FUSED),
-    ([8, 512, 512, 512, 40], "gmm", 3000, FUSED)])
+    ([8, 512, 512, 512, 40], "gmm", 3000, FUSED), ([4, 32, 32, 40], "gmm", 1000, FUSED),
+    ([8, 64, 64, 64, 40], "quad", 777, FUSED), ([2, 32, 32, 32, 5], "quad", 1 << 18, FUSED)])
 def test_residual_mlp_vs_restatement(native, dims, true_kind, chunk, impl):
     """V_hypothesis residual (value + d loss/d theta) vs the fp64 restatement whose adjoint is
     FD-checked in tests/test_oracle.py, on both implementations (rocBLAS library path and the
