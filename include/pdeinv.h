@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define PDEINV_ABI_VERSION 2
+#define PDEINV_ABI_VERSION 3
 #define PDEINV_MAX_DIM 16          /* d (configuration-space dimension) */
 #define PDEINV_MAX_PARAMS 256      /* floats of potential parameters passed by value */
 
@@ -298,6 +298,9 @@ typedef struct {
   float c_nabla, c_hess, c_fric, c_true, c_init, c_term;
   int64_t chunk_rows;     /* rows per GEMM chunk (workspace grows with it); 0 => 2^18 */
   int32_t impl;           /* PDEINV_MLP_IMPL_* */
+  int32_t boundary_value; /* 0: boundary sets weight V' = grad V . v (kinetic FP, :49-50);
+                             1: they weight V itself (overdamped FP, fokker_planck.py:48-52) —
+                             see pdeinv_fp_rows for the overdamped residual's row layout */
 } pdeinv_kfp_mlp_desc;
 #define PDEINV_MLP_IMPL_AUTO 0
 #define PDEINV_MLP_IMPL_LIBRARY 1
@@ -311,6 +314,32 @@ int pdeinv_residual_kfp_mlp(const pdeinv_kfp_mlp_desc* desc, const float* d_init
                             void* d_workspace, double* d_acc, float* d_grad, void* stream);
 int pdeinv_kfp_terms_finalize(const double* d_acc, const float* d_grad, int64_t n_grad, float gamma,
                               float* d_out, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Overdamped Fokker–Planck (example_problems/fokker_planck_example.py,
+ * methods/consistency_instances/fokker_planck.py:33-63) — the reference's default pde_instance.
+ *
+ * Residual: loss = E_0T|grad V|^2 - 2 E_0T[lap V] + E_0T|grad V*|^2 + (2/T)(E_T V - E_0 V) for the
+ * V_hypothesis MLP, through pdeinv_residual_kfp_mlp with boundary_value = 1 on rows built here:
+ *   unit_directions = 1: out[r*d + k] = [x_r | e_k]  (lap V = sum_k e_k^T Hess V e_k: the 0T set
+ *                        with c_nabla = c_true = 1/(d M), c_hess = -2/M, c_fric = 0);
+ *   unit_directions = 0: out[r] = [x_r | 0]          (boundary sets: only V is weighted).
+ * x [n, ldx] rows of d floats (device) -> out [n * (unit_directions ? d : 1), 2d].
+ * --------------------------------------------------------------------------------------- */
+int pdeinv_fp_rows(const float* d_x, int64_t n, int64_t ldx, int32_t dim, int32_t unit_directions,
+                   float* d_out, void* stream);
+
+/* Exact sampler of the overdamped OU law (fokker_planck_example.py:48-61, sample_ground_truth
+ * :88-96): sample r draws its own time t_r ~ U(t_lo, t_hi) (t_lo == t_hi: a fixed time), then
+ * x_r ~ N(m(t_r), P(t_r)) with, in the eigenbasis F = U diag(s) U^T,
+ *   U^T m(t) = e^{-ts} o (U^T m0),  U^T P(t) U = e B0 e + (B / (s_i + s_j)) o (1 - e_i e_j),
+ *   e = diag(e^{-ts}), B0 = U^T P0 U, B = U^T L U                                  (:48-55)
+ * — moments, Cholesky factor and sample all in registers, one thread per sample. Host arrays
+ * (row-major): U [d*d], s [d], Um0 [d], B0 [d*d], B [d*d]; d <= 8. out [n, d]; t_out [n] nullable.
+ * Stream: time u from ctr {row, counter_offset, 0x10000000}, normals as pdeinv_gaussian_sample. */
+int pdeinv_fp_exact_sample(int64_t n, int32_t dim, uint64_t seed, uint32_t counter_offset, int64_t row_offset,
+                           float t_lo, float t_hi, const float* U_host, const float* s_host, const float* Um0_host,
+                           const float* B0_host, const float* B_host, float* d_out, float* d_t_out, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * GMM potential value and gradient over a batch — GMMPotential.value/.gradient

@@ -560,19 +560,75 @@ def kfp_mlp_grad_analytic(params, z_init, z_term, z_0T, gamma, T):
     """d loss / d params for the MLP model by the adjoint mlp.hip implements: Taylor forward
     (h, hd, hdd), the grad_x reverse chain (a, zeta), its forward-mode adjoint (abar, zetabar),
     then reverse over the three forward streams; weight gradients are sums of outer products."""
-    d = params[0][0].shape[0]
-    L = len(params) - 1
     rows, coefs = [], []
-    for z, c in ((z_0T, (1.0 / len(z_0T), -2.0 / len(z_0T), 2 * gamma / len(z_0T))),
-                 (z_init, (0.0, 0.0, -2.0 / (T * max(len(z_init), 1)))),
-                 (z_term, (0.0, 0.0, 2.0 / (T * max(len(z_term), 1))))):
+    for z, c in ((z_0T, (1.0 / len(z_0T), -2.0 / len(z_0T), 2 * gamma / len(z_0T), 0.0)),
+                 (z_init, (0.0, 0.0, -2.0 / (T * max(len(z_init), 1)), 0.0)),
+                 (z_term, (0.0, 0.0, 2.0 / (T * max(len(z_term), 1)), 0.0))):
         z = np.asarray(z, np.float64)
         if len(z):
             rows.append(z)
             coefs.append(np.tile(np.asarray(c)[None], (len(z), 1)))
-    Z = np.concatenate(rows)
-    C = np.concatenate(coefs)
-    c1, c2, c3 = C[:, :1], C[:, 1:2], C[:, 2:3]
+    return mlp_grad_rows(params, np.concatenate(rows), np.concatenate(coefs))
+
+
+# --------------------------------------------------------------------------------------
+# overdamped Fokker–Planck (example_problems/fokker_planck_example.py,
+# methods/consistency_instances/fokker_planck.py:33-63)
+# --------------------------------------------------------------------------------------
+def fp_configuration(F, m0_scale=1.0, P0_scale=5.0, L_scale=2.0):
+    """fokker_planck_example.py:20-46."""
+    F = np.asarray(F, np.float64)
+    d = F.shape[0]
+    U, s, _ = np.linalg.svd(F)
+    L, P0, m0 = np.eye(d) * L_scale, np.eye(d) * P0_scale, np.ones(d) * m0_scale
+    return {"F": F, "L": L, "U": U, "s": s, "B": U.T @ L @ U, "B_0": U.T @ P0 @ U, "m_0": m0, "P_0": P0}
+
+
+def fp_mean_cov(t, cfg):
+    """OU_process (:48-55): dm/dt = -F m, dP/dt = -FP - PF + L in closed form."""
+    e = np.diag(np.exp(-t * cfg["s"]))
+    U = cfg["U"]
+    ss = cfg["s"][:, None] + cfg["s"][None, :]
+    BS = cfg["B"] / ss
+    return U @ e @ U.T @ cfg["m_0"], U @ (e @ cfg["B_0"] @ e + BS - e @ BS @ e) @ U.T
+
+
+def fp_mlp_loss(params, x_init, x_term, x_0T, F, T):
+    """loss_fn (:48-55) / loss_ground_truth_fn (:57-58): lap V = sum_k e_k^T Hess V e_k."""
+    x0 = np.asarray(x_0T, np.float64)
+    d = x0.shape[1]
+    _, g, _, _ = mlp_forward_terms(params, x0, np.zeros_like(x0))
+    lap = sum(mlp_forward_terms(params, x0, np.tile(np.eye(d)[k], (len(x0), 1)))[3] for k in range(d))
+    gt = x0 @ np.asarray(F, np.float64).T
+    V = lambda x: mlp_forward_terms(params, x, np.zeros_like(x))[0] if len(x) else np.zeros(0)
+    vi, vt = V(np.asarray(x_init, np.float64)), V(np.asarray(x_term, np.float64))
+    parts = dict(nabla=np.mean(np.sum(g * g, -1)), laplacian=np.mean(lap), nabla_true=np.mean(np.sum(gt * gt, -1)),
+                 initial=np.mean(vi) if len(vi) else 0.0, terminal=np.mean(vt) if len(vt) else 0.0)
+    loss = parts["nabla"] - 2 * parts["laplacian"] + parts["nabla_true"] + 2 * (parts["terminal"] - parts["initial"]) / T
+    return loss, np.mean(np.sum((gt - g) ** 2, -1)), parts
+
+
+def fp_mlp_grad_analytic(params, x_init, x_term, x_0T, T):
+    """d loss / d params of fp_mlp_loss through mlp_grad_rows: 0T rows [x | e_k] with
+    (c1, c2) = (1/(dM), -2/M); boundary rows [x | 0] weighting V with c0 = -+2/(T n)."""
+    x0 = np.asarray(x_0T, np.float64)
+    M, d = x0.shape
+    rows = [np.concatenate([np.repeat(x0, d, 0), np.tile(np.eye(d), (M, 1))], 1)]
+    coefs = [np.tile([[1.0 / (d * M), -2.0 / M, 0.0, 0.0]], (M * d, 1))]
+    for x, sgn in ((x_init, -1.0), (x_term, 1.0)):
+        x = np.asarray(x, np.float64)
+        if len(x):
+            rows.append(np.concatenate([x, np.zeros_like(x)], 1))
+            coefs.append(np.tile([[0.0, 0.0, 0.0, sgn * 2.0 / (T * len(x))]], (len(x), 1)))
+    return mlp_grad_rows(params, np.concatenate(rows), np.concatenate(coefs))
+
+
+def mlp_grad_rows(params, Z, C):
+    """Gradient of sum_r [c1 |g|^2 + c2 V'' + c3 V' + c0 V](row r) over rows Z = [x | v] with
+    per-row weights C = [c1, c2, c3, c0] (the adjoint of mlp.hip / mlp_fused.hip)."""
+    d = params[0][0].shape[0]
+    L = len(params) - 1
+    c1, c2, c3, c0 = C[:, :1], C[:, 1:2], C[:, 2:3], C[:, 3:4]
     x, v = Z[:, :d], Z[:, d:]
     A = [(x, v, np.zeros_like(x))]          # (h, hd, hdd) per layer input
     Zs, S = [], []
@@ -607,7 +663,7 @@ def kfp_mlp_grad_analytic(params, z_init, z_term, z_0T, gamma, T):
         zetabar[l] = abar[l - 1] @ params[l - 1][0]
         abar[l] = S[l - 1][0] * zetabar[l]
     ubar = abar[L] @ Ko
-    ybar = 2 * c3 * yd + 2 * c2 * ydd + 2 * ubar
+    ybar = 2 * c3 * yd + 2 * c2 * ydd + 2 * ubar + 2 * c0 * y
     ydbar = 2 * c3 * y + 4 * c2 * yd
     yddbar = 2 * c2 * y
     grads = [None] * (L + 1)

@@ -168,13 +168,14 @@ __global__ void mlp_act_fwd(const float* __restrict__ Z, float* __restrict__ A, 
   A[2 * S + e] = fmaf(s1, zdd, s2 * zd * zd);
 }
 
-// output layer: y (+bias) stored back; u = 2y (seed of the grad_x chain); V' = 2 y.y', V'' = 2(y'.y' + y.y'')
+// output layer: y (+bias) stored back; u = 2y (seed of the grad_x chain); per row
+// terms = {V' = 2 y.y', V'' = 2(y'.y' + y.y''), V = y.y, 0}
 // A block owns rb consecutive rows = rb*O consecutive elements of each plane: phase 1 is
 // element-wise and coalesced, the per-element products go to LDS, phase 2 sums them per row.
 __global__ __launch_bounds__(kBlock) void mlp_out(float* __restrict__ Y, const float* __restrict__ bias,
-                                                  float* __restrict__ YB, float2* __restrict__ terms, int64_t R,
+                                                  float* __restrict__ YB, float4* __restrict__ terms, int64_t R,
                                                   int O, int rb) {
-  extern __shared__ float prod[];  // [2][rb*O]
+  extern __shared__ float prod[];  // [3][rb*O]
   const int64_t S = R * O;
   const int64_t r0 = (int64_t)blockIdx.x * rb;
   const int nr = (int)((R - r0) < rb ? (R - r0) : rb);
@@ -187,15 +188,17 @@ __global__ __launch_bounds__(kBlock) void mlp_out(float* __restrict__ Y, const f
     YB[3 * S + e] = 2.f * y;
     prod[k] = y * yd;
     prod[rb * O + k] = fmaf(yd, yd, y * ydd);
+    prod[2 * rb * O + k] = y * y;
   }
   __syncthreads();
   for (int r = threadIdx.x; r < nr; r += kBlock) {
-    float vd = 0.f, vdd = 0.f;
+    float vd = 0.f, vdd = 0.f, v = 0.f;
     for (int o = 0; o < O; ++o) {
       vd += prod[r * O + o];
       vdd += prod[rb * O + r * O + o];
+      v += prod[2 * rb * O + r * O + o];
     }
-    terms[r0 + r] = make_float2(2.f * vd, 2.f * vdd);
+    terms[r0 + r] = make_float4(2.f * vd, 2.f * vdd, v, 0.f);
   }
 }
 
@@ -218,18 +221,19 @@ __global__ void mlp_gadj(const float* __restrict__ zetabar, const float* __restr
 }
 
 struct MlpLossArgs {
-  int d, set, true_kind, KT;
-  float c1, c2, c3, c_true, inv_n;
+  int d, set, true_kind, KT, bval;
+  float c1, c2, c3, c0, c_true, inv_n;
   float s2t, l2st;
   float tp[PDEINV_MAX_PARAMS];  // tilde_F [d*d] or true GMM centres [K*d]
 };
 
-// per row: T1 = |g|^2, T2 = V'', T3 = V', true-potential terms (0T rows); seeds abar_0 = 2 c1 g;
-// block partial sums of the 8 accumulator slots of pdeinv.h (PDEINV_GMM_ACC_*).
+// per row: T1 = |g|^2, T2 = V'', T3 = V', T0 = V, true-potential terms (0T rows); seeds
+// abar_0 = 2 c1 g; block partial sums of the 8 accumulator slots of pdeinv.h (PDEINV_GMM_ACC_*).
+// The boundary slots report the set mean of V' (kinetic FP) or of V (bval: overdamped FP).
 template <int D>
 __global__ __launch_bounds__(kBlock) void mlp_loss(MlpLossArgs a, const float* __restrict__ G,
                                                    const float* __restrict__ X, int64_t ldx,
-                                                   const float2* __restrict__ terms, float* __restrict__ abar0,
+                                                   const float4* __restrict__ terms, float* __restrict__ abar0,
                                                    int64_t R, float* __restrict__ partials) {
   float acc[PDEINV_GMM_NACC] = {0, 0, 0, 0, 0, 0, 0, 0};
   const int64_t stride = (int64_t)gridDim.x * kBlock;
@@ -242,9 +246,9 @@ __global__ __launch_bounds__(kBlock) void mlp_loss(MlpLossArgs a, const float* _
       T1 = fmaf(g[i], g[i], T1);
       abar0[r * D + i] = 2.f * a.c1 * g[i];
     }
-    const float2 t = terms[r];
-    const float T2 = t.y, T3 = t.x;
-    acc[PDEINV_GMM_ACC_LOSS] += a.c1 * T1 + a.c2 * T2 + a.c3 * T3;
+    const float4 t = terms[r];
+    const float T2 = t.y, T3 = t.x, T0 = t.z;
+    acc[PDEINV_GMM_ACC_LOSS] += a.c1 * T1 + a.c2 * T2 + a.c3 * T3 + a.c0 * T0;
     if (a.set == 0) {
       float gt[D];
       if (a.true_kind == PDEINV_POT_QUADRATIC) {
@@ -299,23 +303,23 @@ __global__ __launch_bounds__(kBlock) void mlp_loss(MlpLossArgs a, const float* _
       acc[PDEINV_GMM_ACC_FRICTION] += a.c_true * T3;
       acc[PDEINV_GMM_ACC_NABLA_TRUE] += a.c_true * Tt;
     } else if (a.set == 1) {
-      acc[PDEINV_GMM_ACC_INITIAL] += a.inv_n * T3;
+      acc[PDEINV_GMM_ACC_INITIAL] += a.inv_n * (a.bval ? T0 : T3);
     } else {
-      acc[PDEINV_GMM_ACC_TERMINAL] += a.inv_n * T3;
+      acc[PDEINV_GMM_ACC_TERMINAL] += a.inv_n * (a.bval ? T0 : T3);
     }
   }
   __shared__ float lds[kWavesPerBlock * PDEINV_GMM_NACC];
   block_reduce_to_slab(acc, PDEINV_GMM_NACC, lds, partials, blockIdx.x, gridDim.x);
 }
 
-// seeds of the reverse sweep over the forward streams:
-//   ybar = 2 c3 y' + 2 c2 y'' + 2 ubar,  y'bar = 2 c3 y + 4 c2 y',  y''bar = 2 c2 y
+// seeds of the reverse sweep over the forward streams (c0: weight of the value V = y.y):
+//   ybar = 2 c3 y' + 2 c2 y'' + 2 ubar + 2 c0 y,  y'bar = 2 c3 y + 4 c2 y',  y''bar = 2 c2 y
 __global__ void mlp_seeds(const float* __restrict__ Y, const float* __restrict__ UB, float* __restrict__ YB,
-                          float c2, float c3, int64_t S) {
+                          float c2, float c3, float c0, int64_t S) {
   const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (e >= S) return;
   const float y = Y[e], yd = Y[S + e], ydd = Y[2 * S + e];
-  YB[e] = 2.f * c3 * yd + 2.f * c2 * ydd + 2.f * UB[e];
+  YB[e] = 2.f * c3 * yd + 2.f * c2 * ydd + 2.f * UB[e] + 2.f * c0 * y;
   YB[S + e] = 2.f * c3 * y + 4.f * c2 * yd;
   YB[2 * S + e] = 2.f * c2 * y;
 }
@@ -407,7 +411,7 @@ static MlpPlan make_plan(const pdeinv_kfp_mlp_desc* d) {
   const int64_t wmax = (int64_t)p.W * (p.W > p.d ? (p.W > p.O ? p.W : p.O) : p.d);
   const int64_t cmax = (int64_t)kColsumBlocks * (p.W > p.O ? p.W : p.O);
   p.off_kpart = take((size_t)(kMaxKSplit * wmax > cmax ? kMaxKSplit * wmax : cmax));
-  p.off_terms = take(2 * p.Bc);
+  p.off_terms = take(4 * p.Bc);
   p.off_part = take((size_t)PDEINV_GMM_NACC * kLossGrid);
   p.layer_stride = 16 * p.Bc * p.W;
   p.off_layer0 = take(p.layer_stride * p.L);
@@ -444,7 +448,7 @@ struct LossCtx {
   int D;
 };
 
-static int fused_loss_hook(void* p, const float* G, const float2* terms, float* abar0, int64_t R, hipStream_t st) {
+static int fused_loss_hook(void* p, const float* G, const float4* terms, float* abar0, int64_t R, hipStream_t st) {
   LossCtx* c = (LossCtx*)p;
   const int lg = grid_for(R) < kLossGrid ? grid_for(R) : kLossGrid;
   switch (c->D) {
@@ -504,7 +508,7 @@ extern "C" int pdeinv_residual_kfp_mlp(const pdeinv_kfp_mlp_desc* d, const float
   float* YB = w + p.off_YB;
   float* UB = w + p.off_UB;
   float* G = w + p.off_G;
-  float2* terms = (float2*)(w + p.off_terms);
+  float4* terms = (float4*)(w + p.off_terms);
   float* part = w + p.off_part;
   // planes per hidden layer l: A 0-3, Z 4-6, ZB 7-10, HB 11-13, aL 14, zb 15. Inside a chunk of R rows
   // the planes are packed at stride R*W so that consecutive streams form one [k*R x W] GEMM operand.
@@ -520,10 +524,13 @@ extern "C" int pdeinv_residual_kfp_mlp(const pdeinv_kfp_mlp_desc* d, const float
   const int ntp = d->true_kind == PDEINV_POT_QUADRATIC ? D * D : d->n_centers_true * D;
   for (int k = 0; k < ntp; ++k) la.tp[k] = d->true_params[k];
 
-  struct Set { const float* z; int64_t n, ld; int id; float c1, c2, c3; } sets[3] = {
-      {z0, n0, ld0 ? ld0 : 2 * D, 0, d->c_nabla, d->c_hess, d->c_fric},
-      {zi, ni, ldi ? ldi : 2 * D, 1, 0.f, 0.f, d->c_init},
-      {zt, nt, ldt ? ldt : 2 * D, 2, 0.f, 0.f, d->c_term}};
+  // boundary sets weight V' (kinetic FP, :49-50) or V itself (overdamped FP, fokker_planck.py:48-52)
+  const bool bval = d->boundary_value != 0;
+  la.bval = bval ? 1 : 0;
+  struct Set { const float* z; int64_t n, ld; int id; float c1, c2, c3, c0; } sets[3] = {
+      {z0, n0, ld0 ? ld0 : 2 * D, 0, d->c_nabla, d->c_hess, d->c_fric, 0.f},
+      {zi, ni, ldi ? ldi : 2 * D, 1, 0.f, 0.f, bval ? 0.f : d->c_init, bval ? d->c_init : 0.f},
+      {zt, nt, ldt ? ldt : 2 * D, 2, 0.f, 0.f, bval ? 0.f : d->c_term, bval ? d->c_term : 0.f}};
   if (use_fused(d)) {
     const int64_t Bc = chunk_rows_of(d);
     const size_t fl = mlpf::workspace_floats(D, L, p.W, p.O, Bc);
@@ -534,7 +541,7 @@ extern "C" int pdeinv_residual_kfp_mlp(const pdeinv_kfp_mlp_desc* d, const float
     lc.D = D;
     for (const Set& s : sets) {
       PDEINV_REQUIRE(s.n == 0 || s.ld >= 2 * D, PDEINV_ERR_INVALID, "kfp_mlp: row stride < 2*dim");
-      lc.la.set = s.id; lc.la.c1 = s.c1; lc.la.c2 = s.c2; lc.la.c3 = s.c3; lc.la.c_true = d->c_true;
+      lc.la.set = s.id; lc.la.c1 = s.c1; lc.la.c2 = s.c2; lc.la.c3 = s.c3; lc.la.c0 = s.c0; lc.la.c_true = d->c_true;
       lc.la.inv_n = s.n ? 1.f / (float)s.n : 0.f;
       for (int64_t r0 = 0; r0 < s.n; r0 += Bc) {
         mlpf::Chunk c{};
@@ -543,7 +550,7 @@ extern "C" int pdeinv_residual_kfp_mlp(const pdeinv_kfp_mlp_desc* d, const float
         c.z = s.z + r0 * s.ld;
         c.ldz = s.ld;
         c.params = params; c.grad = grad; c.poff = poff; c.boff = boff;
-        c.c2 = s.c2; c.c3 = s.c3;
+        c.c2 = s.c2; c.c3 = s.c3; c.c0 = s.c0;
         c.ws = (float*)ws; c.Bc = Bc;
         lc.zr = c.z;
         lc.ld = s.ld;
@@ -579,8 +586,8 @@ extern "C" int pdeinv_residual_kfp_mlp(const pdeinv_kfp_mlp_desc* d, const float
       }
       blas.fwd(layer(L, 0), params + poff[L], Y, 3 * R, W, O);
       {
-        const int rb = O >= 2048 ? 1 : 2048 / O;  // 16 KB of LDS products per block
-        hipLaunchKernelGGL(mlp_out, dim3((unsigned)((R + rb - 1) / rb)), dim3(kBlock), 2 * rb * O * sizeof(float), st,
+        const int rb = O >= 2048 ? 1 : 2048 / O;  // 24 KB of LDS products per block
+        hipLaunchKernelGGL(mlp_out, dim3((unsigned)((R + rb - 1) / rb)), dim3(kBlock), 3 * rb * O * sizeof(float), st,
                            Y, params + boff[L], YB, terms, R, O, rb);
       }
       // ---- R1: grad_x chain ---------------------------------------------------------------
@@ -592,7 +599,7 @@ extern "C" int pdeinv_residual_kfp_mlp(const pdeinv_kfp_mlp_desc* d, const float
         else blas.bwd(layer(1, 10), params + poff[0], G, R, D, W);  // g = zeta_1 K_1^T
       }
       // ---- loss terms, seed abar_0 = 2 c1 g ------------------------------------------------
-      la.set = s.id; la.c1 = s.c1; la.c2 = s.c2; la.c3 = s.c3; la.c_true = d->c_true;
+      la.set = s.id; la.c1 = s.c1; la.c2 = s.c2; la.c3 = s.c3; la.c0 = s.c0; la.c_true = d->c_true;
       la.inv_n = 1.f / (float)s.n;
       const int lg = grid_for(R) < kLossGrid ? grid_for(R) : kLossGrid;
       switch (D) {
@@ -611,7 +618,7 @@ extern "C" int pdeinv_residual_kfp_mlp(const pdeinv_kfp_mlp_desc* d, const float
                            layer(l, 3), SW);  // abar_l -> A plane 3
       }
       blas.fwd(layer(L, 3), params + poff[L], UB, R, W, O);  // ubar = abar_L K_o
-      hipLaunchKernelGGL(mlp_seeds, dim3(grid_for(SO)), dim3(kBlock), 0, st, Y, UB, YB, s.c2, s.c3, SO);
+      hipLaunchKernelGGL(mlp_seeds, dim3(grid_for(SO)), dim3(kBlock), 0, st, Y, UB, YB, s.c2, s.c3, s.c0, SO);
       // ---- R2 + G: reverse over the three forward streams, weight gradients ---------------------
       blas.wgrad(layer(L, 0), YB, grad + poff[L], 4 * R, W, O);  // K_o += [h;h';h'';abar]^T [ybar;..;u]
       blas.colsum(YB, grad + boff[L], R, O);

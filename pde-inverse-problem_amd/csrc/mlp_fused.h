@@ -13,8 +13,9 @@ size_t workspace_floats(int d, int L, int W, int O, int64_t Bc);
 
 // Per-set loss hook: the orchestrator computes g [R x d] and the per-row terms (V', V''), then
 // calls this to accumulate the loss slots and write abar0 = 2 c1 g [R x d] (mlp.hip's loss kernel).
+// terms[r] = {V', V'', V, 0}.
 struct LossHook {
-  int (*fn)(void* ctx, const float* g, const float2* terms, float* abar0, int64_t R, hipStream_t st);
+  int (*fn)(void* ctx, const float* g, const float4* terms, float* abar0, int64_t R, hipStream_t st);
   void* ctx;
 };
 
@@ -27,7 +28,7 @@ struct Chunk {
   float* grad;               // accumulated (+=)
   const int64_t* poff;       // kernel offsets per layer (0..L)
   const int64_t* boff;       // bias offsets per layer (0..L)
-  float c2, c3;              // loss weights of V'' and V' for this set
+  float c2, c3, c0;          // loss weights of V'', V' and V for this set
   float* ws;                 // workspace_floats(..., Bc >= R)
   int64_t Bc;
 };

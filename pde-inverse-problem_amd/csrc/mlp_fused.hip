@@ -74,8 +74,8 @@ struct GemmArgs {
   const float* bias;                      // [N], stream 0 (E_ACT_FWD, E_OUT)
   float *po0, *po1, *po2;                 // outputs, ld N
   const float *pe0, *pe1, *pe2, *pe3, *pe4;  // epilogue inputs, ld N
-  float2* terms;
-  float c2, c3;
+  float4* terms;  // per row {V', V'', V, 0}
+  float c2, c3, c0;
   float* part;
 };
 
@@ -244,10 +244,10 @@ __global__ __launch_bounds__(kT) void fgemm(GemmArgs a) {
       constexpr bool CHECK = decltype(check)::value;
   #pragma unroll
       for (int mi = 0; mi < MI; ++mi) {
-        [[maybe_unused]] float t1[16], t2[16];
+        [[maybe_unused]] float t0[16], t1[16], t2[16];
         if constexpr (EM == E_OUT) {
   #pragma unroll
-          for (int q = 0; q < 16; ++q) t1[q] = t2[q] = 0.f;
+          for (int q = 0; q < 16; ++q) t0[q] = t1[q] = t2[q] = 0.f;
         }
   #pragma unroll
         for (int ni = 0; ni < NI; ++ni) {
@@ -280,6 +280,7 @@ __global__ __launch_bounds__(kT) void fgemm(GemmArgs a) {
                 sto(a.po0, o, y);
                 sto(a.po1, o, yd);
                 sto(a.po2, o, ydd);
+                t0[q] = fmaf(y, y, t0[q]);
                 t1[q] = fmaf(y, yd, t1[q]);
                 t2[q] = fmaf(yd, yd, fmaf(y, ydd, t2[q]));
               }
@@ -287,7 +288,7 @@ __global__ __launch_bounds__(kT) void fgemm(GemmArgs a) {
               if (ok) {
                 const float ub = acc[0][mi][ni][q];
                 const float y = ldo(a.pe0, o), yd = ldo(a.pe1, o), ydd = ldo(a.pe2, o);
-                const float yb = 2.f * a.c3 * yd + 2.f * a.c2 * ydd + 2.f * ub;
+                const float yb = 2.f * a.c3 * yd + 2.f * a.c2 * ydd + 2.f * ub + 2.f * a.c0 * y;
                 sto(a.po0, o, yb);
                 sto(a.po1, o, 2.f * a.c3 * y + 4.f * a.c2 * yd);
                 sto(a.po2, o, 2.f * a.c2 * y);
@@ -310,14 +311,15 @@ __global__ __launch_bounds__(kT) void fgemm(GemmArgs a) {
         if constexpr (EM == E_OUT) {
   #pragma unroll
           for (int q = 0; q < 16; ++q) {
-            float p1 = t1[q], p2 = t2[q];
+            float p0 = t0[q], p1 = t1[q], p2 = t2[q];
   #pragma unroll
             for (int off = 16; off > 0; off >>= 1) {
+              p0 += __shfl_xor(p0, off, 64);
               p1 += __shfl_xor(p1, off, 64);
               p2 += __shfl_xor(p2, off, 64);
             }
             const int r = r0 + wm * WM + mi * 32 + (q & 3) + 8 * (q >> 2) + 4 * hi;
-            if (l31 == 0 && r < a.R) a.terms[r] = make_float2(2.f * p1, 2.f * p2);
+            if (l31 == 0 && r < a.R) a.terms[r] = make_float4(2.f * p1, 2.f * p2, p0, 0.f);
           }
         }
       }
@@ -780,7 +782,7 @@ static Layout layout(int d, int L, int W, int O, int64_t Bc) {
   y.hb1 = take(3 * plane);
   y.ys = take((size_t)3 * Bc * O);
   y.yb = take((size_t)3 * Bc * O);
-  y.terms = take((size_t)2 * Bc);
+  y.terms = take((size_t)4 * Bc);
   y.g = take((size_t)Bc * d);
   y.abar0 = take((size_t)Bc * d);
   y.part = take(part_floats(d, W, O));
@@ -812,7 +814,7 @@ static int run_chunk_t(const Chunk& c, const LossHook& loss, hipStream_t st) {
   float* HB1[3] = {ws + y.hb1, ws + y.hb1 + plane, ws + y.hb1 + 2 * plane};
   float* Ys[3] = {ws + y.ys, ws + y.ys + (size_t)c.Bc * O, ws + y.ys + 2 * (size_t)c.Bc * O};
   float* YB[3] = {ws + y.yb, ws + y.yb + (size_t)c.Bc * O, ws + y.yb + 2 * (size_t)c.Bc * O};
-  float2* terms = (float2*)(ws + y.terms);
+  float4* terms = (float4*)(ws + y.terms);
   float* G = ws + y.g;
   float* abar0 = ws + y.abar0;
   float* part = ws + y.part;
@@ -827,6 +829,7 @@ static int run_chunk_t(const Chunk& c, const LossHook& loss, hipStream_t st) {
   base.R = R;
   base.c2 = c.c2;
   base.c3 = c.c3;
+  base.c0 = c.c0;
   base.part = part;
   int rc = 0;
 #define RC(x)          \

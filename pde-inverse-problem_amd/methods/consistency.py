@@ -14,9 +14,12 @@ Deviations (documented in DESIGN.md):
 """
 from __future__ import annotations
 
+import functools
+
 import numpy as np
 import torch
 
+import methods.consistency_instances.fokker_planck as fokker_planck
 import methods.consistency_instances.kinetic_fokker_planck as kinetic_fokker_planck
 import methods.consistency_instances.kinetic_mckean_vlasov as kinetic_mckean_vlasov
 from api import Method
@@ -24,6 +27,7 @@ from utils import distributed as dist
 from utils import native, prng
 
 INSTANCES = {
+    "Fokker-Planck": fokker_planck,
     "Kinetic-Fokker-Planck": kinetic_fokker_planck,
     "Kinetic-McKean-Vlasov": kinetic_mckean_vlasov,
 }
@@ -38,6 +42,7 @@ class ConsistencyBased(Method):
         raise NotImplementedError
 
     def test_fn(self, forward_fn, params, rng):
+        forward_fn = functools.partial(forward_fn, params)  # consistency.py:27
         if self.cfg.pde_instance.name in INSTANCES:
             return INSTANCES[self.cfg.pde_instance.name].test_fn(forward_fn=forward_fn, pde_instance=self.pde_instance,
                                                                 rng=rng)

@@ -1,4 +1,5 @@
 """Plugin registry (registry.py of the reference): problem and method lookup by config name."""
+from example_problems.fokker_planck_example import FokkerPlanck
 from example_problems.kinetic_fokker_planck_example_GMM import KineticFokkerPlanck as KFPGMM
 from example_problems.kinetic_fokker_planck_example_OU import KineticFokkerPlanck as KFPOU
 from example_problems.kinetic_mckean_vlasov_example_quadratic import KineticMcKeanVlasov as KMVOU
@@ -15,10 +16,11 @@ KineticMcKeanVlasovPotential = {
 
 
 def get_pde_instance(cfg):
-    """registry.py:18-26. The overdamped "Fokker-Planck" instance is out of scope for this build
-     and raises. The reference *returns* NotImplementedError for
-    an unknown name (registry.py:25-26); here it is raised, so the failure is not deferred."""
+    """registry.py:18-26. The reference *returns* NotImplementedError for an unknown name
+    (registry.py:25-26); here it is raised, so the failure is not deferred."""
     name = cfg.pde_instance.name
+    if name == "Fokker-Planck":
+        return FokkerPlanck
     if name == "Kinetic-Fokker-Planck":
         return KineticFokkerPlanckPotential[cfg.pde_instance.potential]
     if name == "Kinetic-McKean-Vlasov":

@@ -32,9 +32,11 @@ KFP_NOUT = 9
 KFP_SLOTS = ("loss", "loss ground truth", "grad_norm", "loss_nabla", "loss_Hessian",
              "loss_friction", "loss_nabla_true", "loss_initial", "loss_terminal")
 GMM_NACC = 8
+# PDEINV_GMM_ACC_* slot names (include/pdeinv.h), shared by the GMM and MLP residual accumulators
+GMM_ACC_SLOTS = ("loss", "loss_gt", "nabla", "hessian", "friction", "nabla_true", "initial", "terminal")
 SQRT2 = math.sqrt(2.0)
 
-ABI_VERSION = 2  # PDEINV_ABI_VERSION of include/pdeinv.h this binding was written against
+ABI_VERSION = 3  # PDEINV_ABI_VERSION of include/pdeinv.h this binding was written against
 
 # Every exported symbol of include/pdeinv.h (tests check the library exports all of them).
 EXPORTED_SYMBOLS = (
@@ -43,7 +45,7 @@ EXPORTED_SYMBOLS = (
     "pdeinv_moments_workspace_bytes", "pdeinv_moments", "pdeinv_residual_kfp_quadratic",
     "pdeinv_residual_kfp_gmm_workspace_bytes", "pdeinv_residual_kfp_gmm",
     "pdeinv_residual_kfp_gmm_finalize", "pdeinv_gmm_potential", "pdeinv_gaussian_sample",
-    "pdeinv_gaussian_sample_grouped",
+    "pdeinv_gaussian_sample_grouped", "pdeinv_fp_rows", "pdeinv_fp_exact_sample",
     "pdeinv_philox_fill", "pdeinv_gather_subsample", "pdeinv_abi_version", "pdeinv_last_error",
     "pdeinv_runtime_version", "pdeinv_moments_batched_workspace_bytes", "pdeinv_moments_batched",
     "pdeinv_kmv_weights_workspace_bytes", "pdeinv_kmv_weights", "pdeinv_residual_kmv",
@@ -85,7 +87,7 @@ class KfpMlpDesc(ctypes.Structure):
                 ("sigma_true", ctypes.c_float), ("true_params", ctypes.c_void_p), ("gamma", ctypes.c_float),
                 ("c_nabla", ctypes.c_float), ("c_hess", ctypes.c_float), ("c_fric", ctypes.c_float),
                 ("c_true", ctypes.c_float), ("c_init", ctypes.c_float), ("c_term", ctypes.c_float),
-                ("chunk_rows", ctypes.c_int64), ("impl", ctypes.c_int32)]
+                ("chunk_rows", ctypes.c_int64), ("impl", ctypes.c_int32), ("boundary_value", ctypes.c_int32)]
 
 
 MLP_IMPL_AUTO, MLP_IMPL_LIBRARY, MLP_IMPL_FUSED = 0, 1, 2
@@ -168,6 +170,8 @@ def lib():
         "pdeinv_residual_kfp_mlp": (i32, [P, P, i64, i64, P, i64, i64, P, i64, i64, P, P, P, P, P]),
         "pdeinv_kfp_terms_finalize": (i32, [P, P, i64, f32, P, P]),
         "pdeinv_gather_random_step": (i32, [P, i64, i32, i32, u64, u32, P, P, P]),
+        "pdeinv_fp_rows": (i32, [P, i64, i64, i32, i32, P, P]),
+        "pdeinv_fp_exact_sample": (i32, [i64, i32, u64, u32, i64, f32, f32, P, P, P, P, P, P, P, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -583,9 +587,11 @@ def mf_workspace(desc: SdeDesc, device) -> torch.Tensor:
 def residual_kfp_mlp(dims, params_flat: torch.Tensor, z_init: torch.Tensor, z_term: torch.Tensor,
                      z_0T: torch.Tensor, *, true_kind: int, true_params, gamma: float, total_time: float,
                      sigma_true: float = 1.0, world_scale: float = 1.0, chunk_rows: int = 1 << 18,
-                     impl: int = MLP_IMPL_AUTO):
+                     impl: int = MLP_IMPL_AUTO, coefficients: Optional[dict] = None, boundary_value: bool = False):
     """kinetic_fokker_planck.py:11-69 for V_hypothesis. dims = [d, W, ..., W, out] (equal hidden widths).
-    Returns (acc fp64 [8], grad fp32 [P]) — sums with the reference's loss weights."""
+    Returns (acc fp64 [8], grad fp32 [P]) — sums with the reference's loss weights.
+    `coefficients` overrides the per-term weights (c_nabla, c_hess, c_fric, c_true, c_init, c_term) and
+    `boundary_value` makes the boundary sets weight V instead of V' (overdamped FP: residual_fp_mlp)."""
     _require_gpu()
     d, W, O = dims[0], dims[1], dims[-1]
     L = len(dims) - 2
@@ -602,11 +608,13 @@ def residual_kfp_mlp(dims, params_flat: torch.Tensor, z_init: torch.Tensor, z_te
     M = float(n0)
     c = dict(c_nabla=1.0 / M, c_hess=-2.0 / M, c_fric=2.0 * gamma / M, c_true=1.0 / M,
              c_init=(-2.0 / (total_time * ni)) if ni else 0.0, c_term=(2.0 / (total_time * nt)) if nt else 0.0)
+    if coefficients is not None:
+        c.update(coefficients)
     c = {k: v * world_scale for k, v in c.items()}
     desc = KfpMlpDesc(d, L, W, O, int(true_kind), int(tp.size // d) if true_kind == POT_GMM else 0,
                       float(sigma_true), tp.ctypes.data_as(ctypes.c_void_p), float(gamma), c["c_nabla"],
                       c["c_hess"], c["c_fric"], c["c_true"], c["c_init"], c["c_term"], int(chunk_rows),
-                      int(impl))
+                      int(impl), int(bool(boundary_value)))
     nbytes = lib().pdeinv_residual_kfp_mlp_workspace_bytes(ctypes.byref(desc))
     ws = torch.empty(nbytes // 4, device=z_0T.device, dtype=torch.float32)
     acc = torch.zeros(GMM_NACC, device=z_0T.device, dtype=torch.float64)
@@ -615,6 +623,56 @@ def residual_kfp_mlp(dims, params_flat: torch.Tensor, z_init: torch.Tensor, z_te
                                          _dev(params_flat, "params"), _dev(ws, "ws"), _dev(acc, "acc", torch.float64),
                                          _dev(grad, "grad"), stream_handle()), "pdeinv_residual_kfp_mlp")
     return acc, grad
+
+
+def fp_rows(x: torch.Tensor, unit_directions: bool) -> torch.Tensor:
+    """[x_r | e_k] rows (n*d of them) or [x_r | 0] rows — pdeinv_fp_rows."""
+    _require_gpu()
+    d = x.shape[1]
+    px, n, ldx = _rows(x, "x", d)
+    out = torch.empty((n * (d if unit_directions else 1), 2 * d), device=x.device, dtype=torch.float32)
+    _check(lib().pdeinv_fp_rows(px, n, ldx, d, int(bool(unit_directions)), _dev(out, "out"), stream_handle()),
+           "pdeinv_fp_rows")
+    return out
+
+
+def residual_fp_mlp(dims, params_flat: torch.Tensor, x_init: torch.Tensor, x_term: torch.Tensor,
+                    x_0T: torch.Tensor, *, tilde_F, total_time: float, world_scale: float = 1.0,
+                    chunk_rows: int = 1 << 18, impl: int = MLP_IMPL_AUTO):
+    """methods/consistency_instances/fokker_planck.py:33-63 for V_hypothesis:
+    loss = E|grad V|^2 - 2 E[lap V] + E|grad V*|^2 + (2/T)(E_T V - E_0 V), V* = x^T F x / 2.
+    The 0T rows are replicated along the d unit directions (lap V = sum_k e_k^T Hess V e_k) and go
+    through the same fused residual as the kinetic case with boundary_value = 1. Returns (acc, grad)
+    with the PDEINV_GMM_ACC_* slot meaning of residual_kfp_mlp (friction slot unused)."""
+    d = dims[0]
+    M = float(x_0T.shape[0])
+    ni, nt = x_init.shape[0], x_term.shape[0]
+    coef = dict(c_nabla=1.0 / (d * M), c_hess=-2.0 / M, c_fric=0.0, c_true=1.0 / (d * M),
+                c_init=(-2.0 / (total_time * ni)) if ni else 0.0, c_term=(2.0 / (total_time * nt)) if nt else 0.0)
+    z0 = fp_rows(x_0T, True)
+    zi = fp_rows(x_init, False) if ni else torch.empty((0, 2 * d), device=x_0T.device)
+    zt = fp_rows(x_term, False) if nt else torch.empty((0, 2 * d), device=x_0T.device)
+    return residual_kfp_mlp(dims, params_flat, zi, zt, z0, true_kind=POT_QUADRATIC, true_params=tilde_F, gamma=0.0,
+                            total_time=total_time, world_scale=world_scale, chunk_rows=chunk_rows, impl=impl,
+                            coefficients=coef, boundary_value=True)
+
+
+def fp_exact_sample(n: int, eig: dict, *, seed: int, t_range, counter_offset: int = 0, row_offset: int = 0,
+                    device="cuda", return_t: bool = False):
+    """x_r ~ N(m(t_r), P(t_r)), t_r ~ U(t_range) per sample (fokker_planck_example.py:88-96).
+    eig: host arrays U [d,d], s [d], Um0 [d], B0 [d,d], B [d,d] (fp32-castable)."""
+    _require_gpu()
+    U, s_, Um0, B0, B = (_host_f32(eig[k]) for k in ("U", "s", "Um0", "B0", "B"))
+    d = s_.size
+    out = torch.empty((int(n), d), device=device, dtype=torch.float32)
+    t_out = torch.empty(int(n), device=device, dtype=torch.float32) if return_t else None
+    lo, hi = (float(t_range), float(t_range)) if np.ndim(t_range) == 0 else (float(t_range[0]), float(t_range[1]))
+    _check(lib().pdeinv_fp_exact_sample(int(n), d, int(seed) & 0xFFFFFFFFFFFFFFFF, int(counter_offset) & 0xFFFFFFFF,
+                                        int(row_offset), lo, hi, *(a.ctypes.data_as(ctypes.c_void_p)
+                                                                   for a in (U, s_, Um0, B0, B)),
+                                        _dev(out, "out"), _dev(t_out, "t_out"), stream_handle()),
+           "pdeinv_fp_exact_sample")
+    return (out, t_out) if return_t else out
 
 
 def adam_update(params: torch.Tensor, grad: torch.Tensor, mu: torch.Tensor, nu: torch.Tensor, *, lr: float,

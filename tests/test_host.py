@@ -58,9 +58,11 @@ def test_registry():
     from utils import config
     c = config.compose("config", ["pde_instance=kinetic_fokker_planck", "pde_instance.potential=GMM"])
     assert registry.get_pde_instance(c).__module__.endswith("_GMM")
-    c = config.compose("config", [])
+    c = config.compose("config", [])  # the reference's default: overdamped Fokker-Planck
+    assert registry.get_pde_instance(c).__name__ == "FokkerPlanck"
+    c = config.compose("config", ["pde_instance.name=Heat"])
     with pytest.raises(NotImplementedError):
-        registry.get_pde_instance(c)  # overdamped FP: out of scope, raises
+        registry.get_pde_instance(c)
     c = config.compose("config", ["solver=PINN"])
     with pytest.raises(NotImplementedError):
         registry.get_method(c)
@@ -148,7 +150,7 @@ def test_library_exports_every_header_symbol():
     missing = [s for s in _header_functions() if not hasattr(lib, s)]
     assert not missing
     lib.pdeinv_moment_len.restype = ctypes.c_int
-    assert lib.pdeinv_moment_len(8) == 45 and lib.pdeinv_abi_version() == 2
+    assert lib.pdeinv_moment_len(8) == 45 and lib.pdeinv_abi_version() == native.ABI_VERSION == 3
 
 
 def test_loader_fails_loudly_without_gpu():

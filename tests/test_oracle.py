@@ -230,6 +230,45 @@ def test_mlp_taylor_terms_and_adjoint_vs_finite_differences():
     assert np.allclose(ga, nr.fd_grad(f, flat, eps=1e-6), rtol=1e-6, atol=1e-8)
 
 
+def test_fp_mlp_laplacian_and_adjoint_vs_finite_differences():
+    """Overdamped FP residual (fokker_planck.py:33-63): the Laplacian as d Taylor directions against
+    second differences, and the analytic adjoint (rows [x | e_k] + value-weighted boundary rows, the
+    layout pdeinv_fp_rows builds) against central differences of the loss (tiny net, fp64)."""
+    rng = np.random.default_rng(3)
+    dims = [3, 5, 4, 3]
+    flat = rng.standard_normal(sum(dims[i] * dims[i + 1] + dims[i + 1] for i in range(3))) * 0.6
+    P = nr.mlp_unflat(flat, dims)
+    x = rng.standard_normal((6, 3))
+    e = 1e-4
+    V = lambda y: nr.mlp_forward_terms(P, y, np.zeros_like(y))[0]
+    lap_fd = sum((V(x + e * np.eye(3)[k]) - 2 * V(x) + V(x - e * np.eye(3)[k])) / e ** 2 for k in range(3))
+    lap = sum(nr.mlp_forward_terms(P, x, np.tile(np.eye(3)[k], (6, 1)))[3] for k in range(3))
+    assert np.allclose(lap, lap_fd, atol=1e-5)
+    F = nr.problem_constants(3)
+    xi, xt, x0 = (rng.standard_normal((m, 3)) for m in (20, 15, 40))
+    f = lambda fl: nr.fp_mlp_loss(nr.mlp_unflat(fl, dims), xi, xt, x0, F, 2.0)[0]
+    ga = nr.mlp_flat(nr.fp_mlp_grad_analytic(P, xi, xt, x0, 2.0))
+    assert np.allclose(ga, nr.fd_grad(f, flat, eps=1e-6), rtol=1e-6, atol=1e-8)
+
+
+def test_fp_closed_form_matches_moment_ode():
+    """fokker_planck_example.py:101-116 (test_OU, printed only in the reference): the closed form
+    of OU_process against the moment ODE dm/dt = -F m, dP/dt = -FP - PF + L — asserted here."""
+    from scipy.integrate import solve_ivp
+    cfg = nr.fp_configuration(nr.problem_constants(4))
+    F, L = cfg["F"], cfg["L"]
+
+    def rhs(t, y):
+        m, Pm = y[:4], y[4:].reshape(4, 4)
+        return np.concatenate([-F @ m, (-F @ Pm - Pm @ F + L).ravel()])
+    ts = np.linspace(0, 2.0, 11)
+    sol = solve_ivp(rhs, (0, 2.0), np.concatenate([cfg["m_0"], cfg["P_0"].ravel()]), t_eval=ts, rtol=1e-10,
+                    atol=1e-12)
+    for k, t in enumerate(ts):
+        m, Pc = nr.fp_mean_cov(t, cfg)
+        assert np.abs(m - sol.y[:4, k]).max() < 1e-7 and np.abs(Pc - sol.y[4:, k].reshape(4, 4)).max() < 1e-7
+
+
 def test_shared_clock_stamp_times_match_c_oracle(oracle_lib):
     """utils.mean_field.stamp_times (host, no device sync) reproduces the interacting simulator's
     shared-clock tau rows bit for bit (C oracle of pdeinv_mf_step's tau0 + k dt)."""

@@ -19,6 +19,10 @@ sys.path.insert(0, os.path.join(ROOT, "pde-inverse-problem_amd"))
 import torch  # noqa: E402
 
 WORKLOADS = {
+    # scripts/run_OU.sh — the reference's default pde_instance (overdamped FP), MLP 32 x 2, T = 5
+    "FP-exact-MLP32x2": ["estimation_mode=non-parametric", "neural_network.hidden_dim=32", "neural_network.layers=2",
+                         "train.optimizer.learning_rate.initial=1e-2", "pde_instance.total_evolving_time=5",
+                         "train.optimizer.learning_rate.scheduling=cosine"],
     # solver defaults (ConsistencyBased.yaml): random_time exact samples, 50 000 per set
     "KOU-exact-parametric": ["pde_instance=kinetic_fokker_planck", "pde_instance.domain_dim=4",
                              "estimation_mode=parametric"],
