@@ -57,6 +57,8 @@ def parse():
     p.add_argument("--n-steps", type=int, default=100)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-recovery", action="store_true")
+    p.add_argument("--recovery-passes", type=int, default=128,
+                   help="ensembles per discretisation for the (untimed) drift recovery")
     p.add_argument("--cpu-particles", type=int, default=1 << 20)
     p.add_argument("--cpu-procs", type=int, default=16, help="CPU-baseline shard processes (the box's CPU share)")
     return p.parse_args()
@@ -161,9 +163,18 @@ def run_c2(a, rank, world, dev):
                       traffic_from_profiles("sde_simulate_C2_bytes_per_launch") if (N, n) == (1 << 21, 100) else None)
     out["loss"] = float(last_res[0][0][0].item())
     if not a.no_recovery:
-        S100, _ = recover_quadratic_drift(mom_total, gamma, T, d)
+        # untimed; a fixed Monte-Carlo budget (independent of --steps) of fresh moments-only passes,
+        # on top of the timed steps' moments, at n = 100 and n = 200
+        passes = max(a.recovery_passes, a.steps + a.warmup)
+        mom1 = mom_total.clone()
+        for _ in range(passes - (a.steps + a.warmup)):
+            r1 = native.sde_simulate(z0, n, T / n, gamma, pot, seed=seed, counter_offset=counter[0],
+                                     particle_offset=poff, traj=False, tau=False, last=False, moments=True)
+            counter[0] = (counter[0] + n + 1) & 0xFFFFFFFF
+            mom1 += dist.allreduce_sum(r1["moments"])
+        S100, _ = recover_quadratic_drift(mom1, gamma, T, d)
         mom2 = torch.zeros_like(mom_total)
-        for _ in range(a.steps + a.warmup):  # n = 200: moments only (no trajectory needed)
+        for _ in range(passes):  # n = 200: moments only (no trajectory needed)
             r2 = native.sde_simulate(z0, 2 * n, T / (2 * n), gamma, pot, seed=seed, counter_offset=counter[0],
                                      particle_offset=poff, traj=False, tau=False, last=False, moments=True)
             counter[0] = (counter[0] + 2 * n + 1) & 0xFFFFFFFF
@@ -174,7 +185,7 @@ def run_c2(a, rank, world, dev):
         out["drift_err_l2"] = float(np.linalg.norm(S_rich - F) / np.linalg.norm(F))
         out["drift_err_em_n100"] = float(np.abs(S100 - F).max())
         out["drift_recovery"] = ("max |S - tilde_F|, S = K + K^T the exact residual minimiser, Richardson "
-                                 f"2*S(n=200) - S(n=100), {(a.steps + a.warmup) * world * N} trajectories each")
+                                 f"2*S(n=200) - S(n=100), {passes * world * N} trajectories each")
     if rank == 0 and not a.no_cpu_baseline:
         from oracle import cpu_baseline as cb
         ups1, secs1 = cb.single(F, d, n, T, gamma, a.cpu_particles)
