@@ -30,8 +30,9 @@
  *   Gaussian sampler, sample r (global row), 4-normal block j:
  *       ctr = {lo32(r), hi32(r), counter_offset, 0x40000000 | j}
  *   u32 -> uniform:  u = (x >> 8) * 2^-24 in [0,1)
- *   u32 pair (a,b) -> 2 normals (Box–Muller): u1 = ((a>>8)+1)*2^-24 in (0,1],
- *       u2 = (b>>8)*2^-24, r = sqrt(-2 ln u1), (r cos 2πu2, r sin 2πu2)
+ *   u32 pair (a,b) -> 2 normals (Box–Muller): f(x) = as_float((x & 0x7FFFFF) | 0x3F800000)
+ *       in [1,2); u1 = 2 - f(a) in (0,1], u2 = f(b) - 1 in [0,1) (both exact in fp32),
+ *       r = sqrt(-2 ln u1), (r cos 2πu2, r sin 2πu2)
  *   Philox block j = (x0,x1,x2,x3) yields normals 4j..4j+3 from pairs (x0,x1),(x2,x3).
  */
 #ifndef PDEINV_H

@@ -50,12 +50,19 @@ void oracle_philox4x32_10(const uint32_t ctr_in[4], const uint32_t key_in[2],
 
 static inline float u32_to_unit(uint32_t x) { return (float)(x >> 8) * 0x1p-24f; }
 
-/* Box–Muller of one u32 pair; transcendental in double, rounded once. */
+/* Box–Muller of one u32 pair (include/pdeinv.h): the low 23 bits of each word are the mantissa
+ * of a float f in [1, 2); u1 = 2 - f1 in (0, 1] and the angle is f2 - 1 revolutions (both exact in
+ * fp32); transcendentals in double, rounded once. */
+static inline float unit_1_2(uint32_t x) {
+  union { uint32_t u; float f; } c;
+  c.u = (x & 0x007FFFFFu) | 0x3F800000u;
+  return c.f;
+}
 static inline void box_muller(uint32_t a, uint32_t b, float* z0, float* z1) {
-  float u1 = (float)((a >> 8) + 1u) * 0x1p-24f;
-  float u2 = (float)(b >> 8) * 0x1p-24f;
+  float u1 = 2.0f - unit_1_2(a);
+  float rev = unit_1_2(b) - 1.0f;
   double r = sqrt(-2.0 * log((double)u1));
-  double th = 2.0 * M_PI * (double)u2;
+  double th = 2.0 * M_PI * (double)rev;
   *z0 = (float)(r * cos(th));
   *z1 = (float)(r * sin(th));
 }

@@ -34,9 +34,10 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
     // one v_mad_u64_u32 per product (hi and lo together) instead of v_mul_hi + v_mul_lo
+    // and one v_bitop3_b32 (LUT 0x96 = a ^ b ^ c, gfx950) per three-way xor instead of two v_xor
     const uint64_t p0 = (uint64_t)kM0 * c.x, p1 = (uint64_t)kM1 * c.z;
-    c = make_uint4((uint32_t)(p1 >> 32) ^ c.y ^ k0, (uint32_t)p1, (uint32_t)(p0 >> 32) ^ c.w ^ k1,
-                   (uint32_t)p0);
+    c = make_uint4(__builtin_amdgcn_bitop3_b32((uint32_t)(p1 >> 32), c.y, k0, 0x96), (uint32_t)p1,
+                   __builtin_amdgcn_bitop3_b32((uint32_t)(p0 >> 32), c.w, k1, 0x96), (uint32_t)p0);
     k0 += kW0;
     k1 += kW1;
   }
@@ -46,13 +47,17 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1
 // u32 -> [0,1) with 24 random bits (exact in fp32; identical on host and device).
 __device__ __forceinline__ float u32_unit(uint32_t x) { return (float)(x >> 8) * 0x1p-24f; }
 
-// Box–Muller on the hardware transcendentals: v_log_f32 is log2, v_sin/v_cos take revolutions.
+// Box–Muller on the hardware transcendentals (v_log_f32 is log2, v_sin/v_cos take revolutions).
+// Each u32 becomes a float in [1, 2) with one v_and_or_b32 (the low 23 bits as the mantissa):
+// u1 = 2 - f1 in (0, 1] (exact), and the angle f2 in [1, 2) revolutions is the same angle as
+// f2 - 1 in [0, 1) — no shift / convert / scale per uniform.
+__device__ __forceinline__ float unit_1_2(uint32_t x) { return __uint_as_float((x & 0x007FFFFFu) | 0x3F800000u); }
 __device__ __forceinline__ void box_muller(uint32_t a, uint32_t b, float& z0, float& z1) {
-  const float u1 = (float)((a >> 8) + 1u) * 0x1p-24f;  // (0, 1]
-  const float u2 = (float)(b >> 8) * 0x1p-24f;         // [0, 1)
+  const float u1 = 2.0f - unit_1_2(a);  // (0, 1]
+  const float th = unit_1_2(b);         // [1, 2) revolutions
   const float r = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));
-  z0 = r * __builtin_amdgcn_cosf(u2);
-  z1 = r * __builtin_amdgcn_sinf(u2);
+  z0 = r * __builtin_amdgcn_cosf(th);
+  z1 = r * __builtin_amdgcn_sinf(th);
 }
 
 // ---- wave / block reductions ------------------------------------------------------------

@@ -55,17 +55,15 @@ __device__ __forceinline__ void gen_normals(const SdeArgs& a, uint32_t plo, uint
   }
 }
 
-// grad U(q) = A (q - c)   (KOU: A = tilde_F, …_OU.py:130-138)
+// grad U(q) = A (q - c) = A q - b, b = A c packed on the host (KOU: A = tilde_F, c = 0,
+// …_OU.py:130-138): the FMA chain starts at -b, so a centre costs no per-step instruction.
 template <int D>
 __device__ __forceinline__ void grad_quadratic(const SdeArgs& a, const float* q, float* g) {
-  float y[D];
-#pragma unroll
-  for (int k = 0; k < D; ++k) y[k] = q[k] - a.params[D * D + k];  // c = 0 (exact) without a centre
 #pragma unroll
   for (int r = 0; r < D; ++r) {
-    float acc = 0.f;
+    float acc = -a.params[D * D + r];
 #pragma unroll
-    for (int c = 0; c < D; ++c) acc = fmaf(a.params[r * D + c], y[c], acc);
+    for (int c = 0; c < D; ++c) acc = fmaf(a.params[r * D + c], q[c], acc);
     g[r] = acc;
   }
 }
@@ -510,7 +508,14 @@ static int build_args(const pdeinv_sde_desc* d, SdeArgs& a) {
   }
   if (n_params) {
     PDEINV_REQUIRE(p.params != nullptr, PDEINV_ERR_INVALID, "sde: potential params are null");
-    for (int k = 0; k < n_params; ++k) a.params[k] = p.params[k];
+    for (int k = 0; k < D * D; ++k) a.params[k] = p.params[k];
+    if (a.has_center) {  // b = A c in fp64, rounded once (grad_quadratic)
+      for (int r = 0; r < D; ++r) {
+        double b = 0;
+        for (int c = 0; c < D; ++c) b += (double)p.params[r * D + c] * (double)p.params[D * D + c];
+        a.params[D * D + r] = (float)b;
+      }
+    }
   }
   return PDEINV_OK;
 }

@@ -50,3 +50,19 @@ src = torch.empty(byt // 8, device=dev)
 dst = torch.empty(byt // 8, device=dev)
 ms = bench(lambda: dst.copy_(src))
 print(f"{'torch copy (R+W same bytes)':28s} {ms:7.3f} ms  {byt / ms / 1e6:8.1f} GB/s")
+
+# C3-shaped GMM simulator (d = 4, K = 8, 2^22 particles) and the d = 8 GMM of C5
+from example_problems.kinetic_fokker_planck_example_GMM import gmm_means  # noqa: E402
+from utils import prng  # noqa: E402
+
+for dg, Ng in [(4, 1 << 22), (8, 1 << 22)]:
+    mus = gmm_means(dg, 8, prng.PRNGKey(2))
+    potg = dict(kind=native.POT_GMM, params=mus, n_centers=8, sigma=1.0)
+    zg = torch.randn(Ng, 2 * dg, device=dev)
+    bufs = {"traj": torch.empty((n, Ng, 2 * dg), device=dev), "tau": torch.empty((n, Ng), device=dev),
+            "last": torch.empty((Ng, 2 * dg), device=dev)}
+    nbg = Ng * (8 * dg + n * (8 * dg + 4) + 8 * dg)
+    ms = bench(lambda: native.sde_simulate(zg, n, 0.02, 0.5, potg, seed=1, out=bufs))
+    print(f"{'GMM d=%d K=8 2^22' % dg:28s} {ms:7.3f} ms  {nbg / ms / 1e6:8.1f} GB/s")
+    del bufs, zg
+    torch.cuda.empty_cache()

@@ -28,6 +28,26 @@ __global__ __launch_bounds__(B) void sim_like(f4* traj, long N, int n) {
   }
 }
 
+// sim_like variants: DATA = 0 same data every step, LDS = 1 allocates (and touches) 8 KiB of LDS
+template <int DATA, int LDS>
+__global__ __launch_bounds__(256) void sim_like_v(f4* traj, long N, int n) {
+  __shared__ f4 stage[LDS ? 512 : 1];
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const long wave_row0 = i - lane;
+  f4* base = traj + wave_row0 * 2;
+  float v = (float)i;
+  if (LDS) stage[threadIdx.x] = f4{v, v, v, v};
+  for (int s = 0; s < n; ++s) {
+    f4* dst = base + (long)s * N * 2;
+    f4 a = f4{v, v + 1, v + 2, v + 3}, b = f4{v + 4, v + 5, v + 6, v + 7};
+    if (LDS) a += stage[(threadIdx.x + s) & 255];
+    __builtin_nontemporal_store(a, dst + lane);
+    __builtin_nontemporal_store(b, dst + 64 + lane);
+    if (DATA) v += 1.f;
+  }
+}
+
 // two particles per lane: the wave owns 128 consecutive rows, 4 KiB per step (4 stores)
 template <int B>
 __global__ __launch_bounds__(B) void sim_like2(f4* traj, long N, int n) {
@@ -85,9 +105,14 @@ int main() {
   const size_t bytes = (size_t)N * n * 32;
   f4* traj;
   if (hipMalloc(&traj, bytes) != hipSuccess) return 1;
+  printf("traj %p\n", (void*)traj);
   auto rep = [&](const char* name, float ms) { printf("%-34s %7.3f ms  %7.1f GB/s\n", name, ms, bytes / (ms / 1e3) / 1e9); };
   rep("sim_like B=256 nt", timeit([&] { sim_like<256, 0><<<N / 256, 256>>>(traj, N, n); }));
   rep("sim_like B=256 plain", timeit([&] { sim_like<256, 1><<<N / 256, 256>>>(traj, N, n); }));
+  rep("sim_like_v const data", timeit([&] { sim_like_v<0, 0><<<N / 256, 256>>>(traj, N, n); }));
+  rep("sim_like_v varying data + LDS", timeit([&] { sim_like_v<1, 1><<<N / 256, 256>>>(traj, N, n); }));
+  rep("sim_like_v const data + LDS", timeit([&] { sim_like_v<0, 1><<<N / 256, 256>>>(traj, N, n); }));
+  rep("sim_like B=256 nt (again)", timeit([&] { sim_like<256, 0><<<N / 256, 256>>>(traj, N, n); }));
   rep("sim_like B=512 nt", timeit([&] { sim_like<512, 0><<<N / 512, 512>>>(traj, N, n); }));
   rep("sim_like B=1024 nt", timeit([&] { sim_like<1024, 0><<<N / 1024, 1024>>>(traj, N, n); }));
   rep("sim_like B=1024 plain", timeit([&] { sim_like<1024, 1><<<N / 1024, 1024>>>(traj, N, n); }));
