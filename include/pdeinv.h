@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define PDEINV_ABI_VERSION 3
+#define PDEINV_ABI_VERSION 4
 #define PDEINV_MAX_DIM 16          /* d (configuration-space dimension) */
 #define PDEINV_MAX_PARAMS 256      /* floats of potential parameters passed by value */
 
@@ -315,6 +315,35 @@ int pdeinv_residual_kfp_mlp(const pdeinv_kfp_mlp_desc* desc, const float* d_init
                             void* d_workspace, double* d_acc, float* d_grad, void* stream);
 int pdeinv_kfp_terms_finalize(const double* d_acc, const float* d_grad, int64_t n_grad, float gamma,
                               float* d_out, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * KMV residual for a general interaction Phi_theta = V_hypothesis (the non-parametric model of
+ * core/model.py:109-131 under kinetic_mckean_vlasov.py:11-120): every pair (i, j) of the n_rows
+ * particles of each of the n_sets time stamps, y = x_i - x_j (x_minus_ref, :20-23). Two passes over
+ * pair rows built chunk by chunk (gbar_i = mean_j grad Phi, then the per-pair adjoint with seed
+ * 2 gbar_i / (n^2 n_sets)) on the library MLP path. d_z: rows [x | v] of stamp t at
+ * d_z + t*set_stride + i*ld; d_ds [n_sets][n_rows][2] = (ds log rho, ds2 log rho) from
+ * pdeinv_kmv_weights. d_acc [PDEINV_GMM_NACC] and d_grad are ACCUMULATED (+=, zero them first);
+ * pdeinv_kfp_terms_finalize(acc, grad, P, gamma = 1) gives the PDEINV_KFP_* slots (HESSIAN = the
+ * pair mean of v^T Hess Phi v, FRICTION = 2 x the weighted value mean, as pdeinv_residual_kmv).
+ * Multi-GPU: pairs are formed within each rank's particles (the reference's per-device batch under
+ * pmap, trainer.py:44-53); average the finalized outputs over ranks.
+ * --------------------------------------------------------------------------------------- */
+typedef struct {
+  int32_t dim;            /* d <= 8 */
+  int32_t n_layers;       /* hidden layers (neural_network.layers) */
+  int32_t width;          /* hidden width (neural_network.hidden_dim) */
+  int32_t out_features;   /* 40 in the reference */
+  int32_t n_sets;         /* time stamps */
+  int64_t n_rows;         /* particles per time stamp */
+  float gamma;            /* friction (weights c = ds2 + ds^2 + gamma ds) */
+  const float* tilde_F;   /* HOST [d*d]: Phi* = 0.5 y^T tilde_F y (…_quadratic.py:193-203) */
+  int64_t chunk_rows;     /* pair rows per GEMM chunk; 0 => 2^18 */
+} pdeinv_kmv_mlp_desc;
+size_t pdeinv_residual_kmv_mlp_workspace_bytes(const pdeinv_kmv_mlp_desc* desc);
+int pdeinv_residual_kmv_mlp(const pdeinv_kmv_mlp_desc* desc, const float* d_z, int64_t set_stride, int64_t ld,
+                            const float* d_ds, const float* d_params, void* d_workspace, double* d_acc,
+                            float* d_grad, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Overdamped Fokker–Planck (example_problems/fokker_planck_example.py,

@@ -623,9 +623,10 @@ def fp_mlp_grad_analytic(params, x_init, x_term, x_0T, T):
     return mlp_grad_rows(params, np.concatenate(rows), np.concatenate(coefs))
 
 
-def mlp_grad_rows(params, Z, C):
-    """Gradient of sum_r [c1 |g|^2 + c2 V'' + c3 V' + c0 V](row r) over rows Z = [x | v] with
-    per-row weights C = [c1, c2, c3, c0] (the adjoint of mlp.hip / mlp_fused.hip)."""
+def mlp_grad_rows(params, Z, C, U=None):
+    """Gradient of sum_r [c1 |g|^2 + c2 V'' + c3 V' + c0 V + u . g](row r) over rows Z = [x | v] with
+    per-row weights C = [c1, c2, c3, c0] and optional per-row input-gradient seeds U (the adjoint
+    of mlp.hip / mlp_fused.hip; U is the KMV pass-2 seed of kmv_mlp_grad_analytic)."""
     d = params[0][0].shape[0]
     L = len(params) - 1
     c1, c2, c3, c0 = C[:, :1], C[:, 1:2], C[:, 2:3], C[:, 3:4]
@@ -658,7 +659,7 @@ def mlp_grad_rows(params, Z, C):
     # forward-mode adjoint of the grad chain
     abar = [None] * (L + 1)
     zetabar = [None] * (L + 1)
-    abar[0] = 2 * c1 * g
+    abar[0] = 2 * c1 * g + (0.0 if U is None else U)
     for l in range(1, L + 1):
         zetabar[l] = abar[l - 1] @ params[l - 1][0]
         abar[l] = S[l - 1][0] * zetabar[l]
@@ -682,6 +683,62 @@ def mlp_grad_rows(params, Z, C):
         grads[l - 1] = (gK, zb.sum(0))
         hb, hdb, hddb = zb @ K.T, zdb @ K.T, zddb @ K.T
     return grads
+
+
+# --------------------------------------------------------------------------------------
+# KMV residual for a general (MLP) interaction Phi_theta = V_hypothesis
+# (methods/consistency_instances/kinetic_mckean_vlasov.py:11-120 with get_model non-parametric)
+# --------------------------------------------------------------------------------------
+def kmv_value_weights(x, tau, cfg):
+    """c[i, t] = ds2 + ds^2 + gamma ds of log rho at (tau_t, x_it) (:62-90 of the residual)."""
+    gamma = cfg["gamma_friction"]
+    ps = np.stack([partial_s_log_density(t, x[:, k], cfg) for k, t in enumerate(tau)], 1)
+    ps2 = np.stack([partial_s2_log_density(t, x[:, k], cfg) for k, t in enumerate(tau)], 1)
+    return ps2 + ps ** 2 + gamma * ps
+
+
+def kmv_mlp_pairwise_loss(params, x, v, tau, cfg, weights=None):
+    """Literal restatement with the [m, n, n_time, d] pair tensor x_minus_ref[a, b] = x_b - x_a
+    (:20-23; the particle is b, the reference a), Phi_theta = V_hypothesis, Phi* = 0.5 y^T F y:
+    loss (:74-97) and loss ground truth (:99-110). x, v: [n, n_time, d]; tau [n_time]."""
+    x = np.asarray(x, np.float64); v = np.asarray(v, np.float64)
+    n, nt, d = x.shape
+    F = cfg["tilde_F"]
+    y = x[None] - x[:, None]                                    # [m, n, T, d]
+    vv = np.broadcast_to(v[None], y.shape)                      # v_b
+    Phi, g, _, Hvv = mlp_forward_terms(params, y.reshape(-1, d), vv.reshape(-1, d))
+    Phi, Hvv = Phi.reshape(n, n, nt), Hvv.reshape(n, n, nt)
+    g = g.reshape(n, n, nt, d)
+    gbar = g.mean(0)                                            # [n, T, d]
+    gtrue = (y @ F.T).mean(0)
+    c = kmv_value_weights(x, tau, cfg) if weights is None else weights
+    loss_nabla = np.mean(np.sum(gbar ** 2, -1))
+    loss_hess = np.mean(Hvv.mean(0))
+    loss_value = np.mean(Phi.mean(0) * c)
+    loss_true = np.mean(np.sum(gtrue ** 2, -1))
+    loss = loss_nabla - 2 * loss_hess + 2 * loss_value + loss_true
+    loss_gt = np.mean(np.sum((gtrue - gbar) ** 2, -1))
+    return loss, loss_gt, dict(nabla=loss_nabla, hessian=loss_hess, value=loss_value, nabla_true=loss_true)
+
+
+def kmv_mlp_grad_analytic(params, x, v, tau, cfg, weights=None):
+    """d loss / d theta of kmv_mlp_pairwise_loss in the two passes the HIP path runs:
+    pass 1 gbar_i = mean_j grad Phi(x_i - x_j); pass 2 over the pair rows [x_i - x_j | v_i] with
+    c2 = -2/(n^2 T), c0 = 2 c_it/(n^2 T) per row and the input-gradient seed u_i = 2 gbar_i/(n^2 T)
+    (the |mean_j grad Phi|^2 term is quadratic in the mean, so its adjoint is linear per pair)."""
+    x = np.asarray(x, np.float64); v = np.asarray(v, np.float64)
+    n, nt, d = x.shape
+    y = (x[None] - x[:, None])                                  # [j, i, T, d]
+    _, g, _, _ = mlp_forward_terms(params, y.reshape(-1, d), np.zeros((y.size // d, d)))
+    gbar = g.reshape(n, n, nt, d).mean(0)                       # [i, T, d]
+    c = kmv_value_weights(x, tau, cfg) if weights is None else weights
+    s = 1.0 / (n * n * nt)
+    rows = np.concatenate([y.reshape(-1, d), np.broadcast_to(v[None], y.shape).reshape(-1, d)], 1)
+    C = np.zeros((rows.shape[0], 4))
+    C[:, 1] = -2 * s
+    C[:, 3] = (2 * s * np.broadcast_to(c[None], (n, n, nt))).reshape(-1)
+    U = (2 * s * np.broadcast_to(gbar[None], y.shape)).reshape(-1, d)
+    return mlp_grad_rows(params, rows, C, U)
 
 
 # --------------------------------------------------------------------------------------

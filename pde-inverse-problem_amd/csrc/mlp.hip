@@ -222,6 +222,8 @@ __global__ void mlp_gadj(const float* __restrict__ zetabar, const float* __restr
 
 struct MlpLossArgs {
   int d, set, true_kind, KT, bval;
+  int uw;  // rows carry [x | v | u | w]: input-gradient seed u (added to abar_0) and value weight w
+           // (KMV pair rows, set 3: pdeinv_residual_kmv_mlp)
   float c1, c2, c3, c0, c_true, inv_n;
   float s2t, l2st;
   float tp[PDEINV_MAX_PARAMS];  // tilde_F [d*d] or true GMM centres [K*d]
@@ -244,12 +246,16 @@ __global__ __launch_bounds__(kBlock) void mlp_loss(MlpLossArgs a, const float* _
       g[i] = G[r * D + i];
       x[i] = X[r * ldx + i];
       T1 = fmaf(g[i], g[i], T1);
-      abar0[r * D + i] = 2.f * a.c1 * g[i];
+      abar0[r * D + i] = 2.f * a.c1 * g[i] + (a.uw ? X[r * ldx + 2 * D + i] : 0.f);
     }
     const float4 t = terms[r];
     const float T2 = t.y, T3 = t.x, T0 = t.z;
-    acc[PDEINV_GMM_ACC_LOSS] += a.c1 * T1 + a.c2 * T2 + a.c3 * T3 + a.c0 * T0;
-    if (a.set == 0) {
+    const float wr = a.uw ? X[r * ldx + 3 * D] : 1.f;
+    acc[PDEINV_GMM_ACC_LOSS] += a.c1 * T1 + a.c2 * T2 + a.c3 * T3 + a.c0 * wr * T0;
+    if (a.set == 3) {  // KMV pair rows: -2 x Hessian mean and 2 x value mean (scaled by c2, c0)
+      acc[PDEINV_GMM_ACC_HESSIAN] += -0.5f * a.c2 * T2;
+      acc[PDEINV_GMM_ACC_FRICTION] += a.c0 * wr * T0;
+    } else if (a.set == 0) {
       float gt[D];
       if (a.true_kind == PDEINV_POT_QUADRATIC) {
 #pragma unroll
@@ -314,12 +320,14 @@ __global__ __launch_bounds__(kBlock) void mlp_loss(MlpLossArgs a, const float* _
 
 // seeds of the reverse sweep over the forward streams (c0: weight of the value V = y.y):
 //   ybar = 2 c3 y' + 2 c2 y'' + 2 ubar + 2 c0 y,  y'bar = 2 c3 y + 4 c2 y',  y''bar = 2 c2 y
+// (rw: optional per-row weight of the value term, rw[r * ldw] for element e = r * O + o)
 __global__ void mlp_seeds(const float* __restrict__ Y, const float* __restrict__ UB, float* __restrict__ YB,
-                          float c2, float c3, float c0, int64_t S) {
+                          float c2, float c3, float c0, int64_t S, const float* __restrict__ rw, int64_t ldw, int O) {
   const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (e >= S) return;
   const float y = Y[e], yd = Y[S + e], ydd = Y[2 * S + e];
-  YB[e] = 2.f * c3 * yd + 2.f * c2 * ydd + 2.f * UB[e] + 2.f * c0 * y;
+  const float cv = rw ? c0 * rw[(e / O) * ldw] : c0;
+  YB[e] = 2.f * c3 * yd + 2.f * c2 * ydd + 2.f * UB[e] + 2.f * cv * y;
   YB[S + e] = 2.f * c3 * y + 4.f * c2 * yd;
   YB[2 * S + e] = 2.f * c2 * y;
 }
@@ -463,6 +471,117 @@ static int fused_loss_hook(void* p, const float* G, const float4* terms, float* 
 }
 }  // namespace pdeinv
 
+namespace pdeinv {
+// parameter offsets (flax order: K_1, b_1, ..., K_L, b_L, K_o, b_o)
+static void param_offsets(int D, int W, int O, int L, int64_t* poff, int64_t* boff) {
+  int64_t o = 0;
+  for (int l = 0; l <= L; ++l) {
+    const int n_in = (l == 0) ? D : W, n_out = (l == L) ? O : W;
+    poff[l] = o; o += (int64_t)n_in * n_out;
+    boff[l] = o; o += n_out;
+  }
+}
+
+// One chunk of R rows through the library path: F1 Taylor forward, R1 grad_x chain, the loss
+// terms (mlp_loss, accumulated into acc), F2 forward adjoint, R2 + weight gradients (accumulated
+// into grad). grad_only stops after R1 and leaves g = grad_x V of every row in G (KMV pass 1).
+struct LibRun {
+  MlpPlan p;
+  Blas* blas;
+  float* w;
+  const float* params;
+  float* grad;
+  const int64_t* poff;
+  const int64_t* boff;
+  hipStream_t st;
+  double* acc;
+  int64_t R = 0;
+  float* layer(int l, int plane) const {
+    return w + p.off_layer0 + p.layer_stride * (l - 1) + (size_t)plane * R * p.W;
+  }
+  float* G() const { return w + p.off_G; }
+  int chunk(const float* zr, int64_t ld, int64_t rows, const MlpLossArgs& la, bool grad_only) {
+    R = rows;
+    const int D = p.d, W = p.W, O = p.O, L = p.L;
+    float* A0 = w + p.off_A0;
+    float* Y = w + p.off_Y;
+    float* YB = w + p.off_YB;
+    float* UB = w + p.off_UB;
+    float* Gp = G();
+    float4* terms = (float4*)(w + p.off_terms);
+    float* part = w + p.off_part;
+    Blas& b = *blas;
+    // planes per hidden layer l: A 0-3, Z 4-6, ZB 7-10, HB 11-13, aL 14, zb 15. Inside a chunk of R
+    // rows the planes are packed at stride R*W so that consecutive streams form one [k*R x W] operand.
+    const int64_t SD = R * D, SW = R * W, SO = R * O;
+    // ---- F1: Taylor-mode forward --------------------------------------------------------
+    hipLaunchKernelGGL(mlp_load_rows, dim3(grid_for(SD)), dim3(kBlock), 0, st, zr, ld, D, A0, R);
+    if (hipMemsetAsync(A0 + 2 * SD, 0, sizeof(float) * SD, st) != hipSuccess) return fail(PDEINV_ERR_HIP, "memset");
+    for (int l = 1; l <= L; ++l) {
+      const int n_in = (l == 1) ? D : W;
+      const float* Ain = (l == 1) ? A0 : layer(l - 1, 0);
+      float* Z = layer(l, 4);
+      b.fwd(Ain, params + poff[l - 1], Z, 3 * R, n_in, W);  // three streams: one GEMM with 3R rows
+      hipLaunchKernelGGL(mlp_act_fwd, dim3(grid_for(SW)), dim3(kBlock), 0, st, Z, layer(l, 0), params + boff[l - 1],
+                         R, W);
+    }
+    b.fwd(layer(L, 0), params + poff[L], Y, 3 * R, W, O);
+    {
+      const int rb = O >= 2048 ? 1 : 2048 / O;  // 24 KB of LDS products per block
+      hipLaunchKernelGGL(mlp_out, dim3((unsigned)((R + rb - 1) / rb)), dim3(kBlock), 3 * rb * O * sizeof(float), st,
+                         Y, params + boff[L], YB, terms, R, O, rb);
+    }
+    // ---- R1: grad_x chain ---------------------------------------------------------------
+    b.bwd(YB + 3 * SO, params + poff[L], layer(L, 14), R, W, O);  // a_L = u K_o^T
+    for (int l = L; l >= 1; --l) {
+      hipLaunchKernelGGL(mlp_gchain, dim3(grid_for(SW)), dim3(kBlock), 0, st, layer(l, 14), layer(l, 0),
+                         layer(l, 10), SW);  // zeta_l -> ZB plane 3
+      if (l > 1) b.bwd(layer(l, 10), params + poff[l - 1], layer(l - 1, 14), R, W, W);
+      else b.bwd(layer(1, 10), params + poff[0], Gp, R, D, W);  // g = zeta_1 K_1^T
+    }
+    if (grad_only) {
+      if (b.status) return fail(PDEINV_ERR_HIP, "mlp: rocBLAS call failed");
+      return check_launch("mlp grad_x kernels");
+    }
+    // ---- loss terms, seed abar_0 = 2 c1 g (+ u) ------------------------------------------
+    const int lg = grid_for(R) < kLossGrid ? grid_for(R) : kLossGrid;
+    switch (D) {
+#define CASE(DD) case DD: hipLaunchKernelGGL(mlp_loss<DD>, dim3(lg), dim3(kBlock), 0, st, la, Gp, zr, ld, terms, A0 + 3 * SD, R, part); break;
+      CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) CASE(10) CASE(12) CASE(16)
+#undef CASE
+      default:
+        return fail(PDEINV_ERR_UNSUPPORTED, "mlp: dim must be one of 1-8, 10, 12, 16");
+    }
+    hipLaunchKernelGGL(slab_reduce_accum_kernel, dim3(PDEINV_GMM_NACC), dim3(kBlock), 0, st, part, lg, acc);
+    // ---- F2: forward-mode adjoint of the grad_x chain --------------------------------------
+    for (int l = 1; l <= L; ++l) {
+      const float* abar_prev = (l == 1) ? A0 + 3 * SD : layer(l - 1, 3);
+      b.fwd(abar_prev, params + poff[l - 1], layer(l, 15), R, (l == 1) ? D : W, W);  // zetabar_l
+      hipLaunchKernelGGL(mlp_gadj, dim3(grid_for(SW)), dim3(kBlock), 0, st, layer(l, 15), layer(l, 0),
+                         layer(l, 3), SW);  // abar_l -> A plane 3
+    }
+    b.fwd(layer(L, 3), params + poff[L], UB, R, W, O);  // ubar = abar_L K_o
+    hipLaunchKernelGGL(mlp_seeds, dim3(grid_for(SO)), dim3(kBlock), 0, st, Y, UB, YB, la.c2, la.c3, la.c0, SO,
+                       la.uw ? zr + 3 * D : nullptr, ld, O);
+    // ---- R2 + G: reverse over the three forward streams, weight gradients ---------------------
+    b.wgrad(layer(L, 0), YB, grad + poff[L], 4 * R, W, O);  // K_o += [h;h';h'';abar]^T [ybar;..;u]
+    b.colsum(YB, grad + boff[L], R, O);
+    b.bwd(YB, params + poff[L], layer(L, 11), 3 * R, W, O);  // hbar streams of layer L
+    for (int l = L; l >= 1; --l) {
+      hipLaunchKernelGGL(mlp_act_bwd, dim3(grid_for(SW)), dim3(kBlock), 0, st, layer(l, 11), layer(l, 0),
+                         layer(l, 4), layer(l, 14), layer(l, 15), layer(l, 7), SW);
+      const int n_in = (l == 1) ? D : W;
+      const float* Ain = (l == 1) ? A0 : layer(l - 1, 0);
+      b.wgrad(Ain, layer(l, 7), grad + poff[l - 1], 4 * R, n_in, W);
+      b.colsum(layer(l, 7), grad + boff[l - 1], R, W);
+      if (l > 1) b.bwd(layer(l, 7), params + poff[l - 1], layer(l - 1, 11), 3 * R, W, W);
+    }
+    if (b.status) return fail(PDEINV_ERR_HIP, "mlp: rocBLAS call failed");
+    return check_launch("mlp kernels");
+  }
+};
+}  // namespace pdeinv
+
 extern "C" int64_t pdeinv_mlp_param_count(int32_t dim, int32_t n_layers, int32_t width, int32_t out_features) {
   int64_t n = (int64_t)dim * width + width;
   for (int l = 1; l < n_layers; ++l) n += (int64_t)width * width + width;
@@ -495,25 +614,8 @@ extern "C" int pdeinv_residual_kfp_mlp(const pdeinv_kfp_mlp_desc* d, const float
   float* w = (float*)ws;
   const int W = p.W, O = p.O, L = p.L;
   PDEINV_REQUIRE(L <= 16, PDEINV_ERR_UNSUPPORTED, "kfp_mlp: at most 16 hidden layers");
-  // parameter offsets (flax order: K_1, b_1, ..., K_L, b_L, K_o, b_o)
   int64_t poff[18], boff[18];
-  int64_t o = 0;
-  for (int l = 0; l <= L; ++l) {
-    const int n_in = (l == 0) ? D : W, n_out = (l == L) ? O : W;
-    poff[l] = o; o += (int64_t)n_in * n_out;
-    boff[l] = o; o += n_out;
-  }
-  float* A0 = w + p.off_A0;
-  float* Y = w + p.off_Y;
-  float* YB = w + p.off_YB;
-  float* UB = w + p.off_UB;
-  float* G = w + p.off_G;
-  float4* terms = (float4*)(w + p.off_terms);
-  float* part = w + p.off_part;
-  // planes per hidden layer l: A 0-3, Z 4-6, ZB 7-10, HB 11-13, aL 14, zb 15. Inside a chunk of R rows
-  // the planes are packed at stride R*W so that consecutive streams form one [k*R x W] GEMM operand.
-  int64_t R = 0;
-  auto layer = [&](int l, int plane) { return w + p.off_layer0 + p.layer_stride * (l - 1) + (size_t)plane * R * W; };
+  param_offsets(D, W, O, L, poff, boff);
 
   MlpLossArgs la{};
   la.d = D;
@@ -565,79 +667,259 @@ extern "C" int pdeinv_residual_kfp_mlp(const pdeinv_kfp_mlp_desc* d, const float
   Blas blas{blas_handle(dev), st, w + p.off_kpart};
   if (!blas.h) return fail(PDEINV_ERR_HIP, "kfp_mlp: rocblas_create_handle failed");
   if (rocblas_set_stream(blas.h, st) != rocblas_status_success) return fail(PDEINV_ERR_HIP, "kfp_mlp: rocblas_set_stream");
+  LibRun run{p, &blas, w, params, grad, poff, boff, st, acc};
   for (const Set& s : sets) {
     PDEINV_REQUIRE(s.n == 0 || s.ld >= 2 * D, PDEINV_ERR_INVALID, "kfp_mlp: row stride < 2*dim");
+    la.set = s.id; la.c1 = s.c1; la.c2 = s.c2; la.c3 = s.c3; la.c0 = s.c0; la.c_true = d->c_true;
+    la.inv_n = s.n ? 1.f / (float)s.n : 0.f;
     for (int64_t r0 = 0; r0 < s.n; r0 += p.Bc) {
-      R = (s.n - r0) < p.Bc ? (s.n - r0) : p.Bc;
-      const float* zr = s.z + r0 * s.ld;
-      const int64_t SD = R * D, SW = R * W, SO = R * O;
-      // ---- F1: Taylor-mode forward --------------------------------------------------------
-      hipLaunchKernelGGL(mlp_load_rows, dim3(grid_for(SD)), dim3(kBlock), 0, st, zr, s.ld, D, A0, R);
-      if (hipMemsetAsync(A0 + 2 * SD, 0, sizeof(float) * SD, st) != hipSuccess) return fail(PDEINV_ERR_HIP, "memset");
-      // A planes are [4][R][n] within a chunk buffer sized for Bc rows: streams packed at stride R*n
-      for (int l = 1; l <= L; ++l) {
-        const int n_in = (l == 1) ? D : W;
-        const float* Ain = (l == 1) ? A0 : layer(l - 1, 0);
-        float* Z = layer(l, 4);
-        // three streams packed contiguously: one GEMM with 3R rows
-        blas.fwd(Ain, params + poff[l - 1], Z, 3 * R, n_in, W);
-        hipLaunchKernelGGL(mlp_act_fwd, dim3(grid_for(SW)), dim3(kBlock), 0, st, Z, layer(l, 0), params + boff[l - 1],
-                           R, W);
-      }
-      blas.fwd(layer(L, 0), params + poff[L], Y, 3 * R, W, O);
-      {
-        const int rb = O >= 2048 ? 1 : 2048 / O;  // 24 KB of LDS products per block
-        hipLaunchKernelGGL(mlp_out, dim3((unsigned)((R + rb - 1) / rb)), dim3(kBlock), 3 * rb * O * sizeof(float), st,
-                           Y, params + boff[L], YB, terms, R, O, rb);
-      }
-      // ---- R1: grad_x chain ---------------------------------------------------------------
-      blas.bwd(YB + 3 * SO, params + poff[L], layer(L, 14), R, W, O);  // a_L = u K_o^T
-      for (int l = L; l >= 1; --l) {
-        hipLaunchKernelGGL(mlp_gchain, dim3(grid_for(SW)), dim3(kBlock), 0, st, layer(l, 14), layer(l, 0),
-                           layer(l, 10), SW);  // zeta_l -> ZB plane 3
-        if (l > 1) blas.bwd(layer(l, 10), params + poff[l - 1], layer(l - 1, 14), R, W, W);
-        else blas.bwd(layer(1, 10), params + poff[0], G, R, D, W);  // g = zeta_1 K_1^T
-      }
-      // ---- loss terms, seed abar_0 = 2 c1 g ------------------------------------------------
-      la.set = s.id; la.c1 = s.c1; la.c2 = s.c2; la.c3 = s.c3; la.c0 = s.c0; la.c_true = d->c_true;
-      la.inv_n = 1.f / (float)s.n;
-      const int lg = grid_for(R) < kLossGrid ? grid_for(R) : kLossGrid;
-      switch (D) {
-#define CASE(DD) case DD: hipLaunchKernelGGL(mlp_loss<DD>, dim3(lg), dim3(kBlock), 0, st, la, G, zr, s.ld, terms, A0 + 3 * SD, R, part); break;
-        CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) CASE(10) CASE(12) CASE(16)
-#undef CASE
-        default:
-          return fail(PDEINV_ERR_UNSUPPORTED, "kfp_mlp: dim must be one of 1-8, 10, 12, 16");
-      }
-      hipLaunchKernelGGL(slab_reduce_accum_kernel, dim3(PDEINV_GMM_NACC), dim3(kBlock), 0, st, part, lg, acc);
-      // ---- F2: forward-mode adjoint of the grad_x chain --------------------------------------
-      for (int l = 1; l <= L; ++l) {
-        const float* abar_prev = (l == 1) ? A0 + 3 * SD : layer(l - 1, 3);
-        blas.fwd(abar_prev, params + poff[l - 1], layer(l, 15), R, (l == 1) ? D : W, W);  // zetabar_l
-        hipLaunchKernelGGL(mlp_gadj, dim3(grid_for(SW)), dim3(kBlock), 0, st, layer(l, 15), layer(l, 0),
-                           layer(l, 3), SW);  // abar_l -> A plane 3
-      }
-      blas.fwd(layer(L, 3), params + poff[L], UB, R, W, O);  // ubar = abar_L K_o
-      hipLaunchKernelGGL(mlp_seeds, dim3(grid_for(SO)), dim3(kBlock), 0, st, Y, UB, YB, s.c2, s.c3, s.c0, SO);
-      // ---- R2 + G: reverse over the three forward streams, weight gradients ---------------------
-      blas.wgrad(layer(L, 0), YB, grad + poff[L], 4 * R, W, O);  // K_o += [h;h';h'';abar]^T [ybar;..;u]
-      blas.colsum(YB, grad + boff[L], R, O);
-      blas.bwd(YB, params + poff[L], layer(L, 11), 3 * R, W, O);  // hbar streams of layer L
-      for (int l = L; l >= 1; --l) {
-        hipLaunchKernelGGL(mlp_act_bwd, dim3(grid_for(SW)), dim3(kBlock), 0, st, layer(l, 11), layer(l, 0),
-                           layer(l, 4), layer(l, 14), layer(l, 15), layer(l, 7), SW);
-        const int n_in = (l == 1) ? D : W;
-        const float* Ain = (l == 1) ? A0 : layer(l - 1, 0);
-        blas.wgrad(Ain, layer(l, 7), grad + poff[l - 1], 4 * R, n_in, W);
-        blas.colsum(layer(l, 7), grad + boff[l - 1], R, W);
-        if (l > 1) blas.bwd(layer(l, 7), params + poff[l - 1], layer(l - 1, 11), 3 * R, W, W);
-      }
-      if (blas.status) return fail(PDEINV_ERR_HIP, "kfp_mlp: rocBLAS call failed");
-      int rc = check_launch("kfp_mlp kernels");
+      const int64_t R = (s.n - r0) < p.Bc ? (s.n - r0) : p.Bc;
+      const int rc = run.chunk(s.z + r0 * s.ld, s.ld, R, la, false);
       if (rc) return rc;
     }
   }
   return PDEINV_OK;
+}
+
+// ---- KMV residual for a general (MLP) interaction Phi_theta = V_hypothesis ----------------------
+// (methods/consistency_instances/kinetic_mckean_vlasov.py:11-120 under get_model non-parametric.)
+// Per time stamp t the reference forms every pair (i, j) of its particles, y = x_i - x_j
+// (x_minus_ref, :20-23), and needs  gbar_i = mean_j grad Phi(y_ij),  mean_j v_i^T Hess Phi(y_ij) v_i
+// and  mean_j Phi(y_ij)  weighted by c_it = ds2 + ds^2 + gamma ds of log rho. The loss is quadratic
+// in gbar, so its parameter adjoint is per pair once gbar is known — two passes over pair rows
+// [y_ij | v_i | u_i | w_it] (built chunk by chunk, never the whole n^2 tensor):
+//   pass 1  grad_x V of the pair rows (F1 + R1 of the library path), mean over j -> gbar (fp32 ws);
+//           |gbar|^2, |gbar*|^2, |gbar* - gbar|^2 with gbar* = tilde_F (x_i - xbar_t) (Phi* quadratic);
+//   pass 2  the full library path with c2 = -2 s, c0 = 2 s w_it and the input-gradient seed
+//           u_i = 2 s gbar_i, s = 1 / (n^2 n_time)  (oracle/numpy_ref.py kmv_mlp_grad_analytic).
+template <int D>
+__global__ void kmv_pair_rows_kernel(const float* __restrict__ z, int64_t set_stride, int64_t ld, int64_t t,
+                                     int64_t i0, int64_t ni, int64_t j0, int64_t nj, int64_t n_rows,
+                                     const float* __restrict__ gbar, const float* __restrict__ ds, float gamma,
+                                     float u_scale, float* __restrict__ rows) {
+  const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (r >= ni * nj) return;
+  const int64_t il = r / nj, i = i0 + il, j = j0 + (r - il * nj);
+  const float* zi = z + t * set_stride + i * ld;
+  const float* zj = z + t * set_stride + j * ld;
+  float* o = rows + r * (3 * D + 1);
+  const int64_t p = t * n_rows + i;
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    o[k] = zi[k] - zj[k];
+    o[D + k] = zi[D + k];
+    o[2 * D + k] = gbar ? u_scale * gbar[p * D + k] : 0.f;
+  }
+  float wv = 0.f;
+  if (ds) {
+    const float a = ds[2 * p], b2 = ds[2 * p + 1];
+    wv = b2 + a * a + gamma * a;  // ds2 + ds^2 + gamma ds (kinetic_mckean_vlasov.py:84-89)
+  }
+  o[3 * D] = wv;
+}
+
+// gbar[t][i0 + il] += inv_n * sum_jl G[il * nj + jl] (one block per il; fixed-order LDS tree)
+template <int D>
+__global__ __launch_bounds__(kBlock) void kmv_group_mean_kernel(const float* __restrict__ G, int64_t nj, float inv_n,
+                                                                float* __restrict__ gbar_rows) {
+  const int64_t il = blockIdx.x;
+  float s[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) s[k] = 0.f;
+  for (int64_t jl = threadIdx.x; jl < nj; jl += kBlock) {
+#pragma unroll
+    for (int k = 0; k < D; ++k) s[k] += G[(il * nj + jl) * D + k];
+  }
+  __shared__ float red[kBlock];
+  for (int k = 0; k < D; ++k) {
+    red[threadIdx.x] = s[k];
+    __syncthreads();
+    for (int h = kBlock / 2; h > 0; h >>= 1) {
+      if (threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) gbar_rows[il * D + k] += inv_n * red[0];
+    __syncthreads();
+  }
+}
+
+struct KmvTrueArgs {
+  float F[PDEINV_MAX_DIM * PDEINV_MAX_DIM];
+};
+
+// per time stamp t (one block): xbar_t, then sum_i |gbar|^2, |gbar*|^2, |gbar* - gbar|^2 -> part[t][3]
+template <int D>
+__global__ __launch_bounds__(kBlock) void kmv_stamp_terms_kernel(KmvTrueArgs a, const float* __restrict__ z,
+                                                                int64_t set_stride, int64_t ld, int64_t n_rows,
+                                                                const float* __restrict__ gbar,
+                                                                double* __restrict__ part) {
+  const int64_t t = blockIdx.x;
+  const float* zt = z + t * set_stride;
+  __shared__ double red[kBlock];
+  __shared__ float xbar[D];
+  for (int k = 0; k < D; ++k) {
+    double sk = 0.0;
+    for (int64_t i = threadIdx.x; i < n_rows; i += kBlock) sk += (double)zt[i * ld + k];
+    red[threadIdx.x] = sk;
+    __syncthreads();
+    for (int h = kBlock / 2; h > 0; h >>= 1) {
+      if (threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) xbar[k] = (float)(red[0] / (double)n_rows);
+    __syncthreads();
+  }
+  double acc[3] = {0.0, 0.0, 0.0};
+  for (int64_t i = threadIdx.x; i < n_rows; i += kBlock) {
+    float y[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) y[k] = zt[i * ld + k] - xbar[k];
+    const float* g = gbar + (t * n_rows + i) * D;
+    float n1 = 0.f, n2 = 0.f, n3 = 0.f;
+#pragma unroll
+    for (int r = 0; r < D; ++r) {
+      float gt = 0.f;
+#pragma unroll
+      for (int c = 0; c < D; ++c) gt = fmaf(a.F[r * D + c], y[c], gt);
+      n1 = fmaf(g[r], g[r], n1);
+      n2 = fmaf(gt, gt, n2);
+      n3 = fmaf(gt - g[r], gt - g[r], n3);
+    }
+    acc[0] += n1; acc[1] += n2; acc[2] += n3;
+  }
+  for (int c = 0; c < 3; ++c) {
+    red[threadIdx.x] = acc[c];
+    __syncthreads();
+    for (int h = kBlock / 2; h > 0; h >>= 1) {
+      if (threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) part[t * 3 + c] = red[0];
+    __syncthreads();
+  }
+}
+
+// fixed-order combine of the per-stamp sums into the PDEINV_GMM_ACC_* slots (+=)
+__global__ void kmv_stamp_combine_kernel(const double* __restrict__ part, int64_t n_sets, double inv,
+                                         double* __restrict__ acc) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  double n1 = 0.0, n2 = 0.0, n3 = 0.0;
+  for (int64_t t = 0; t < n_sets; ++t) {
+    n1 += part[t * 3];
+    n2 += part[t * 3 + 1];
+    n3 += part[t * 3 + 2];
+  }
+  acc[PDEINV_GMM_ACC_LOSS] += (n1 + n2) * inv;
+  acc[PDEINV_GMM_ACC_LOSS_GT] += n3 * inv;
+  acc[PDEINV_GMM_ACC_NABLA] += n1 * inv;
+  acc[PDEINV_GMM_ACC_NABLA_TRUE] += n2 * inv;
+}
+
+namespace {
+struct KmvPlan {
+  MlpPlan lib;
+  int64_t ni, nj;           // pair-row block: ni particles x nj references
+  size_t off_rows, off_gbar, off_part, total;  // floats past the library plan (part: doubles)
+};
+
+KmvPlan kmv_plan(const pdeinv_kmv_mlp_desc* d) {
+  pdeinv_kfp_mlp_desc m{};
+  m.dim = d->dim; m.n_layers = d->n_layers; m.width = d->width; m.out_features = d->out_features;
+  m.chunk_rows = d->chunk_rows > 0 ? d->chunk_rows : (1 << 18);
+  KmvPlan k{};
+  k.lib = make_plan(&m);
+  const int64_t Bc = k.lib.Bc, n = d->n_rows;
+  k.nj = n <= Bc ? n : Bc;
+  k.ni = n <= Bc ? (Bc / n < n ? Bc / n : n) : 1;
+  size_t o = k.lib.total / sizeof(float);
+  auto take = [&](size_t floats) { const size_t at = o; o += (floats + 63) & ~(size_t)63; return at; };
+  k.off_rows = take((size_t)Bc * (3 * d->dim + 1));
+  k.off_gbar = take((size_t)d->n_sets * n * d->dim);
+  k.off_part = take((size_t)d->n_sets * 3 * 2);
+  k.total = o * sizeof(float);
+  return k;
+}
+}  // namespace
+
+template <int D>
+static int kmv_mlp_run(const pdeinv_kmv_mlp_desc* d, const KmvPlan& k, const float* z, int64_t set_stride,
+                       int64_t ld, const float* ds, const float* params, float* w, double* acc, float* grad,
+                       hipStream_t st) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return fail(PDEINV_ERR_HIP, "kmv_mlp: hipGetDevice failed");
+  Blas blas{blas_handle(dev), st, w + k.lib.off_kpart};
+  if (!blas.h) return fail(PDEINV_ERR_HIP, "kmv_mlp: rocblas_create_handle failed");
+  if (rocblas_set_stream(blas.h, st) != rocblas_status_success) return fail(PDEINV_ERR_HIP, "kmv_mlp: rocblas_set_stream");
+  int64_t poff[18], boff[18];
+  param_offsets(D, d->width, d->out_features, d->n_layers, poff, boff);
+  LibRun run{k.lib, &blas, w, params, grad, poff, boff, st, acc};
+  const int64_t n = d->n_rows, T = d->n_sets, rld = 3 * D + 1;
+  float* rows = w + k.off_rows;
+  float* gbar = w + k.off_gbar;
+  double* part = (double*)(w + k.off_part);
+  const double s = 1.0 / ((double)n * (double)n * (double)T);
+  if (hipMemsetAsync(gbar, 0, sizeof(float) * (size_t)T * n * D, st) != hipSuccess)
+    return fail(PDEINV_ERR_HIP, "kmv_mlp: memset");
+  MlpLossArgs la{};
+  la.d = D;
+  for (int pass = 0; pass < 2; ++pass) {
+    if (pass == 1) {
+      la.set = 3; la.uw = 1;
+      la.c1 = 0.f; la.c3 = 0.f; la.c2 = (float)(-2.0 * s); la.c0 = (float)(2.0 * s);
+    }
+    for (int64_t t = 0; t < T; ++t) {
+      for (int64_t i0 = 0; i0 < n; i0 += k.ni) {
+        const int64_t ni = (n - i0) < k.ni ? (n - i0) : k.ni;
+        for (int64_t j0 = 0; j0 < n; j0 += k.nj) {
+          const int64_t nj = (n - j0) < k.nj ? (n - j0) : k.nj;
+          const int64_t R = ni * nj;
+          hipLaunchKernelGGL(kmv_pair_rows_kernel<D>, dim3(grid_for(R)), dim3(kBlock), 0, st, z, set_stride, ld, t,
+                             i0, ni, j0, nj, n, pass ? gbar : nullptr, pass ? ds : nullptr, d->gamma,
+                             (float)(2.0 * s), rows);
+          const int rc = run.chunk(rows, rld, R, la, pass == 0);
+          if (rc) return rc;
+          if (pass == 0)
+            hipLaunchKernelGGL(kmv_group_mean_kernel<D>, dim3((unsigned)ni), dim3(kBlock), 0, st, run.G(), nj,
+                               (float)(1.0 / (double)n), gbar + (t * n + i0) * D);
+        }
+      }
+    }
+    if (pass == 0) {
+      KmvTrueArgs ta{};
+      for (int q = 0; q < D * D; ++q) ta.F[q] = d->tilde_F[q];
+      hipLaunchKernelGGL(kmv_stamp_terms_kernel<D>, dim3((unsigned)T), dim3(kBlock), 0, st, ta, z, set_stride, ld, n,
+                         gbar, part);
+      hipLaunchKernelGGL(kmv_stamp_combine_kernel, dim3(1), dim3(64), 0, st, part, T, 1.0 / ((double)n * (double)T),
+                         acc);
+    }
+  }
+  return check_launch("kmv_mlp kernels");
+}
+
+extern "C" size_t pdeinv_residual_kmv_mlp_workspace_bytes(const pdeinv_kmv_mlp_desc* d) {
+  if (!d || d->dim < 1 || d->n_layers < 1 || d->width < 1 || d->out_features < 1 || d->n_sets < 1 || d->n_rows < 1)
+    return 0;
+  return kmv_plan(d).total;
+}
+
+extern "C" int pdeinv_residual_kmv_mlp(const pdeinv_kmv_mlp_desc* d, const float* z, int64_t set_stride, int64_t ld,
+                                       const float* ds, const float* params, void* ws, double* acc, float* grad,
+                                       void* stream) {
+  PDEINV_REQUIRE(d != nullptr, PDEINV_ERR_INVALID, "kmv_mlp: null descriptor");
+  PDEINV_REQUIRE(d->n_layers >= 1 && d->n_layers <= 16 && d->width >= 1 && d->out_features >= 1, PDEINV_ERR_INVALID,
+                 "kmv_mlp: need 1 <= n_layers <= 16, width, out_features >= 1");
+  PDEINV_REQUIRE(d->n_sets >= 1 && d->n_rows >= 1, PDEINV_ERR_INVALID, "kmv_mlp: need n_sets, n_rows >= 1");
+  PDEINV_REQUIRE(ld >= 2 * d->dim && set_stride >= 0, PDEINV_ERR_INVALID, "kmv_mlp: row stride < 2*dim");
+  PDEINV_REQUIRE(z && ds && params && ws && acc && grad && d->tilde_F, PDEINV_ERR_INVALID, "kmv_mlp: null pointer");
+  const KmvPlan k = kmv_plan(d);
+  hipStream_t st = (hipStream_t)stream;
+  switch (d->dim) {
+#define CASE(DD) case DD: return kmv_mlp_run<DD>(d, k, z, set_stride, ld, ds, params, (float*)ws, acc, grad, st);
+    CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
+#undef CASE
+    default:
+      return fail(PDEINV_ERR_UNSUPPORTED, "kmv_mlp: dim must be in [1, 8]");
+  }
 }
 
 extern "C" int pdeinv_kfp_terms_finalize(const double* acc, const float* grad, int64_t n_grad, float gamma,

@@ -3,7 +3,10 @@
 loss = mean_i |mean_j grad Phi_theta(x_i - x_j)|^2 - 2 mean_i mean_j v_i^T Hess Phi_theta v_i
      + 2 mean_i [mean_j Phi_theta(x_i - x_j)] (ds2 log rho + (ds log rho)^2 + gamma ds log rho)
      + mean_i |mean_j grad Phi*(x_i - x_j)|^2                                   (:74-97, pairs per time)
-For the quadratic Phi_theta every pairwise mean is a function of the time stamp's moments, so
+For a general Phi_theta (the non-parametric V_hypothesis of get_model) the pairs are evaluated
+as they are in the reference — every (i, j) of each time stamp's particles — in two passes over
+pair rows on the MLP path (pdeinv_residual_kmv_mlp: gbar_i = mean_j grad Phi, then the per-pair
+adjoint). For the quadratic Phi_theta every pairwise mean is a function of the time stamp's moments, so
 the [m, n, n_time, d] pair tensor of :20-23 is replaced by:
   pass 1  pdeinv_moments_batched — per time stamp [count, sum z, sum z z^T];
   pass 2  pdeinv_kmv_weights     — per particle ds/ds2 log rho (the score/log-density
@@ -41,9 +44,10 @@ def layout(data: dict, d: int):
 
 def value_and_grad_fn(forward_fn, params, data, rng, pde_instance):
     model = resolve_model(forward_fn)
+    if model.residual_kind == "mlp":
+        return _value_and_grad_mlp(model, params, data, pde_instance)
     if model.residual_kind != "quadratic":
-        raise NotImplementedError(f"no native KMV residual for model kind '{model.residual_kind}' "
-                                  "(general Phi: tiled N-body kernel, SURVEY.md §8(f) rank 3)")
+        raise NotImplementedError(f"no native KMV residual for model kind '{model.residual_kind}'")
     d = pde_instance.dim
     gamma = float(pde_instance.initial_configuration["gamma_friction"])
     z, n_sets, n_rows, set_stride, ld, tau = layout(data, d)
@@ -63,6 +67,24 @@ def value_and_grad_fn(forward_fn, params, data, rng, pde_instance):
             both = dist.allreduce_mean(torch.cat([out, grad]))
             out, grad = both[: out.numel()], both[out.numel():]
     return _result(out, model.unflat(grad))
+
+
+def _value_and_grad_mlp(model, params, data, pde_instance):
+    """General Phi_theta = V_hypothesis: pairs within this rank's particles (the reference forms them
+    within each device's batch, trainer.py:44-53), outputs averaged over ranks."""
+    d = pde_instance.dim
+    gamma = float(pde_instance.initial_configuration["gamma_friction"])
+    z, n_sets, n_rows, set_stride, ld, tau = layout(data, d)
+    coef = pde_instance.coefficients(tau, z.device)
+    _, ds = native.kmv_weights(d, gamma, coef, z, n_sets, n_rows, set_stride, ld, want_ds=True)
+    flat = model.flat(params)
+    acc, grad = native.residual_kmv_mlp(model.dims(d), flat, z, n_sets, n_rows, set_stride, ld, ds,
+                                        pde_instance.initial_configuration["tilde_F"], gamma)
+    out = native.kfp_terms_finalize(acc, grad, 1.0)
+    if dist.world_size() > 1:
+        both = dist.allreduce_mean(torch.cat([out, grad]))
+        out, grad = both[: out.numel()], both[out.numel():]  # incl. grad_norm: the pmap mean, trainer.py:52
+    return _result(out, model.unflat(grad, d))
 
 
 def test_fn(forward_fn, pde_instance, rng):

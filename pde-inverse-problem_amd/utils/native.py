@@ -36,7 +36,7 @@ GMM_NACC = 8
 GMM_ACC_SLOTS = ("loss", "loss_gt", "nabla", "hessian", "friction", "nabla_true", "initial", "terminal")
 SQRT2 = math.sqrt(2.0)
 
-ABI_VERSION = 3  # PDEINV_ABI_VERSION of include/pdeinv.h this binding was written against
+ABI_VERSION = 4  # PDEINV_ABI_VERSION of include/pdeinv.h this binding was written against
 
 # Every exported symbol of include/pdeinv.h (tests check the library exports all of them).
 EXPORTED_SYMBOLS = (
@@ -53,6 +53,7 @@ EXPORTED_SYMBOLS = (
     "pdeinv_mlp_param_count", "pdeinv_residual_kfp_mlp_workspace_bytes", "pdeinv_residual_kfp_mlp",
     "pdeinv_kfp_terms_finalize", "pdeinv_gather_random_step", "pdeinv_mlp_fused_supported",
     "pdeinv_adam_update", "pdeinv_realnvp_param_count", "pdeinv_realnvp_logdensity",
+    "pdeinv_residual_kmv_mlp_workspace_bytes", "pdeinv_residual_kmv_mlp",
 )
 
 
@@ -88,6 +89,12 @@ class KfpMlpDesc(ctypes.Structure):
                 ("c_nabla", ctypes.c_float), ("c_hess", ctypes.c_float), ("c_fric", ctypes.c_float),
                 ("c_true", ctypes.c_float), ("c_init", ctypes.c_float), ("c_term", ctypes.c_float),
                 ("chunk_rows", ctypes.c_int64), ("impl", ctypes.c_int32), ("boundary_value", ctypes.c_int32)]
+
+
+class KmvMlpDesc(ctypes.Structure):
+    _fields_ = [("dim", ctypes.c_int32), ("n_layers", ctypes.c_int32), ("width", ctypes.c_int32),
+                ("out_features", ctypes.c_int32), ("n_sets", ctypes.c_int32), ("n_rows", ctypes.c_int64),
+                ("gamma", ctypes.c_float), ("tilde_F", ctypes.c_void_p), ("chunk_rows", ctypes.c_int64)]
 
 
 MLP_IMPL_AUTO, MLP_IMPL_LIBRARY, MLP_IMPL_FUSED = 0, 1, 2
@@ -169,6 +176,8 @@ def lib():
         "pdeinv_residual_kfp_mlp_workspace_bytes": (ctypes.c_size_t, [P]),
         "pdeinv_residual_kfp_mlp": (i32, [P, P, i64, i64, P, i64, i64, P, i64, i64, P, P, P, P, P]),
         "pdeinv_kfp_terms_finalize": (i32, [P, P, i64, f32, P, P]),
+        "pdeinv_residual_kmv_mlp_workspace_bytes": (ctypes.c_size_t, [P]),
+        "pdeinv_residual_kmv_mlp": (i32, [P, P, i64, i64, P, P, P, P, P, P]),
         "pdeinv_gather_random_step": (i32, [P, i64, i32, i32, u64, u32, P, P, P]),
         "pdeinv_fp_rows": (i32, [P, i64, i64, i32, i32, P, P]),
         "pdeinv_fp_exact_sample": (i32, [i64, i32, u64, u32, i64, f32, f32, P, P, P, P, P, P, P, P]),
@@ -531,6 +540,37 @@ def kmv_weights(d: int, gamma: float, coef: torch.Tensor, z: torch.Tensor, n_set
                                     ld, _dev(ds, "ds"), _dev(ws, "ws"), _dev(out, "out", torch.float64),
                                     stream_handle()), "pdeinv_kmv_weights")
     return out, ds
+
+
+def residual_kmv_mlp(dims, params_flat: torch.Tensor, z: torch.Tensor, n_sets: int, n_rows: int, set_stride: int,
+                     ld: int, ds: torch.Tensor, tilde_F, gamma: float, chunk_rows: int = 1 << 18):
+    """kinetic_mckean_vlasov.py:11-120 for Phi_theta = V_hypothesis over every pair of each time
+    stamp's particles (pdeinv_residual_kmv_mlp). ds = (ds log rho, ds2 log rho) [n_sets, n_rows, 2]
+    from kmv_weights(want_ds=True). Returns (acc fp64 [8], grad fp32 [P]) — finalize with
+    kfp_terms_finalize(acc, grad, 1.0)."""
+    _require_gpu()
+    d, W, O = dims[0], dims[1], dims[-1]
+    L = len(dims) - 2
+    if L < 1 or any(w != W for w in dims[1:-1]):
+        raise NotImplementedError("KMV MLP residual: hidden layers must share one width (V_hypothesis)")
+    P = lib().pdeinv_mlp_param_count(d, L, W, O)
+    if params_flat.numel() != P or not params_flat.is_contiguous():
+        raise ValueError(f"KMV MLP residual: params must be a contiguous flat vector of {P} floats")
+    _set_view(z, n_sets, n_rows, set_stride, ld, 2 * d)
+    if tuple(ds.shape) != (n_sets, n_rows, 2) or not ds.is_contiguous():
+        raise ValueError(f"KMV MLP residual: ds must be contiguous [{n_sets}, {n_rows}, 2]")
+    F = _host_f32(tilde_F)
+    desc = KmvMlpDesc(d, L, W, O, int(n_sets), int(n_rows), float(gamma), F.ctypes.data_as(ctypes.c_void_p),
+                      int(chunk_rows))
+    nbytes = lib().pdeinv_residual_kmv_mlp_workspace_bytes(ctypes.byref(desc))
+    ws = torch.empty(nbytes // 4, device=z.device, dtype=torch.float32)
+    acc = torch.zeros(GMM_NACC, device=z.device, dtype=torch.float64)
+    grad = torch.zeros(P, device=z.device, dtype=torch.float32)
+    _check(lib().pdeinv_residual_kmv_mlp(ctypes.byref(desc), _dev(z, "z"), int(set_stride), int(ld), _dev(ds, "ds"),
+                                         _dev(params_flat, "params"), _dev(ws, "ws"),
+                                         _dev(acc, "acc", torch.float64), _dev(grad, "grad"), stream_handle()),
+           "pdeinv_residual_kmv_mlp")
+    return acc, grad
 
 
 def residual_kmv(mom: torch.Tensor, wst: torch.Tensor, theta_flat: torch.Tensor, tilde_F, gamma: float):

@@ -50,6 +50,51 @@ def test_kmv_residual_vs_pairwise_restatement(native):
     assert np.allclose(g.cpu().numpy(), g_fd, rtol=1e-3, atol=1e-3)
 
 
+@pytest.mark.parametrize("d,n,chunk", [(2, 40, 1 << 18), (4, 37, 300)])
+def test_kmv_general_phi_mlp_vs_pairwise_restatement(native, d, n, chunk):
+    """General Phi_theta = V_hypothesis (non-parametric KMV, kinetic_mckean_vlasov.py:11-120):
+    the two-pass pair-row HIP path == the literal pair-tensor restatement (loss, loss ground truth,
+    terms) and its FD-checked analytic gradient (oracle kmv_mlp_grad_analytic). chunk = 300 forces
+    partial i-blocks and j-chunking of the pair rows. Tolerance 2e-4 relative (fp32 GEMMs)."""
+    from example_problems.kinetic_mckean_vlasov_example_quadratic import KineticMcKeanVlasov
+    from methods.consistency_instances import kinetic_mckean_vlasov as kmv
+    from core.model import V_hypothesis
+    from utils import native as nat, prng
+    n_t, W, L = 3, 20, 3
+    cfg = _cfg(["pde_instance=kinetic_mckean_vlasov", f"pde_instance.domain_dim={d}"])
+    pi = KineticMcKeanVlasov(cfg, prng.PRNGKey(0))
+    rng = np.random.default_rng(7)
+    x = rng.standard_normal((n, n_t, d)); v = rng.standard_normal((n, n_t, d))
+    tau = np.array([0.3, 0.9, 1.6])
+    net = V_hypothesis(output_dim=1, hidden_dims=[W] * L)
+    params = net.init(prng.PRNGKey(11), np.zeros(d), device=DEV)
+    dims = net.dims(d)
+    flat = net.flat(params)
+    P = nr.mlp_unflat(flat.double().cpu().numpy(), dims)
+    cfg_np = nr.ou_configuration(pi.initial_configuration["tilde_F"], gamma=1.0)
+    loss, loss_gt, parts = nr.kmv_mlp_pairwise_loss(P, x, v, tau, cfg_np)
+    ga = nr.mlp_flat(nr.kmv_mlp_grad_analytic(P, x, v, tau, cfg_np))
+    z = _t(np.concatenate([x, v], -1).reshape(-1, 2 * d))  # reference order rows (i, t)
+    if chunk == 1 << 18:
+        res = kmv.value_and_grad_fn(net.apply, params, {"0T": z, "tau_0T": tau}, None, pi)
+        out, g = None, torch.cat([t.reshape(-1) for lay in res["grad"]["params"].values()
+                                  for t in (lay["kernel"], lay["bias"])])
+        got_loss, got_gt = float(res["loss"]), float(res["loss ground truth"])
+    else:
+        coef = pi.coefficients(tau, z.device)
+        _, ds = nat.kmv_weights(d, 1.0, coef, z, n_t, n, 2 * d, n_t * 2 * d, want_ds=True)
+        acc, g = nat.residual_kmv_mlp(dims, flat, z, n_t, n, 2 * d, n_t * 2 * d, ds,
+                                      pi.initial_configuration["tilde_F"], 1.0, chunk_rows=chunk)
+        out = nat.kfp_terms_finalize(acc, g, 1.0).cpu().numpy()
+        got_loss, got_gt = float(out[nat.KFP_SLOTS.index("loss")]), float(out[nat.KFP_SLOTS.index("loss ground truth")])
+        assert abs(out[nat.KFP_SLOTS.index("loss_Hessian")] - parts["hessian"]) < 2e-4 * (1 + abs(parts["hessian"]))
+        assert abs(out[nat.KFP_SLOTS.index("loss_nabla")] - parts["nabla"]) < 2e-4 * (1 + abs(parts["nabla"]))
+    assert abs(got_loss - loss) < 2e-4 * (1 + abs(loss))
+    assert abs(got_gt - loss_gt) < 2e-4 * (1 + abs(loss_gt))
+    g = g.double().cpu().numpy()
+    assert np.abs(g - ga).max() < 2e-4 * (1 + np.abs(ga).max())
+
+
 def test_partial_s_log_density_kat(native):
     """test_partial_s_log_density.py:241-311 re-created and ASSERTED: d = 10, s = 0.1,
     central differences delta = 1e-4 (ds) and 1e-3 (ds2), relative RMSE < 1e-3; plus a direct

@@ -210,6 +210,22 @@ def test_constants_recipe():
         assert np.array_equal(nr.problem_constants(d), g[f"tilde_F_d{d}"])
 
 
+def test_kmv_mlp_two_pass_adjoint_vs_finite_differences():
+    """General-Phi KMV (Phi_theta = V_hypothesis): the two-pass adjoint the HIP path runs
+    (gbar = mean_j grad Phi, then per-pair seeds) equals central differences of the literal
+    pair-tensor loss of kinetic_mckean_vlasov.py:74-97 (tiny net, fp64)."""
+    rng = np.random.default_rng(4)
+    d, n, n_t = 2, 9, 2
+    dims = [d, 5, 5, 3]
+    flat = rng.standard_normal(sum(dims[i] * dims[i + 1] + dims[i + 1] for i in range(3))) * 0.5
+    cfg = nr.ou_configuration(nr.problem_constants(d))
+    x, v = rng.standard_normal((n, n_t, d)), rng.standard_normal((n, n_t, d))
+    tau = np.array([0.4, 1.3])
+    f = lambda fl: nr.kmv_mlp_pairwise_loss(nr.mlp_unflat(fl, dims), x, v, tau, cfg)[0]
+    ga = nr.mlp_flat(nr.kmv_mlp_grad_analytic(nr.mlp_unflat(flat, dims), x, v, tau, cfg))
+    assert np.allclose(ga, nr.fd_grad(f, flat, eps=1e-6), rtol=1e-6, atol=1e-8)
+
+
 def test_mlp_taylor_terms_and_adjoint_vs_finite_differences():
     """The MLP residual's per-sample terms (grad, V', V'') and the analytic parameter adjoint that
     mlp.hip implements, against central differences (tiny net, fp64)."""
