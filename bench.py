@@ -98,6 +98,20 @@ def timed(step, K, W, dev):
     return el * 1e3 / K, kern_ms
 
 
+def write_ceiling(buf, reps=5):
+    """This box's plain streaming-write rate: torch fill_ of an HBM buffer of the trajectory's size,
+    timed with events after the timed region (context for roofline.frac: HBM write bandwidth
+    differs by several tens of percent between MI355X boxes of the pool, MI355X_MICROARCH.md)."""
+    buf.fill_(0.0)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        buf.fill_(1.0)
+    e.record()
+    torch.cuda.synchronize()
+    return buf.numel() * buf.element_size() / (s.elapsed_time(e) / reps / 1e3) / 1e9
+
+
 def traffic_from_profiles(key):
     try:
         with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
@@ -162,6 +176,9 @@ def run_c2(a, rank, world, dev):
                       "sde_simulate_kernel<4,QUADRATIC,moments,staged> (+ its slab reduce)",
                       traffic_from_profiles("sde_simulate_C2_bytes_per_launch") if (N, n) == (1 << 21, 100) else None)
     out["loss"] = float(last_res[0][0][0].item())
+    ceil = dist.allreduce_max_scalar(-write_ceiling(bufs["traj"]), device=dev) * -1.0  # min over ranks
+    out["roofline"]["box_write_ceiling_GBps"] = ceil
+    out["roofline"]["frac_of_box_write_ceiling"] = out["roofline"]["achieved"] / ceil
     if not a.no_recovery:
         # untimed; a fixed Monte-Carlo budget (independent of --steps) of fresh moments-only passes,
         # on top of the timed steps' moments, at n = 100 and n = 200

@@ -197,6 +197,16 @@ def test_trainer_kmv_exact_and_sde(native):
     assert all(np.isfinite(h["loss"]) for h in tr.history)
 
 
+def test_trainer_kmv_non_parametric(native):
+    """estimation_mode=non-parametric under KMV (get_model -> V_hypothesis, the MLP.yaml net of
+    width 20 x 8 layers): the general-Phi pair-row residual drives the trainer end to end."""
+    base = ["pde_instance=kinetic_mckean_vlasov", "pde_instance.domain_dim=2", "solver.train.sample_mode=grid_time",
+            "solver.train.sample_per_time=300", "solver.train.n_time_stamps=1", "pde_instance.total_evolving_time=1",
+            "estimation_mode=non-parametric"]
+    tr = _run(base)
+    assert all(np.isfinite(h["loss"]) for h in tr.history)
+
+
 def test_no_cpu_fallback_for_callables(native):
     from utils.sampling_utils import underdamped_langevin_dynamics_scan
     from utils import prng
