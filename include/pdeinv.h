@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define PDEINV_ABI_VERSION 4
+#define PDEINV_ABI_VERSION 5
 #define PDEINV_MAX_DIM 16          /* d (configuration-space dimension) */
 #define PDEINV_MAX_PARAMS 256      /* floats of potential parameters passed by value */
 
@@ -452,6 +452,15 @@ int64_t pdeinv_realnvp_param_count(const pdeinv_realnvp_desc* desc);
 int pdeinv_realnvp_logdensity(const pdeinv_realnvp_desc* desc, const float* d_params, const float* d_t,
                               int64_t t_stride, const float* d_x, int64_t n, int64_t ld_x, float* d_out,
                               void* stream);
+
+/* Maximum-likelihood value_and_grad of the flow (replaces jax.value_and_grad(loss_fn) in
+ * core/log_density_estimation.py:47-58): *d_loss = -mean_i log p_{t_i}(x_i), d_grad[param_count]
+ * = d loss / d params (same flat layout as d_params). d_workspace: pdeinv_realnvp_grad_workspace
+ * bytes (a per-block partial slab; reduced in a fixed order, deterministic). n >= 1. */
+int64_t pdeinv_realnvp_grad_workspace(const pdeinv_realnvp_desc* desc, int64_t n);
+int pdeinv_realnvp_value_and_grad(const pdeinv_realnvp_desc* desc, const float* d_params, const float* d_t,
+                                  int64_t t_stride, const float* d_x, int64_t n, int64_t ld_x, float* d_loss,
+                                  float* d_grad, void* d_workspace, int64_t workspace_bytes, void* stream);
 
 /* Fused optimizer step of the trainer (core/trainer.py:85-86 + main.py:11-29):
  * optax.chain(add_decayed_weights(weight_decay), adam(lr, b1, b2, eps)) then apply_updates, in

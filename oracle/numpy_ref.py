@@ -909,3 +909,80 @@ def nvp_init(dim, n_layers, E, ignore_time, seed=0, scale=1.0, perturb=False):
     flat = np.concatenate(parts)
     assert flat.size == nvp_param_count(dim, n_layers, E, ignore_time)
     return flat
+
+
+def realnvp_nll_value_and_grad(flat, t, x, *, dim, masks, base_mean, base_cov, E=10, ignore_time=False,
+                               soft_init=1.0, act="celu"):
+    """(loss, grad) of the maximum-likelihood step (log_density_estimation.py:47-58):
+    loss = -mean log p_t(x), grad = d loss / d params in the flat layout of include/pdeinv.h.
+    The same restatement as realnvp_apply / realnvp_logdensity, written in torch fp64 (CPU) so
+    autograd stands in for jax.value_and_grad; the value is checked against the NumPy
+    restatement and the gradient against central differences in tests/test_oracle.py."""
+    import torch
+
+    acts = {"celu": torch.nn.functional.celu, "elu": torch.nn.functional.elu, "relu": torch.relu,
+            "tanh": torch.tanh, "silu": torch.nn.functional.silu, "softplus": torch.nn.functional.softplus,
+            "gelu": lambda z: torch.nn.functional.gelu(z, approximate="tanh")}
+    f = acts[act]
+    n_layers = masks.shape[0]
+    p = torch.tensor(np.asarray(flat, dtype=np.float64), requires_grad=True)
+    X = torch.tensor(np.asarray(x, dtype=np.float64))
+    T = torch.tensor(np.broadcast_to(np.asarray(t, dtype=np.float64), X.shape[:1]).copy())
+    o = [0]
+
+    def take(*shape):
+        k = int(np.prod(shape))
+        v = p[o[0]:o[0] + k].reshape(shape)
+        o[0] += k
+        return v
+
+    Et = 0 if ignore_time else E
+    if Et > 0:
+        W1, b1, W2, b2 = take(Et, Et), take(Et), take(Et, Et), take(Et)
+        half = Et // 2
+        freq = torch.exp(torch.arange(half, dtype=torch.float64) * -(math.log(10000) / (half - 1)))
+        e = T[:, None] * freq
+        se = torch.cat([torch.sin(e), torch.cos(e)], -1)
+        tcat = f(se @ W1 + b1) @ W2 + b2
+    elif ignore_time:
+        tcat = torch.zeros((X.shape[0], 0), dtype=torch.float64)
+    else:
+        tcat = T[:, None]
+    i_dim = nvp_in_dim(dim, E, ignore_time)
+    layers = []
+    for _ in range(n_layers):
+        sf = take(dim)
+        nets = [[(take(i_dim, 8), take(8)), (take(8, 16), take(16)), (take(16, 16), take(16)), (take(16, dim), take(dim))]
+                for _ in range(2)]
+        layers.append((sf, nets[0], nets[1]))
+    assert o[0] == p.numel()
+
+    def mlp(net, h):
+        for k, (W, b) in enumerate(net):
+            h = h @ W + b
+            if k < 3:
+                h = f(h)
+        return h
+
+    M = torch.tensor(np.asarray(masks, dtype=np.float64))
+    ldj = torch.zeros(X.shape[0], dtype=torch.float64)
+    hard = (not ignore_time) and soft_init == 0.0
+    for l in range(n_layers - 1, -1, -1):   # likelihood direction (RealNVP.__call__, reverse=True)
+        sf, snet, tnet = layers[l]
+        m = M[l]
+        xt = torch.cat([X * m, tcat], -1)
+        s, tr = mlp(snet, xt), mlp(tnet, xt)
+        if hard:
+            s, tr = T[:, None] * s, T[:, None] * tr
+        sfe = torch.exp(sf)
+        s = torch.tanh(s / sfe) * sfe * (1 - m)
+        tr = tr * (1 - m)
+        X = (X + tr) * torch.exp(s)
+        ldj = ldj + s.sum(-1)
+    off = X - torch.tensor(np.asarray(base_mean, dtype=np.float64))
+    icov = torch.tensor(np.linalg.inv(base_cov))
+    quad = torch.einsum("ni,ij,nj->n", off, icov, off)
+    log_det = float(np.log(np.linalg.det(base_cov * 2 * np.pi)))
+    loss = -(-0.5 * (log_det + quad) + ldj).mean()
+    loss.backward()
+    return float(loss.detach()), p.grad.numpy().copy()

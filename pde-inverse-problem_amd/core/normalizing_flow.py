@@ -123,4 +123,12 @@ class RealNVP:
         out = native.realnvp_logdensity(self._desc, flat, tt, rows)
         return out[0] if single else out
 
+    def value_and_grad(self, params, t, x):
+        """(loss, grad) with loss = -mean_i log p_{t_i}(x_i) and grad flat like params
+        (log_density_estimation.py:47-58), on the HIP kernel. celu / elu flows only."""
+        flat = params["params"] if isinstance(params, dict) else params
+        x = torch.as_tensor(x, dtype=torch.float32, device=flat.device)
+        tt = torch.as_tensor(t, dtype=torch.float32, device=flat.device).reshape(-1)
+        return native.realnvp_value_and_grad(self._desc, flat, tt, x.reshape(-1, self.mnf.dim) if x.dim() == 1 else x)
+
     __call__ = apply

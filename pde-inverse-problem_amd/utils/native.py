@@ -36,7 +36,7 @@ GMM_NACC = 8
 GMM_ACC_SLOTS = ("loss", "loss_gt", "nabla", "hessian", "friction", "nabla_true", "initial", "terminal")
 SQRT2 = math.sqrt(2.0)
 
-ABI_VERSION = 4  # PDEINV_ABI_VERSION of include/pdeinv.h this binding was written against
+ABI_VERSION = 5  # PDEINV_ABI_VERSION of include/pdeinv.h this binding was written against
 
 # Every exported symbol of include/pdeinv.h (tests check the library exports all of them).
 EXPORTED_SYMBOLS = (
@@ -53,6 +53,7 @@ EXPORTED_SYMBOLS = (
     "pdeinv_mlp_param_count", "pdeinv_residual_kfp_mlp_workspace_bytes", "pdeinv_residual_kfp_mlp",
     "pdeinv_kfp_terms_finalize", "pdeinv_gather_random_step", "pdeinv_mlp_fused_supported",
     "pdeinv_adam_update", "pdeinv_realnvp_param_count", "pdeinv_realnvp_logdensity",
+    "pdeinv_realnvp_grad_workspace", "pdeinv_realnvp_value_and_grad",
     "pdeinv_residual_kmv_mlp_workspace_bytes", "pdeinv_residual_kmv_mlp",
 )
 
@@ -173,6 +174,8 @@ def lib():
         "pdeinv_adam_update": (i32, [P, P, P, P, i64, f32, f32, f32, f32, f32, i32, P]),
         "pdeinv_realnvp_param_count": (i64, [P]),
         "pdeinv_realnvp_logdensity": (i32, [P, P, P, i64, P, i64, i64, P, P]),
+        "pdeinv_realnvp_grad_workspace": (i64, [P, i64]),
+        "pdeinv_realnvp_value_and_grad": (i32, [P, P, P, i64, P, i64, i64, P, P, P, i64, P]),
         "pdeinv_residual_kfp_mlp_workspace_bytes": (ctypes.c_size_t, [P]),
         "pdeinv_residual_kfp_mlp": (i32, [P, P, i64, i64, P, i64, i64, P, i64, i64, P, P, P, P, P]),
         "pdeinv_kfp_terms_finalize": (i32, [P, P, i64, f32, P, P]),
@@ -764,6 +767,30 @@ def realnvp_logdensity(desc, params: torch.Tensor, t: torch.Tensor, x: torch.Ten
                                            0 if t.numel() == 1 else 1, px, n, ld, _dev(out, "out"),
                                            stream_handle()), "pdeinv_realnvp_logdensity")
     return out
+
+
+def realnvp_value_and_grad(desc, params: torch.Tensor, t: torch.Tensor, x: torch.Tensor):
+    """(loss, grad): loss = -mean log p_t(x) (log_density_estimation.py:51-58), grad flat like params."""
+    _require_gpu()
+    n = x.shape[0]
+    P = realnvp_param_count(desc)
+    if params.numel() != P or not params.is_contiguous():
+        raise ValueError("RealNVP: params must be a contiguous flat vector of pdeinv_realnvp_param_count floats")
+    if n < 1:
+        raise ValueError("RealNVP: value_and_grad needs at least one sample")
+    t = t.reshape(-1)
+    if t.numel() not in (1, n):
+        raise ValueError("RealNVP: t must have one entry per row or a single entry")
+    px, _, ld = _rows(x, "x", desc.dim)
+    ws_bytes = int(lib().pdeinv_realnvp_grad_workspace(ctypes.byref(desc), n))
+    ws = torch.empty((ws_bytes + 3) // 4, device=x.device, dtype=torch.float32)
+    loss = torch.empty((), device=x.device, dtype=torch.float32)
+    grad = torch.empty(P, device=x.device, dtype=torch.float32)
+    _check(lib().pdeinv_realnvp_value_and_grad(ctypes.byref(desc), _dev(params, "params"), _dev(t.contiguous(), "t"),
+                                               0 if t.numel() == 1 else 1, px, n, ld, _dev(loss, "loss"),
+                                               _dev(grad, "grad"), _dev(ws, "workspace"), ws_bytes,
+                                               stream_handle()), "pdeinv_realnvp_value_and_grad")
+    return loss, grad
 
 
 def mlp_fused_supported(dims) -> bool:

@@ -408,3 +408,69 @@ def test_realnvp_logdensity_vs_restatement(native, dim, mask_type, E, soft_init,
     f2 = create_normalizing_flow_fn(Gaussian(np.zeros(2), np.eye(2)).logdensity, 2)
     p2 = f2.init(prng.PRNGKey(0), 0.0, np.zeros(2))
     assert torch.isfinite(f2.apply(p2, _t(t[:10]), _t(x[:10, :2] if dim >= 2 else np.zeros((10, 2))))).all()
+
+
+@pytest.mark.parametrize("dim,mask_type,E,soft_init,ignore_time,n", [
+    (2, "loop", 10, 1.0, False, 3000), (1, "loop", 4, 0.0, False, 700), (3, "random", 0, 1.0, False, 1000),
+    (4, "loop", 10, 1.0, False, 2561), (5, "random", 6, 0.0, False, 900), (8, "loop", 16, 1.0, True, 513)])
+def test_realnvp_value_and_grad_vs_autograd(native, dim, mask_type, E, soft_init, ignore_time, n):
+    """pdeinv_realnvp_value_and_grad (log_density_estimation.py:47-58: loss = -mean log p and its
+    gradient, which the reference takes with jax.value_and_grad) vs the fp64 torch-autograd
+    restatement (oracle/numpy_ref.py, FD-checked in tests/test_oracle.py). fp32 kernel: loss within
+    2e-5 relative, gradient within 1e-4 of its norm (and 5e-4 of its max entry) elementwise."""
+    from core.distribution import Gaussian
+    from core.normalizing_flow import MNF, RealNVP
+    couple = 2 if mask_type == "loop" else 3
+    mnf = MNF(dim, couple, mask_type, soft_init, ignore_time, "celu", E)
+    rng = np.random.default_rng(10 + dim)
+    mean = rng.standard_normal(dim) * 0.3
+    Lc = rng.standard_normal((dim, dim)) * 0.3
+    cov = Lc @ Lc.T + np.eye(dim)
+    flow = RealNVP(mnf, Gaussian(mean, cov).logdensity)
+    flat = nr.nvp_init(dim, mnf.n_layers, E, ignore_time, seed=dim + 3, scale=1.2, perturb=True)
+    x = rng.standard_normal((n, dim)) * 1.5
+    t = rng.uniform(0, 2, n)
+    loss, grad = flow.value_and_grad({"params": _t(flat)}, _t(t), _t(x))
+    ref_loss, ref_grad = nr.realnvp_nll_value_and_grad(flat, t, x, dim=dim, masks=mnf.masks, base_mean=mean,
+                                                       base_cov=cov, E=E, ignore_time=ignore_time,
+                                                       soft_init=soft_init, act="celu")
+    g = grad.cpu().numpy().astype(np.float64)
+    assert abs(loss.item() - ref_loss) < 2e-5 * (1 + abs(ref_loss)), (loss.item(), ref_loss)
+    err = np.abs(g - ref_grad)
+    assert np.linalg.norm(g - ref_grad) < 1e-4 * np.linalg.norm(ref_grad) + 1e-6, np.linalg.norm(g - ref_grad)
+    assert err.max() < 5e-4 * (1 + np.abs(ref_grad).max()), err.max()
+    # deterministic: fixed-order reductions, no float atomics
+    loss2, grad2 = flow.value_and_grad({"params": _t(flat)}, _t(t), _t(x))
+    assert loss2.item() == loss.item() and torch.equal(grad, grad2)
+
+
+def test_realnvp_value_and_grad_chunks_and_errors(native):
+    """Past 2048 tiles the slab is reduced in chunks into an fp64 accumulator: the mean gradient over
+    n rows must equal the row-count-weighted mean of the gradients over two disjoint parts
+    (linearity, size-independent). Also: a broadcast t, the unsupported-activation and empty-batch
+    errors."""
+    from core.distribution import Gaussian
+    from core.normalizing_flow import MNF, RealNVP
+    dim, E = 2, 10
+    mnf = MNF(dim, 4, "loop", 1.0, False, "celu", E)
+    flow = RealNVP(mnf, Gaussian(np.zeros(dim), np.eye(dim)).logdensity)
+    flat = _t(nr.nvp_init(dim, mnf.n_layers, E, False, seed=5, scale=1.2, perturb=True))
+    n = 2048 * 256 + 777
+    gen = torch.Generator(device=DEV).manual_seed(0)
+    x = torch.randn((n, dim), device=DEV, generator=gen) * 1.5
+    t = torch.rand(n, device=DEV, generator=gen) * 2
+    loss, grad = flow.value_and_grad(flat, t, x)
+    n1 = 300_001
+    l1, g1 = flow.value_and_grad(flat, t[:n1], x[:n1])
+    l2, g2 = flow.value_and_grad(flat, t[n1:], x[n1:])
+    mix = (n1 * g1.double() + (n - n1) * g2.double()) / n
+    assert torch.linalg.norm(grad.double() - mix) < 1e-5 * torch.linalg.norm(mix)
+    assert abs(loss.item() - (n1 * l1.item() + (n - n1) * l2.item()) / n) < 1e-5 * (1 + abs(loss.item()))
+    lb, gb = flow.value_and_grad(flat, torch.full((1,), 0.7, device=DEV), x[:1000])   # broadcast t
+    lr_, gr = flow.value_and_grad(flat, torch.full((1000,), 0.7, device=DEV), x[:1000])
+    assert lb.item() == lr_.item() and torch.equal(gb, gr)
+    with pytest.raises(ValueError):
+        flow.value_and_grad(flat, t[:0], x[:0])
+    tanh_flow = RealNVP(MNF(dim, 4, "loop", 1.0, False, "tanh", E), Gaussian(np.zeros(dim), np.eye(dim)).logdensity)
+    with pytest.raises(NotImplementedError):
+        tanh_flow.value_and_grad(flat, t[:10], x[:10])

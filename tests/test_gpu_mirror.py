@@ -224,3 +224,27 @@ def test_reference_shaped_scan_outputs(native):
     # tau = tau0 + k dt with tau0 in [0, dt)  (sampling_utils.py:32, 48)
     t = tau.cpu().numpy()
     assert np.all((t[:, 0] >= 0) & (t[:, 0] < 0.05)) and np.allclose(np.diff(t, axis=1), 0.05, atol=1e-6)
+
+
+def test_estimate_log_density_trains_on_offline_dataset(native):
+    """core/log_density_estimation.py:13-100 on a small offline GMM dataset: the per-epoch strided
+    subsample (1 in 5 time stamps, 1 in 5 trajectories), the native value_and_grad and Adam with the
+    reference's schedule. The negative log-likelihood must fall, and the learned density must beat the
+    untrained flow on held-out rows of the dataset."""
+    from core import log_density_estimation as lde
+    from registry import get_pde_instance
+    from utils import prng
+    cfg = _cfg(["pde_instance=kinetic_fokker_planck", "pde_instance.potential=GMM", "pde_instance.sample_mode=offline",
+                "pde_instance.domain_dim=2", "pde_instance.sample_initial_size=2000",
+                "pde_instance.sample_terminal_size=1000", "pde_instance.sample_0T_size=2000",
+                "pde_instance.n_steps_terminal=40", "pde_instance.n_steps_0T=40"])
+    rng = prng.PRNGKey(int(cfg.seed))
+    pi = get_pde_instance(cfg)(cfg=cfg, rng=rng)
+    fn = lde.estimate_log_density(cfg, pi, prng.PRNGKey(3), num_epochs=300, frequency=100, verbose=False)
+    h = fn.history
+    assert len(h) == 3 and all(np.isfinite(h)) and h[-1] < h[0] - 0.05, h
+    rows = pi.dataset["0T"][:, 1::5, :2].reshape(-1, 2)
+    times = pi.dataset["tau_0T"][:, 1::5].reshape(-1)
+    fresh = lde.create_normalizing_flow_fn(pi.distribution_initial_x.logdensity, 2)
+    p0 = fresh.init(prng.split(prng.PRNGKey(3), 2)[0], 0.0, np.zeros(2))
+    assert fn(times, rows).mean().item() > fresh.apply(p0, times, rows).mean().item()
