@@ -1,0 +1,39 @@
+"""Worker for the multi-rank GPU tests (tests/test_gpu_multirank.py), launched by
+torch.distributed.run with PDEINV_DIST_BACKEND=gloo so that several ranks can share the one GPU
+of a test box (RCCL needs one GPU per rank; the data path and the all-reduce call sites are the
+same). Writes this rank's shard of the result to <out>/rank<r>.npz."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "pde-inverse-problem_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def mean_field(out_dir, N=6000, n=30, d=4):
+    from core.potential import MeanFieldQuadraticPotential
+    from oracle import numpy_ref as nr
+    from utils import distributed as dist
+    from utils.mean_field import simulate_mean_field
+    from utils.prng import PRNGKey
+    rank, world = dist.rank(), dist.world_size()
+    off, cnt = dist.shard(N)
+    z0 = np.random.default_rng(7).standard_normal((N, 2 * d)).astype(np.float32)
+    z0[:, :d] += 0.5                                   # a non-centred ensemble: the mean field matters
+    dev = torch.device("cuda", dist.local_device())
+    pot = MeanFieldQuadraticPotential(nr.problem_constants(d))
+    r = simulate_mean_field(torch.as_tensor(z0[off:off + cnt], device=dev), n, 0.02, PRNGKey(11), pot, 1.0,
+                            particle_offset=off, counter_offset=3)
+    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), traj=r["traj"].cpu().numpy(), last=r["last"].cpu().numpy(),
+             xsum=r["xsum"].cpu().numpy(), off=off, world=world)
+
+
+if __name__ == "__main__":
+    from utils import distributed as dist
+    dist.init_from_env()
+    {"mean_field": mean_field}[sys.argv[1]](sys.argv[2])
+    if dist.is_distributed():
+        torch.distributed.destroy_process_group()

@@ -1,0 +1,65 @@
+"""Multi-rank paths on the one GPU of a test box: several ranks launched by
+torch.distributed.run share cuda:0 with the gloo backend (PDEINV_DIST_BACKEND=gloo; RCCL needs one
+GPU per rank, the call sites are the same).
+
+* McKean–Vlasov simulator: one all-reduce of [count, sum x] per update. The Philox counter is the
+  global particle id and the mean field is the all-reduced ensemble mean, so the 2- and 3-rank
+  trajectories must equal the 1-rank trajectory of the whole ensemble (up to the fp64 summation
+  order of the partial sums: 2e-5 after 31 updates).
+* bench.py --gpus 2 (the driver's scaling launch): one JSON line, n_gpus = 2, value = both ranks'
+  particle-updates / the max-over-ranks step time.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _launch(nproc, args, port, timeout=180):
+    env = dict(os.environ, PDEINV_DIST_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr=127.0.0.1", f"--master-port={port}"] + args
+    return subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=timeout)
+
+
+def _gather(out_dir, world):
+    parts = [dict(np.load(os.path.join(out_dir, f"rank{r}.npz"))) for r in range(world)]
+    traj = np.concatenate([p["traj"] for p in parts], axis=1)
+    last = np.concatenate([p["last"] for p in parts], axis=0)
+    return traj, last, parts[0]["xsum"]
+
+
+def test_mean_field_simulator_is_rank_count_invariant(native, tmp_path):
+    ref_dir = tmp_path / "w1"
+    ref_dir.mkdir()
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "mp_gpu_worker.py"), "mean_field", str(ref_dir)],
+                       cwd=ROOT, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr[-3000:]
+    t1, l1, x1 = _gather(ref_dir, 1)
+    for world, port in ((2, 29611), (3, 29612)):
+        d = tmp_path / f"w{world}"
+        d.mkdir()
+        r = _launch(world, [os.path.join(ROOT, "tests", "mp_gpu_worker.py"), "mean_field", str(d)], port)
+        assert r.returncode == 0, r.stderr[-3000:]
+        tw, lw, xw = _gather(d, world)
+        scale = 1 + np.abs(t1).max()
+        assert np.max(np.abs(tw - t1)) < 2e-5 * scale, (world, np.max(np.abs(tw - t1)))
+        assert np.max(np.abs(lw - l1)) < 2e-5 * scale
+        assert np.allclose(xw, x1, rtol=1e-6, atol=1e-6 * np.abs(x1).max())
+
+
+def test_bench_two_ranks(native):
+    r = _launch(2, [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+                    "--particles", "65536", "--no-cpu-baseline", "--no-recovery"], 29613)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["value"] > 0 and out["config"]["particles_per_gpu"] == 65536
+    assert abs(out["value"] * out["ms_per_step"] / 1e3 - 2 * 65536 * 101) < 1e-6 * out["value"]
