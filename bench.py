@@ -50,8 +50,8 @@ HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--steps", type=int, default=100)
+    p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--config", default="C2", choices=["C2", "C3", "C4", "C5"])
     p.add_argument("--particles", type=int, default=0, help="particles per GPU (0 = the config's)")
     p.add_argument("--n-steps", type=int, default=100)
@@ -80,9 +80,22 @@ def cpu_model():
     return platform.processor() or "unknown"
 
 
-def timed(step, K, W, dev):
-    """W untimed warmup steps, then K steps between barrier+synchronize; max over ranks.
-    step(record) records record[0]/record[1] around the dominant kernel's launch."""
+RAMP_S = 0.3
+
+
+def timed(step, K, W, dev, ramp=None):
+    """Clock ramp, W untimed warmup steps, then K steps between barrier+synchronize; max over ranks.
+    step(record) records record[0]/record[1] around the dominant kernel's launch.
+    The ramp (untimed setup, like allocating the buffers) repeats the step's work for RAMP_S seconds
+    first: an MI355X raises its clocks over the first ~0.1-0.3 s of sustained load (one box measured a
+    20-step run 8 % below its 200-step rate without it; on another the ramp changed nothing).
+    ramp() (default: step(None)) must not feed any result of the run."""
+    ramp = ramp or (lambda: step(None))
+    t_end = time.perf_counter() + RAMP_S
+    while time.perf_counter() < t_end:
+        for _ in range(8):
+            ramp()
+        torch.cuda.synchronize()
     for _ in range(W):
         step(None)
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
@@ -167,7 +180,11 @@ def run_c2(a, rank, world, dev):
         last_res[0] = native.residual_kfp_quadratic(mom, theta, F, gamma, T)
         mom_total.add_(mom)
 
-    ms, kern_ms = timed(step, a.steps, a.warmup, dev)
+    def ramp():  # the same launch, results discarded (mom_total feeds the drift recovery)
+        native.sde_simulate(z0, n, T / n, gamma, pot, seed=seed, counter_offset=counter[0], particle_offset=poff,
+                            moments=True, out=bufs)
+
+    ms, kern_ms = timed(step, a.steps, a.warmup, dev, ramp=ramp)
     value = world * N * (n + 1) / (ms / 1e3)
     cfg = {"workload": "C2 kinetic OU d=4: EM simulate (traj+tau+last, fused moments) + KFP residual "
                        "value_and_grad", "dim": d, "n_steps": n, "particles_per_gpu": N, "total_time": T,
@@ -268,7 +285,11 @@ def run_c3(a, rank, world, dev):
         acc = dist.allreduce_sum(acc)
         native.residual_kfp_gmm_finalize(desc, acc)
 
-    ms, kern_ms = timed(step, a.steps, a.warmup, dev)
+    def ramp():  # the same launch, results discarded (mom_total feeds the drift recovery)
+        native.sde_simulate(z0, n, T / n, gamma, pot, seed=seed, counter_offset=counter[0], particle_offset=poff,
+                            moments=True, out=bufs)
+
+    ms, kern_ms = timed(step, a.steps, a.warmup, dev, ramp=ramp)
     value = world * N * (n + 1) / (ms / 1e3)
     cfg = {"workload": "C3 kinetic FP, GMM potential K=8, d=4: EM simulate (traj+tau+last) + fused GMM "
                        "residual value_and_grad over init/0T/terminal", "dim": d, "n_centers": K, "n_steps": n,
@@ -324,7 +345,11 @@ def run_c4(a, rank, world, dev):
         native.residual_kmv(both[: mom.numel()].view_as(mom), both[mom.numel():].view_as(wst), theta, A, gamma)
         coef_next[0] = host_coef(counter[0])
 
-    ms, kern_ms = timed(step, a.steps, a.warmup, dev)
+    def ramp():  # the same launch, results discarded (mom_total feeds the drift recovery)
+        native.sde_simulate(z0, n, T / n, gamma, pot, seed=seed, counter_offset=counter[0], particle_offset=poff,
+                            moments=True, out=bufs)
+
+    ms, kern_ms = timed(step, a.steps, a.warmup, dev, ramp=ramp)
     value = world * N * (n + 1) / (ms / 1e3)
     cfg = {"workload": "C4 kinetic McKean-Vlasov quadratic interaction d=8: interacting-particle EM "
                        "(one all-reduced mean field per update) + KMV residual value_and_grad",
