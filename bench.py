@@ -285,11 +285,7 @@ def run_c3(a, rank, world, dev):
         acc = dist.allreduce_sum(acc)
         native.residual_kfp_gmm_finalize(desc, acc)
 
-    def ramp():  # the same launch, results discarded (mom_total feeds the drift recovery)
-        native.sde_simulate(z0, n, T / n, gamma, pot, seed=seed, counter_offset=counter[0], particle_offset=poff,
-                            moments=True, out=bufs)
-
-    ms, kern_ms = timed(step, a.steps, a.warmup, dev, ramp=ramp)
+    ms, kern_ms = timed(step, a.steps, a.warmup, dev)
     value = world * N * (n + 1) / (ms / 1e3)
     cfg = {"workload": "C3 kinetic FP, GMM potential K=8, d=4: EM simulate (traj+tau+last) + fused GMM "
                        "residual value_and_grad over init/0T/terminal", "dim": d, "n_centers": K, "n_steps": n,
@@ -345,11 +341,7 @@ def run_c4(a, rank, world, dev):
         native.residual_kmv(both[: mom.numel()].view_as(mom), both[mom.numel():].view_as(wst), theta, A, gamma)
         coef_next[0] = host_coef(counter[0])
 
-    def ramp():  # the same launch, results discarded (mom_total feeds the drift recovery)
-        native.sde_simulate(z0, n, T / n, gamma, pot, seed=seed, counter_offset=counter[0], particle_offset=poff,
-                            moments=True, out=bufs)
-
-    ms, kern_ms = timed(step, a.steps, a.warmup, dev, ramp=ramp)
+    ms, kern_ms = timed(step, a.steps, a.warmup, dev)
     value = world * N * (n + 1) / (ms / 1e3)
     cfg = {"workload": "C4 kinetic McKean-Vlasov quadratic interaction d=8: interacting-particle EM "
                        "(one all-reduced mean field per update) + KMV residual value_and_grad",

@@ -11,6 +11,7 @@
 // terminal = last) that the parametric-quadratic residual needs, so the KFP residual
 // (kinetic_fokker_planck.py:33-58) costs no second pass over the trajectory.
 #include <math.h>
+#include <stdlib.h>
 
 #include "common.h"
 
@@ -19,6 +20,7 @@ namespace pdeinv {
 struct SdeArgs {
   int64_t N, poff, ld_z0;
   int32_t n_steps, random_shift, K, has_center;
+  int32_t remap;  // 1 (default): XCD-contiguous block order (xcd_block); PDEINV_SIM_REMAP=0 disables
   float dt, gamma, ns, neg_half_inv_s2_log2e, inv_s2, l2s;
   uint32_t k0, k1, ctr_off;
   const float* noise;
@@ -118,6 +120,19 @@ __device__ __forceinline__ void grad_gmm(const SdeArgs& a, const GmmCentres<D, K
   const float inv = __builtin_amdgcn_rcpf(den);
 #pragma unroll
   for (int i = 0; i < D; ++i) g[i] = a.inv_s2 * fmaf(-acc[i], inv, q[i]);
+}
+
+// Dispatch order -> particle block: the hardware hands consecutive workgroups to the 8 XCDs in
+// turn (b -> XCD b % 8); this map gives XCD x the contiguous block range [x*nb/8, (x+1)*nb/8), so
+// each XCD's L2 sees one contiguous stretch of every trajectory slab instead of every 8th 8 KiB
+// piece. Measured on the C2 launch, same buffers A/B in one process: 1.53 -> 1.46 ms and
+// 1.26 -> 1.20 ms (4-5 %, every allocation; tools/sim_alloc.py, profiles/r01_sim_remap_ab.log).
+// Results are unchanged: a particle's numbers depend only on its global id, and the moment
+// partial slots are indexed by the mapped block. (Not used by mf_step_kernel: there the C4 bench
+// measured 6.8 ms without vs 7.5 ms with it, across processes.)
+__device__ __forceinline__ int xcd_block(int b, int nb) {
+  const int q = nb / 8, r = nb % 8, x = b % 8, l = b / 8;
+  return x < r ? x * (q + 1) + l : r * (q + 1) + (x - r) * q + l;
 }
 
 // Store modes for the per-step trajectory rows (M = 2d floats per particle):
@@ -275,7 +290,8 @@ __global__ __launch_bounds__(kBlock, MINW) void sde_simulate_kernel(SdeArgs a, c
                                                               float* __restrict__ last,
                                                               float* __restrict__ partials) {
   constexpr int M = 2 * D;
-  const int64_t i_raw = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int bid = a.remap ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  const int64_t i_raw = (int64_t)bid * kBlock + threadIdx.x;
   const bool active = i_raw < a.N;
   const int64_t i = active ? i_raw : a.N - 1;  // inactive lanes compute on a valid row, store nothing
   const float w = active ? 1.f : 0.f;
@@ -295,7 +311,7 @@ __global__ __launch_bounds__(kBlock, MINW) void sde_simulate_kernel(SdeArgs a, c
     MomentAcc<M> init;
     init.zero();
     init.add(z, w);
-    block_reduce_to_slab(init.v, L, lds, partials, blockIdx.x, nb);
+    block_reduce_to_slab(init.v, L, lds, partials, bid, nb);
   }
 
   const float tau0 = a.random_shift ? shift_u(a, plo, phi, i) * a.dt : 0.f;
@@ -356,11 +372,11 @@ __global__ __launch_bounds__(kBlock, MINW) void sde_simulate_kernel(SdeArgs a, c
   if constexpr (MOM) {
     float mv[L];
     acc.finish((float)a.n_steps, w, mv);
-    block_reduce_to_slab(mv, L, lds, partials + (int64_t)L * nb, blockIdx.x, nb);
+    block_reduce_to_slab(mv, L, lds, partials + (int64_t)L * nb, bid, nb);
     MomentAcc<M> term;
     term.zero();
     term.add(z, w);
-    block_reduce_to_slab(term.v, L, lds, partials + (int64_t)2 * L * nb, blockIdx.x, nb);
+    block_reduce_to_slab(term.v, L, lds, partials + (int64_t)2 * L * nb, bid, nb);
   }
 }
 
@@ -466,6 +482,10 @@ static int build_args(const pdeinv_sde_desc* d, SdeArgs& a) {
   a.ctr_off = d->counter_offset;
   a.noise = d->d_noise;
   a.shift_u = d->d_shift_u;
+  {
+    const char* r = getenv("PDEINV_SIM_REMAP");  // A/B switch for tools/sim_alloc.py
+    a.remap = r ? atoi(r) : 1;
+  }
   const pdeinv_potential& p = d->potential;
   int n_params = 0;
   switch (p.kind) {

@@ -97,6 +97,31 @@ def test_sde_philox_vs_c_oracle(native, oracle_lib, d):
     assert np.max(np.abs(res["last"].cpu().numpy() - o["last"])) < 2e-4
 
 
+@pytest.mark.parametrize("poff", [(1 << 32) - 128, (1 << 32) - 100, (1 << 33) + 3, 0])
+@pytest.mark.parametrize("kind", ["quadratic", "gmm"])
+def test_sde_philox_id_high_word(native, oracle_lib, poff, kind):
+    """Particle ids across a multiple of 2^32: the uniform-high-word kernel (64-aligned offsets or
+    no crossing) and the general one (unaligned + crossing) draw the oracle's stream."""
+    d, N, n = 4, 700, 20
+    rng = np.random.default_rng(7)
+    z0 = rng.standard_normal((N, 2 * d)).astype(np.float32)
+    if kind == "quadratic":
+        params, pot = nr.problem_constants(d), dict(kind=native.POT_QUADRATIC)
+        pot["params"] = params
+        ok = {}
+    else:
+        params = rng.uniform(-2, 2, (3, d)).astype(np.float32)
+        pot = dict(kind=native.POT_GMM, params=params, n_centers=3, sigma=1.0)
+        ok = dict(n_centers=3, sigma=1.0)
+    res = native.sde_simulate(_t(z0), n, 0.02, 0.5, pot, seed=99, counter_offset=5, particle_offset=poff)
+    o = oracle_lib.sde_simulate(z0, n, 0.02, 0.5, kind, params, seed=99, counter_offset=5, particle_offset=poff,
+                                **ok)
+    assert np.array_equal(res["tau"].cpu().numpy(), o["tau"])
+    scale = np.abs(o["traj"]).max(axis=(0, 2), keepdims=True) + 1.0
+    assert np.max(np.abs(res["traj"].cpu().numpy() - o["traj"]) / scale) < 1e-4
+    assert np.max(np.abs(res["last"].cpu().numpy() - o["last"]) / scale[0]) < 1e-4
+
+
 def test_sde_moments_match_discrete_chain(native):
     """Philox-mode law == exact law of the chain, 5 sigma_MC."""
     d, N, n, T = 4, 1 << 18, 100, 2.0
