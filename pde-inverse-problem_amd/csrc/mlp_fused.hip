@@ -178,7 +178,7 @@ __device__ __forceinline__ void store_b(const GemmArgs& a, const float (&rb)[BK 
 }
 
 template <int S, int BM, int BN, int WGM, int AM, int BMD, int EM>
-__global__ __launch_bounds__(kT) void fgemm(GemmArgs a) {
+__global__ __launch_bounds__(kT, 2) void fgemm(GemmArgs a) {
   constexpr int WGN = 4 / WGM;
   constexpr int WM = BM / WGM, WN = BN / WGN, MI = WM / 32, NI = WN / 32;
   static_assert(MI >= 1 && NI >= 1 && MI * 32 == WM && NI * 32 == WN, "wave tile must be 32-multiples");
