@@ -61,6 +61,16 @@ __device__ __forceinline__ void sto(float* base, uint32_t idx, float v) {
   *reinterpret_cast<float*>(reinterpret_cast<char*>(base) + (idx << 2)) = v;
 }
 
+// Workgroup placement: the dispatcher hands linear workgroup b to XCD b % 8. xcd_linear(b, nb)
+// renumbers so that each XCD runs one contiguous range of logical ids; kernels then split the
+// logical id so that the workgroups that read the same rows (the column blocks of a row GEMM, the
+// output tiles of a weight-gradient slice) are consecutive — same XCD, resident together, so the
+// second reader of a plane hits that XCD's L2 instead of HBM. Pure renumbering (same results).
+__device__ __forceinline__ int xcd_linear(int b, int nb) {
+  const int q = nb / 8, r = nb % 8, x = b % 8, l = b / 8;
+  return x < r ? x * (q + 1) + l : r * (q + 1) + (x - r) * q + l;
+}
+
 enum { A_RAW1 = 0, A_FWD, A_S1MUL, A_U, A_S3 };
 enum { B_NN = 0, B_NT };
 enum { E_ACT_FWD = 0, E_OUT, E_STORE, E_STORE3, E_SEEDS, E_ACT_BWD };
@@ -190,12 +200,15 @@ __global__ __launch_bounds__(kT, 2) void fgemm(GemmArgs a) {
   float* Bs = As + S * BK * LDA;    // [BK][LDB]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WGN, wn = wave - (wave / WGN) * WGN, l31 = lane & 31, hi = lane >> 5;
-  const int n0 = blockIdx.y * BN;
+  const int gx = gridDim.x, gy = gridDim.y;
+  const int lid = xcd_linear(blockIdx.x + blockIdx.y * gx, gx * gy);
+  const int bx = lid / gy, by = lid - (lid / gy) * gy;  // column blocks of a row block adjacent
+  const int n0 = by * BN;
   [[maybe_unused]] float pacc[NI];
 #pragma unroll
   for (int ni = 0; ni < NI; ++ni) pacc[ni] = 0.f;
 
-  for (int mb = blockIdx.x; mb < a.n_mblocks; mb += gridDim.x) {
+  for (int mb = bx; mb < a.n_mblocks; mb += gx) {
     const int r0 = mb * BM;
     f32x16 acc[S][MI][NI];
 #pragma unroll
@@ -341,7 +354,7 @@ __global__ __launch_bounds__(kT, 2) void fgemm(GemmArgs a) {
       float s = 0.f;
 #pragma unroll
       for (int w = 0; w < WGM; ++w) s += red[w * BN + c];
-      if (n0 + c < a.N) a.part[(int64_t)blockIdx.x * a.N + n0 + c] = s;
+      if (n0 + c < a.N) a.part[(int64_t)bx * a.N + n0 + c] = s;
     }
   }
 }
@@ -501,8 +514,11 @@ __global__ __launch_bounds__(kT) void fwgrad(WgradArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1, l31 = lane & 31, hi = lane >> 5;
   const int tiles_n = (a.n_out + BN - 1) / BN;
-  const int i0 = (blockIdx.x / tiles_n) * BM, n0 = (blockIdx.x % tiles_n) * BN;
-  const int rs0 = (int)((int64_t)blockIdx.y * a.rows_per_slice);
+  const int n_tiles = gridDim.x;
+  const int lid = xcd_linear(blockIdx.x + blockIdx.y * n_tiles, n_tiles * gridDim.y);
+  const int tile = lid % n_tiles, slice = lid / n_tiles;  // the tiles of one row slice adjacent
+  const int i0 = (tile / tiles_n) * BM, n0 = (tile % tiles_n) * BN;
+  const int rs0 = (int)((int64_t)slice * a.rows_per_slice);
   const int rs1 = (int)(rs0 + a.rows_per_slice < a.R ? rs0 + a.rows_per_slice : a.R);
   f32x16 acc[MI][NI];
 #pragma unroll
@@ -597,7 +613,7 @@ __global__ __launch_bounds__(kT) void fwgrad(WgradArgs a) {
         }
       }
   }
-  float* out = a.part + (int64_t)blockIdx.y * a.n_in * a.n_out;
+  float* out = a.part + (int64_t)slice * a.n_in * a.n_out;
 #pragma unroll
   for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
