@@ -13,8 +13,11 @@
 #include <stdlib.h>
 typedef float f4 __attribute__((ext_vector_type(4)));
 
-template <int LAYOUT>
-__global__ __launch_bounds__(256) void writer(f4* traj, long N, int n, int work) {
+// FEAT bits (time-major only): 1 = also store tau [n, N] (4 B per lane per step, nt);
+// 2 = stage the rows through LDS as the simulator does (row -> LDS -> 16 B chunks)
+template <int LAYOUT, int FEAT = 0>
+__global__ __launch_bounds__(256) void writer(f4* traj, long N, int n, int work, float* tau) {
+  __shared__ f4 stage[(FEAT & 2) ? 512 : 1];
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const long w = i >> 6;  // global wave
@@ -25,9 +28,19 @@ __global__ __launch_bounds__(256) void writer(f4* traj, long N, int n, int work)
     if (LAYOUT == 0) dst = traj + ((long)s * N + w * 64) * 2;
     else if (LAYOUT == 1) dst = traj + (w * n + s) * 128;
     else dst = traj + ((long)blockIdx.x * n + s) * 512 + wave * 128;
-    const f4 a = f4{acc, v + 1, v + 2, v + 3}, b = f4{v + 4, v + 5, v + 6, acc};
+    f4 a = f4{acc, v + 1, v + 2, v + 3}, b = f4{v + 4, v + 5, v + 6, acc};
+    if constexpr ((FEAT & 2) != 0) {
+      f4* slot = stage + wave * 128;
+      slot[2 * lane] = a;
+      slot[2 * lane + 1] = b;
+      __builtin_amdgcn_wave_barrier();
+      a = slot[lane];
+      b = slot[64 + lane];
+      __builtin_amdgcn_wave_barrier();
+    }
     __builtin_nontemporal_store(a, dst + lane);
     __builtin_nontemporal_store(b, dst + 64 + lane);
+    if constexpr ((FEAT & 1) != 0) __builtin_nontemporal_store(acc, tau + (long)s * N + i);
     v += 1.f;
   }
 }
@@ -54,14 +67,21 @@ int main(int argc, char** argv) {
         printf("contiguous alloc failed\n");
         continue;
       }
-      for (int work : {0, 64}) {
-        float ms[4];
-        for (int L = 0; L < 4; ++L) {
+      float* tau;
+      CK(hipMalloc(&tau, (size_t)N * n * 4));
+      for (int work : {0, 64, 200}) {
+        float ms[8];
+        for (int L = 0; L < 8; ++L) {
+          // dynamic LDS 24 KiB on variant 7: at most 6 workgroups per CU (the simulator's ~5)
           auto run = [&]() {
-            if (L == 0) writer<0><<<N / 256, 256>>>(p, N, n, work);
-            if (L == 1) writer<1><<<N / 256, 256>>>(p, N, n, work);
-            if (L == 2) writer<2><<<N / 256, 256>>>(p, N, n, work);
+            if (L == 0) writer<0><<<N / 256, 256>>>(p, N, n, work, tau);
+            if (L == 1) writer<1><<<N / 256, 256>>>(p, N, n, work, tau);
+            if (L == 2) writer<2><<<N / 256, 256>>>(p, N, n, work, tau);
             if (L == 3) CK(hipMemsetAsync(p, 0, bytes, nullptr));
+            if (L == 4) writer<0, 1><<<N / 256, 256>>>(p, N, n, work, tau);
+            if (L == 5) writer<0, 2><<<N / 256, 256>>>(p, N, n, work, tau);
+            if (L == 6) writer<0, 3><<<N / 256, 256>>>(p, N, n, work, tau);
+            if (L == 7) writer<0, 3><<<N / 256, 256, 24576>>>(p, N, n, work, tau);
           };
           for (int r = 0; r < 3; ++r) run();
           CK(hipEventRecord(e0, nullptr));
@@ -71,9 +91,10 @@ int main(int argc, char** argv) {
           CK(hipEventElapsedTime(&ms[L], e0, e1));
           ms[L] /= 10;
         }
-        printf("%-10s set %d work %2d: time-major %.0f | wave-tiles %.0f | block-tiles %.0f | memset %.0f GB/s\n",
+        printf("%-10s set %d work %3d: time-major %.0f | wave-tiles %.0f | block-tiles %.0f | memset %.0f | "
+               "tm+tau %.3f ms | tm+lds %.3f ms | tm+tau+lds %.3f ms | +occ6 %.3f ms\n",
                kind ? "contiguous" : "hipMalloc", k, work, bytes / ms[0] / 1e6, bytes / ms[1] / 1e6,
-               bytes / ms[2] / 1e6, bytes / ms[3] / 1e6);
+               bytes / ms[2] / 1e6, bytes / ms[3] / 1e6, ms[4], ms[5], ms[6], ms[7]);
         fflush(stdout);
       }
       // not freed: the next set must get different memory
