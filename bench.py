@@ -299,10 +299,13 @@ def run_c3(a, rank, world, dev):
 
 
 def run_c4(a, rank, world, dev):
+    """Kinetic McKean-Vlasov d=8 (BASELINE configs[3]): the fused driver (utils/mean_field.py) — noise/z0
+    sums, ONE all-reduce per simulate, the closed-form mean path, all n+1 updates in registers — then the
+    KMV residual from one fused read of the trajectory (per-stamp moments + d_s log rho weights)."""
+    import ctypes
     from example_problems.kinetic_fokker_planck_example_OU import initialize_configuration
     from example_problems.kinetic_mckean_vlasov_example_quadratic import dlogrho_coefficients
-    from core.potential import MeanFieldQuadraticPotential
-    from utils.mean_field import simulate_mean_field, stamp_times
+    from utils.mean_field import stamp_times
     from utils import prng
 
     d, n, T = 8, a.n_steps, 2.0
@@ -316,7 +319,8 @@ def run_c4(a, rank, world, dev):
     theta = torch.zeros(d * d + d, device=dev)
     key = prng.Key(0x5EED_0004)
     counter = [0]
-    pot = MeanFieldQuadraticPotential(A)
+    bufs = {"traj": torch.empty((n, N, 2 * d), device=dev), "tau": torch.empty((n, N), device=dev),
+            "last": torch.empty((N, 2 * d), device=dev)}
 
     def host_coef(ctr):
         # the shared-clock stamps are known from (seed, counter) without touching the device, so the
@@ -325,31 +329,53 @@ def run_c4(a, rank, world, dev):
         return torch.from_numpy(dlogrho_coefficients(tau, ic, d).astype(np.float32)).pin_memory()
 
     coef_next = [host_coef(counter[0])]
+    ev = {"sums": [], "res": []}
 
     def step(record):
         coef = coef_next[0].to(dev, non_blocking=True)
+        desc, keep = native.mf_desc(N, d, n, T / n, gamma, A, seed=key.seed, counter_offset=counter[0],
+                                    particle_offset=poff)
+        e0 = torch.cuda.Event(enable_timing=True) if record is not None else None
+        if e0 is not None:
+            e0.record()
+        sums = dist.allreduce_sum(native.mf_sums(desc, z0))  # the one collective of the simulate
+        xbar, _ = native.mf_mean_path(desc, sums, xsum=False)
+        desc.d_meanfield = ctypes.c_void_p(xbar.data_ptr())
         if record is not None:
             record[0].record()
-        r = simulate_mean_field(z0, n, T / n, key, pot, gamma, particle_offset=poff, counter_offset=counter[0])
+        native.sde_simulate_desc(desc, z0, bufs["traj"], bufs["tau"], bufs["last"])
         if record is not None:
             record[1].record()
+        del keep
         counter[0] = (counter[0] + n + 1) & 0xFFFFFFFF
-        traj = r["traj"]
-        mom = native.moments_batched(traj, n, N, 2 * d, N * 2 * d, 2 * d)
-        wst, _ = native.kmv_weights(d, gamma, coef, traj, n, N, N * 2 * d, 2 * d)
+        mom, wst = native.kmv_moments_weights(d, gamma, coef, bufs["traj"], n, N, N * 2 * d, 2 * d)
+        if record is not None:
+            e3 = torch.cuda.Event(enable_timing=True)
+            e3.record()
+            ev["sums"].append((e0, record[0]))
+            ev["res"].append((record[1], e3))
         both = dist.allreduce_sum(torch.cat([mom.reshape(-1), wst.reshape(-1)]))
         native.residual_kmv(both[: mom.numel()].view_as(mom), both[mom.numel():].view_as(wst), theta, A, gamma)
         coef_next[0] = host_coef(counter[0])
 
     ms, kern_ms = timed(step, a.steps, a.warmup, dev)
     value = world * N * (n + 1) / (ms / 1e3)
-    cfg = {"workload": "C4 kinetic McKean-Vlasov quadratic interaction d=8: interacting-particle EM "
-                       "(one all-reduced mean field per update) + KMV residual value_and_grad",
+    cfg = {"workload": "C4 kinetic McKean-Vlasov quadratic interaction d=8: interacting-particle EM (closed-form "
+                       "mean path from one all-reduced noise/z0 sum per simulate, all updates in registers) + KMV "
+                       "residual value_and_grad (one fused read of the trajectory)",
            "dim": d, "n_steps": n, "particles_per_gpu": N, "total_time": T, "gamma": gamma,
            "parallelism": f"dp{world}"}
-    mf_bytes = N * (n + 1) * (16 * d) + N * n * 4  # each update reads and writes the state; tau
-    return base_record(a, world, value, ms, cfg, kern_ms, mf_bytes,
-                       "101 x (mf_step_kernel<8> + slab reduce + all-reduce): the whole simulator")
+    out = base_record(a, world, value, ms, cfg, kern_ms, sim_bytes(N, n, d),
+                      "sde_simulate_kernel<8,MEANFIELD_QUADRATIC,staged> (all 101 updates)",
+                      traffic_from_profiles("sde_simulate_C4_bytes_per_launch") if (N, n) == (1 << 21, 100) else None)
+    sums_ms = float(np.mean([s.elapsed_time(e) for s, e in ev["sums"]]))
+    res_ms = float(np.mean([s.elapsed_time(e) for s, e in ev["res"]]))
+    res_bytes = N * n * 8 * d
+    out["mean_path"] = {"kernel": "mf_sums_kernel<8> + slab reduce (+ all-reduce) + mf_path_kernel", "ms": sums_ms,
+                        "normals_per_s": N * (n + 1) * d / (sums_ms / 1e3)}
+    out["residual"] = {"kernel": "kmv_moments_weights_kernel<8> + slab reduce + split", "ms": res_ms,
+                       "algorithmic_bytes": res_bytes, "GBps": res_bytes / (res_ms / 1e3) / 1e9}
+    return out
 
 
 def run_c5(a, rank, world, dev):

@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define PDEINV_ABI_VERSION 5
+#define PDEINV_ABI_VERSION 6
 #define PDEINV_MAX_DIM 16          /* d (configuration-space dimension) */
 #define PDEINV_MAX_PARAMS 256      /* floats of potential parameters passed by value */
 
@@ -63,8 +63,10 @@ typedef enum {
   /* GMM: U(x) = -logsumexp_k(-|x-mu_k|^2 / (2 sigma^2)); grad by the analytic softmax form.
      params = mu[K*d] row-major (core/potential.py:32-61). */
   PDEINV_POT_GMM = 1,
-  /* McKean–Vlasov quadratic interaction: grad U(q_i) = A (q_i - xbar), xbar read from device
-     (one all-reduced mean per update). params = A[d*d]. */
+  /* McKean–Vlasov quadratic interaction: grad U(q_i) = A (q_i - xbar_s), xbar_s the ensemble mean
+     of the positions before update s. params = A[d*d]. Two drivers:
+     pdeinv_sde_simulate with d_meanfield = the precomputed mean path (pdeinv_mf_sums ->
+     all-reduce -> pdeinv_mf_mean_path), or update by update with pdeinv_mf_step. */
   PDEINV_POT_MEANFIELD_QUADRATIC = 2,
   /* U = 0 (core/potential.py VoidPotential). */
   PDEINV_POT_NONE = 3
@@ -111,7 +113,8 @@ typedef struct {
   pdeinv_potential potential;
   const float* d_noise;     /* nullable: explicit xi [n_steps+1, N, d] (parity mode) */
   const float* d_shift_u;   /* nullable: explicit u [N] in [0,1) for tau0 = u*dt */
-  const float* d_meanfield; /* MEANFIELD only: xbar [n_steps+1, d] fp32, one row per update */
+  const float* d_meanfield; /* MEANFIELD + pdeinv_sde_simulate: xbar [n_steps+1, d] fp32, the mean
+                               path of pdeinv_mf_mean_path (row s is used by update s) */
 } pdeinv_sde_desc;
 
 int pdeinv_moment_len(int m); /* 1 + m + m(m+1)/2 */
@@ -130,6 +133,23 @@ size_t pdeinv_mf_workspace_bytes(const pdeinv_sde_desc* desc);
 int pdeinv_mf_step(const pdeinv_sde_desc* desc, int32_t s, const float* d_z, float* d_z_out,
                    float* d_tau_row, const float* d_tau0, const double* d_xbar_sum,
                    void* d_workspace, double* d_xsum, void* stream);
+/* McKean–Vlasov, fused multi-step path. For the quadratic interaction the ensemble mean obeys
+ *   vbar' = (1 - gamma h) vbar + sqrt(h) noise_scale xibar_s,  xbar' = xbar + h vbar'
+ * exactly (the drift A (x_i - xbar) averages to zero), xibar_s the mean of update s's noise — a
+ * function of the particle ids and the RNG stream only. So the mean path needs ONE reduction:
+ *   pdeinv_mf_sums:  d_sums [pdeinv_mf_sums_len(desc)] fp64 =
+ *                    [count, sum x0 (d), sum v0 (d), sum_i xi_{i,s} (d) for s = 0..n_steps]
+ *                    over this call's particles (rank-local; all-reduce(sum) it across ranks);
+ *   pdeinv_mf_mean_path: the all-reduced sums -> d_xbar [n_steps+1, d] fp32 (mean before update s)
+ *                    and optionally d_xsum [n_steps+2, 1+d] fp64 = [count, count * xbar_s];
+ *   pdeinv_sde_simulate(desc with d_meanfield = d_xbar): all n_steps+1 updates in registers.
+ * The explicit-noise mode (d_noise) is honoured by pdeinv_mf_sums and the simulator alike. */
+int64_t pdeinv_mf_sums_len(const pdeinv_sde_desc* desc);
+size_t pdeinv_mf_sums_workspace_bytes(const pdeinv_sde_desc* desc);
+int pdeinv_mf_sums(const pdeinv_sde_desc* desc, const float* d_z0, void* d_workspace, double* d_sums,
+                   void* stream);
+int pdeinv_mf_mean_path(const pdeinv_sde_desc* desc, const double* d_sums, float* d_xbar, double* d_xsum,
+                        void* stream);
 /* tau0 per particle (u*dt from the shift stream, or d_shift_u) -> d_tau0 [N]. */
 int pdeinv_sde_tau0(const pdeinv_sde_desc* desc, float* d_tau0, void* stream);
 
@@ -254,6 +274,14 @@ size_t pdeinv_kmv_weights_workspace_bytes(int64_t n_sets, int64_t n_rows, int32_
 int pdeinv_kmv_weights(int32_t dim, float gamma, const float* d_coef, const float* d_z,
                        int64_t n_sets, int64_t n_rows, int64_t set_stride, int64_t ld,
                        float* d_ds, void* d_workspace, double* d_out, void* stream);
+
+/* Fused pdeinv_moments_batched(m = 2d) + pdeinv_kmv_weights: one read of each row z = [x, v] gives
+ * d_mom [n_sets][pdeinv_moment_len(2d)] and d_wstats [n_sets][pdeinv_moment_len(d)] (the same sums,
+ * the same layout). dim <= 8. Workspace: pdeinv_kmv_moments_weights_workspace_bytes(). */
+size_t pdeinv_kmv_moments_weights_workspace_bytes(int64_t n_sets, int64_t n_rows, int32_t dim);
+int pdeinv_kmv_moments_weights(int32_t dim, float gamma, const float* d_coef, const float* d_z, int64_t n_sets,
+                               int64_t n_rows, int64_t set_stride, int64_t ld, void* d_workspace, double* d_mom,
+                               double* d_wstats, void* stream);
 
 /* KMV residual for Phi_theta(y) = y . Dense_d(y) (…_quadratic.py:205-216) from the per-time-stamp
  * moments of z (mom [n_sets][moment_len(2d)]) and weighted stats (wst [n_sets][moment_len(d)]):

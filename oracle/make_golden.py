@@ -79,6 +79,39 @@ def main():
     np.savez_compressed(os.path.join(OUT, "kmv_pairwise.npz"), K=K, b=b, x=x, v=v, tau=tau, F=F, loss=loss,
                         loss_gt=loss_gt, grad=g)
 
+    # the same at the C4 dimension d = 8 (BASELINE config C4: kinetic McKean-Vlasov, quadratic, d = 8)
+    d, m_, nt = 8, 150, 2
+    F = nr.problem_constants(d)
+    cfg = nr.ou_configuration(F, gamma=1.0)
+    x = rng.standard_normal((m_, nt, d)); v = rng.standard_normal((m_, nt, d))
+    tau = np.array([0.4, 1.3])
+    K = 0.2 * rng.standard_normal((d, d)); b = 0.2 * rng.standard_normal(d)
+    loss, loss_gt = nr.kmv_pairwise_loss(K, b, x, v, tau, cfg)
+    g = nr.fd_grad(lambda th: nr.kmv_pairwise_loss(th[:64].reshape(8, 8), th[64:], x, v, tau, cfg)[0],
+                   np.concatenate([K.ravel(), b]), eps=1e-6)
+    np.savez_compressed(os.path.join(OUT, "kmv_pairwise_d8.npz"), K=K, b=b, x=x, v=v, tau=tau, F=F, loss=loss,
+                        loss_gt=loss_gt, grad=g)
+
+    # the reference's runnable KMV recipe (scripts/parametric/KMV/run_quadratic_online.sh:15-19: d = 2,
+    # one time stamp, 5 000 samples per stamp, T = 1, exact OU samples at a uniform time s0): there the
+    # reference's [n_time, n] -> [n, n_time] reshape of d_s log rho (kinetic_mckean_vlasov.py:57-72)
+    # coincides with the build's transposed pairing, so this fixture is the reference's
+    # own pairing. Pair tensor of 25 M pairs, built 500 particles at a time.
+    d, m_ = 2, 5000
+    F = nr.problem_constants(d)
+    cfg = nr.ou_configuration(F, gamma=1.0)
+    s0 = 0.37
+    mean, P = nr.ou_mean_cov(s0, cfg)
+    z = rng.multivariate_normal(mean, P, size=m_).astype(np.float32).astype(np.float64)  # stored as fp32
+    x, v = z[:, None, :d], z[:, None, d:]
+    tau = np.array([s0])
+    K = 0.3 * rng.standard_normal((d, d)); b = 0.2 * rng.standard_normal(d)
+    loss, loss_gt = nr.kmv_pairwise_loss(K, b, x, v, tau, cfg, chunk=500)
+    g = nr.fd_grad(lambda th: nr.kmv_pairwise_loss(th[:4].reshape(2, 2), th[4:], x, v, tau, cfg, chunk=500)[0],
+                   np.concatenate([K.ravel(), b]), eps=1e-6)
+    np.savez_compressed(os.path.join(OUT, "kmv_pairwise_recipe.npz"), K=K, b=b, x=x.astype(np.float32),
+                        v=v.astype(np.float32), tau=tau, F=F, loss=loss, loss_gt=loss_gt, grad=g)
+
     # ds log rho KAT inputs/outputs (test_partial_s_log_density.py:241-311 shape: d = 10, s = 0.1)
     d = 10
     F = nr.problem_constants(d)

@@ -185,6 +185,32 @@ def em_chain_moments(tilde_F, gamma, dt, n_steps, m0, P0, noise_scale=SQRT2, ran
     return mean_tr, sec_tr, mean_last, sec_last
 
 
+def mf_mean_path(sums, d, n_steps, dt, tau0, gamma, noise_scale=SQRT2):
+    """Closed-form mean path of the interacting (McKean–Vlasov) ensemble — the restatement behind
+    utils/mean_field.py's fused driver (sde.hip mf_path_kernel). The quadratic interaction's drift
+    A (x_i - xbar) (kinetic_mckean_vlasov.py:20-23 for Phi* = x^T A x / 2) averages to zero over the
+    ensemble, so the update of sampling_utils.py:17,20 averaged over particles is
+        vbar' = (1 - gamma h) vbar + sqrt(h) ns xibar_s ,  xbar' = xbar + h vbar'.
+    sums = [count, sum x0 (d), sum v0 (d), sum_i xi_{i,s} (d) for s = 0..n]. Returns xbar [n+2, d]:
+    row s is the mean before update s (row n+1: after the last update). h_s = tau0, dt, ..., dt - tau0
+    (the particles' fp32 step sizes)."""
+    sums = np.asarray(sums, np.float64)
+    cnt = sums[0]
+    inv = 1.0 / cnt if cnt > 0 else 0.0
+    xb, vb = sums[1:1 + d] * inv, sums[1 + d:1 + 2 * d] * inv
+    xi = sums[1 + 2 * d:].reshape(n_steps + 1, d) * inv
+    out = np.zeros((n_steps + 2, d))
+    dt32, t032 = np.float32(dt), np.float32(tau0)
+    for s in range(n_steps + 1):
+        out[s] = xb
+        h = t032 if s == 0 else (dt32 - t032 if s == n_steps else dt32)
+        sh = float(np.sqrt(np.float32(h)) * np.float32(noise_scale))
+        vb = vb - gamma * float(h) * vb + sh * xi[s]
+        xb = xb + float(h) * vb
+    out[n_steps + 1] = xb
+    return out
+
+
 # --------------------------------------------------------------------------------------
 # moments layout of include/pdeinv.h
 # --------------------------------------------------------------------------------------
@@ -381,27 +407,33 @@ def partial_s2_log_density(s, x, cfg):
 # --------------------------------------------------------------------------------------
 # KMV residual: methods/consistency_instances/kinetic_mckean_vlasov.py:11-120 (pairwise, O(n^2))
 # --------------------------------------------------------------------------------------
-def kmv_pairwise_loss(K, b, x, v, tau, cfg):
+def kmv_pairwise_loss(K, b, x, v, tau, cfg, chunk=None):
     """Literal restatement with the [m, n, n_time, d] pairwise tensor (:20-23, :74-97), for
     Phi_theta(y) = y . (y K + b) (…_quadratic.py:205-216), Phi* = 0.5 y^T tilde_F y (:193-203).
-    x, v: [n, n_time, d]; tau [n_time]."""
+    x, v: [n, n_time, d]; tau [n_time]. `chunk` bounds memory for large n: the pair tensor is built
+    for `chunk` particles i at a time (the means over the reference axis j are unchanged)."""
     K = np.asarray(K, np.float64); b = np.asarray(b, np.float64)
     S = K + K.T
     F = cfg["tilde_F"]
     gamma = cfg["gamma_friction"]
     x = np.asarray(x, np.float64); v = np.asarray(v, np.float64)
-    y = x[None] - x[:, None]  # [m, n, T, d] (x_minus_ref, :23)
-    gPhi = y @ S.T + b
-    Phi = np.einsum("...i,ij,...j->...", y, K, y) + y @ b
-    gTrue = y @ F.T
-    loss_nabla = np.mean(np.sum(np.mean(gPhi, 0) ** 2, -1))
+    n = x.shape[0]
+    cb = n if chunk is None else int(chunk)
+    mg, mP, mT = [], [], []
+    for i0 in range(0, n, cb):
+        y = x[None, i0:i0 + cb] - x[:, None]  # [m, chunk, T, d] (x_minus_ref, :23): y[j, i] = x_i - x_j
+        mg.append(np.mean(y @ S.T + b, 0))
+        mP.append(np.mean(np.einsum("...i,ij,...j->...", y, K, y) + y @ b, 0))
+        mT.append(np.mean(y @ F.T, 0))
+    gPhi_m, Phi_m, gTrue_m = (np.concatenate(a, 0) for a in (mg, mP, mT))
+    loss_nabla = np.mean(np.sum(gPhi_m ** 2, -1))
     loss_hess = np.mean(np.einsum("nti,ij,ntj->nt", v, S, v))  # Hessian constant in j
     ps = np.stack([partial_s_log_density(t, x[:, k], cfg) for k, t in enumerate(tau)], 1)
     ps2 = np.stack([partial_s2_log_density(t, x[:, k], cfg) for k, t in enumerate(tau)], 1)
-    loss_value = np.mean(np.mean(Phi, 0) * (ps2 + ps ** 2 + gamma * ps))
-    loss_true = np.mean(np.sum(np.mean(gTrue, 0) ** 2, -1))
+    loss_value = np.mean(Phi_m * (ps2 + ps ** 2 + gamma * ps))
+    loss_true = np.mean(np.sum(gTrue_m ** 2, -1))
     loss = loss_nabla - 2 * loss_hess + 2 * loss_value + loss_true
-    loss_gt = np.mean(np.sum((np.mean(gTrue, 0) - np.mean(gPhi, 0)) ** 2, -1))
+    loss_gt = np.mean(np.sum((gTrue_m - gPhi_m) ** 2, -1))
     return loss, loss_gt
 
 
@@ -464,6 +496,7 @@ def kfp_gmm_grad_analytic(mus, z_init, z_term, z_0T, mus_true, gamma, T, sigma=1
 def kmv_from_moments(K, b, x, v, tau, cfg):
     """kmv.hip's formulation: per time stamp moments + c-weighted moments -> loss, loss_gt, grad."""
     K = np.asarray(K, np.float64); b = np.asarray(b, np.float64)
+    x = np.asarray(x, np.float64); v = np.asarray(v, np.float64)
     S = K + K.T
     F = cfg["tilde_F"]
     gamma = cfg["gamma_friction"]

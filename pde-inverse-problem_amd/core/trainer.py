@@ -84,6 +84,8 @@ def get_optimizer(optimizer_cfg):
 
 
 class JaxTrainer:
+    ema_start = 40000  # trainer.py:87 (the switch epoch; a class attribute so tests can lower it)
+
     def __init__(self, cfg, method, rng, optimizer, forward_fn, params, log_path=None):
         self.cfg = cfg
         self.forward_fn = forward_fn
@@ -131,14 +133,17 @@ class JaxTrainer:
             rng = prng.fold_in(self.rng, epoch)  # trainer.py:80-83 (one key per iteration)
             rng_train, rng_test, _ = prng.split(rng, 3)
             v_g_etc = self.method.value_and_grad_fn(self.forward_fn, self.params, rng_train)
+            if use_ema and epoch == self.ema_start:
+                # trainer.py:97-100: EmaState(count=0, ema=params) from the params BEFORE this step's
+                # update (cloned: the device Adam updates the parameter tensors in place)
+                ema = {"count": 0, "ema": tree_map(lambda p: p.clone(), self.params)}
             self.params, opt_state = self.optimizer.update(v_g_etc["grad"], opt_state, self.params)
-            if use_ema and epoch >= 40000:  # trainer.py:87-103, optax.ema(0.999)
-                if ema is None:
-                    ema = {"count": 0, "ema": tree_map(lambda p: p.clone(), self.params)}
+            if ema is not None:
+                # trainer.py:66-69 with optax.ema(0.999): ema <- 0.999 ema + 0.001 params, and the
+                # params become the RAW ema_state.ema (optax's debiased `updates` are discarded)
                 ema["count"] += 1
-                c = 1 - 0.999 ** ema["count"]
                 ema["ema"] = tree_map(lambda e, p: 0.999 * e + 0.001 * p, ema["ema"], self.params)
-                self.params = tree_map(lambda e: e / c, ema["ema"])
+                self.params = tree_map(lambda e: e.clone(), ema["ema"])
             v_g_etc.pop("grad")
             v_g_etc["params_norm"] = compute_pytree_norm(self.params)
             names = list(v_g_etc.keys())

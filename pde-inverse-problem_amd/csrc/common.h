@@ -120,6 +120,62 @@ struct MomentAcc {
   }
 };
 
+// Step-loop moment accumulator: sum z and the Gram sum z z^T of one particle's rows, laid out so
+// that every packed FMA (v_pk_fma_f32) multiplies an ALIGNED register pair (z[2p], z[2p+1]) by a
+// broadcast z[i]: row i keeps pairs p = i/2 .. M/2-1 (for odd i the first pair's low lane
+// duplicates entry (i-1, i) and is dropped). No register shuffles on the hot loop; finish() maps
+// the pairs onto the MomentAcc triangle (count, sums, i <= j) and applies the 0/1 lane weight.
+template <int M>
+struct PairGram {
+  static constexpr int P = M / 2;
+  static constexpr int npairs() {
+    int n = 0;
+    for (int i = 0; i < M; ++i) n += P - i / 2;
+    return n;
+  }
+  f32x2 s[P];
+  f32x2 g[npairs()];
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int p = 0; p < P; ++p) s[p] = f32x2{0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < npairs(); ++k) g[k] = f32x2{0.f, 0.f};
+  }
+  __device__ __forceinline__ void add(const float* z) {
+    f32x2 zp[P];
+#pragma unroll
+    for (int p = 0; p < P; ++p) zp[p] = f32x2{z[2 * p], z[2 * p + 1]};
+#pragma unroll
+    for (int p = 0; p < P; ++p) s[p] += zp[p];
+    int k = 0;
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      const f32x2 zi = f32x2{z[i], z[i]};
+#pragma unroll
+      for (int p = i / 2; p < P; ++p) {
+        g[k] = zi * zp[p] + g[k];
+        ++k;
+      }
+    }
+  }
+  __device__ __forceinline__ void finish(float rows, float w, float* v) const {
+    v[0] = rows * w;
+#pragma unroll
+    for (int i = 0; i < M; ++i) v[1 + i] = w * s[i / 2][i % 2];
+    int o = 1 + M, k = 0;
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+#pragma unroll
+      for (int p = i / 2; p < P; ++p) {
+#pragma unroll
+        for (int l = 0; l < 2; ++l)
+          if (2 * p + l >= i) v[o++] = w * g[k][l];
+        ++k;
+      }
+    }
+  }
+};
+
 // fp64 column reducer launched after any kernel that wrote a partial slab.
 void launch_slab_reduce(const float* partials, int n_blocks, int n_cols, double* out,
                         hipStream_t stream);

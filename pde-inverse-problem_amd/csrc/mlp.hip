@@ -26,15 +26,25 @@
 namespace pdeinv {
 
 // ---- rocBLAS plumbing ------------------------------------------------------------------------
-static rocblas_handle blas_handle(int device) {
-  static std::mutex mu;
-  static rocblas_handle handles[64] = {};
-  std::lock_guard<std::mutex> lock(mu);
-  if (device < 0 || device >= 64) return nullptr;
-  if (!handles[device]) {
-    if (rocblas_create_handle(&handles[device]) != rocblas_status_success) handles[device] = nullptr;
+// One handle per (host thread, device): a rocBLAS handle carries its stream, so a handle shared
+// between threads lets one thread's rocblas_set_stream retarget another thread's GEMMs (the ABI
+// promises reentrancy across distinct streams, include/pdeinv.h). Thread-local handles need no lock
+// around set_stream + the GEMM sequence; they are destroyed when the thread exits.
+struct ThreadBlasHandles {
+  rocblas_handle h[64] = {};
+  ~ThreadBlasHandles() {
+    for (rocblas_handle& x : h)
+      if (x) rocblas_destroy_handle(x);
   }
-  return handles[device];
+};
+
+static rocblas_handle blas_handle(int device) {
+  thread_local ThreadBlasHandles handles;
+  if (device < 0 || device >= 64) return nullptr;
+  if (!handles.h[device]) {
+    if (rocblas_create_handle(&handles.h[device]) != rocblas_status_success) handles.h[device] = nullptr;
+  }
+  return handles.h[device];
 }
 
 // K-split factor of the weight-gradient GEMMs: the reduction runs over 4 x chunk rows while the

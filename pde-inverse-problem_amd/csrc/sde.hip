@@ -25,6 +25,10 @@ struct SdeArgs {
   uint32_t k0, k1, ctr_off;
   const float* noise;
   const float* shift_u;
+  // MEANFIELD_QUADRATIC (fused multi-step path): xbar [n_steps+1, d], the ensemble mean of the
+  // positions before each update (pdeinv_mf_mean_path), and the shared clock tau0 of the ensemble
+  const float* xbar;
+  float tau0_mf;
   // QUADRATIC: A (d*d) then c (d). GMM (packed on the host at compile-time offsets):
   // GMM: [kMaxGmmK*d raw mu | kMaxGmmK constants c_k = -|mu_k|^2 log2e / (2 s^2)]
   float params[2 * 16 * PDEINV_MAX_DIM + 16];
@@ -120,6 +124,23 @@ __device__ __forceinline__ void grad_gmm(const SdeArgs& a, const GmmCentres<D, K
   const float inv = __builtin_amdgcn_rcpf(den);
 #pragma unroll
   for (int i = 0; i < D; ++i) g[i] = a.inv_s2 * fmaf(-acc[i], inv, q[i]);
+}
+
+// McKean–Vlasov drift with the mean path precomputed: grad U(q) = A (q - xbar_s), the same
+// operation order as the per-update exchange (mf_step_kernel) and the C oracle (y = q - xbar, then
+// A y). xbar_s is wave-uniform (scalar loads from a small device array, one row per update).
+template <int D>
+__device__ __forceinline__ void grad_meanfield(const SdeArgs& a, const float* q, const float* xb, float* g) {
+  float y[D];
+#pragma unroll
+  for (int c = 0; c < D; ++c) y[c] = q[c] - xb[c];
+#pragma unroll
+  for (int r = 0; r < D; ++r) {
+    float acc = 0.f;
+#pragma unroll
+    for (int c = 0; c < D; ++c) acc = fmaf(a.params[r * D + c], y[c], acc);
+    g[r] = acc;
+  }
 }
 
 // Dispatch order -> particle block: the hardware hands consecutive workgroups to the 8 XCDs in
@@ -227,62 +248,6 @@ __device__ __forceinline__ float shift_u(const SdeArgs& a, uint32_t plo, uint32_
   return u32_unit(r.x);
 }
 
-// Step-loop moment accumulator: sum z and the Gram sum z z^T of one particle's rows, laid out so
-// that every packed FMA (v_pk_fma_f32) multiplies an ALIGNED register pair (z[2p], z[2p+1]) by a
-// broadcast z[i]: row i keeps pairs p = i/2 .. M/2-1 (for odd i the first pair's low lane
-// duplicates entry (i-1, i) and is dropped). No register shuffles on the hot loop; finish() maps
-// the pairs onto the MomentAcc triangle (count, sums, i <= j) and applies the 0/1 lane weight.
-template <int M>
-struct PairGram {
-  static constexpr int P = M / 2;
-  static constexpr int npairs() {
-    int n = 0;
-    for (int i = 0; i < M; ++i) n += P - i / 2;
-    return n;
-  }
-  f32x2 s[P];
-  f32x2 g[npairs()];
-  __device__ __forceinline__ void zero() {
-#pragma unroll
-    for (int p = 0; p < P; ++p) s[p] = f32x2{0.f, 0.f};
-#pragma unroll
-    for (int k = 0; k < npairs(); ++k) g[k] = f32x2{0.f, 0.f};
-  }
-  __device__ __forceinline__ void add(const float* z) {
-    f32x2 zp[P];
-#pragma unroll
-    for (int p = 0; p < P; ++p) zp[p] = f32x2{z[2 * p], z[2 * p + 1]};
-#pragma unroll
-    for (int p = 0; p < P; ++p) s[p] += zp[p];
-    int k = 0;
-#pragma unroll
-    for (int i = 0; i < M; ++i) {
-      const f32x2 zi = f32x2{z[i], z[i]};
-#pragma unroll
-      for (int p = i / 2; p < P; ++p) {
-        g[k] = zi * zp[p] + g[k];
-        ++k;
-      }
-    }
-  }
-  __device__ __forceinline__ void finish(float rows, float w, float* v) const {
-    v[0] = rows * w;
-#pragma unroll
-    for (int i = 0; i < M; ++i) v[1 + i] = w * s[i / 2][i % 2];
-    int o = 1 + M, k = 0;
-#pragma unroll
-    for (int i = 0; i < M; ++i) {
-#pragma unroll
-      for (int p = i / 2; p < P; ++p) {
-#pragma unroll
-        for (int l = 0; l < 2; ++l)
-          if (2 * p + l >= i) v[o++] = w * g[k][l];
-        ++k;
-      }
-    }
-  }
-};
-
 template <int D, int POT, bool MOM, int STORE, int KM = 1, bool NOISE = false, int MINW = 1>
 __global__ __launch_bounds__(kBlock, MINW) void sde_simulate_kernel(SdeArgs a, const float* __restrict__ z0,
                                                               float* __restrict__ traj,
@@ -314,7 +279,8 @@ __global__ __launch_bounds__(kBlock, MINW) void sde_simulate_kernel(SdeArgs a, c
     block_reduce_to_slab(init.v, L, lds, partials, bid, nb);
   }
 
-  const float tau0 = a.random_shift ? shift_u(a, plo, phi, i) * a.dt : 0.f;
+  const float tau0 = (POT == PDEINV_POT_MEANFIELD_QUADRATIC) ? a.tau0_mf
+                                                              : (a.random_shift ? shift_u(a, plo, phi, i) * a.dt : 0.f);
   const float h_last = a.dt - tau0;
 
   PairGram<(MOM ? M : 2)> acc;
@@ -338,6 +304,7 @@ __global__ __launch_bounds__(kBlock, MINW) void sde_simulate_kernel(SdeArgs a, c
   auto update = [&](float h, float sh, uint32_t s) {
     float g[D], xi[D];
     if constexpr (POT == PDEINV_POT_GMM) grad_gmm<D, KM>(a, centres, z, g);
+    else if constexpr (POT == PDEINV_POT_MEANFIELD_QUADRATIC) grad_meanfield<D>(a, z, a.xbar + (int64_t)s * D, g);
     else grad_quadratic<D>(a, z, g);
     gen_normals<D, NOISE>(a, plo, phi, s, i, xi);
     const float gh = a.gamma * h;
@@ -402,7 +369,9 @@ __global__ __launch_bounds__(kBlock) void mf_step_kernel(SdeArgs a, int s, float
   const int n_valid = (int)((a.N - wave_row0) < kWave ? (a.N - wave_row0) : kWave);
   __shared__ float stage[kStaged ? kBlock * M : 1];
   float* slot = stage + (threadIdx.x - lane) * M;
-  float z[M];
+  // zero-initialised: a wave wholly past N (n_valid <= 0) skips the staged load, and its lanes must
+  // not feed garbage (0 * Inf = NaN) into the block's Σx partials below
+  float z[M] = {};
   if constexpr (kStaged) {
     if (n_valid > 0) load_rows_staged<D>(zin + wave_row0 * M, z, slot, lane, n_valid);
   } else {
@@ -443,7 +412,7 @@ __global__ __launch_bounds__(kBlock) void mf_step_kernel(SdeArgs a, int s, float
   float v[1 + D];
   v[0] = active ? 1.f : 0.f;
 #pragma unroll
-  for (int k = 0; k < D; ++k) v[1 + k] = v[0] * z[k];
+  for (int k = 0; k < D; ++k) v[1 + k] = active ? z[k] : 0.f;  // a select, not 0 * z
   __shared__ float lds[kWavesPerBlock * (1 + D)];
   block_reduce_to_slab(v, 1 + D, lds, partials, blockIdx.x, gridDim.x);
 }
@@ -576,6 +545,10 @@ static void launch_gmm_sim(const SdeArgs& a, const float* z0, float* traj, float
 template <int D>
 static int dispatch_sim(const SdeArgs& a, int pot, bool mom, const float* z0, float* traj,
                         float* tau, float* last, float* ws, hipStream_t st) {
+  if (pot == PDEINV_POT_MEANFIELD_QUADRATIC) {
+    launch_sim<D, PDEINV_POT_MEANFIELD_QUADRATIC, false>(a, z0, traj, tau, last, ws, st);
+    return 0;
+  }
   if (pot == PDEINV_POT_GMM) {
     if constexpr (D <= 8) {
       if (mom) { launch_gmm_sim<D, true>(a, z0, traj, tau, last, ws, st); return 0; }
@@ -590,6 +563,8 @@ static int dispatch_sim(const SdeArgs& a, int pot, bool mom, const float* z0, fl
   return 0;
 }
 
+static float shared_tau0_host(const SdeArgs& a, const pdeinv_sde_desc* d);
+
 static bool aligned(const void* p, size_t a) { return p == nullptr || ((uintptr_t)p % a) == 0; }
 
 extern "C" int pdeinv_sde_simulate(const pdeinv_sde_desc* d, const float* z0, float* traj,
@@ -598,10 +573,19 @@ extern "C" int pdeinv_sde_simulate(const pdeinv_sde_desc* d, const float* z0, fl
   SdeArgs a;
   int rc = build_args(d, a);
   if (rc) return rc;
-  PDEINV_REQUIRE(d->potential.kind != PDEINV_POT_MEANFIELD_QUADRATIC, PDEINV_ERR_INVALID,
-                 "sde: McKean–Vlasov runs through pdeinv_mf_step (one all-reduce per update)");
   const int D = d->dim;
   const bool mom = moments != nullptr;
+  if (d->potential.kind == PDEINV_POT_MEANFIELD_QUADRATIC) {
+    // the fused multi-step McKean–Vlasov path needs the mean path xbar [n+1, d] (pdeinv_mf_sums ->
+    // all-reduce -> pdeinv_mf_mean_path); without it the ensemble runs update by update (pdeinv_mf_step)
+    PDEINV_REQUIRE(d->d_meanfield != nullptr, PDEINV_ERR_INVALID,
+                   "sde: McKean–Vlasov needs d_meanfield (pdeinv_mf_mean_path) or pdeinv_mf_step");
+    PDEINV_REQUIRE(d->d_shift_u == nullptr, PDEINV_ERR_INVALID,
+                   "sde: McKean–Vlasov draws its shared tau0 from the stream (shift_u unsupported)");
+    PDEINV_REQUIRE(!mom, PDEINV_ERR_UNSUPPORTED, "sde: fused KFP moments are not defined for McKean–Vlasov");
+    a.xbar = d->d_meanfield;
+    a.tau0_mf = shared_tau0_host(a, d);
+  }
   PDEINV_REQUIRE(!mom || D <= 8, PDEINV_ERR_UNSUPPORTED, "sde: fused moments need dim <= 8");
   hipStream_t st = (hipStream_t)stream;
   const int L = moment_len(2 * D);
@@ -636,8 +620,6 @@ extern "C" size_t pdeinv_mf_workspace_bytes(const pdeinv_sde_desc* d) {
   if (!d || d->dim < 1 || d->dim > PDEINV_MAX_DIM || d->n_particles <= 0) return 0;
   return (size_t)(1 + d->dim) * sim_grid(d->n_particles) * sizeof(float);
 }
-
-static float shared_tau0_host(const SdeArgs& a, const pdeinv_sde_desc* d);
 
 extern "C" int pdeinv_mf_step(const pdeinv_sde_desc* d, int32_t s, const float* z, float* z_out,
                               float* tau_row, const float* /*d_tau0*/, const double* xbar_sum,
@@ -696,6 +678,149 @@ static float shared_tau0_host(const SdeArgs& a, const pdeinv_sde_desc* d) {
   const float u = (float)(c0 >> 8) * 0x1p-24f;
   (void)d;
   return u * a.dt;
+}
+
+// ---- McKean–Vlasov, fused multi-step path ----------------------------------------------------
+// The quadratic interaction makes the ensemble mean exactly solvable: averaged over the particles
+// the drift A (x_i - xbar) vanishes, so one update of the ensemble mean is
+//     vbar' = (1 - gamma h) vbar + sqrt(h) ns xibar_s ,   xbar' = xbar + h vbar'
+// with xibar_s = (1/N) sum_i xi_{i,s}, the mean of the update's noise. The noise is a function of
+// (global particle id, update) only, so the whole mean path xbar_0..xbar_n follows from ONE reduction
+// over the ensemble — [count, sum x0, sum v0, sum_i xi_{i,s} for every s] — done before the
+// simulation (pdeinv_mf_sums), all-reduced once across ranks, and unrolled in fp64
+// (pdeinv_mf_mean_path). The simulator then runs all n+1 updates of a particle in registers like the
+// uncoupled kernels (no per-update state re-read, no per-update collective), reading xbar_s per update.
+// The per-update exchange (pdeinv_mf_step) computes the same xbar_s from the fp32 states; the two
+// agree to fp32 rounding (tests/test_gpu_meanfield.py).
+constexpr int kMfSumsPerThread = 16;  // particles per thread in pdeinv_mf_sums
+
+__host__ __device__ inline int64_t mf_sums_len(int D, int n_steps) { return 1 + 2 * D + (int64_t)(n_steps + 1) * D; }
+
+// grid.x: particle tiles of kBlock*kMfSumsPerThread; grid.y = n_steps + 2: y <= n_steps sums the update-y
+// noise, y = n_steps + 1 sums [count, x0, v0]. Slab columns: [count, x0 (D), v0 (D), xi_0 (D), ..., xi_n (D)].
+template <int D, bool EXPLICIT>
+__global__ __launch_bounds__(kBlock) void mf_sums_kernel(SdeArgs a, const float* __restrict__ z0,
+                                                         float* __restrict__ partials) {
+  const int nb = gridDim.x, b = blockIdx.x;
+  const int y = blockIdx.y;
+  const int64_t base = (int64_t)b * kBlock * kMfSumsPerThread + threadIdx.x;
+  __shared__ float lds[kWavesPerBlock * (1 + 2 * D)];
+  if (y == a.n_steps + 1) {
+    float v[1 + 2 * D] = {};
+#pragma unroll 4
+    for (int j = 0; j < kMfSumsPerThread; ++j) {
+      const int64_t i = base + (int64_t)j * kBlock;
+      if (i < a.N) {
+        v[0] += 1.f;
+#pragma unroll
+        for (int k = 0; k < 2 * D; ++k) v[1 + k] += z0[i * a.ld_z0 + k];
+      }
+    }
+    block_reduce_to_slab(v, 1 + 2 * D, lds, partials, b, nb);
+    return;
+  }
+  float acc[D] = {};
+  const uint32_t s = (uint32_t)y;
+#pragma unroll 2
+  for (int j = 0; j < kMfSumsPerThread; ++j) {
+    const int64_t i = base + (int64_t)j * kBlock;
+    if (i < a.N) {
+      const uint64_t gid = (uint64_t)(a.poff + i);
+      float xi[D];
+      gen_normals<D, EXPLICIT>(a, (uint32_t)gid, (uint32_t)(gid >> 32), s, i, xi);
+#pragma unroll
+      for (int k = 0; k < D; ++k) acc[k] += xi[k];
+    }
+  }
+  block_reduce_to_slab(acc, D, lds, partials + (int64_t)(1 + 2 * D + y * D) * nb, b, nb);
+}
+
+// One lane per coordinate (the mean recursion is coordinate-wise): sums (all-reduced) -> xbar
+// [n+1, D] fp32 (the mean BEFORE update s) and optionally xsum [n+2, 1+D] fp64 = [count, count*xbar_s]
+// (the per-update exchange's record, s = 0..n+1). h_s are the particles' own fp32 step sizes.
+__global__ void mf_path_kernel(int D, int n_steps, float dt, float tau0, float gamma, float ns,
+                               const double* __restrict__ sums, float* __restrict__ xbar,
+                               double* __restrict__ xsum) {
+  const int k = threadIdx.x;
+  const double cnt = sums[0];
+  if (xsum && k == 0)
+    for (int s = 0; s <= n_steps + 1; ++s) xsum[(int64_t)s * (1 + D)] = cnt;
+  if (k >= D) return;
+  const double inv = cnt > 0 ? 1.0 / cnt : 0.0;
+  double xb = sums[1 + k] * inv, vb = sums[1 + D + k] * inv;
+  for (int s = 0; s <= n_steps; ++s) {
+    xbar[(int64_t)s * D + k] = (float)xb;
+    if (xsum) xsum[(int64_t)s * (1 + D) + 1 + k] = cnt * xb;
+    const float hf = (s == 0) ? tau0 : ((s == n_steps) ? dt - tau0 : dt);
+    const double h = (double)hf, sh = (double)(sqrtf(hf) * ns);
+    vb = vb - gamma * h * vb + sh * (sums[1 + 2 * D + (int64_t)s * D + k] * inv);
+    xb = xb + h * vb;
+  }
+  if (xsum) xsum[(int64_t)(n_steps + 1) * (1 + D) + 1 + k] = cnt * xb;
+}
+
+static int mf_sums_grid(int64_t N) { return (int)((N + (int64_t)kBlock * kMfSumsPerThread - 1) / ((int64_t)kBlock * kMfSumsPerThread)); }
+
+extern "C" int64_t pdeinv_mf_sums_len(const pdeinv_sde_desc* d) {
+  if (!d || d->dim < 1 || d->dim > PDEINV_MAX_DIM || d->n_steps < 1) return 0;
+  return mf_sums_len(d->dim, d->n_steps);
+}
+
+extern "C" size_t pdeinv_mf_sums_workspace_bytes(const pdeinv_sde_desc* d) {
+  if (!d || d->dim < 1 || d->dim > PDEINV_MAX_DIM || d->n_steps < 1 || d->n_particles <= 0) return 0;
+  return (size_t)mf_sums_len(d->dim, d->n_steps) * mf_sums_grid(d->n_particles) * sizeof(float);
+}
+
+extern "C" int pdeinv_mf_sums(const pdeinv_sde_desc* d, const float* z0, void* ws, double* sums, void* stream) {
+  SdeArgs a;
+  int rc = build_args(d, a);
+  if (rc) return rc;
+  PDEINV_REQUIRE(d->potential.kind == PDEINV_POT_MEANFIELD_QUADRATIC, PDEINV_ERR_INVALID,
+                 "mf_sums: potential must be MEANFIELD_QUADRATIC");
+  PDEINV_REQUIRE(sums != nullptr, PDEINV_ERR_INVALID, "mf_sums: sums is null");
+  const int D = d->dim;
+  const int64_t L = mf_sums_len(D, d->n_steps);
+  hipStream_t st = (hipStream_t)stream;
+  if (a.N == 0) {
+    if (hipMemsetAsync(sums, 0, sizeof(double) * L, st) != hipSuccess)
+      return fail(PDEINV_ERR_HIP, "mf_sums: hipMemsetAsync failed");
+    return PDEINV_OK;
+  }
+  PDEINV_REQUIRE(z0 && ws, PDEINV_ERR_INVALID, "mf_sums: null pointer");
+  PDEINV_REQUIRE(d->n_steps + 2 <= 65535, PDEINV_ERR_UNSUPPORTED, "mf_sums: n_steps too large");
+  const int nb = mf_sums_grid(a.N);
+  const dim3 g(nb, d->n_steps + 2);
+  float* p = (float*)ws;
+  switch (D) {
+#define CASE(DD)                                                                                         \
+  case DD:                                                                                               \
+    if (a.noise) hipLaunchKernelGGL((mf_sums_kernel<DD, true>), g, dim3(kBlock), 0, st, a, z0, p);       \
+    else hipLaunchKernelGGL((mf_sums_kernel<DD, false>), g, dim3(kBlock), 0, st, a, z0, p);              \
+    break;
+    CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) CASE(10) CASE(12) CASE(16)
+#undef CASE
+    default:
+      return fail(PDEINV_ERR_UNSUPPORTED, "mf_sums: dim must be one of 1-8, 10, 12, 16");
+  }
+  rc = check_launch("mf_sums_kernel");
+  if (rc) return rc;
+  launch_slab_reduce(p, nb, (int)L, sums, st);
+  return check_launch("slab_reduce_kernel");
+}
+
+extern "C" int pdeinv_mf_mean_path(const pdeinv_sde_desc* d, const double* sums, float* xbar, double* xsum,
+                                   void* stream) {
+  SdeArgs a;
+  int rc = build_args(d, a);
+  if (rc) return rc;
+  PDEINV_REQUIRE(d->potential.kind == PDEINV_POT_MEANFIELD_QUADRATIC, PDEINV_ERR_INVALID,
+                 "mf_mean_path: potential must be MEANFIELD_QUADRATIC");
+  PDEINV_REQUIRE(d->d_shift_u == nullptr, PDEINV_ERR_INVALID,
+                 "mf_mean_path: the shared tau0 is drawn from the stream (shift_u unsupported)");
+  PDEINV_REQUIRE(sums && xbar, PDEINV_ERR_INVALID, "mf_mean_path: null pointer");
+  hipLaunchKernelGGL(mf_path_kernel, dim3(1), dim3(kWave), 0, (hipStream_t)stream, d->dim, d->n_steps, a.dt,
+                     shared_tau0_host(a, d), a.gamma, a.ns, sums, xbar, xsum);
+  return check_launch("mf_path_kernel");
 }
 
 extern "C" int pdeinv_sde_tau0(const pdeinv_sde_desc* d, float* out, void* stream) {

@@ -5,7 +5,8 @@ Replaces the reference's `jax.pmap(value_and_grad_fn, in_axes=(None, 0))` follow
 contiguous global-id ranges, so every rank's Philox streams are those of a single-process run
 over the same ids. The only exchanges are one all-reduce per residual evaluation (the fp64
 moment / loss-term sums and the parameter gradient, a few hundred bytes) and, for
-McKean–Vlasov, one all-reduce of sum(x) per simulator update.
+McKean–Vlasov, one all-reduce per simulate of [count, sum z0, sum of every update's noise]
+(utils/mean_field.py; the per-update driver instead all-reduces sum(x) once per update).
 """
 from __future__ import annotations
 

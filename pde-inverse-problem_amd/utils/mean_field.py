@@ -1,14 +1,26 @@
-"""McKean–Vlasov particle system driver: one native update per step + one all-reduce.
+"""McKean–Vlasov particle system drivers.
 
 The interaction drift on particle i is mean_j grad Phi*(x_i - x_j) = A (x_i - xbar) for the
-quadratic Phi* (kinetic_mckean_vlasov.py:20-23; README.md:55-80). xbar of the whole ensemble
-(all ranks) is needed before every update, so each of the n+1 updates is one pdeinv_mf_step
-launch (update + fp64 partial sums of the new positions) followed by one RCCL all-reduce of
-d+1 doubles. The reference never simulates this system (it samples the
-equivalent OU law exactly); with a centred ensemble the two laws coincide (tests check it).
+quadratic Phi* (kinetic_mckean_vlasov.py:20-23; README.md:55-80), so every update needs xbar, the
+mean of the whole ensemble (all ranks) before it. Two drivers, the same system:
+
+* exchange="fused" (default): averaged over the particles the drift vanishes, so the mean obeys
+  vbar' = (1 - gamma h) vbar + sqrt(h) ns xibar_s, xbar' = xbar + h vbar' exactly, with xibar_s the
+  mean of update s's noise — a function of particle ids and the RNG stream only. One native pass
+  (pdeinv_mf_sums) sums z0 and every update's noise, ONE all-reduce makes them global, a one-block
+  kernel unrolls the mean path, and the simulator then runs all n+1 updates of each particle in
+  registers (one collective per simulate instead of one per update).
+* exchange="per_update": n+1 pdeinv_mf_step launches, each followed by one all-reduce of
+  [count, sum x] (d+1 doubles) — xbar from the fp32 states themselves. Kept as the cross-check of the
+  closed form (tests/test_gpu_meanfield.py) and as the driver for interactions without a closed-form
+  mean.
+
+The reference never simulates this system (it samples the equivalent OU law exactly); with a centred
+ensemble the two laws coincide (tests check it).
 """
 from __future__ import annotations
 
+import ctypes
 import math
 from typing import Optional
 
@@ -39,7 +51,10 @@ def stamp_times(seed: int, counter_offset: int, n_steps: int, dt: float, random_
 def simulate_mean_field(q0_p0: torch.Tensor, n_steps: int, dt: float, key: Key, potential, gamma: float, *,
                         particle_offset: int = 0, counter_offset: int = 0, noise_scale: float = math.sqrt(2.0),
                         random_shift: bool = True, noise: Optional[torch.Tensor] = None, traj: bool = True,
-                        tau: bool = True) -> dict:
+                        tau: bool = True, exchange: str = "fused", out: Optional[dict] = None) -> dict:
+    """Returns {"last" [N, 2d], "xsum" [n+2, 1+d] fp64 ([count, sum x] before each update and after the
+    last, global over ranks), "traj" [n, N, 2d] time-major, "tau" [n, N]}. `out` may hold preallocated
+    "traj" / "tau" / "last" buffers (fused path)."""
     N, m = q0_p0.shape
     d = m // 2
     dev = q0_p0.device
@@ -47,6 +62,25 @@ def simulate_mean_field(q0_p0: torch.Tensor, n_steps: int, dt: float, key: Key, 
                                 particle_offset=particle_offset, noise_scale=noise_scale,
                                 random_shift=random_shift, noise=noise)
     z0 = q0_p0.contiguous()
+    if exchange == "fused":
+        res = {} if out is None else out
+        if traj and "traj" not in res:
+            res["traj"] = torch.empty((n_steps, N, m), device=dev, dtype=torch.float32)
+        if tau and "tau" not in res:
+            res["tau"] = torch.empty((n_steps, N), device=dev, dtype=torch.float32)
+        if "last" not in res:
+            res["last"] = torch.empty((N, m), device=dev, dtype=torch.float32)
+        sums = dist.allreduce_sum(native.mf_sums(desc, z0))  # the one collective of the simulate
+        xbar, xs = native.mf_mean_path(desc, sums)
+        desc.d_meanfield = ctypes.c_void_p(xbar.data_ptr())
+        native.sde_simulate_desc(desc, z0, res.get("traj") if traj else None, res.get("tau") if tau else None,
+                                 res["last"])
+        del keep
+        res["xsum"] = xs
+        res["xbar"] = xbar
+        return res
+    if exchange != "per_update":
+        raise ValueError(f"exchange must be 'fused' or 'per_update', got {exchange!r}")
     states = torch.empty((n_steps if traj else 2, N, m), device=dev, dtype=torch.float32)
     taus = torch.empty((n_steps, N), device=dev, dtype=torch.float32) if tau else None
     last = torch.empty((N, m), device=dev, dtype=torch.float32)

@@ -36,7 +36,7 @@ GMM_NACC = 8
 GMM_ACC_SLOTS = ("loss", "loss_gt", "nabla", "hessian", "friction", "nabla_true", "initial", "terminal")
 SQRT2 = math.sqrt(2.0)
 
-ABI_VERSION = 5  # PDEINV_ABI_VERSION of include/pdeinv.h this binding was written against
+ABI_VERSION = 6  # PDEINV_ABI_VERSION of include/pdeinv.h this binding was written against
 
 # Every exported symbol of include/pdeinv.h (tests check the library exports all of them).
 EXPORTED_SYMBOLS = (
@@ -55,6 +55,8 @@ EXPORTED_SYMBOLS = (
     "pdeinv_adam_update", "pdeinv_realnvp_param_count", "pdeinv_realnvp_logdensity",
     "pdeinv_realnvp_grad_workspace", "pdeinv_realnvp_value_and_grad",
     "pdeinv_residual_kmv_mlp_workspace_bytes", "pdeinv_residual_kmv_mlp",
+    "pdeinv_mf_sums_len", "pdeinv_mf_sums_workspace_bytes", "pdeinv_mf_sums", "pdeinv_mf_mean_path",
+    "pdeinv_kmv_moments_weights_workspace_bytes", "pdeinv_kmv_moments_weights",
 )
 
 
@@ -149,6 +151,12 @@ def lib():
         "pdeinv_mf_workspace_bytes": (ctypes.c_size_t, [P]),
         "pdeinv_mf_step": (i32, [P, i32, P, P, P, P, P, P, P, P]),
         "pdeinv_sde_tau0": (i32, [P, P, P]),
+        "pdeinv_mf_sums_len": (i64, [P]),
+        "pdeinv_mf_sums_workspace_bytes": (ctypes.c_size_t, [P]),
+        "pdeinv_mf_sums": (i32, [P, P, P, P, P]),
+        "pdeinv_mf_mean_path": (i32, [P, P, P, P, P]),
+        "pdeinv_kmv_moments_weights_workspace_bytes": (ctypes.c_size_t, [i64, i64, i32]),
+        "pdeinv_kmv_moments_weights": (i32, [i32, f32, P, P, i64, i64, i64, i64, P, P, P, P]),
         "pdeinv_moments_workspace_bytes": (ctypes.c_size_t, [i64, i32]),
         "pdeinv_moments": (i32, [P, i64, i32, i64, P, P, P]),
         "pdeinv_residual_kfp_quadratic": (i32, [P, P, P, P, P, P]),
@@ -331,6 +339,54 @@ def sde_tau0(N: int, dt: float, *, seed: int, counter_offset: int = 0, particle_
     return out
 
 
+def mf_sums(desc: SdeDesc, z0: torch.Tensor) -> torch.Tensor:
+    """Rank-local [count, sum x0, sum v0, sum_i xi_{i,s} (s = 0..n)] fp64 of the McKean–Vlasov
+    ensemble (pdeinv_mf_sums) — all-reduce(sum) it, then mf_mean_path."""
+    _require_gpu()
+    L = int(lib().pdeinv_mf_sums_len(ctypes.byref(desc)))
+    if L <= 0:
+        raise ValueError("mf_sums: bad descriptor")
+    if z0.dim() != 2 or z0.shape[0] != desc.n_particles or z0.shape[1] != 2 * desc.dim:
+        raise ValueError(f"mf_sums: z0 must be [{desc.n_particles}, {2 * desc.dim}]")
+    if z0.shape[0] and z0.stride(1) != 1:
+        raise ValueError("mf_sums: z0 must have unit inner stride")
+    desc.ld_z0 = z0.stride(0) if z0.shape[0] > 1 else 2 * desc.dim
+    ws = torch.empty(max(int(lib().pdeinv_mf_sums_workspace_bytes(ctypes.byref(desc))) // 4, 1), device=z0.device,
+                     dtype=torch.float32)
+    out = torch.empty(L, device=z0.device, dtype=torch.float64)
+    _check(lib().pdeinv_mf_sums(ctypes.byref(desc), _dev(z0, "z0") if z0.shape[0] else None, _dev(ws, "ws"),
+                                _dev(out, "sums", torch.float64), stream_handle()), "pdeinv_mf_sums")
+    return out
+
+
+def mf_mean_path(desc: SdeDesc, sums: torch.Tensor, xsum: bool = True):
+    """(xbar [n+1, d] fp32, xsum [n+2, 1+d] fp64 or None) from the all-reduced mf_sums."""
+    _require_gpu()
+    n, d = desc.n_steps, desc.dim
+    xbar = torch.empty((n + 1, d), device=sums.device, dtype=torch.float32)
+    xs = torch.empty((n + 2, 1 + d), device=sums.device, dtype=torch.float64) if xsum else None
+    _check(lib().pdeinv_mf_mean_path(ctypes.byref(desc), _dev(sums, "sums", torch.float64), _dev(xbar, "xbar"),
+                                     _dev(xs, "xsum", torch.float64), stream_handle()), "pdeinv_mf_mean_path")
+    return xbar, xs
+
+
+def sde_simulate_desc(desc: SdeDesc, z0: torch.Tensor, traj: Optional[torch.Tensor], tau: Optional[torch.Tensor],
+                      last: Optional[torch.Tensor]) -> None:
+    """pdeinv_sde_simulate with a prepared descriptor (the McKean–Vlasov fused path: desc.d_meanfield
+    set to mf_mean_path's xbar). Outputs are caller-allocated (time-major traj [n, N, 2d])."""
+    _require_gpu()
+    N, m, n = desc.n_particles, 2 * desc.dim, desc.n_steps
+    for t, shape, name in ((traj, (n, N, m), "traj"), (tau, (n, N), "tau"), (last, (N, m), "last")):
+        if t is not None and (tuple(t.shape) != shape or not t.is_contiguous()):
+            raise ValueError(f"{name} must be contiguous {shape}")
+    if N and (z0.dim() != 2 or tuple(z0.shape) != (N, m) or z0.stride(1) != 1):
+        raise ValueError(f"z0 must be [{N}, {m}] with unit inner stride")
+    desc.ld_z0 = z0.stride(0) if N > 1 else m
+    _check(lib().pdeinv_sde_simulate(ctypes.byref(desc), _dev(z0, "z0") if N else None, _dev(traj, "traj"),
+                                     _dev(tau, "tau"), _dev(last, "last"), None, None, stream_handle()),
+           "pdeinv_sde_simulate")
+
+
 def mf_step(desc: SdeDesc, s: int, z: torch.Tensor, z_out: torch.Tensor, tau_row, xbar_sum: torch.Tensor,
             ws: torch.Tensor, xsum_out: torch.Tensor) -> None:
     rc = lib().pdeinv_mf_step(ctypes.byref(desc), int(s), _dev(z, "z"), _dev(z_out, "z_out"),
@@ -372,8 +428,9 @@ def residual_kfp_quadratic(mom3: torch.Tensor, theta_flat: torch.Tensor, tilde_F
     desc = KfpQuadDesc(d, float(gamma), float(total_time), F.ctypes.data_as(ctypes.c_void_p))
     out = torch.empty(KFP_NOUT, device=mom3.device, dtype=torch.float32)
     grad = torch.empty_like(theta_flat)
+    theta_c = theta_flat.contiguous()  # bound to a name: alive until the launch has been issued
     _check(lib().pdeinv_residual_kfp_quadratic(ctypes.byref(desc), _dev(mom3, "moments", torch.float64),
-                                               _dev(theta_flat.contiguous(), "theta"), _dev(out, "out"),
+                                               _dev(theta_c, "theta"), _dev(out, "out"),
                                                _dev(grad, "grad"), stream_handle()),
            "pdeinv_residual_kfp_quadratic")
     return out, grad
@@ -410,8 +467,9 @@ def residual_kfp_gmm(desc_keep, z_init: torch.Tensor, z_term: torch.Tensor, z_0T
     nbytes = lib().pdeinv_residual_kfp_gmm_workspace_bytes(ctypes.byref(desc), ni, nt, n0)
     ws = torch.empty(max(nbytes // 4, 1), device=z_0T.device, dtype=torch.float32)
     acc = torch.empty(GMM_NACC + K * d, device=z_0T.device, dtype=torch.float64)
+    mus_c = mus.contiguous()
     rc = lib().pdeinv_residual_kfp_gmm(ctypes.byref(desc), pi, ni, ldi, pt, nt, ldt, p0, n0, ld0,
-                                       _dev(mus.contiguous(), "mus"), _dev(ws, "ws"),
+                                       _dev(mus_c, "mus"), _dev(ws, "ws"),
                                        _dev(acc, "acc", torch.float64), stream_handle())
     _check(rc, "pdeinv_residual_kfp_gmm")
     return acc
@@ -449,9 +507,10 @@ def gaussian_sample(n: int, mean: torch.Tensor, cov_half: torch.Tensor, *, seed:
     _require_gpu()
     m = mean.shape[0]
     out = torch.empty((n, m), device=mean.device, dtype=torch.float32)
+    mean_c, cov_c = mean.contiguous(), cov_half.contiguous()
     _check(lib().pdeinv_gaussian_sample(int(n), int(m), int(seed) & 0xFFFFFFFFFFFFFFFF,
                                         int(counter_offset) & 0xFFFFFFFF, int(row_offset),
-                                        _dev(mean.contiguous(), "mean"), _dev(cov_half.contiguous(), "cov_half"),
+                                        _dev(mean_c, "mean"), _dev(cov_c, "cov_half"),
                                         _dev(out, "out"), stream_handle()), "pdeinv_gaussian_sample")
     return out
 
@@ -464,10 +523,11 @@ def gaussian_sample_grouped(rows_per_group: int, means: torch.Tensor, cov_halves
     if cov_halves.shape != (G, m, m):
         raise ValueError(f"cov_halves must be [{G}, {m}, {m}], got {tuple(cov_halves.shape)}")
     out = torch.empty((G * int(rows_per_group), m), device=means.device, dtype=torch.float32)
+    means_c, covs_c = means.contiguous(), cov_halves.contiguous()
     _check(lib().pdeinv_gaussian_sample_grouped(int(G), int(rows_per_group), int(m), int(seed) & 0xFFFFFFFFFFFFFFFF,
                                                 int(counter_offset) & 0xFFFFFFFF, int(row_offset),
-                                                _dev(means.contiguous(), "means"),
-                                                _dev(cov_halves.contiguous(), "cov_halves"), _dev(out, "out"),
+                                                _dev(means_c, "means"),
+                                                _dev(covs_c, "cov_halves"), _dev(out, "out"),
                                                 stream_handle()), "pdeinv_gaussian_sample_grouped")
     return out
 
@@ -545,6 +605,27 @@ def kmv_weights(d: int, gamma: float, coef: torch.Tensor, z: torch.Tensor, n_set
     return out, ds
 
 
+def kmv_moments_weights(d: int, gamma: float, coef: torch.Tensor, z: torch.Tensor, n_sets: int, n_rows: int,
+                        set_stride: int, ld: int):
+    """moments_batched(m = 2d) and kmv_weights in one read of the rows: (mom [n_sets, moment_len(2d)],
+    wst [n_sets, moment_len(d)]) fp64 (pdeinv_kmv_moments_weights)."""
+    _require_gpu()
+    if tuple(coef.shape) != (n_sets, kmv_ncoef(d)) or not coef.is_contiguous():
+        raise ValueError(f"coef must be contiguous [{n_sets}, {kmv_ncoef(d)}]")
+    _set_view(z, n_sets, n_rows, set_stride, ld, 2 * d)
+    nbytes = lib().pdeinv_kmv_moments_weights_workspace_bytes(n_sets, n_rows, d)
+    if nbytes == 0:
+        raise NotImplementedError(f"kmv_moments_weights: dim={d} unsupported (1..8)")
+    ws = torch.empty((nbytes + 3) // 4, device=z.device, dtype=torch.float32)
+    mom = torch.empty((n_sets, moment_len(2 * d)), device=z.device, dtype=torch.float64)
+    wst = torch.empty((n_sets, moment_len(d)), device=z.device, dtype=torch.float64)
+    _check(lib().pdeinv_kmv_moments_weights(d, float(gamma), _dev(coef, "coef"), _dev(z, "z"), n_sets, n_rows,
+                                            set_stride, ld, _dev(ws, "ws"), _dev(mom, "mom", torch.float64),
+                                            _dev(wst, "wst", torch.float64), stream_handle()),
+           "pdeinv_kmv_moments_weights")
+    return mom, wst
+
+
 def residual_kmv_mlp(dims, params_flat: torch.Tensor, z: torch.Tensor, n_sets: int, n_rows: int, set_stride: int,
                      ld: int, ds: torch.Tensor, tilde_F, gamma: float, chunk_rows: int = 1 << 18):
     """kinetic_mckean_vlasov.py:11-120 for Phi_theta = V_hypothesis over every pair of each time
@@ -588,8 +669,9 @@ def residual_kmv(mom: torch.Tensor, wst: torch.Tensor, theta_flat: torch.Tensor,
     grad = torch.empty_like(theta_flat)
     ws = torch.empty(max(1, lib().pdeinv_residual_kmv_workspace_bytes(ctypes.byref(desc)) // 8), device=mom.device,
                      dtype=torch.float64)
-    _check(lib().pdeinv_residual_kmv(ctypes.byref(desc), _dev(mom.contiguous(), "mom", torch.float64),
-                                     _dev(wst.contiguous(), "wst", torch.float64), _dev(theta_flat.contiguous(), "theta"),
+    mom_c, wst_c, theta_c = mom.contiguous(), wst.contiguous(), theta_flat.contiguous()
+    _check(lib().pdeinv_residual_kmv(ctypes.byref(desc), _dev(mom_c, "mom", torch.float64),
+                                     _dev(wst_c, "wst", torch.float64), _dev(theta_c, "theta"),
                                      _dev(ws, "ws", torch.float64), _dev(out, "out"), _dev(grad, "grad"),
                                      stream_handle()), "pdeinv_residual_kmv")
     return out, grad
@@ -763,7 +845,8 @@ def realnvp_logdensity(desc, params: torch.Tensor, t: torch.Tensor, x: torch.Ten
         raise ValueError("RealNVP: t must have one entry per row or a single entry")
     px, _, ld = _rows(x, "x", desc.dim)
     out = torch.empty(n, device=x.device, dtype=torch.float32)
-    _check(lib().pdeinv_realnvp_logdensity(ctypes.byref(desc), _dev(params, "params"), _dev(t.contiguous(), "t"),
+    t = t.contiguous()
+    _check(lib().pdeinv_realnvp_logdensity(ctypes.byref(desc), _dev(params, "params"), _dev(t, "t"),
                                            0 if t.numel() == 1 else 1, px, n, ld, _dev(out, "out"),
                                            stream_handle()), "pdeinv_realnvp_logdensity")
     return out
@@ -786,7 +869,8 @@ def realnvp_value_and_grad(desc, params: torch.Tensor, t: torch.Tensor, x: torch
     ws = torch.empty((ws_bytes + 3) // 4, device=x.device, dtype=torch.float32)
     loss = torch.empty((), device=x.device, dtype=torch.float32)
     grad = torch.empty(P, device=x.device, dtype=torch.float32)
-    _check(lib().pdeinv_realnvp_value_and_grad(ctypes.byref(desc), _dev(params, "params"), _dev(t.contiguous(), "t"),
+    t = t.contiguous()
+    _check(lib().pdeinv_realnvp_value_and_grad(ctypes.byref(desc), _dev(params, "params"), _dev(t, "t"),
                                                0 if t.numel() == 1 else 1, px, n, ld, _dev(loss, "loss"),
                                                _dev(grad, "grad"), _dev(ws, "workspace"), ws_bytes,
                                                stream_handle()), "pdeinv_realnvp_value_and_grad")

@@ -13,7 +13,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 
-def mean_field(out_dir, N=6000, n=30, d=4):
+def mean_field(out_dir, exchange="fused", N=6000, n=30, d=8):
     from core.potential import MeanFieldQuadraticPotential
     from oracle import numpy_ref as nr
     from utils import distributed as dist
@@ -26,7 +26,7 @@ def mean_field(out_dir, N=6000, n=30, d=4):
     dev = torch.device("cuda", dist.local_device())
     pot = MeanFieldQuadraticPotential(nr.problem_constants(d))
     r = simulate_mean_field(torch.as_tensor(z0[off:off + cnt], device=dev), n, 0.02, PRNGKey(11), pot, 1.0,
-                            particle_offset=off, counter_offset=3)
+                            particle_offset=off, counter_offset=3, exchange=exchange)
     np.savez(os.path.join(out_dir, f"rank{rank}.npz"), traj=r["traj"].cpu().numpy(), last=r["last"].cpu().numpy(),
              xsum=r["xsum"].cpu().numpy(), off=off, world=world)
 
@@ -34,6 +34,6 @@ def mean_field(out_dir, N=6000, n=30, d=4):
 if __name__ == "__main__":
     from utils import distributed as dist
     dist.init_from_env()
-    {"mean_field": mean_field}[sys.argv[1]](sys.argv[2])
+    {"mean_field": mean_field}[sys.argv[1]](*sys.argv[2:])
     if dist.is_distributed():
         torch.distributed.destroy_process_group()

@@ -365,6 +365,46 @@ def test_residual_mlp_fused_matches_library(native):
     assert np.max(np.abs(g_f - g_l)) < 2e-4 * np.abs(g_l).max(), np.max(np.abs(g_f - g_l))
 
 
+def test_residual_mlp_library_two_threads_two_streams(native):
+    """ABI thread contract (include/pdeinv.h): two host threads call the rocBLAS
+    library path concurrently on two streams (ctypes releases the GIL during the call). Each must get
+    exactly the single-threaded result — a rocBLAS handle shared between threads would let one
+    thread's set_stream retarget the other's GEMMs."""
+    import threading
+    dims = [4, 32, 32, 40]
+    rng = np.random.default_rng(21)
+    flat = np.concatenate([np.concatenate([rng.standard_normal((dims[i], dims[i + 1])).ravel() * np.sqrt(1.0 / dims[i]),
+                                           0.1 * rng.standard_normal(dims[i + 1])]) for i in range(len(dims) - 1)])
+    F = nr.problem_constants(4)
+    sets = [tuple(_t(rng.standard_normal((m, 8))) for m in (1000, 1000, 60000)) for _ in range(2)]
+    kw = dict(true_kind=native.POT_QUADRATIC, true_params=F, gamma=0.5, total_time=2.0, chunk_rows=4096, impl=LIB)
+    ref = [native.residual_kfp_mlp(dims, _t(flat), *s, **kw) for s in sets]
+    torch.cuda.synchronize()
+    got, errs = [[None] * 4 for _ in range(2)], []
+
+    def work(t):
+        try:
+            st = torch.cuda.Stream()
+            with torch.cuda.stream(st):
+                for rep in range(4):
+                    a, g = native.residual_kfp_mlp(dims, _t(flat), *sets[t], **kw)
+                    got[t][rep] = (a, g)
+            st.synchronize()
+        except Exception as e:  # surfaced below
+            errs.append(e)
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(2)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=120)
+    assert not errs, errs
+    for t in range(2):  # 1e-6: run-to-run reassociation at most (a stream mix-up reads garbage)
+        for a, g in got[t]:
+            assert torch.allclose(a, ref[t][0], rtol=1e-6, atol=1e-9 * ref[t][0].abs().max().item())
+            assert torch.allclose(g, ref[t][1], rtol=1e-6, atol=1e-6 * ref[t][1].abs().max().item())
+
+
 def test_gather_random_step(native):
     rng = np.random.default_rng(3)
     n, N, m = 37, 5000, 8

@@ -1,0 +1,183 @@
+"""BASELINE config C4 (kinetic McKean–Vlasov, quadratic interaction, d = 8) on the GPU, against the
+CPU oracle (oracle/pdeinv_oracle.c, oracle/numpy_ref.py) and the committed golden fixtures.
+
+Reference: methods/consistency_instances/kinetic_mckean_vlasov.py:11-120 (pairwise residual),
+example_problems/kinetic_mckean_vlasov_example_quadratic.py:18-216 (d_s log rho, Phi*), README.md:55-80
+(the mean-field equivalence). Tolerances (written per test): Philox-mode trajectories 2e-4 absolute vs
+the C oracle (hardware v_log / v_sin / v_cos vs libm in the normals); explicit-noise trajectories 2e-5
+of the state scale; the two McKean–Vlasov drivers against each other 2e-5 of the state scale; moment
+sums 1e-5 relative (fp32 per thread / block, fp64 across blocks); residual 1e-4 relative, gradient 1e-3.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import numpy_ref as nr
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _t(a):
+    return torch.as_tensor(np.ascontiguousarray(a), dtype=torch.float32, device=DEV)
+
+
+def _sim(z0, n, A, exchange, seed=0x5EED_0004, ctr=5, noise=None, random_shift=True, dt=0.02):
+    from core.potential import MeanFieldQuadraticPotential
+    from utils import prng
+    from utils.mean_field import simulate_mean_field
+    return simulate_mean_field(z0, n, dt, prng.Key(seed), MeanFieldQuadraticPotential(A), 1.0, counter_offset=ctr,
+                               noise=noise, random_shift=random_shift, exchange=exchange)
+
+
+@pytest.mark.parametrize("exchange", ["fused", "per_update"])
+@pytest.mark.parametrize("d,N", [(8, 4099), (8, 6000), (2, 2000), (3, 333)])
+def test_mean_field_vs_c_oracle(native, oracle_lib, exchange, d, N):
+    """Both McKean–Vlasov drivers vs the interacting C oracle (which recomputes xbar from all fp32 states
+    before every update), n = 100. N = 4099 / 6000 leave whole waves of the last block past N (the staged
+    row load/store of mf_step_kernel and its zero-initialised lanes); d = 3 takes the unstaged rows."""
+    n = 100
+    A = nr.problem_constants(d)
+    z0 = (np.random.default_rng(d * 7 + N).standard_normal((N, 2 * d)) + 0.5).astype(np.float32)
+    r = _sim(_t(z0), n, A, exchange)
+    o = oracle_lib.sde_simulate(z0, n, 0.02, 1.0, "meanfield", A, seed=0x5EED_0004, counter_offset=5)
+    assert np.array_equal(r["tau"].cpu().numpy(), o["tau"])
+    assert np.max(np.abs(r["traj"].cpu().numpy() - o["traj"])) < 2e-4
+    assert np.max(np.abs(r["last"].cpu().numpy() - o["last"])) < 2e-4
+    assert torch.isfinite(r["xsum"]).all()
+
+
+@pytest.mark.parametrize("d,N", [(8, 4099), (4, 777)])
+def test_mean_field_explicit_noise_vs_c_oracle(native, oracle_lib, d, N):
+    """Explicit-noise parity mode (no transcendental differences): the fused driver (noise sums from the
+    noise buffer) and the per-update driver vs the C oracle on the same xi: 2e-5 of the state scale."""
+    n = 100
+    A = nr.problem_constants(d)
+    rng = np.random.default_rng(N)
+    z0 = (rng.standard_normal((N, 2 * d)) - 0.3).astype(np.float32)
+    xi = rng.standard_normal((n + 1, N, d)).astype(np.float32)
+    o = oracle_lib.sde_simulate(z0, n, 0.02, 1.0, "meanfield", A, seed=0x5EED_0004, counter_offset=5, noise=xi)
+    scale = 1 + np.abs(o["traj"]).max()
+    for exchange in ("fused", "per_update"):
+        r = _sim(_t(z0), n, A, exchange, noise=_t(xi))
+        assert np.max(np.abs(r["traj"].cpu().numpy() - o["traj"])) < 2e-5 * scale, exchange
+        assert np.max(np.abs(r["last"].cpu().numpy() - o["last"])) < 2e-5 * scale, exchange
+
+
+def test_mean_field_drivers_agree(native):
+    """The closed-form mean path (one all-reduce per simulate) and the per-update exchange (xbar from the
+    fp32 states) give the same ensemble: trajectories to 2e-5 of the state scale, the recorded
+    [count, sum x] per update to 1e-6 relative."""
+    d, N, n = 8, 50_000, 100
+    A = nr.problem_constants(d)
+    z0 = native.gaussian_sample(N, _t(np.full(2 * d, 0.4)), _t(np.eye(2 * d)), seed=3)
+    a = _sim(z0, n, A, "fused")
+    b = _sim(z0, n, A, "per_update")
+    scale = 1 + b["traj"].abs().max().item()
+    assert (a["traj"] - b["traj"]).abs().max().item() < 2e-5 * scale
+    assert (a["last"] - b["last"]).abs().max().item() < 2e-5 * scale
+    xa, xb = a["xsum"].cpu().numpy(), b["xsum"].cpu().numpy()
+    assert np.array_equal(xa[:, 0], xb[:, 0])
+    assert np.max(np.abs(xa[:, 1:] - xb[:, 1:])) < 1e-6 * N * (1 + np.abs(xb[:, 1:] / N).max())
+
+
+def test_mean_field_full_size_centred_law(native):
+    """SURVEY.md §8(c) P4 at the C4 size (2^21 particles per GPU, d = 8, n = 100, fused driver): with a
+    centred initial ensemble the interacting system's second moments are the EM chain's with
+    tilde_F = A (em_chain_moments) — every entry of E[z z^T] at three time stamps and at T within 5.5
+    sigma_MC. The closed-form mean path also matches the actual mean of the simulated states (1e-6)."""
+    d, N, n = 8, 1 << 21, 100
+    A = nr.problem_constants(d)
+    z0 = native.gaussian_sample(N, _t(np.zeros(2 * d)), _t(np.eye(2 * d)), seed=5)
+    z0 = z0 - z0.mean(0)
+    r = _sim(z0, n, A, "fused", seed=9, random_shift=False)
+    P0 = (z0.double().T @ z0.double() / N).cpu().numpy()
+    _, sec, _, sec_last = nr.em_chain_moments(A, 1.0, 0.02, n, np.zeros(2 * d), P0, random_shift=False)
+    xbar = r["xbar"].double().cpu().numpy()
+    for s in (9, 49, 99, n):
+        z = r["last"] if s == n else r["traj"][s]
+        mom = native.moments(z).cpu().numpy()
+        _, mean, M = nr.unpack_moments(mom, 2 * d)
+        P = sec_last if s == n else sec[s]
+        sig = np.sqrt((np.outer(np.diag(P), np.diag(P)) + P ** 2) / N)
+        assert np.max(np.abs(M - P) / sig) < 5.5, (s, np.max(np.abs(M - P) / sig))
+        if s < n:  # xbar row s + 1 = the mean after update s
+            assert np.max(np.abs(mean[:d] - xbar[s + 1])) < 1e-6, (s, np.abs(mean[:d] - xbar[s + 1]).max())
+
+
+def test_moments_batched_m16(native):
+    """moments_batched_kernel<16> (the C4 per-time-stamp moments of z = [x, v], d = 8) vs fp64 sums."""
+    rng = np.random.default_rng(16)
+    n_t, n = 5, 3001
+    z = rng.standard_normal((n_t, n, 16)).astype(np.float32) + 0.2
+    out = native.moments_batched(_t(z), n_t, n, 16, n * 16, 16).cpu().numpy()
+    for t in range(n_t):
+        ref = nr.moments(z[t].astype(np.float64))
+        assert np.allclose(out[t], ref, rtol=1e-5, atol=1e-5 * np.abs(ref).max())
+
+
+def _coef(d, tau):
+    from example_problems.kinetic_mckean_vlasov_example_quadratic import dlogrho_coefficients
+    cfg = nr.ou_configuration(nr.problem_constants(d))
+    return cfg, _t(dlogrho_coefficients(np.asarray(tau, np.float64), cfg, d))
+
+
+def test_kmv_weights_d8(native):
+    """kmv_weights_kernel<8>: per-particle (d_s log rho, d_s^2 log rho) vs the fp64 restatement
+    (…_quadratic.py:18-191) and the per-stamp c-weighted moments (c = ds2 + ds^2 + gamma ds)."""
+    d, n = 8, 2500
+    tau = [0.3, 1.1, 1.9]
+    cfg, coef = _coef(d, tau)
+    rng = np.random.default_rng(8)
+    z = rng.standard_normal((len(tau), n, 2 * d)).astype(np.float32)
+    wst, ds = native.kmv_weights(d, 1.0, coef, _t(z), len(tau), n, n * 2 * d, 2 * d, want_ds=True)
+    wst, ds = wst.cpu().numpy(), ds.double().cpu().numpy()
+    for t, s in enumerate(tau):
+        x = z[t, :, :d].astype(np.float64)
+        r1, r2 = nr.partial_s_log_density(s, x, cfg), nr.partial_s2_log_density(s, x, cfg)
+        assert np.max(np.abs(ds[t, :, 0] - r1) / (1 + np.abs(r1))) < 1e-4
+        assert np.max(np.abs(ds[t, :, 1] - r2) / (1 + np.abs(r2))) < 1e-3
+        c = r2 + r1 ** 2 + 1.0 * r1
+        ref = np.concatenate([[c.sum()], c @ x, ((x * c[:, None]).T @ x)[np.triu_indices(d)]])
+        assert np.allclose(wst[t], ref, rtol=1e-3, atol=1e-3 * np.abs(ref).max())
+
+
+@pytest.mark.parametrize("d,n_t,n", [(8, 7, 50_001), (2, 3, 999), (5, 2, 4096)])
+def test_kmv_moments_weights_fused_equals_separate(native, d, n_t, n):
+    """The fused one-read pass == moments_batched(2d) + kmv_weights(d) on the same rows (the sums are
+    reassociated differently: 1e-5 relative)."""
+    rng = np.random.default_rng(d + n)
+    tau = np.linspace(0.2, 1.8, n_t)
+    _, coef = _coef(d, tau)
+    z = _t(rng.standard_normal((n_t, n, 2 * d)) * 1.3 + 0.1)
+    mom, wst = native.kmv_moments_weights(d, 1.0, coef, z, n_t, n, n * 2 * d, 2 * d)
+    mom_s = native.moments_batched(z, n_t, n, 2 * d, n * 2 * d, 2 * d)
+    wst_s, _ = native.kmv_weights(d, 1.0, coef, z, n_t, n, n * 2 * d, 2 * d)
+    for a, b in ((mom, mom_s), (wst, wst_s)):
+        a, b = a.cpu().numpy(), b.cpu().numpy()
+        assert np.allclose(a, b, rtol=1e-5, atol=1e-5 * np.abs(b).max())
+
+
+@pytest.mark.parametrize("name", ["kmv_pairwise_d8.npz", "kmv_pairwise_recipe.npz"])
+def test_kmv_residual_vs_pairwise_golden(native, name):
+    """residual_kmv at the C4 dimension (d = 8, 2 time stamps) and on the reference's runnable recipe
+    (scripts/parametric/KMV/run_quadratic_online.sh: d = 2, one stamp, 5 000 exact OU samples) against
+    the literal O(n^2) pair-tensor restatement frozen in tests/golden (oracle/make_golden.py), gradient
+    against its central differences. Both the separate and the fused moment passes."""
+    import os
+    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", name))
+    x, v, tau = g["x"], g["v"], g["tau"]
+    n, n_t, d = x.shape
+    z = _t(np.concatenate([x, v], -1).reshape(-1, 2 * d))  # reference row order (i, t)
+    from example_problems.kinetic_mckean_vlasov_example_quadratic import dlogrho_coefficients
+    coef = _t(dlogrho_coefficients(tau, nr.ou_configuration(g["F"]), d))
+    theta = _t(np.concatenate([g["K"].ravel(), g["b"]]))
+    fused = native.kmv_moments_weights(d, 1.0, coef, z, n_t, n, 2 * d, n_t * 2 * d)
+    sep = (native.moments_batched(z, n_t, n, 2 * d, 2 * d, n_t * 2 * d),
+           native.kmv_weights(d, 1.0, coef, z, n_t, n, 2 * d, n_t * 2 * d)[0])
+    for mom, wst in (fused, sep):
+        out, grad = native.residual_kmv(mom, wst, theta, g["F"], 1.0)
+        out = out.cpu().numpy()
+        assert abs(out[0] - g["loss"]) < 1e-4 * (1 + abs(g["loss"])), (out[0], g["loss"])
+        assert abs(out[1] - g["loss_gt"]) < 1e-4 * (1 + abs(g["loss_gt"]))
+        assert np.allclose(grad.cpu().numpy(), g["grad"], rtol=1e-3, atol=1e-3 * (1 + np.abs(g["grad"]).max()))

@@ -2,10 +2,12 @@
 torch.distributed.run share cuda:0 with the gloo backend (PDEINV_DIST_BACKEND=gloo; RCCL needs one
 GPU per rank, the call sites are the same).
 
-* McKean–Vlasov simulator: one all-reduce of [count, sum x] per update. The Philox counter is the
-  global particle id and the mean field is the all-reduced ensemble mean, so the 2- and 3-rank
-  trajectories must equal the 1-rank trajectory of the whole ensemble (up to the fp64 summation
-  order of the partial sums: 2e-5 after 31 updates).
+* McKean–Vlasov simulator (d = 8, the C4 dimension), both drivers: the fused one (one all-reduce per
+  simulate of [count, sum z0, the noise sums of every update]) and the per-update exchange (one
+  all-reduce of [count, sum x] per update). The Philox counter is the global particle id and the mean
+  field is the all-reduced ensemble mean, so the 2- and 3-rank trajectories must equal the 1-rank
+  trajectory of the whole ensemble (up to the fp64 summation order of the partial sums: 2e-5 after 31
+  updates).
 * bench.py --gpus 2 (the driver's scaling launch): one JSON line, n_gpus = 2, value = both ranks'
   particle-updates / the max-over-ranks step time.
 """
@@ -35,17 +37,19 @@ def _gather(out_dir, world):
     return traj, last, parts[0]["xsum"]
 
 
-def test_mean_field_simulator_is_rank_count_invariant(native, tmp_path):
+@pytest.mark.parametrize("exchange,port0", [("fused", 29611), ("per_update", 29621)])
+def test_mean_field_simulator_is_rank_count_invariant(native, tmp_path, exchange, port0):
     ref_dir = tmp_path / "w1"
     ref_dir.mkdir()
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "mp_gpu_worker.py"), "mean_field", str(ref_dir)],
+    worker = [os.path.join(ROOT, "tests", "mp_gpu_worker.py"), "mean_field"]
+    r = subprocess.run([sys.executable] + worker + [str(ref_dir), exchange],
                        cwd=ROOT, capture_output=True, text=True, timeout=180)
     assert r.returncode == 0, r.stderr[-3000:]
     t1, l1, x1 = _gather(ref_dir, 1)
-    for world, port in ((2, 29611), (3, 29612)):
+    for world, port in ((2, port0), (3, port0 + 1)):
         d = tmp_path / f"w{world}"
         d.mkdir()
-        r = _launch(world, [os.path.join(ROOT, "tests", "mp_gpu_worker.py"), "mean_field", str(d)], port)
+        r = _launch(world, worker + [str(d), exchange], port)
         assert r.returncode == 0, r.stderr[-3000:]
         tw, lw, xw = _gather(d, world)
         scale = 1 + np.abs(t1).max()

@@ -131,6 +131,48 @@ def test_adam_matches_optax_semantics():
     assert f(0) == 1.0 and abs(f(20000) - 1e-3) < 1e-12 and abs(f(10000) - (0.5 * 0.999 + 1e-3)) < 1e-9
 
 
+def test_trainer_ema_matches_optax_restatement():
+    """core/trainer.py:87-103 (use_ema) across a lowered switch epoch, against an fp64 restatement of
+    optax.adam + optax.ema(0.999): at the switch epoch EmaState(count=0, ema=params) is taken from the
+    params before that step's update; every later step sets ema <- 0.999 ema + 0.001 params and the
+    params become the raw ema (no debias division). The parameters must stay O(1)."""
+    import torch
+    from core.trainer import Adam, JaxTrainer
+    from utils import config, prng
+
+    cfg = config.compose("config", ["train.optimizer.use_ema=True", "test.frequency=1000"])
+    c = np.array([0.7, -1.3, 2.1])
+
+    class Quadratic:  # loss 0.5 |p - c|^2, grad p - c
+        def value_and_grad_fn(self, forward_fn, params, rng):
+            p = params["w"]
+            g = p - torch.as_tensor(c, dtype=p.dtype)
+            return {"loss": 0.5 * (g * g).sum(), "grad": {"w": g}, "grad_norm": g.norm(),
+                    "loss ground truth": 0.5 * (g * g).sum()}
+
+        def test_fn(self, forward_fn, params, rng):
+            return {}
+
+    start, iters, lr, wd = 3, 9, 0.1, 0.0
+    tr = JaxTrainer(cfg, Quadratic(), prng.PRNGKey(0), Adam(lr, weight_decay=wd), None,
+                    {"w": torch.zeros(3, dtype=torch.float64)})
+    tr.ema_start = start
+    out = tr.fit(number_of_iterations=iters)["w"].numpy()
+
+    p, mu, nu, ema = np.zeros(3), np.zeros(3), np.zeros(3), None
+    for k in range(iters):
+        g = p - c
+        if k == start:
+            ema = p.copy()
+        mu, nu = 0.9 * mu + 0.1 * g, 0.999 * nu + 0.001 * g * g
+        p = p - lr * (mu / (1 - 0.9 ** (k + 1))) / (np.sqrt(nu / (1 - 0.999 ** (k + 1))) + 1e-4)
+        if ema is not None:
+            ema = 0.999 * ema + 0.001 * p
+            p = ema.copy()
+    assert np.abs(out - p).max() < 1e-12, (out, p)
+    assert np.abs(out).max() < 1.0  # O(1): the old debiased branch blew the params up ~1000x
+
+
 def _header_functions():
     txt = open(os.path.join(ROOT, "include", "pdeinv.h")).read()
     return set(re.findall(r"^(?:int|int64_t|size_t|const char\*)\s+(pdeinv_\w+)\(", txt, flags=re.M))
@@ -150,7 +192,7 @@ def test_library_exports_every_header_symbol():
     missing = [s for s in _header_functions() if not hasattr(lib, s)]
     assert not missing
     lib.pdeinv_moment_len.restype = ctypes.c_int
-    assert lib.pdeinv_moment_len(8) == 45 and lib.pdeinv_abi_version() == native.ABI_VERSION == 5
+    assert lib.pdeinv_moment_len(8) == 45 and lib.pdeinv_abi_version() == native.ABI_VERSION == 6
 
 
 def test_loader_fails_loudly_without_gpu():

@@ -195,11 +195,14 @@ def test_residual_goldens():
     assert np.isclose(loss, g["loss"], rtol=1e-12)
     G = nr.kfp_gmm_grad_analytic(g["mus"], g["zi"], g["zt"], g["z0"], g["mus_true"], 0.5, 2.0)
     assert np.allclose(G, g["grad"], rtol=1e-5, atol=1e-7)
-    g = np.load(os.path.join(GOLD, "kmv_pairwise.npz"))
-    cfg = nr.ou_configuration(g["F"])
-    loss, gt, gK, gb = nr.kmv_from_moments(g["K"], g["b"], g["x"], g["v"], g["tau"], cfg)
-    assert np.isclose(loss, g["loss"], rtol=1e-10)
-    assert np.allclose(np.concatenate([gK.ravel(), gb]), g["grad"], rtol=1e-5, atol=1e-7)
+    for name in ("kmv_pairwise.npz", "kmv_pairwise_d8.npz", "kmv_pairwise_recipe.npz"):
+        # the moment form (what kmv.hip implements) == the literal O(n^2) pair tensor of the fixture
+        g = np.load(os.path.join(GOLD, name))
+        cfg = nr.ou_configuration(g["F"])
+        loss, gt, gK, gb = nr.kmv_from_moments(g["K"], g["b"], g["x"], g["v"], g["tau"], cfg)
+        assert np.isclose(loss, g["loss"], rtol=1e-9), name
+        assert np.isclose(gt, g["loss_gt"], rtol=1e-9), name
+        assert np.allclose(np.concatenate([gK.ravel(), gb]), g["grad"], rtol=1e-5, atol=1e-6), name
 
 
 def test_constants_recipe():
@@ -297,6 +300,33 @@ def test_shared_clock_stamp_times_match_c_oracle(oracle_lib):
     for seed, ctr in ((0xABCDEF, 5), (0x5EED_0004, 101 * 7), (2**40 + 3, 0)):
         o = oracle_lib.sde_simulate(z0, 30, 0.02, 1.0, "meanfield", A, seed=seed, counter_offset=ctr)
         assert np.array_equal(o["tau"][:, 0], stamp_times(seed, ctr, 30, 0.02))
+
+
+@pytest.mark.parametrize("d,N,n,explicit", [(2, 300, 25, False), (3, 257, 12, True), (8, 130, 20, False)])
+def test_mean_field_closed_form_mean_path_matches_interacting_oracle(oracle_lib, d, N, n, explicit):
+    """The fused McKean–Vlasov driver's premise, pinned on the CPU: the mean path unrolled from
+    [count, sum z0, sum of each update's noise] (numpy_ref.mf_mean_path) equals the mean of the
+    interacting C-oracle simulation, whose every update recomputes xbar from all fp32 states
+    (oracle_sde_simulate kind=meanfield). Both the Philox and the explicit-noise stream. Tolerance 2e-6
+    of the state scale (the oracle's fp32 states vs the fp64 recursion)."""
+    A = nr.problem_constants(d)
+    rng = np.random.default_rng(d + N)
+    z0 = (rng.standard_normal((N, 2 * d)) + 0.7).astype(np.float32)  # non-centred: the mean moves
+    seed, ctr, dt = 0x5EED_0004 + d, 17, 0.02
+    noise = rng.standard_normal((n + 1, N, d)).astype(np.float32) if explicit else None
+    o = oracle_lib.sde_simulate(z0, n, dt, 1.0, "meanfield", A, seed=seed, counter_offset=ctr, noise=noise)
+    if explicit:
+        xi_sum = noise.astype(np.float64).sum(1)
+    else:
+        xi_sum = np.array([[oracle_lib.sim_normals(seed, i, ctr + s, d) for i in range(N)] for s in range(n + 1)],
+                          np.float64).sum(1)
+    sums = np.concatenate([[N], z0[:, :d].astype(np.float64).sum(0), z0[:, d:].astype(np.float64).sum(0),
+                           xi_sum.ravel()])
+    tau0 = float(o["tau"][0, 0])
+    path = nr.mf_mean_path(sums, d, n, dt, tau0, 1.0)
+    actual = np.concatenate([z0[None, :, :d], o["traj"][:, :, :d], o["last"][None, :, :d]]).astype(np.float64).mean(1)
+    scale = 1 + np.abs(o["traj"]).max()
+    assert np.abs(path - actual).max() < 2e-6 * scale, np.abs(path - actual).max()
 
 
 @pytest.mark.parametrize("dim,mask_type,E,soft_init,act", [(1, "loop", 10, 1.0, "celu"), (2, "loop", 10, 1.0, "celu"),
