@@ -98,67 +98,129 @@ __global__ __launch_bounds__(kBlock) void kmv_weights_kernel(float gamma, const 
 }
 
 // Fused per-time-stamp pass: one read of each row z = [x, v] (2D floats) yields both the moments of
-// z (the moments_batched sums, PairGram packed FMAs) and the c-weighted sums of x (the kmv_weights
-// sums): the McKean–Vlasov residual then reads its 2^21 x 100 x 64 B trajectory once instead of
-// 1.5 times. Slab columns of set t: [moment_len(2D) | moment_len(D)].
+// z (the moments_batched sums) and the c-weighted sums of x (the kmv_weights sums): the McKean–Vlasov
+// residual then reads its 2^21 x 100 x 64 B trajectory once instead of 1.5 times. Slab columns of set
+// t: [moment_len(2D) | moment_len(D)].
+//  * the Gram sum z z^T of a wave's 64 rows is 16 v_mfma_f32_16x16x4_f32 (A = B = the rows, K = rows,
+//    features zero-padded to 16) into 4 accumulator registers per lane, fed through a per-wave LDS
+//    transpose (row stride 20 floats: conflict-free 16-byte row writes); the lane-private alternative
+//    (136 packed accumulators) left room for 2 waves per SIMD only;
+//  * the per-row quadratic forms of d_s log rho and d_s^2 log rho run as packed pairs over coefficient
+//    pairs (Gamma1_ij, Gamma2_ij) broadcast from LDS (as kernel SGPRs the 2 d^2 + 2 d coefficients spill);
+//  * count, sum z and the weighted moments stay lane-private (wave / block reduction at the end).
+constexpr int kMwStride = 20;  // floats per staged row (16 features + pad)
+
 template <int D>
 __global__ __launch_bounds__(kBlock) void kmv_moments_weights_kernel(float gamma, const float* __restrict__ coef,
                                                                      const float* __restrict__ z, int64_t n_rows,
                                                                      int64_t set_stride, int64_t ld,
                                                                      float* __restrict__ partials) {
   constexpr int M = 2 * D, NC = 3 * D + 2 + 2 * D * D, LZ = moment_len(M), LW = moment_len(D);
+  static_assert(M <= 16, "the 16x16 MFMA Gram holds 2d <= 16 features");
   const int t = blockIdx.y;
-  const float* c = coef + (int64_t)t * NC;  // wave-uniform: scalar loads
-  const float* m1 = c;
-  const float a1 = c[D];
-  const float* b1 = c + D + 1;
-  const float* G1 = c + 2 * D + 1;
-  const float a2 = c[2 * D + 1 + D * D];
-  const float* b2 = c + 2 * D + 2 + D * D;
-  const float* G2 = c + 3 * D + 2 + D * D;
-  PairGram<M> gz;
-  gz.zero();
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  const float* c = coef + (int64_t)t * NC;  // [m1 (D), a1, b1 (D), G1 (D*D), a2, b2 (D), G2 (D*D)]
+  __shared__ f32x2 cpair[D * D + D];        // (G1_ij, G2_ij) row-major, then (b1_i, b2_i)
+  __shared__ float stage[kWavesPerBlock][kWave * kMwStride];
+  __shared__ float gram[kWavesPerBlock][16 * 16];
+  for (int e = threadIdx.x; e < D * D + D; e += kBlock)
+    cpair[e] = e < D * D ? f32x2{c[2 * D + 1 + e], c[3 * D + 2 + D * D + e]}
+                         : f32x2{c[D + 1 + (e - D * D)], c[2 * D + 2 + D * D + (e - D * D)]};
+  float* srow = &stage[wave][lane * kMwStride];
+#pragma unroll
+  for (int k = M; k < 16; ++k) srow[k] = 0.f;  // padding features read as 0 by the MFMA
+  __syncthreads();
+  float m1[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) m1[k] = c[k];
+  const f32x2 a12 = f32x2{c[D], c[2 * D + 1 + D * D]};
+
+  f32x4 g4 = {0.f, 0.f, 0.f, 0.f};
+  float zs[M] = {};
+  float rows = 0.f;
   MomentAcc<D> acc;
   acc.zero();
-  float rows = 0.f;
   const float* base = z + (int64_t)t * set_stride;
-  const int64_t stride = (int64_t)gridDim.x * kBlock;
   const bool vec4 = (M % 4 == 0) && (ld % 4 == 0) && (set_stride % 4 == 0) && (((uintptr_t)z & 15) == 0);
-  for (int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x; r < n_rows; r += stride) {
-    const float* row = base + r * ld;
-    float v[M];
-    if (vec4) {
+  auto load = [&](int64_t r, float* v) {
+    if (r < n_rows) {
+      const float* row = base + r * ld;
+      if (vec4) {
 #pragma unroll
-      for (int k = 0; k < M; k += 4) {
-        const f32x4 q = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(row + k));
-        v[k] = q[0]; v[k + 1] = q[1]; v[k + 2] = q[2]; v[k + 3] = q[3];
+        for (int k = 0; k < M; k += 4) {
+          const f32x4 q = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(row + k));
+          v[k] = q[0]; v[k + 1] = q[1]; v[k + 2] = q[2]; v[k + 3] = q[3];
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < M; ++k) v[k] = row[k];
       }
     } else {
 #pragma unroll
-      for (int k = 0; k < M; ++k) v[k] = row[k];
+      for (int k = 0; k < M; ++k) v[k] = 0.f;
     }
-    rows += 1.f;
-    gz.add(v);
-    // (ds log rho, ds2 log rho) as one packed pair per coefficient: r = m1 - x
+  };
+  // wave-uniform trip count: every lane joins every MFMA (rows past the end are zeros, weight 0)
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  int64_t r0 = (int64_t)blockIdx.x * kBlock + wave * kWave;
+  float vn[M];
+  load(r0 + lane, vn);
+  for (; r0 < n_rows; r0 += stride) {
+    const bool active = r0 + lane < n_rows;
+    // keep the coefficient pairs in LDS: hoisted out of the loop they would take 2 d^2 + 2 d VGPRs
+    asm volatile("" ::: "memory");
+    float v[M];
+#pragma unroll
+    for (int k = 0; k < M; ++k) v[k] = vn[k];
+    load(r0 + stride + lane, vn);  // software prefetch of the next row
+    // stage the row, then the Gram of the wave's 64 rows on the matrix pipe
+#pragma unroll
+    for (int k = 0; k < M; k += 2) *reinterpret_cast<f32x2*>(srow + k) = f32x2{v[k], v[k + 1]};
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const float a = stage[wave][(4 * j + lane / 16) * kMwStride + (lane & 15)];
+      g4 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, a, g4, 0, 0, 0);
+    }
+    __builtin_amdgcn_wave_barrier();
+    rows += active ? 1.f : 0.f;
+#pragma unroll
+    for (int k = 0; k < M; ++k) zs[k] += v[k];
+    // (ds log rho, ds2 log rho) = (a1, a2) + (b1, b2) . r + r^T (G1, G2) r, r = m1 - x
     float rr[D];
 #pragma unroll
     for (int k = 0; k < D; ++k) rr[k] = m1[k] - v[k];
-    f32x2 q = f32x2{a1, a2};
+    f32x2 q = a12;
 #pragma unroll
     for (int i = 0; i < D; ++i) {
-      f32x2 g = f32x2{b1[i], b2[i]};
+      f32x2 g = cpair[D * D + i];
 #pragma unroll
-      for (int j = 0; j < D; ++j) g = f32x2{G1[i * D + j], G2[i * D + j]} * f32x2{rr[j], rr[j]} + g;
+      for (int j = 0; j < D; ++j) g = cpair[i * D + j] * f32x2{rr[j], rr[j]} + g;
       q = g * f32x2{rr[i], rr[i]} + q;
     }
-    const float w = q[1] + q[0] * q[0] + gamma * q[0];  // kinetic_mckean_vlasov.py:243-248
+    const float w = active ? q[1] + q[0] * q[0] + gamma * q[0] : 0.f;  // kinetic_mckean_vlasov.py:243-248
     acc.add(v, w);
   }
-  float mz[LZ];
-  gz.finish(rows, 1.f, mz);
-  __shared__ float lds[kWavesPerBlock * LZ];
+  // the wave's 16 x 16 Gram: lane holds rows 4 (lane / 16) + i, column lane % 16 (symmetric, so the
+  // row / column convention of the accumulator layout does not matter)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) gram[wave][(4 * (lane / 16) + i) * 16 + (lane & 15)] = g4[i];
   float* slab = partials + (int64_t)t * (LZ + LW) * gridDim.x;
-  block_reduce_to_slab(mz, LZ, lds, slab, blockIdx.x, gridDim.x);
+  float cs[1 + M];
+  cs[0] = rows;
+#pragma unroll
+  for (int k = 0; k < M; ++k) cs[1 + k] = zs[k];
+  __shared__ float lds[kWavesPerBlock * LW];
+  block_reduce_to_slab(cs, 1 + M, lds, slab, blockIdx.x, gridDim.x);  // syncs: gram[] is complete
+  for (int o = threadIdx.x; o < M * (M + 1) / 2; o += kBlock) {
+    int i = 0, rem = o;
+    while (rem >= M - i) { rem -= M - i; ++i; }
+    const int j = i + rem;
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < kWavesPerBlock; ++w) s += gram[w][i * 16 + j];
+    slab[(int64_t)(1 + M + o) * gridDim.x + blockIdx.x] = s;
+  }
   block_reduce_to_slab(acc.v, LW, lds, slab + (int64_t)LZ * gridDim.x, blockIdx.x, gridDim.x);
 }
 
