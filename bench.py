@@ -251,6 +251,9 @@ def run_c2(a, rank, world, dev):
 
 
 def run_c3(a, rank, world, dev):
+    """KFP-GMM d=4, K=8 (BASELINE configs[2]), the reference's online iteration: simulate (traj, tau, last
+    written) with the KFP-GMM residual value_and_grad over init = z0, 0T = every trajectory row,
+    terminal = last fused into the same launch (pdeinv_sde_simulate_kfp_gmm), all-reduce, finalize."""
     from example_problems.kinetic_fokker_planck_example_GMM import gmm_means
     from utils import prng
 
@@ -265,36 +268,53 @@ def run_c3(a, rank, world, dev):
     mus_model = torch.as_tensor(np.random.default_rng(0).standard_normal((K, d)), dtype=torch.float32, device=dev)
     bufs = {"traj": torch.empty((n, N, 2 * d), device=dev), "tau": torch.empty((n, N), device=dev),
             "last": torch.empty((N, 2 * d), device=dev)}
-    desc = native.kfp_gmm_desc(d, K, mus, gamma, T, N, N, N * n, world_scale=1.0 / world)
+    Ng = world * N
+    desc = native.kfp_gmm_desc(d, K, mus, gamma, T, Ng, Ng, Ng * n)
     counter = [0]
-    res_ev = []
+    last_out = [None]
 
     def step(record):
         if record is not None:
             record[0].record()
-        r = native.sde_simulate(z0, n, T / n, gamma, pot, seed=seed, counter_offset=counter[0],
-                                particle_offset=poff, out=bufs)
+        r = native.sde_simulate_kfp_gmm(z0, n, T / n, gamma, pot, desc, mus_model, seed=seed,
+                                        counter_offset=counter[0], particle_offset=poff, out=bufs)
         if record is not None:
             record[1].record()
         counter[0] = (counter[0] + n + 1) & 0xFFFFFFFF
-        acc = native.residual_kfp_gmm(desc, z0, r["last"], r["traj"].view(-1, 2 * d), mus_model)
-        if record is not None:
-            e2 = torch.cuda.Event(enable_timing=True)
-            e2.record()
-            res_ev.append((record[1], e2))
-        acc = dist.allreduce_sum(acc)
-        native.residual_kfp_gmm_finalize(desc, acc)
+        acc = dist.allreduce_sum(r["acc"])
+        last_out[0] = native.residual_kfp_gmm_finalize(desc, acc)
 
     ms, kern_ms = timed(step, a.steps, a.warmup, dev)
     value = world * N * (n + 1) / (ms / 1e3)
-    cfg = {"workload": "C3 kinetic FP, GMM potential K=8, d=4: EM simulate (traj+tau+last) + fused GMM "
-                       "residual value_and_grad over init/0T/terminal", "dim": d, "n_centers": K, "n_steps": n,
-           "particles_per_gpu": N, "total_time": T, "gamma": gamma, "parallelism": f"dp{world}"}
-    out = base_record(a, world, value, ms, cfg, kern_ms, sim_bytes(N, n, d), "sde_simulate_kernel<4,GMM,staged>")
-    r_ms = float(np.mean([s.elapsed_time(e) for s, e in res_ev]))
-    res_bytes = (N * (n + 2)) * 8 * d
-    out["residual"] = {"kernel": "kfp_gmm_kernel<4,8> + slab reduce", "ms": r_ms,
-                       "algorithmic_bytes": res_bytes, "GBps": res_bytes / (r_ms / 1e3) / 1e9}
+    cfg = {"workload": "C3 kinetic FP, GMM potential K=8, d=4: EM simulate (traj+tau+last) with the GMM-model KFP "
+                       "residual value_and_grad over init/0T/terminal fused into the same launch",
+           "dim": d, "n_centers": K, "n_steps": n, "particles_per_gpu": N, "total_time": T, "gamma": gamma,
+           "parallelism": f"dp{world}"}
+    out = base_record(a, world, value, ms, cfg, kern_ms, sim_bytes(N, n, d),
+                      "sde_simulate_kernel<4,GMM,staged,KM=8,fused KFP-GMM residual> (+ its slab reduce)",
+                      traffic_from_profiles("sde_simulate_C3_bytes_per_launch") if (N, n) == (1 << 22, 100) else None)
+    out["loss"] = float(last_out[0][0][0].item())
+
+    # untimed context: the same simulator without the residual, and the standalone residual kernel
+    # (the offline-dataset path) over the same trajectory, each timed with events on its stream
+    def ev_time(fn, reps=5):
+        fn()
+        s_, e_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s_.record()
+        for _ in range(reps):
+            fn()
+        e_.record()
+        torch.cuda.synchronize()
+        return s_.elapsed_time(e_) / reps
+
+    sim_ms = ev_time(lambda: native.sde_simulate(z0, n, T / n, gamma, pot, seed=seed, counter_offset=counter[0],
+                                                 particle_offset=poff, out=bufs))
+    res_ms = ev_time(lambda: native.residual_kfp_gmm(desc, z0, bufs["last"], bufs["traj"].view(-1, 2 * d), mus_model))
+    res_bytes = N * (n + 2) * 8 * d
+    out["simulate_only_ms"] = sim_ms
+    out["fused_over_simulate_only"] = kern_ms / sim_ms
+    out["standalone_residual"] = {"kernel": "kfp_gmm_kernel<4,8> + slab reduce (offline path)", "ms": res_ms,
+                                  "algorithmic_bytes": res_bytes, "GBps": res_bytes / (res_ms / 1e3) / 1e9}
     return out
 
 

@@ -242,6 +242,21 @@ int pdeinv_residual_kfp_gmm(const pdeinv_kfp_gmm_desc* desc, const float* d_init
                             int64_t ld_0T, const float* d_mus, void* d_workspace,
                             double* d_acc, void* stream);
 /* d_acc -> d_out[PDEINV_KFP_NOUT] (same slots as the quadratic residual), d_grad [K*d]. */
+
+/* The GMM simulator with this residual fused in (the reference's online KFP-GMM iteration:
+ * …_GMM.py:104-142 simulate, then kinetic_fokker_planck.py:11-69 over initial = z0, 0T = every
+ * trajectory row, terminal = last). Each particle's rows are consumed in registers as they are
+ * produced (no re-read of the trajectory); grad V* of a 0T row is the simulator's grad U at that
+ * state, so the residual's true GMM (n_centers_true, sigma_true, mus_true) must be the simulated
+ * potential (checked: PDEINV_ERR_INVALID otherwise). d_mus = the model centres [K*d] (device).
+ * Coefficients as above with n_init = n_term = N, n_0T = N * n_steps (global counts over ranks);
+ * the INITIAL / TERMINAL slots hold sum T3 / N of this call. Outputs: the simulator's (each nullable)
+ * and d_acc [PDEINV_GMM_NACC + K*d] fp64 (all-reduce, then pdeinv_residual_kfp_gmm_finalize).
+ * dim <= 8, model n_centers * dim <= 64. */
+size_t pdeinv_sde_simulate_kfp_gmm_workspace_bytes(const pdeinv_sde_desc* desc, const pdeinv_kfp_gmm_desc* res);
+int pdeinv_sde_simulate_kfp_gmm(const pdeinv_sde_desc* desc, const pdeinv_kfp_gmm_desc* res, const float* d_mus,
+                                const float* d_z0, float* d_traj, float* d_tau, float* d_last, void* d_workspace,
+                                double* d_acc, void* stream);
 int pdeinv_residual_kfp_gmm_finalize(const pdeinv_kfp_gmm_desc* desc, const double* d_acc,
                                      float* d_out, float* d_grad, void* stream);
 

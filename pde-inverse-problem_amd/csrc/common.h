@@ -176,6 +176,132 @@ struct PairGram {
   }
 };
 
+// softmax weights w_k of a_k = -|x - mu_k|^2 / (2 s^2) = (x.mu_k - |mu_k|^2/2)/s^2 + const(x)
+// (the |x|^2 term cancels in the softmax); returns w, mbar = sum_k w_k mu_k and t_k = x.mu_k.
+// l2s = log2(e)/s^2, nh[k] = -|mu_k|^2/2. Even d runs on packed pairs (v_pk_fma_f32).
+template <int D>
+__device__ __forceinline__ float dotd(const float* a, const float* b) {
+  if constexpr (D % 2 == 0) {
+    f32x2 t = {0.f, 0.f};
+#pragma unroll
+    for (int p = 0; p < D / 2; ++p) t = f32x2{a[2 * p], a[2 * p + 1]} * f32x2{b[2 * p], b[2 * p + 1]} + t;
+    return t[0] + t[1];
+  } else {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < D; ++i) t = fmaf(a[i], b[i], t);
+    return t;
+  }
+}
+
+// out[i] += s * a[i] (packed pairs for even d)
+template <int D>
+__device__ __forceinline__ void axpyd(float s, const float* a, float* out) {
+  if constexpr (D % 2 == 0) {
+#pragma unroll
+    for (int p = 0; p < D / 2; ++p) {
+      const f32x2 r = f32x2{s, s} * f32x2{a[2 * p], a[2 * p + 1]} + f32x2{out[2 * p], out[2 * p + 1]};
+      out[2 * p] = r[0];
+      out[2 * p + 1] = r[1];
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < D; ++i) out[i] = fmaf(s, a[i], out[i]);
+  }
+}
+
+template <int D, int KM>
+__device__ __forceinline__ void gmm_softmax(const float* x, const float (*mu)[D], const float* nh, float l2s,
+                                            float* w, float* mbar, float* t) {
+  // unused centre slots carry nh = -inf: weight exactly 0, no per-centre branches
+  float amax = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < KM; ++k) {
+    t[k] = dotd<D>(x, mu[k]);
+    w[k] = (t[k] + nh[k]) * l2s;
+    amax = fmaxf(amax, w[k]);
+  }
+  float den = 0.f;
+#pragma unroll
+  for (int k = 0; k < KM; ++k) {
+    w[k] = __builtin_amdgcn_exp2f(w[k] - amax);
+    den += w[k];
+  }
+  const float inv = __builtin_amdgcn_rcpf(den);
+#pragma unroll
+  for (int i = 0; i < D; ++i) mbar[i] = 0.f;
+#pragma unroll
+  for (int k = 0; k < KM; ++k) {
+    w[k] *= inv;
+    axpyd<D>(w[k], mu[k], mbar);
+  }
+}
+
+// One sample (x, v) of the KFP residual for the GMM model V_theta = -logsumexp_k(-|x-mu_k|^2/(2 s^2))
+// (kinetic_fokker_planck.py:33-50 per sample, …_GMM.py:214-234): returns grad V_theta = s2 (x - mbar) in g,
+// T1 = |g|^2, T2 = v^T Hess V_theta v, T3 = g . v, and adds the analytic adjoint of
+// c1 T1 + c2 T2 + c3 T3 with respect to mu (softmax chain rule; derivation and FD check:
+// oracle/numpy_ref.py kfp_gmm_grad_analytic) to gacc[K*D]. Shared by the standalone residual
+// (residual.hip kfp_gmm_kernel) and the simulator-fused one (sde.hip). The d-vector work runs on
+// packed pairs for even d; the per-centre scalars are folded so that each costs one or two FMAs.
+template <int D, int KM>
+__device__ __forceinline__ void gmm_residual_sample(const float (*mu)[D], const float* nh, float s2, float l2s,
+                                                    const float* x, const float* v, float c1, float c2, float c3,
+                                                    float* gacc, float* g, float& T1, float& T2, float& T3) {
+  float w[KM], mbar[D], xm[KM];
+  gmm_softmax<D, KM>(x, mu, nh, l2s, w, mbar, xm);
+  float e[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) {
+    e[i] = x[i] - mbar[i];
+    g[i] = s2 * e[i];
+  }
+  const float ee = dotd<D>(e, e), ev = dotd<D>(e, v), vv = dotd<D>(v, v);
+  T1 = s2 * s2 * ee;
+  T3 = s2 * ev;
+  float pk[KM], em[KM], pbar = 0.f, wp2 = 0.f;
+#pragma unroll
+  for (int k = 0; k < KM; ++k) {
+    pk[k] = dotd<D>(mu[k], v);
+    em[k] = dotd<D>(e, mu[k]);  // e.mu_k
+    pbar = fmaf(w[k], pk[k], pbar);
+    wp2 = fmaf(w[k] * pk[k], pk[k], wp2);
+  }
+  const float s4 = s2 * s2;
+  T2 = s2 * vv - s4 * (wp2 - pbar * pbar);  // v^T (I/s^2 - Cov_w(mu)/s^4) v
+  // adjoint: F_k = d f / d w_k = A1 em_k + pk_k (A2 (pk_k - 2 pbar) + A3), then the softmax chain rule
+  const float A1 = -2.f * c1 * s4, A2 = -c2 * s4, A3 = -c3 * s2;
+  float Fk[KM], Fbar = 0.f;
+#pragma unroll
+  for (int k = 0; k < KM; ++k) {
+    Fk[k] = fmaf(A1, em[k], pk[k] * fmaf(A2, pk[k] - 2.f * pbar, A3));
+    Fbar = fmaf(w[k], Fk[k], Fbar);
+  }
+#pragma unroll
+  for (int k = 0; k < KM; ++k) {
+    // cw (x - mu_k) + ce e + cv v with cw = w (F_k - Fbar) s2, ce = A1 w, cv = w (2 A2 (pk_k - pbar) + A3)
+    const float cw = w[k] * s2 * (Fk[k] - Fbar);
+    const float ce = A1 * w[k];
+    const float cv = w[k] * fmaf(2.f * A2, pk[k] - pbar, A3);
+    float* gk = gacc + k * D;
+    if constexpr (D % 2 == 0) {
+#pragma unroll
+      for (int p = 0; p < D / 2; ++p) {
+        const f32x2 xp = f32x2{x[2 * p], x[2 * p + 1]}, mp = f32x2{mu[k][2 * p], mu[k][2 * p + 1]};
+        f32x2 r = f32x2{gk[2 * p], gk[2 * p + 1]};
+        r = f32x2{cw, cw} * (xp - mp) + r;
+        r = f32x2{ce, ce} * f32x2{e[2 * p], e[2 * p + 1]} + r;
+        r = f32x2{cv, cv} * f32x2{v[2 * p], v[2 * p + 1]} + r;
+        gk[2 * p] = r[0];
+        gk[2 * p + 1] = r[1];
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < D; ++i) gk[i] += cw * (x[i] - mu[k][i]) + ce * e[i] + cv * v[i];
+    }
+  }
+}
+
 // fp64 column reducer launched after any kernel that wrote a partial slab.
 void launch_slab_reduce(const float* partials, int n_blocks, int n_cols, double* out,
                         hipStream_t stream);

@@ -137,40 +137,6 @@ struct GmmResArgs {
 
 constexpr int kGmmGridCap = 1024;
 
-// softmax weights w_k of a_k = -|x - mu_k|^2 / (2 s^2) = (x.mu_k - |mu_k|^2/2)/s^2 + const(x)
-// (the |x|^2 term cancels in the softmax); returns w, mbar = sum_k w_k mu_k and t_k = x.mu_k.
-// l2s = log2(e)/s^2, nh[k] = -|mu_k|^2/2.
-template <int D, int KM>
-__device__ __forceinline__ void gmm_softmax(const float* x, const float (*mu)[D], const float* nh, float l2s,
-                                            float* w, float* mbar, float* t) {
-  // unused centre slots carry nh = -inf: weight exactly 0, no per-centre branches
-  float amax = -INFINITY;
-#pragma unroll
-  for (int k = 0; k < KM; ++k) {
-    float dot = 0.f;
-#pragma unroll
-    for (int i = 0; i < D; ++i) dot = fmaf(x[i], mu[k][i], dot);
-    t[k] = dot;
-    w[k] = (dot + nh[k]) * l2s;
-    amax = fmaxf(amax, w[k]);
-  }
-  float den = 0.f;
-#pragma unroll
-  for (int k = 0; k < KM; ++k) {
-    w[k] = __builtin_amdgcn_exp2f(w[k] - amax);
-    den += w[k];
-  }
-  const float inv = __builtin_amdgcn_rcpf(den);
-#pragma unroll
-  for (int i = 0; i < D; ++i) mbar[i] = 0.f;
-#pragma unroll
-  for (int k = 0; k < KM; ++k) {
-    w[k] *= inv;
-#pragma unroll
-    for (int i = 0; i < D; ++i) mbar[i] = fmaf(w[k], mu[k][i], mbar[i]);
-  }
-}
-
 template <int D, int KM>
 __global__ __launch_bounds__(kBlock) void kfp_gmm_kernel(GmmResArgs a, const float* __restrict__ mus,
                                                          float* __restrict__ partials) {
@@ -230,50 +196,11 @@ __global__ __launch_bounds__(kBlock) void kfp_gmm_kernel(GmmResArgs a, const flo
       for (int i = 0; i < D; ++i) { xn[i] = row[i]; vn[i] = row[D + i]; }
     }
 
-    float w[KM], mbar[D], xm[KM];
-    gmm_softmax<D, KM>(x, mu, nh, a.l2s, w, mbar, xm);
-    float e[D], g[D], T1 = 0.f, T3 = 0.f, vv = 0.f;
-#pragma unroll
-    for (int i = 0; i < D; ++i) {
-      e[i] = x[i] - mbar[i];
-      g[i] = s2 * e[i];
-      T1 = fmaf(g[i], g[i], T1);
-      T3 = fmaf(g[i], v[i], T3);
-      vv = fmaf(v[i], v[i], vv);
-    }
-    float pk[KM], em[KM], pbar = 0.f, wp2 = 0.f;
-#pragma unroll
-    for (int k = 0; k < KM; ++k) {
-      float p = 0.f, q = xm[k];  // e.mu_k = x.mu_k - mbar.mu_k
-#pragma unroll
-      for (int i = 0; i < D; ++i) { p = fmaf(mu[k][i], v[i], p); q = fmaf(-mu[k][i], mbar[i], q); }
-      pk[k] = p;
-      em[k] = q;
-      pbar = fmaf(w[k], p, pbar);
-      wp2 = fmaf(w[k] * p, p, wp2);
-    }
-    const float s4 = s2 * s2;
-    const float T2 = s2 * vv - s4 * (wp2 - pbar * pbar);  // v^T (I/s^2 - Cov_w(mu)/s^4) v
-
     const float c1 = set == 0 ? a.c_nabla : 0.f;
     const float c2 = set == 0 ? a.c_hess : 0.f;
     const float c3 = set == 0 ? a.c_fric : (set == 1 ? a.c_init : a.c_term);
-    // adjoint: F_k = d f / d w_k, explicit d f / d mu_j, then softmax chain rule
-    float Fk[KM], Fbar = 0.f;
-#pragma unroll
-    for (int k = 0; k < KM; ++k) {
-      Fk[k] = -2.f * c1 * s4 * em[k] - c2 * s4 * (pk[k] * pk[k] - 2.f * pbar * pk[k]) - c3 * s2 * pk[k];
-      Fbar = fmaf(w[k], Fk[k], Fbar);
-    }
-#pragma unroll
-    for (int k = 0; k < KM; ++k) {
-      const float cw = w[k] * (Fk[k] - Fbar) * s2;
-      const float ce = -2.f * c1 * s4 * w[k];
-      const float cv = -w[k] * (2.f * c2 * s4 * (pk[k] - pbar) + c3 * s2);
-#pragma unroll
-      for (int i = 0; i < D; ++i)
-        acc[NS + k * D + i] += cw * (x[i] - mu[k][i]) + ce * e[i] + cv * v[i];
-    }
+    float g[D], T1, T2, T3;
+    gmm_residual_sample<D, KM>(mu, nh, s2, a.l2s, x, v, c1, c2, c3, acc + NS, g, T1, T2, T3);
     acc[PDEINV_GMM_ACC_LOSS] += c1 * T1 + c2 * T2 + c3 * T3;
     if (set == 0) {
       float wt[KM], mbt[D], xmt[KM];

@@ -100,15 +100,16 @@ struct GmmCentres {
 };
 
 template <int D, int KM>
-__device__ __forceinline__ void grad_gmm(const SdeArgs& a, const GmmCentres<D, KM>& C, const float* q, float* g) {
+__device__ __forceinline__ void grad_gmm(const SdeArgs& a, const float (*mu)[D], const float* cc, const float* q,
+                                         float* g) {
   float al[KM];
   float amax = -INFINITY;
 #pragma unroll
   for (int k = 0; k < KM; ++k) {
     float t = 0.f;
 #pragma unroll
-    for (int i = 0; i < D; ++i) t = fmaf(q[i], C.mu[k][i], t);
-    al[k] = fmaf(a.l2s, t, C.c[k]);
+    for (int i = 0; i < D; ++i) t = fmaf(q[i], mu[k][i], t);
+    al[k] = fmaf(a.l2s, t, cc[k]);
     amax = fmaxf(amax, al[k]);
   }
   float den = 0.f, acc[D];
@@ -119,7 +120,7 @@ __device__ __forceinline__ void grad_gmm(const SdeArgs& a, const GmmCentres<D, K
     const float e = __builtin_amdgcn_exp2f(al[k] - amax);
     den += e;
 #pragma unroll
-    for (int i = 0; i < D; ++i) acc[i] = fmaf(e, C.mu[k][i], acc[i]);
+    for (int i = 0; i < D; ++i) acc[i] = fmaf(e, mu[k][i], acc[i]);
   }
   const float inv = __builtin_amdgcn_rcpf(den);
 #pragma unroll
@@ -248,13 +249,28 @@ __device__ __forceinline__ float shift_u(const SdeArgs& a, uint32_t plo, uint32_
   return u32_unit(r.x);
 }
 
-template <int D, int POT, bool MOM, int STORE, int KM = 1, bool NOISE = false, int MINW = 1>
+// KFP residual of a GMM model fused into the GMM simulator (RES): the reference's online KFP-GMM
+// iteration simulates (…_GMM.py:104-142) and then evaluates kinetic_fokker_planck.py:11-69 over
+// initial = z0, 0T = every trajectory row, terminal = last. Here each particle's rows are consumed
+// in registers as they are produced — the trajectory is never re-read — and grad V* of a 0T row is
+// the simulator's own grad U at that state (computed by the next update anyway), so only the model
+// softmax and its adjoint are extra work. Coefficients as pdeinv_kfp_gmm_desc.
+struct GmmResFused {
+  const float* mus;  // model centres [K, d] (device)
+  int32_t K;
+  float s2, l2s;     // model 1/sigma^2, log2(e)/sigma^2
+  float c_nabla, c_hess, c_fric, c_true, c_init, c_term, inv_ni, inv_nt;
+};
+
+template <int D, int POT, bool MOM, int STORE, int KM = 1, bool NOISE = false, int MINW = 1, bool RES = false>
 __global__ __launch_bounds__(kBlock, MINW) void sde_simulate_kernel(SdeArgs a, const float* __restrict__ z0,
                                                               float* __restrict__ traj,
                                                               float* __restrict__ tau,
                                                               float* __restrict__ last,
-                                                              float* __restrict__ partials) {
+                                                              float* __restrict__ partials,
+                                                              GmmResFused rf = GmmResFused{}) {
   constexpr int M = 2 * D;
+  static_assert(!RES || (POT == PDEINV_POT_GMM && !MOM), "the fused residual is the GMM simulator's");
   const int bid = a.remap ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
   const int64_t i_raw = (int64_t)bid * kBlock + threadIdx.x;
   const bool active = i_raw < a.N;
@@ -267,7 +283,7 @@ __global__ __launch_bounds__(kBlock, MINW) void sde_simulate_kernel(SdeArgs a, c
 #pragma unroll
   for (int k = 0; k < M; ++k) z[k] = z0[i * a.ld_z0 + k];
   [[maybe_unused]] GmmCentres<D, KM> centres;
-  if constexpr (POT == PDEINV_POT_GMM) centres.load(a);
+  if constexpr (POT == PDEINV_POT_GMM && !RES) centres.load(a);
 
   __shared__ float lds[kWavesPerBlock * moment_len(M > 16 ? 2 : M)];
   const int nb = gridDim.x;
@@ -278,6 +294,68 @@ __global__ __launch_bounds__(kBlock, MINW) void sde_simulate_kernel(SdeArgs a, c
     init.add(z, w);
     block_reduce_to_slab(init.v, L, lds, partials, bid, nb);
   }
+
+  // fused GMM residual state: model centres (nh = -|mu|^2 / 2, empty slots -inf) and the accumulators
+  // With the residual fused, the true (simulated) and the model centres live in LDS and are read
+  // with wave-uniform broadcasts: in VGPRs they would take 2 (K d + K) registers and, beside the
+  // K d gradient accumulators, leave one wave per SIMD.
+  constexpr int NR = RES ? PDEINV_GMM_NACC + KM * D : 1;
+  struct LdsCentres {
+    float mu[KM][D];
+    float c[KM];
+  };
+  __shared__ LdsCentres lcen_s[RES ? 2 : 1];
+  [[maybe_unused]] LdsCentres& lcen = lcen_s[0];
+  [[maybe_unused]] LdsCentres& lmod = lcen_s[RES ? 1 : 0];
+  [[maybe_unused]] float racc[NR];
+  if constexpr (RES) {
+    for (int e = threadIdx.x; e < KM * (D + 1); e += kBlock) {
+      const int k = e / (D + 1), c = e % (D + 1);
+      if (c < D) {
+        lcen.mu[k][c] = k < a.K ? a.params[k * D + c] : 0.f;
+        lmod.mu[k][c] = k < rf.K ? rf.mus[k * D + c] : 0.f;
+      } else {
+        lcen.c[k] = k < a.K ? a.params[kMaxGmmK * D + k] : -INFINITY;
+        float n2 = 0.f;
+        for (int q = 0; q < D && k < rf.K; ++q) n2 = fmaf(rf.mus[k * D + q], rf.mus[k * D + q], n2);
+        lmod.c[k] = k < rf.K ? -0.5f * n2 : -INFINITY;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < NR; ++c) racc[c] = 0.f;
+  }
+  // set 0 = 0T (gt = grad V* at the row), 1 = initial, 2 = terminal; w = 0 for lanes past N
+  [[maybe_unused]] auto res_add = [&](const float* zz, const float* gt, int set) {
+    if constexpr (RES) {
+      const float c1 = set == 0 ? w * rf.c_nabla : 0.f;
+      const float c2 = set == 0 ? w * rf.c_hess : 0.f;
+      const float c3 = w * (set == 0 ? rf.c_fric : (set == 1 ? rf.c_init : rf.c_term));
+      float gm[D], T1, T2, T3;
+      gmm_residual_sample<D, KM>(lmod.mu, lmod.c, rf.s2, rf.l2s, zz, zz + D, c1, c2, c3, racc + PDEINV_GMM_NACC,
+                                 gm, T1, T2, T3);
+      racc[PDEINV_GMM_ACC_LOSS] += c1 * T1 + c2 * T2 + c3 * T3;
+      if (set == 0) {
+        float Tt = 0.f, Tgt = 0.f;
+#pragma unroll
+        for (int c = 0; c < D; ++c) {
+          Tt = fmaf(gt[c], gt[c], Tt);
+          Tgt = fmaf(gt[c] - gm[c], gt[c] - gm[c], Tgt);
+        }
+        const float ct = w * rf.c_true;
+        racc[PDEINV_GMM_ACC_LOSS] += ct * Tt;
+        racc[PDEINV_GMM_ACC_LOSS_GT] += ct * Tgt;
+        racc[PDEINV_GMM_ACC_NABLA] += ct * T1;
+        racc[PDEINV_GMM_ACC_HESSIAN] += ct * T2;
+        racc[PDEINV_GMM_ACC_FRICTION] += ct * T3;
+        racc[PDEINV_GMM_ACC_NABLA_TRUE] += ct * Tt;
+      } else if (set == 1) {
+        racc[PDEINV_GMM_ACC_INITIAL] += w * rf.inv_ni * T3;
+      } else {
+        racc[PDEINV_GMM_ACC_TERMINAL] += w * rf.inv_nt * T3;
+      }
+    }
+  };
 
   const float tau0 = (POT == PDEINV_POT_MEANFIELD_QUADRATIC) ? a.tau0_mf
                                                               : (a.random_shift ? shift_u(a, plo, phi, i) * a.dt : 0.f);
@@ -302,10 +380,18 @@ __global__ __launch_bounds__(kBlock, MINW) void sde_simulate_kernel(SdeArgs a, c
   };
 
   auto update = [&](float h, float sh, uint32_t s) {
+    // RES: re-read the LDS centres every update (hoisted out of the step loop they would take the
+    // registers this layout exists to save)
+    if constexpr (RES) asm volatile("" ::: "memory");
     float g[D], xi[D];
-    if constexpr (POT == PDEINV_POT_GMM) grad_gmm<D, KM>(a, centres, z, g);
+    if constexpr (POT == PDEINV_POT_GMM && RES) grad_gmm<D, KM>(a, lcen.mu, lcen.c, z, g);
+    else if constexpr (POT == PDEINV_POT_GMM) grad_gmm<D, KM>(a, centres.mu, centres.c, z, g);
     else if constexpr (POT == PDEINV_POT_MEANFIELD_QUADRATIC) grad_meanfield<D>(a, z, a.xbar + (int64_t)s * D, g);
     else grad_quadratic<D>(a, z, g);
+    if constexpr (RES) {
+      if (s == 0) res_add(z, g, 1);  // z0: the initial set
+      else res_add(z, g, 0);         // traj row s-1 (g = grad V* there): the 0T set
+    }
     gen_normals<D, NOISE>(a, plo, phi, s, i, xi);
     const float gh = a.gamma * h;
 #pragma unroll
@@ -335,6 +421,11 @@ __global__ __launch_bounds__(kBlock, MINW) void sde_simulate_kernel(SdeArgs a, c
   // final update: h = dt - tau0, lands exactly at T = n*dt (sampling_utils.py:44-46)
   update(h_last, sqrtf(h_last) * a.ns, (uint32_t)a.n_steps);
   if (active && last) store_row<D, kStoreNT>(last + i * M, z);
+  if constexpr (RES) {
+    res_add(z, z, 2);  // last: the terminal set
+    __shared__ float rlds[kWavesPerBlock * NR];
+    block_reduce_to_slab(racc, PDEINV_GMM_NACC + rf.K * D, rlds, partials, bid, nb);
+  }
 
   if constexpr (MOM) {
     float mv[L];
@@ -534,6 +625,23 @@ static void launch_sim(const SdeArgs& a, const float* z0, float* traj, float* ta
                        last, ws);
 }
 
+// Occupancy of the fused kernel: at d <= 4 the allocator fits 168 VGPRs (3 waves / SIMD) with a few
+// dwords of spill; at d = 8 forcing it spills hundreds, so the compiler chooses.
+template <int D> constexpr int kResMinWaves = D <= 4 ? 3 : 1;
+
+template <int D, int KM>
+static void launch_sim_res(const SdeArgs& a, const GmmResFused& rf, const float* z0, float* traj, float* tau,
+                           float* last, float* ws, hipStream_t st) {
+  const dim3 g(sim_grid(a.N)), b(kBlock);
+  constexpr int W = kResMinWaves<D>;
+  if (a.noise)
+    hipLaunchKernelGGL((sde_simulate_kernel<D, PDEINV_POT_GMM, false, kStoreStaged, KM, true, W, true>), g, b, 0, st,
+                       a, z0, traj, tau, last, ws, rf);
+  else
+    hipLaunchKernelGGL((sde_simulate_kernel<D, PDEINV_POT_GMM, false, kStoreStaged, KM, false, W, true>), g, b, 0,
+                       st, a, z0, traj, tau, last, ws, rf);
+}
+
 template <int D, bool MOM>
 static void launch_gmm_sim(const SdeArgs& a, const float* z0, float* traj, float* tau, float* last, float* ws,
                            hipStream_t st) {
@@ -614,6 +722,73 @@ extern "C" int pdeinv_sde_simulate(const pdeinv_sde_desc* d, const float* z0, fl
     rc = check_launch("slab_reduce_kernel");
   }
   return rc;
+}
+
+static int gmm_res_km(int K) { return K <= 4 ? 4 : (K <= 8 ? 8 : 16); }
+
+extern "C" size_t pdeinv_sde_simulate_kfp_gmm_workspace_bytes(const pdeinv_sde_desc* d, const pdeinv_kfp_gmm_desc* r) {
+  if (!d || !r || d->dim < 1 || d->dim > 8 || d->n_particles <= 0 || r->n_centers < 1) return 0;
+  return (size_t)(PDEINV_GMM_NACC + r->n_centers * d->dim) * sim_grid(d->n_particles) * sizeof(float);
+}
+
+extern "C" int pdeinv_sde_simulate_kfp_gmm(const pdeinv_sde_desc* d, const pdeinv_kfp_gmm_desc* r, const float* mus,
+                                           const float* z0, float* traj, float* tau, float* last, void* ws, double* acc,
+                                           void* stream) {
+  SdeArgs a;
+  int rc = build_args(d, a);
+  if (rc) return rc;
+  PDEINV_REQUIRE(r != nullptr, PDEINV_ERR_INVALID, "sde_kfp_gmm: null residual descriptor");
+  const int D = d->dim;
+  PDEINV_REQUIRE(d->potential.kind == PDEINV_POT_GMM, PDEINV_ERR_INVALID, "sde_kfp_gmm: the simulated potential must be GMM");
+  PDEINV_REQUIRE(r->dim == D, PDEINV_ERR_INVALID, "sde_kfp_gmm: residual dim != simulator dim");
+  PDEINV_REQUIRE(D <= 8, PDEINV_ERR_UNSUPPORTED, "sde_kfp_gmm: dim must be <= 8");
+  PDEINV_REQUIRE(r->n_centers >= 1 && r->n_centers <= kMaxGmmK && r->n_centers * D <= 64, PDEINV_ERR_UNSUPPORTED,
+                 "sde_kfp_gmm: need 1 <= model n_centers <= 16 and n_centers * dim <= 64");
+  // grad V* of a 0T row is the simulator's grad U there: the true potential must be the simulated one
+  bool same = r->n_centers_true == d->potential.n_centers && r->sigma_true == d->potential.sigma && r->mus_true;
+  for (int k = 0; same && k < r->n_centers_true * D; ++k) same = r->mus_true[k] == d->potential.params[k];
+  PDEINV_REQUIRE(same, PDEINV_ERR_INVALID, "sde_kfp_gmm: the residual's true GMM must be the simulated potential");
+  PDEINV_REQUIRE(std::isfinite(r->sigma) && r->sigma > 0.f, PDEINV_ERR_INVALID, "sde_kfp_gmm: model sigma must be > 0");
+  hipStream_t st = (hipStream_t)stream;
+  PDEINV_REQUIRE(acc != nullptr, PDEINV_ERR_INVALID, "sde_kfp_gmm: acc is null");
+  if (a.N == 0) {
+    if (hipMemsetAsync(acc, 0, sizeof(double) * (PDEINV_GMM_NACC + r->n_centers * D), st) != hipSuccess)
+      return fail(PDEINV_ERR_HIP, "sde_kfp_gmm: hipMemsetAsync failed");
+    return PDEINV_OK;
+  }
+  PDEINV_REQUIRE(z0 && mus && ws, PDEINV_ERR_INVALID, "sde_kfp_gmm: null pointer");
+  const size_t va = (D % 2 == 0) ? 16 : 8;
+  PDEINV_REQUIRE(aligned(traj, va) && aligned(last, va) && aligned(tau, 4), PDEINV_ERR_INVALID,
+                 "sde_kfp_gmm: traj/last must be 16-byte (even dim) or 8-byte (odd dim) aligned");
+  GmmResFused rf{};
+  rf.mus = mus;
+  rf.K = r->n_centers;
+  rf.s2 = 1.f / (r->sigma * r->sigma);
+  rf.l2s = rf.s2 * 1.4426950408889634f;
+  rf.c_nabla = r->c_nabla; rf.c_hess = r->c_hess; rf.c_fric = r->c_fric; rf.c_true = r->c_true;
+  rf.c_init = r->c_init; rf.c_term = r->c_term;
+  // the boundary sets are this call's z0 and last rows: their per-set means use the GLOBAL set sizes
+  // folded into c_init / c_term by the caller; INITIAL / TERMINAL report sum T3 / N of this call
+  rf.inv_ni = 1.f / (float)a.N;
+  rf.inv_nt = 1.f / (float)a.N;
+  const int km = gmm_res_km(a.K > rf.K ? a.K : rf.K);
+  float* wsf = (float*)ws;
+  switch (D) {
+#define CASE(DD)                                                                          \
+  case DD:                                                                                \
+    if (km == 4) launch_sim_res<DD, 4>(a, rf, z0, traj, tau, last, wsf, st);              \
+    else if (km == 8) launch_sim_res<DD, 8>(a, rf, z0, traj, tau, last, wsf, st);         \
+    else launch_sim_res<DD, 16>(a, rf, z0, traj, tau, last, wsf, st);                     \
+    break;
+    CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
+#undef CASE
+    default:
+      return fail(PDEINV_ERR_UNSUPPORTED, "sde_kfp_gmm: dim must be in [1, 8]");
+  }
+  rc = check_launch("sde_simulate_kernel<GMM, fused residual>");
+  if (rc) return rc;
+  launch_slab_reduce(wsf, sim_grid(a.N), PDEINV_GMM_NACC + r->n_centers * D, acc, st);
+  return check_launch("slab_reduce_kernel");
 }
 
 extern "C" size_t pdeinv_mf_workspace_bytes(const pdeinv_sde_desc* d) {

@@ -57,6 +57,7 @@ EXPORTED_SYMBOLS = (
     "pdeinv_residual_kmv_mlp_workspace_bytes", "pdeinv_residual_kmv_mlp",
     "pdeinv_mf_sums_len", "pdeinv_mf_sums_workspace_bytes", "pdeinv_mf_sums", "pdeinv_mf_mean_path",
     "pdeinv_kmv_moments_weights_workspace_bytes", "pdeinv_kmv_moments_weights",
+    "pdeinv_sde_simulate_kfp_gmm_workspace_bytes", "pdeinv_sde_simulate_kfp_gmm",
 )
 
 
@@ -151,6 +152,8 @@ def lib():
         "pdeinv_mf_workspace_bytes": (ctypes.c_size_t, [P]),
         "pdeinv_mf_step": (i32, [P, i32, P, P, P, P, P, P, P, P]),
         "pdeinv_sde_tau0": (i32, [P, P, P]),
+        "pdeinv_sde_simulate_kfp_gmm_workspace_bytes": (ctypes.c_size_t, [P, P]),
+        "pdeinv_sde_simulate_kfp_gmm": (i32, [P, P, P, P, P, P, P, P, P, P]),
         "pdeinv_mf_sums_len": (i64, [P]),
         "pdeinv_mf_sums_workspace_bytes": (ctypes.c_size_t, [P]),
         "pdeinv_mf_sums": (i32, [P, P, P, P, P]),
@@ -261,14 +264,10 @@ def make_potential(kind: int, params=None, n_centers: int = 0, sigma: float = 1.
     return desc, host  # keep `host` alive while desc is used
 
 
-def sde_simulate(z0: torch.Tensor, n_steps: int, dt: float, gamma: float, potential: dict, *,
-                 seed: int, counter_offset: int = 0, particle_offset: int = 0,
-                 noise_scale: float = SQRT2, random_shift: bool = True,
-                 noise: Optional[torch.Tensor] = None, shift_u: Optional[torch.Tensor] = None,
-                 traj: bool = True, tau: bool = True, last: bool = True,
-                 moments: bool = False, out: Optional[dict] = None) -> dict:
-    """utils/sampling_utils.py:25-52 on the GPU. Returns time-major traj [n, N, 2d]."""
-    _require_gpu()
+def _sim_desc(z0: torch.Tensor, n_steps: int, dt: float, gamma: float, potential: dict, seed: int,
+              counter_offset: int, particle_offset: int, noise_scale: float, random_shift: bool,
+              noise: Optional[torch.Tensor], shift_u: Optional[torch.Tensor]):
+    """(SdeDesc, keep-alive host params, z0 pointer) for the simulator entry points."""
     if z0.dim() != 2 or z0.shape[1] % 2:
         raise ValueError("q0_p0 must be [N, 2d]")
     N, m = z0.shape
@@ -296,20 +295,39 @@ def sde_simulate(z0: torch.Tensor, n_steps: int, dt: float, gamma: float, potent
         if tuple(shift_u.shape) != (N,) or not shift_u.is_contiguous():
             raise ValueError(f"shift_u must be contiguous [{N}]")
         desc.d_shift_u = _dev(shift_u, "shift_u")
+    return desc, p_host, z0p
+
+
+def _sim_outputs(res: dict, z0: torch.Tensor, n_steps: int, traj: bool, tau: bool, last: bool) -> dict:
+    N, m = z0.shape
     dev = z0.device
-    res = {} if out is None else out
     if traj and "traj" not in res:
         res["traj"] = torch.empty((n_steps, N, m), device=dev, dtype=torch.float32)
     if tau and "tau" not in res:
         res["tau"] = torch.empty((n_steps, N), device=dev, dtype=torch.float32)
     if last and "last" not in res:
         res["last"] = torch.empty((N, m), device=dev, dtype=torch.float32)
+    return res
+
+
+def sde_simulate(z0: torch.Tensor, n_steps: int, dt: float, gamma: float, potential: dict, *,
+                 seed: int, counter_offset: int = 0, particle_offset: int = 0,
+                 noise_scale: float = SQRT2, random_shift: bool = True,
+                 noise: Optional[torch.Tensor] = None, shift_u: Optional[torch.Tensor] = None,
+                 traj: bool = True, tau: bool = True, last: bool = True,
+                 moments: bool = False, out: Optional[dict] = None) -> dict:
+    """utils/sampling_utils.py:25-52 on the GPU. Returns time-major traj [n, N, 2d]."""
+    _require_gpu()
+    desc, p_host, z0p = _sim_desc(z0, n_steps, dt, gamma, potential, seed, counter_offset, particle_offset,
+                                  noise_scale, random_shift, noise, shift_u)
+    m = z0.shape[1]
+    res = _sim_outputs({} if out is None else out, z0, n_steps, traj, tau, last)
     ws = None
     if moments:
         if "moments" not in res:
-            res["moments"] = torch.empty((3, moment_len(m)), device=dev, dtype=torch.float64)
+            res["moments"] = torch.empty((3, moment_len(m)), device=z0.device, dtype=torch.float64)
         nbytes = lib().pdeinv_sde_workspace_bytes(ctypes.byref(desc))
-        ws = torch.empty(max(nbytes // 4, 1), device=dev, dtype=torch.float32)
+        ws = torch.empty(max(nbytes // 4, 1), device=z0.device, dtype=torch.float32)
     rc = lib().pdeinv_sde_simulate(
         ctypes.byref(desc), z0p, _dev(res.get("traj") if traj else None, "traj"),
         _dev(res.get("tau") if tau else None, "tau"), _dev(res.get("last") if last else None, "last"),
@@ -317,6 +335,38 @@ def sde_simulate(z0: torch.Tensor, n_steps: int, dt: float, gamma: float, potent
         stream_handle())
     del p_host
     _check(rc, "pdeinv_sde_simulate")
+    return res
+
+
+def sde_simulate_kfp_gmm(z0: torch.Tensor, n_steps: int, dt: float, gamma: float, potential: dict, res_desc,
+                         mus: torch.Tensor, *, seed: int, counter_offset: int = 0, particle_offset: int = 0,
+                         noise_scale: float = SQRT2, random_shift: bool = True, noise: Optional[torch.Tensor] = None,
+                         shift_u: Optional[torch.Tensor] = None, traj: bool = True, tau: bool = True,
+                         last: bool = True, out: Optional[dict] = None) -> dict:
+    """The GMM simulator with the KFP residual of a GMM model fused in (pdeinv_sde_simulate_kfp_gmm):
+    initial = z0, 0T = every trajectory row, terminal = last; the trajectory is never re-read. res_desc
+    from kfp_gmm_desc(..., n_init=N_global, n_term=N_global, n_0T=N_global * n_steps) whose true GMM is
+    the simulated potential. Returns the simulator outputs plus "acc" (fp64 [8 + K d], the
+    residual_kfp_gmm accumulator: all-reduce, then residual_kfp_gmm_finalize)."""
+    _require_gpu()
+    desc, p_host, z0p = _sim_desc(z0, n_steps, dt, gamma, potential, seed, counter_offset, particle_offset,
+                                  noise_scale, random_shift, noise, shift_u)
+    rdesc, _keep = res_desc
+    K, d = rdesc.n_centers, rdesc.dim
+    if tuple(mus.shape) != (K, d):
+        raise ValueError(f"mus must be [{K}, {d}]")
+    mus_c = mus.contiguous()
+    res = _sim_outputs({} if out is None else out, z0, n_steps, traj, tau, last)
+    nbytes = lib().pdeinv_sde_simulate_kfp_gmm_workspace_bytes(ctypes.byref(desc), ctypes.byref(rdesc))
+    ws = torch.empty(max(nbytes // 4, 1), device=z0.device, dtype=torch.float32)
+    res["acc"] = torch.empty(GMM_NACC + K * d, device=z0.device, dtype=torch.float64)
+    rc = lib().pdeinv_sde_simulate_kfp_gmm(
+        ctypes.byref(desc), ctypes.byref(rdesc), _dev(mus_c, "mus"), z0p,
+        _dev(res.get("traj") if traj else None, "traj"), _dev(res.get("tau") if tau else None, "tau"),
+        _dev(res.get("last") if last else None, "last"), _dev(ws, "workspace"), _dev(res["acc"], "acc", torch.float64),
+        stream_handle())
+    del p_host
+    _check(rc, "pdeinv_sde_simulate_kfp_gmm")
     return res
 
 
