@@ -459,7 +459,7 @@ def run_c5(a, rank, world, dev):
         "dtype": "f32", "data": "synthetic: Philox Gaussian-init ensembles, fresh noise per step", "config": cfg,
         "residual_samples_per_s": world * rows / (kern_ms / 1e3),
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": 157.3, "unit": "TFLOP/s", "frac": achieved / 157.3,
-                     "traffic": None,
+                     "traffic": traffic_from_profiles("mlp_residual_C5_bytes_per_launch") if N == 1 << 22 else None,
                      "kernel": ("MLP residual, fused fp32-MFMA path (hand-written GEMMs with fused prologues/epilogues)"
                                 if native.mlp_fused_supported(dims) else
                                 "MLP residual, library path (rocBLAS sgemm + element-wise kernels)"),
