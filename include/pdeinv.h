@@ -381,7 +381,10 @@ typedef struct {
   int64_t n_rows;         /* particles per time stamp */
   float gamma;            /* friction (weights c = ds2 + ds^2 + gamma ds) */
   const float* tilde_F;   /* HOST [d*d]: Phi* = 0.5 y^T tilde_F y (…_quadratic.py:193-203) */
-  int64_t chunk_rows;     /* pair rows per GEMM chunk; 0 => 2^18 */
+  int64_t chunk_rows;     /* pair rows per GEMM chunk (library path); 0 => 2^18 */
+  int32_t impl;           /* PDEINV_MLP_IMPL_*: AUTO / FUSED = the pair kernels (pairs built in registers,
+                             MFMA weight gradients; dim <= 8, width <= 28, n_layers <= 16, out <= 64),
+                             LIBRARY = pair rows through rocBLAS (any shape) */
 } pdeinv_kmv_mlp_desc;
 size_t pdeinv_residual_kmv_mlp_workspace_bytes(const pdeinv_kmv_mlp_desc* desc);
 int pdeinv_residual_kmv_mlp(const pdeinv_kmv_mlp_desc* desc, const float* d_z, int64_t set_stride, int64_t ld,

@@ -906,10 +906,44 @@ static int kmv_mlp_run(const pdeinv_kmv_mlp_desc* d, const KmvPlan& k, const flo
   return check_launch("kmv_mlp kernels");
 }
 
+// the narrow-net pair kernels (mlp_pairs.hip): pairs generated in registers, MFMA weight gradients
+namespace pdeinv {
+bool kmv_pairs_supported(const pdeinv_kmv_mlp_desc* d);
+size_t kmv_pairs_workspace_bytes(const pdeinv_kmv_mlp_desc* d);
+int kmv_pairs_run(const pdeinv_kmv_mlp_desc* d, const float* z, int64_t set_stride, int64_t ld, const float* ds,
+                  const float* params, void* ws, double* acc, float* grad, float** gbar_out, int pass, hipStream_t st);
+}  // namespace pdeinv
+
+static bool kmv_use_pairs(const pdeinv_kmv_mlp_desc* d) {
+  return d->impl != PDEINV_MLP_IMPL_LIBRARY && kmv_pairs_supported(d);
+}
+
+static size_t kmv_pairs_part_offset(const pdeinv_kmv_mlp_desc* d) { return (kmv_pairs_workspace_bytes(d) + 255) & ~(size_t)255; }
+
 extern "C" size_t pdeinv_residual_kmv_mlp_workspace_bytes(const pdeinv_kmv_mlp_desc* d) {
   if (!d || d->dim < 1 || d->n_layers < 1 || d->width < 1 || d->out_features < 1 || d->n_sets < 1 || d->n_rows < 1)
     return 0;
+  if (kmv_use_pairs(d)) return kmv_pairs_part_offset(d) + sizeof(double) * (size_t)d->n_sets * 3;
   return kmv_plan(d).total;
+}
+
+template <int D>
+static int kmv_pairs_orchestrate(const pdeinv_kmv_mlp_desc* d, const float* z, int64_t set_stride, int64_t ld,
+                                 const float* ds, const float* params, void* ws, double* acc, float* grad,
+                                 hipStream_t st) {
+  float* gbar = nullptr;
+  int rc = kmv_pairs_run(d, z, set_stride, ld, ds, params, ws, acc, grad, &gbar, 0, st);
+  if (rc) return rc;
+  double* part = (double*)((char*)ws + kmv_pairs_part_offset(d));
+  KmvTrueArgs ta{};
+  for (int q = 0; q < D * D; ++q) ta.F[q] = d->tilde_F[q];
+  const int64_t n = d->n_rows, T = d->n_sets;
+  hipLaunchKernelGGL(kmv_stamp_terms_kernel<D>, dim3((unsigned)T), dim3(kBlock), 0, st, ta, z, set_stride, ld, n, gbar,
+                     part);
+  hipLaunchKernelGGL(kmv_stamp_combine_kernel, dim3(1), dim3(64), 0, st, part, T, 1.0 / ((double)n * (double)T), acc);
+  rc = check_launch("kmv_stamp kernels");
+  if (rc) return rc;
+  return kmv_pairs_run(d, z, set_stride, ld, ds, params, ws, acc, grad, nullptr, 1, st);
 }
 
 extern "C" int pdeinv_residual_kmv_mlp(const pdeinv_kmv_mlp_desc* d, const float* z, int64_t set_stride, int64_t ld,
@@ -921,8 +955,17 @@ extern "C" int pdeinv_residual_kmv_mlp(const pdeinv_kmv_mlp_desc* d, const float
   PDEINV_REQUIRE(d->n_sets >= 1 && d->n_rows >= 1, PDEINV_ERR_INVALID, "kmv_mlp: need n_sets, n_rows >= 1");
   PDEINV_REQUIRE(ld >= 2 * d->dim && set_stride >= 0, PDEINV_ERR_INVALID, "kmv_mlp: row stride < 2*dim");
   PDEINV_REQUIRE(z && ds && params && ws && acc && grad && d->tilde_F, PDEINV_ERR_INVALID, "kmv_mlp: null pointer");
-  const KmvPlan k = kmv_plan(d);
   hipStream_t st = (hipStream_t)stream;
+  if (kmv_use_pairs(d)) {
+    switch (d->dim) {
+#define CASE(DD) case DD: return kmv_pairs_orchestrate<DD>(d, z, set_stride, ld, ds, params, ws, acc, grad, st);
+      CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
+#undef CASE
+    }
+  }
+  PDEINV_REQUIRE(d->impl != PDEINV_MLP_IMPL_FUSED, PDEINV_ERR_UNSUPPORTED,
+                 "kmv_mlp: the pair kernels need dim <= 8, width <= 28, n_layers <= 16, out_features <= 64");
+  const KmvPlan k = kmv_plan(d);
   switch (d->dim) {
 #define CASE(DD) case DD: return kmv_mlp_run<DD>(d, k, z, set_stride, ld, ds, params, (float*)ws, acc, grad, st);
     CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)

@@ -98,7 +98,8 @@ class KfpMlpDesc(ctypes.Structure):
 class KmvMlpDesc(ctypes.Structure):
     _fields_ = [("dim", ctypes.c_int32), ("n_layers", ctypes.c_int32), ("width", ctypes.c_int32),
                 ("out_features", ctypes.c_int32), ("n_sets", ctypes.c_int32), ("n_rows", ctypes.c_int64),
-                ("gamma", ctypes.c_float), ("tilde_F", ctypes.c_void_p), ("chunk_rows", ctypes.c_int64)]
+                ("gamma", ctypes.c_float), ("tilde_F", ctypes.c_void_p), ("chunk_rows", ctypes.c_int64),
+                ("impl", ctypes.c_int32)]
 
 
 MLP_IMPL_AUTO, MLP_IMPL_LIBRARY, MLP_IMPL_FUSED = 0, 1, 2
@@ -677,7 +678,8 @@ def kmv_moments_weights(d: int, gamma: float, coef: torch.Tensor, z: torch.Tenso
 
 
 def residual_kmv_mlp(dims, params_flat: torch.Tensor, z: torch.Tensor, n_sets: int, n_rows: int, set_stride: int,
-                     ld: int, ds: torch.Tensor, tilde_F, gamma: float, chunk_rows: int = 1 << 18):
+                     ld: int, ds: torch.Tensor, tilde_F, gamma: float, chunk_rows: int = 1 << 18,
+                     impl: int = MLP_IMPL_AUTO):
     """kinetic_mckean_vlasov.py:11-120 for Phi_theta = V_hypothesis over every pair of each time
     stamp's particles (pdeinv_residual_kmv_mlp). ds = (ds log rho, ds2 log rho) [n_sets, n_rows, 2]
     from kmv_weights(want_ds=True). Returns (acc fp64 [8], grad fp32 [P]) — finalize with
@@ -695,7 +697,7 @@ def residual_kmv_mlp(dims, params_flat: torch.Tensor, z: torch.Tensor, n_sets: i
         raise ValueError(f"KMV MLP residual: ds must be contiguous [{n_sets}, {n_rows}, 2]")
     F = _host_f32(tilde_F)
     desc = KmvMlpDesc(d, L, W, O, int(n_sets), int(n_rows), float(gamma), F.ctypes.data_as(ctypes.c_void_p),
-                      int(chunk_rows))
+                      int(chunk_rows), int(impl))
     nbytes = lib().pdeinv_residual_kmv_mlp_workspace_bytes(ctypes.byref(desc))
     ws = torch.empty(nbytes // 4, device=z.device, dtype=torch.float32)
     acc = torch.zeros(GMM_NACC, device=z.device, dtype=torch.float64)

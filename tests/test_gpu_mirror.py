@@ -50,17 +50,23 @@ def test_kmv_residual_vs_pairwise_restatement(native):
     assert np.allclose(g.cpu().numpy(), g_fd, rtol=1e-3, atol=1e-3)
 
 
-@pytest.mark.parametrize("d,n,chunk", [(2, 40, 1 << 18), (4, 37, 300)])
-def test_kmv_general_phi_mlp_vs_pairwise_restatement(native, d, n, chunk):
-    """General Phi_theta = V_hypothesis (non-parametric KMV, kinetic_mckean_vlasov.py:11-120):
-    the two-pass pair-row HIP path == the literal pair-tensor restatement (loss, loss ground truth,
-    terms) and its FD-checked analytic gradient (oracle kmv_mlp_grad_analytic). chunk = 300 forces
-    partial i-blocks and j-chunking of the pair rows. Tolerance 2e-4 relative (fp32 GEMMs)."""
+@pytest.mark.parametrize("d,n,chunk,W,L,impl", [(2, 40, 1 << 18, 20, 3, 0), (4, 37, 300, 20, 3, 1),
+                                                (4, 37, 300, 20, 3, 2), (3, 70, 300, 10, 2, 2),
+                                                (2, 130, 300, 20, 8, 2), (8, 65, 300, 28, 2, 2),
+                                                (1, 66, 300, 16, 4, 2)])
+def test_kmv_general_phi_mlp_vs_pairwise_restatement(native, d, n, chunk, W, L, impl):
+    """General Phi_theta = V_hypothesis (non-parametric KMV, kinetic_mckean_vlasov.py:11-120) == the
+    literal pair-tensor restatement (loss, loss ground truth, terms) and its FD-checked analytic gradient
+    (oracle kmv_mlp_grad_analytic), on both implementations: impl 2 / auto = the narrow-net pair kernels
+    (pairs built in registers, MFMA weight gradients; odd widths / dims zero-padded; n not a multiple of
+    the 64-pair tile), impl 1 = pair rows through rocBLAS (chunk = 300 forces partial i-blocks and
+    j-chunking). (2, 130, ..., 20, 8) is the reference's default net (MLP.yaml: width 20, 8 layers).
+    Tolerance 2e-4 relative (fp32)."""
     from example_problems.kinetic_mckean_vlasov_example_quadratic import KineticMcKeanVlasov
     from methods.consistency_instances import kinetic_mckean_vlasov as kmv
     from core.model import V_hypothesis
     from utils import native as nat, prng
-    n_t, W, L = 3, 20, 3
+    n_t = 3
     cfg = _cfg(["pde_instance=kinetic_mckean_vlasov", f"pde_instance.domain_dim={d}"])
     pi = KineticMcKeanVlasov(cfg, prng.PRNGKey(0))
     rng = np.random.default_rng(7)
@@ -84,7 +90,7 @@ def test_kmv_general_phi_mlp_vs_pairwise_restatement(native, d, n, chunk):
         coef = pi.coefficients(tau, z.device)
         _, ds = nat.kmv_weights(d, 1.0, coef, z, n_t, n, 2 * d, n_t * 2 * d, want_ds=True)
         acc, g = nat.residual_kmv_mlp(dims, flat, z, n_t, n, 2 * d, n_t * 2 * d, ds,
-                                      pi.initial_configuration["tilde_F"], 1.0, chunk_rows=chunk)
+                                      pi.initial_configuration["tilde_F"], 1.0, chunk_rows=chunk, impl=impl)
         out = nat.kfp_terms_finalize(acc, g, 1.0).cpu().numpy()
         got_loss, got_gt = float(out[nat.KFP_SLOTS.index("loss")]), float(out[nat.KFP_SLOTS.index("loss ground truth")])
         assert abs(out[nat.KFP_SLOTS.index("loss_Hessian")] - parts["hessian"]) < 2e-4 * (1 + abs(parts["hessian"]))
