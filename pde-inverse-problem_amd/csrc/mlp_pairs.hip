@@ -25,6 +25,8 @@
 // z = 0, h = tanh 0 = 0 and zero outgoing weights).
 #include <math.h>
 
+#include <type_traits>
+
 #include "common.h"
 
 namespace pdeinv {
@@ -188,7 +190,9 @@ __device__ __forceinline__ void wave_fence() { __builtin_amdgcn_wave_barrier(); 
 template <int D, int W>
 __global__ __launch_bounds__(kWavesPB * kWave) void kmvp_gbar_kernel(Args a) {
   const int lane = threadIdx.x & (kWave - 1);
-  const int64_t wave = (int64_t)blockIdx.x * kWavesPB + threadIdx.x / kWave;
+  // wave-uniform by construction; readfirstlane makes the compiler see it, so every per-wave base
+  // (ring, slab) lives in SGPRs and each ring access is SGPR base + one lane-offset VGPR + immediate
+  const int64_t wave = (int64_t)blockIdx.x * kWavesPB + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const int64_t n_waves = (int64_t)gridDim.x * kWavesPB;
   const Ring<W> ring{a.scratch + wave * (int64_t)5 * W * a.L * kWave, lane};
   cfloat* Ko = a.prm + kofs<D, W>(a.L);
@@ -273,7 +277,7 @@ template <int D, int W>
 __global__ __launch_bounds__(kWavesPB * kWave) void kmvp_grad_kernel(Args a) {
   static_assert(W < 32 && D < 32, "a constant-1 input feature must fit the 32-wide MFMA tile");
   const int lane = threadIdx.x & (kWave - 1);
-  const int wib = threadIdx.x / kWave;
+  const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);  // wave-uniform: SGPR bases
   const int64_t wave = (int64_t)blockIdx.x * kWavesPB + wib;
   const int64_t n_waves = (int64_t)gridDim.x * kWavesPB;
   __shared__ float stage[kWavesPB][2][kWave * kSR];
@@ -416,86 +420,130 @@ __global__ __launch_bounds__(kWavesPB * kWave) void kmvp_grad_kernel(Args a) {
         for (int k = 0; k < W; ++k) abar[0][k] = (1.f - hl[k] * hl[k]) * zb[0][k];
       }
       // ---- output seeds, Ko / bo gradient, hb streams into layer L ----
-      // ybar = 2 c2 y'' + 2 ubar + 2 c0 y,  y'bar = 4 c2 y',  y''bar = 2 c2 y,  u = 2 y (c1 = c3 = 0)
-      float hb[3][W] = {};
-      // A operands of the four outer products: h_L (+ const 1 for bo), h'_L, h''_L, abar_L
-#pragma unroll 1
-      for (int ty = 0; ty < 4; ++ty) {
+      // ybar = 2 c2 y'' + 2 ubar + 2 c0 y,  y'bar = 4 c2 y',  y''bar = 2 c2 y,  u = 2 y (c1 = c3 = 0).
+      // The four outer products (A = h_L + const 1 for bo, h'_L, h''_L, abar_L) run one type at a time,
+      // compile-time unrolled (a runtime type index into register arrays would demote them to scratch);
+      // the layer-L streams are re-read from the ring rather than held through the adjoint chains.
+      float hb[3][W];
+#pragma unroll
+      for (int k = 0; k < W; ++k) hb[0][k] = hb[1][k] = hb[2][k] = 0.f;
+      auto seed_type = [&](auto tyc) {
+        constexpr int ty = decltype(tyc)::value;
+        float st[3][W];  // the streams this type needs: h_L (0, 2, 3), h'_L (1), h''_L (0), abar_L (0, 3)
+        {
+          float hl[W], zd[W];
+          ring.get(L - 1, 0, hl);
+#pragma unroll
+          for (int k = 0; k < W; ++k) st[0][k] = hl[k];
+          if constexpr (ty == 1) {
+            ring.get(L - 1, 1, zd);
+#pragma unroll
+            for (int k = 0; k < W; ++k) st[1][k] = (1.f - hl[k] * hl[k]) * zd[k];
+          }
+          if constexpr (ty == 0) {
+            ring.get(L - 1, 1, zd);
+            ring.get(L - 1, 2, st[1]);  // z''
+#pragma unroll
+            for (int k = 0; k < W; ++k) {
+              const float s1 = 1.f - hl[k] * hl[k], s2 = -2.f * hl[k] * s1;
+              st[1][k] = fmaf(s1, st[1][k], s2 * zd[k] * zd[k]);  // h''_L
+            }
+          }
+          if constexpr (ty == 0 || ty == 3) {
+            ring.get(L - 1, 4, st[2]);
+#pragma unroll
+            for (int k = 0; k < W; ++k) st[2][k] *= 1.f - hl[k] * hl[k];  // abar_L = s1 zetabar_L
+          }
+        }
         wave_fence();
-        if (ty < 3) stage_row<W>(As, hs[ty], ty == 0, active);
-        else stage_row<W>(As, abar[0], false, active);
+        if constexpr (ty == 0) stage_row<W>(As, st[0], true, active);
+        else if constexpr (ty == 1) stage_row<W>(As, st[1], false, active);
+        else if constexpr (ty == 2) {
+          // h''_L for the A operand
+          float hl[W], zd[W], zdd[W];
+          ring.get(L - 1, 0, hl);
+          ring.get(L - 1, 1, zd);
+          ring.get(L - 1, 2, zdd);
+#pragma unroll
+          for (int k = 0; k < W; ++k) {
+            const float s1 = 1.f - hl[k] * hl[k], s2 = -2.f * hl[k] * s1;
+            zdd[k] = fmaf(s1, zdd[k], s2 * zd[k] * zd[k]);
+          }
+          stage_row<W>(As, zdd, false, active);
+        } else stage_row<W>(As, st[2], false, active);
         for (int n0 = 0; n0 < O; n0 += 32) {
           for (int o0 = n0; o0 < n0 + 32 && o0 < O; o0 += kOC) {
-            float yo[3][kOC], ub[kOC];
+            // y (all types), y' (type 1), y'' and ubar (type 0) of this output chunk
+            float y0[kOC], y1[kOC];
 #pragma unroll
             for (int c = 0; c < kOC; ++c) {
-              yo[0][c] = bo[o0 + c];
-              yo[1][c] = yo[2][c] = ub[c] = 0.f;
+              y0[c] = bo[o0 + c];
+              y1[c] = 0.f;
             }
+            [[maybe_unused]] float ub[kOC] = {};
 #pragma unroll
             for (int k = 0; k < W; ++k) {
               __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-              for (int c = 0; c < kOC; ++c)
-                {
-                  const float w = Ko[(int64_t)k * O + o0 + c];
-#pragma unroll
-                  for (int s = 0; s < 3; ++s) yo[s][c] = fmaf(hs[s][k], w, yo[s][c]);
-                  if (ty == 0) ub[c] = fmaf(abar[0][k], w, ub[c]);
+              for (int c = 0; c < kOC; ++c) {
+                const float w = Ko[(int64_t)k * O + o0 + c];
+                if constexpr (ty == 1) y1[c] = fmaf(st[1][k], w, y1[c]);
+                else y0[c] = fmaf(st[0][k], w, y0[c]);
+                if constexpr (ty == 0) {
+                  y1[c] = fmaf(st[1][k], w, y1[c]);  // y''
+                  ub[c] = fmaf(st[2][k], w, ub[c]);
                 }
+              }
             }
             float sb[kOC];
 #pragma unroll
             for (int c = 0; c < kOC; ++c) {
-              if (ty == 0) sb[c] = 2.f * c2 * yo[2][c] + 2.f * ub[c] + 2.f * c0 * yo[0][c];
-              else if (ty == 1) sb[c] = 4.f * c2 * yo[1][c];
-              else if (ty == 2) sb[c] = 2.f * c2 * yo[0][c];
-              else sb[c] = 2.f * yo[0][c];
+              if constexpr (ty == 0) sb[c] = 2.f * c2 * y1[c] + 2.f * ub[c] + 2.f * c0 * y0[c];
+              else if constexpr (ty == 1) sb[c] = 4.f * c2 * y1[c];
+              else if constexpr (ty == 2) sb[c] = 2.f * c2 * y0[c];
+              else sb[c] = 2.f * y0[c];
               if (!active) sb[c] = 0.f;
               Bs[lane * kSR + (o0 - n0) + c] = sb[c];
             }
-            if (ty < 3) {
+            if constexpr (ty < 3) {
 #pragma unroll
               for (int k = 0; k < W; ++k) {
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                for (int c = 0; c < kOC; ++c)
-                  hb[ty][k] = fmaf(sb[c], Ko[(int64_t)k * O + o0 + c], hb[ty][k]);
+                for (int c = 0; c < kOC; ++c) hb[ty][k] = fmaf(sb[c], Ko[(int64_t)k * O + o0 + c], hb[ty][k]);
               }
             }
           }
-          // columns of this 32-tile past O stay from earlier use: clear them
-          for (int c = O - n0; c < 32; ++c) Bs[lane * kSR + c] = 0.f;
+          for (int c = O - n0; c < 32; ++c) Bs[lane * kSR + c] = 0.f;  // columns past O in this tile
           wave_fence();
           f32x16 acc = {};
           mfma_tile(As, Bs, acc);
           fold<W>(slab, kofs<D, W>(L), ty == 0 ? bofs<D, W>(L, a.L, a.O) : -1, O, n0, acc);
           wave_fence();
         }
-      }
-      // ---- reverse sweep over the hidden layers ----
+      };
+      seed_type(std::integral_constant<int, 0>{});
+      seed_type(std::integral_constant<int, 1>{});
+      seed_type(std::integral_constant<int, 2>{});
+      seed_type(std::integral_constant<int, 3>{});
+      // ---- reverse sweep over the hidden layers (z-bars computed in place of the h-bars) ----
       for (int l = L - 1; l >= 0; --l) {
-        float zb[3][W], ze[W];
-        {
-          float hl[W], zd[W], zdd[W], al[W], zbar[W];
-          ring.get(l, 0, hl);
-          ring.get(l, 1, zd);
-          ring.get(l, 2, zdd);
-          ring.get(l, 3, al);
-          ring.get(l, 4, zbar);
+        float ze[W];
 #pragma unroll
-          for (int k = 0; k < W; ++k) {
-            const float hn = hl[k], s1 = 1.f - hn * hn, s2 = -2.f * hn * s1, s3 = -2.f * s1 * s1 - 2.f * hn * s2;
-            zb[0][k] = s1 * hb[0][k] + s2 * zd[k] * hb[1][k] + fmaf(s2, zdd[k], s3 * zd[k] * zd[k]) * hb[2][k] +
-                       s2 * al[k] * zbar[k];
-            zb[1][k] = s1 * hb[1][k] + 2.f * s2 * zd[k] * hb[2][k];
-            zb[2][k] = s1 * hb[2][k];
-            ze[k] = s1 * al[k];
-          }
+        for (int k = 0; k < W; ++k) {
+          __builtin_amdgcn_sched_barrier(0);
+          const float hn = *ring.at(l, 0, k), zd = *ring.at(l, 1, k), zdd = *ring.at(l, 2, k);
+          const float al = *ring.at(l, 3, k), zbar = *ring.at(l, 4, k);
+          const float s1 = 1.f - hn * hn, s2 = -2.f * hn * s1, s3 = -2.f * s1 * s1 - 2.f * hn * s2;
+          const float b0 = hb[0][k], b1 = hb[1][k], b2 = hb[2][k];
+          hb[0][k] = s1 * b0 + s2 * zd * b1 + fmaf(s2, zdd, s3 * zd * zd) * b2 + s2 * al * zbar;
+          hb[1][k] = s1 * b1 + 2.f * s2 * zd * b2;
+          hb[2][k] = s1 * b2;
+          ze[k] = s1 * al;
         }
         // gK_l += [h, h', h'', abar]_{l-1}^T [zb, z'b, z''b, zeta]_l ; gb_l += zb (const-1 feature)
-#pragma unroll 1
-        for (int ty = 0; ty < 4; ++ty) {
+        auto outer = [&](auto tyc) {
+          constexpr int ty = decltype(tyc)::value;
           wave_fence();
           if (l == 0) {
             float pv[D];
@@ -503,41 +551,42 @@ __global__ __launch_bounds__(kWavesPB * kWave) void kmvp_grad_kernel(Args a) {
             for (int k = 0; k < D; ++k) pv[k] = ty == 0 ? y[k] : (ty == 1 ? vi[k] : (ty == 2 ? 0.f : ab0[k]));
             stage_row<D>(As, pv, ty == 0, active);
           } else {
-            float hp[W], pv[W];
-            ring.get(l - 1, 0, hp);
-            if (ty == 0) {
+            float pv[W];
 #pragma unroll
-              for (int k = 0; k < W; ++k) pv[k] = hp[k];
-            } else if (ty == 3) {
-              ring.get(l - 1, 4, pv);
-#pragma unroll
-              for (int k = 0; k < W; ++k) pv[k] *= 1.f - hp[k] * hp[k];
-            } else {
-              float zd[W];
-              ring.get(l - 1, 1, zd);
-              if (ty == 1) {
-#pragma unroll
-                for (int k = 0; k < W; ++k) pv[k] = (1.f - hp[k] * hp[k]) * zd[k];
-              } else {
-                ring.get(l - 1, 2, pv);
-#pragma unroll
-                for (int k = 0; k < W; ++k) {
-                  const float s1 = 1.f - hp[k] * hp[k], s2 = -2.f * hp[k] * s1;
-                  pv[k] = fmaf(s1, pv[k], s2 * zd[k] * zd[k]);
-                }
-              }
+            for (int k = 0; k < W; ++k) {
+              const float hp = *ring.at(l - 1, 0, k), s1 = 1.f - hp * hp;
+              if constexpr (ty == 0) pv[k] = hp;
+              else if constexpr (ty == 1) pv[k] = s1 * *ring.at(l - 1, 1, k);
+              else if constexpr (ty == 2) {
+                const float zd = *ring.at(l - 1, 1, k);
+                pv[k] = fmaf(s1, *ring.at(l - 1, 2, k), -2.f * hp * s1 * zd * zd);
+              } else pv[k] = s1 * *ring.at(l - 1, 4, k);
             }
             stage_row<W>(As, pv, ty == 0, active);
           }
-          stage_row<W>(Bs, ty < 3 ? zb[ty] : ze, false, active);
+          if constexpr (ty < 3) stage_row<W>(Bs, hb[ty], false, active);
+          else stage_row<W>(Bs, ze, false, active);
           wave_fence();
           f32x16 acc = {};
           mfma_tile(As, Bs, acc);
           if (l == 0) fold<D>(slab, kofs<D, W>(0), ty == 0 ? bofs<D, W>(0, a.L, a.O) : -1, W, 0, acc);
           else fold<W>(slab, kofs<D, W>(l), ty == 0 ? bofs<D, W>(l, a.L, a.O) : -1, W, 0, acc);
           wave_fence();
+        };
+        outer(std::integral_constant<int, 0>{});
+        outer(std::integral_constant<int, 1>{});
+        outer(std::integral_constant<int, 2>{});
+        outer(std::integral_constant<int, 3>{});
+        if (l > 0) {
+          float nb[3][W];
+          mvT<W, W, 3>(a.prm + kofs<D, W>(l), hb, nb);
+#pragma unroll
+          for (int k = 0; k < W; ++k) {
+            hb[0][k] = nb[0][k];
+            hb[1][k] = nb[1][k];
+            hb[2][k] = nb[2][k];
+          }
         }
-        if (l > 0) mvT<W, W, 3>(a.prm + kofs<D, W>(l), zb, hb);
       }
     }
   }
