@@ -325,6 +325,8 @@ int pdeinv_residual_kmv(const pdeinv_kmv_desc* desc, const double* d_mom, const 
  * epilogues carry all of the element-wise algebra (layer 1 is recomputed from the rows, never
  * stored). PDEINV_MLP_IMPL_LIBRARY forces the rocBLAS + element-wise-kernel path (any shape);
  * PDEINV_MLP_IMPL_FUSED forces the fused path (PDEINV_ERR_UNSUPPORTED if the shape is not).
+ * Narrower widths (e.g. the reference default 20 x 8 layers, MLP.yaml) run the fused kernels
+ * zero-padded to the next compiled width (exact; parameters padded / gradient unpadded on the device).
  * d_params / d_grad: flat flax order [K_1 (d x W), b_1, K_2 (W x W), b_2, ..., K_o (W x out), b_o]
  * (pdeinv_mlp_param_count floats). d_acc [PDEINV_GMM_NACC] and d_grad are ACCUMULATED (+=): zero
  * them first. pdeinv_kfp_terms_finalize turns (acc, grad) into the PDEINV_KFP_* slots.

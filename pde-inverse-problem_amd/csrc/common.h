@@ -302,6 +302,31 @@ __device__ __forceinline__ void gmm_residual_sample(const float (*mu)[D], const 
   }
 }
 
+// V_hypothesis parameters zero-padded to wider compiled shapes (exact: a padded hidden unit has zero
+// incoming and outgoing weights, z = 0, h = tanh 0 = 0, so it changes no output and no real gradient).
+constexpr int kMlpPadMaxL = 16;
+// Padded <-> real flat parameter index (flax order: per layer kernel [in, out] then bias [out]).
+struct MlpPadMap {
+  int L;
+  int din[kMlpPadMaxL + 1], dout[kMlpPadMaxL + 1];     // real dims of layer l
+  int pin[kMlpPadMaxL + 1], pout[kMlpPadMaxL + 1];     // padded dims
+  int64_t roff[kMlpPadMaxL + 1], poff[kMlpPadMaxL + 1];  // kernel offsets (real / padded); bias follows the kernel
+  __host__ __device__ int64_t real_of(int64_t q) const {  // padded index -> real index or -1
+    for (int l = 0; l <= L; ++l) {
+      const int64_t kb = poff[l], bb = kb + (int64_t)pin[l] * pout[l], be = bb + pout[l];
+      if (q < kb || q >= be) continue;
+      if (q >= bb) {
+        const int n = (int)(q - bb);
+        return n < dout[l] ? roff[l] + (int64_t)din[l] * dout[l] + n : -1;
+      }
+      const int m = (int)((q - kb) / pout[l]), n = (int)((q - kb) % pout[l]);
+      return (m < din[l] && n < dout[l]) ? roff[l] + (int64_t)m * dout[l] + n : -1;
+    }
+    return -1;
+  }
+};
+
+
 // fp64 column reducer launched after any kernel that wrote a partial slab.
 void launch_slab_reduce(const float* partials, int n_blocks, int n_cols, double* out,
                         hipStream_t stream);

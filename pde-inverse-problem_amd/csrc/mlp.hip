@@ -446,10 +446,60 @@ static bool use_fused(const pdeinv_kfp_mlp_desc* d) {
   return mlpf::supported(d->dim, d->n_layers, d->width, d->out_features);
 }
 
+// Widths the fused MFMA kernels do not compile (the reference's default V_hypothesis is 20 wide,
+// configurations/neural_network/MLP.yaml:4-5) run them zero-padded to the next compiled width: exact
+// (common.h MlpPadMap), at the cost of the padded MACs.
+static int fused_pad_width(const pdeinv_kfp_mlp_desc* d) {
+  if (d->impl == PDEINV_MLP_IMPL_LIBRARY || use_fused(d) || d->n_layers > kMlpPadMaxL) return 0;
+  for (int w : {32, 64, 128, 256, 512})
+    if (w >= d->width && mlpf::supported(d->dim, d->n_layers, w, d->out_features)) return w;
+  return 0;
+}
+
+static MlpPadMap width_pad_map(const pdeinv_kfp_mlp_desc* d, int WP) {
+  MlpPadMap pm{};
+  pm.L = d->n_layers;
+  int64_t ro = 0, po = 0;
+  for (int l = 0; l <= pm.L; ++l) {
+    pm.din[l] = l == 0 ? d->dim : d->width;
+    pm.dout[l] = l == pm.L ? d->out_features : d->width;
+    pm.pin[l] = l == 0 ? d->dim : WP;
+    pm.pout[l] = l == pm.L ? d->out_features : WP;
+    pm.roff[l] = ro;
+    pm.poff[l] = po;
+    ro += (int64_t)pm.din[l] * pm.dout[l] + pm.dout[l];
+    po += (int64_t)pm.pin[l] * pm.pout[l] + pm.pout[l];
+  }
+  return pm;
+}
+
+static int64_t pad_param_count(const MlpPadMap& pm) {
+  return pm.poff[pm.L] + (int64_t)pm.pin[pm.L] * pm.pout[pm.L] + pm.pout[pm.L];
+}
+
+__global__ void mlp_pad_params_kernel(MlpPadMap pm, const float* __restrict__ src, int64_t P, float* __restrict__ dst) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= P) return;
+  const int64_t r = pm.real_of(q);
+  dst[q] = r >= 0 ? src[r] : 0.f;
+}
+
+__global__ void mlp_unpad_grad_kernel(MlpPadMap pm, const float* __restrict__ gp, int64_t P, float* __restrict__ grad) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= P) return;
+  const int64_t r = pm.real_of(q);
+  if (r >= 0) grad[r] += gp[q];
+}
+
 static int64_t chunk_rows_of(const pdeinv_kfp_mlp_desc* d) { return d->chunk_rows > 0 ? d->chunk_rows : (1 << 18); }
 
 extern "C" size_t pdeinv_residual_kfp_mlp_workspace_bytes(const pdeinv_kfp_mlp_desc* d) {
   if (!d || d->dim < 1 || d->n_layers < 1 || d->width < 1 || d->out_features < 1) return 0;
+  if (const int WP = fused_pad_width(d)) {
+    const int64_t P = pad_param_count(width_pad_map(d, WP));
+    return (mlpf::workspace_floats(d->dim, d->n_layers, WP, d->out_features, chunk_rows_of(d)) +
+            (size_t)PDEINV_GMM_NACC * kLossGrid + 2 * (((size_t)P + 63) & ~(size_t)63)) * sizeof(float);
+  }
   if (use_fused(d))
     return (mlpf::workspace_floats(d->dim, d->n_layers, d->width, d->out_features, chunk_rows_of(d)) +
             (size_t)PDEINV_GMM_NACC * kLossGrid) * sizeof(float);
@@ -643,9 +693,27 @@ extern "C" int pdeinv_residual_kfp_mlp(const pdeinv_kfp_mlp_desc* d, const float
       {z0, n0, ld0 ? ld0 : 2 * D, 0, d->c_nabla, d->c_hess, d->c_fric, 0.f},
       {zi, ni, ldi ? ldi : 2 * D, 1, 0.f, 0.f, bval ? 0.f : d->c_init, bval ? d->c_init : 0.f},
       {zt, nt, ldt ? ldt : 2 * D, 2, 0.f, 0.f, bval ? 0.f : d->c_term, bval ? d->c_term : 0.f}};
-  if (use_fused(d)) {
+  const int WP = fused_pad_width(d);
+  if (use_fused(d) || WP) {
     const int64_t Bc = chunk_rows_of(d);
-    const size_t fl = mlpf::workspace_floats(D, L, p.W, p.O, Bc);
+    const int Wf = WP ? WP : p.W;
+    const size_t fl = mlpf::workspace_floats(D, L, Wf, p.O, Bc);
+    const float* fparams = params;
+    float* fgrad = grad;
+    MlpPadMap pm{};
+    int64_t PP = 0;
+    if (WP) {  // zero-padded copy of the parameters and a padded gradient accumulator behind the workspace
+      pm = width_pad_map(d, WP);
+      PP = pad_param_count(pm);
+      float* pbuf = (float*)ws + fl + (size_t)PDEINV_GMM_NACC * kLossGrid;
+      float* gbuf = pbuf + ((PP + 63) & ~(int64_t)63);
+      hipLaunchKernelGGL(mlp_pad_params_kernel, dim3((unsigned)((PP + 255) / 256)), dim3(256), 0, st, pm, params, PP,
+                         pbuf);
+      if (hipMemsetAsync(gbuf, 0, sizeof(float) * PP, st) != hipSuccess) return fail(PDEINV_ERR_HIP, "kfp_mlp: memset");
+      fparams = pbuf;
+      fgrad = gbuf;
+      param_offsets(D, WP, O, L, poff, boff);
+    }
     LossCtx lc{};
     lc.la = la;
     lc.part = (float*)ws + fl;
@@ -657,11 +725,11 @@ extern "C" int pdeinv_residual_kfp_mlp(const pdeinv_kfp_mlp_desc* d, const float
       lc.la.inv_n = s.n ? 1.f / (float)s.n : 0.f;
       for (int64_t r0 = 0; r0 < s.n; r0 += Bc) {
         mlpf::Chunk c{};
-        c.d = D; c.L = L; c.W = p.W; c.O = p.O;
+        c.d = D; c.L = L; c.W = Wf; c.O = p.O;
         c.R = (s.n - r0) < Bc ? (s.n - r0) : Bc;
         c.z = s.z + r0 * s.ld;
         c.ldz = s.ld;
-        c.params = params; c.grad = grad; c.poff = poff; c.boff = boff;
+        c.params = fparams; c.grad = fgrad; c.poff = poff; c.boff = boff;
         c.c2 = s.c2; c.c3 = s.c3; c.c0 = s.c0;
         c.ws = (float*)ws; c.Bc = Bc;
         lc.zr = c.z;
@@ -669,6 +737,11 @@ extern "C" int pdeinv_residual_kfp_mlp(const pdeinv_kfp_mlp_desc* d, const float
         const int rc = mlpf::run_chunk(c, mlpf::LossHook{fused_loss_hook, &lc}, st);
         if (rc) return rc;
       }
+    }
+    if (WP) {
+      hipLaunchKernelGGL(mlp_unpad_grad_kernel, dim3((unsigned)((PP + 255) / 256)), dim3(256), 0, st, pm, fgrad, PP,
+                         grad);
+      return check_launch("mlp_unpad_grad_kernel");
     }
     return PDEINV_OK;
   }

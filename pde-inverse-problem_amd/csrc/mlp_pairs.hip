@@ -598,28 +598,7 @@ __global__ __launch_bounds__(kWavesPB * kWave) void kmvp_grad_kernel(Args a) {
   }
 }
 
-// Padded <-> real flat parameter index (flax order: per layer kernel [in, out] then bias [out]).
-struct PadMap {
-  int L;
-  int din[kMaxL + 1], dout[kMaxL + 1];     // real dims of layer l
-  int pin[kMaxL + 1], pout[kMaxL + 1];     // padded dims
-  int64_t roff[kMaxL + 1], poff[kMaxL + 1];  // kernel offsets (real / padded); bias follows the kernel
-  __host__ __device__ int64_t real_of(int64_t q) const {  // padded index -> real index or -1
-    for (int l = 0; l <= L; ++l) {
-      const int64_t kb = poff[l], bb = kb + (int64_t)pin[l] * pout[l], be = bb + pout[l];
-      if (q < kb || q >= be) continue;
-      if (q >= bb) {
-        const int n = (int)(q - bb);
-        return n < dout[l] ? roff[l] + (int64_t)din[l] * dout[l] + n : -1;
-      }
-      const int m = (int)((q - kb) / pout[l]), n = (int)((q - kb) % pout[l]);
-      return (m < din[l] && n < dout[l]) ? roff[l] + (int64_t)m * dout[l] + n : -1;
-    }
-    return -1;
-  }
-};
-
-__global__ void kmvp_pad_kernel(PadMap pm, const float* __restrict__ src, int64_t P, float* __restrict__ dst) {
+__global__ void kmvp_pad_kernel(MlpPadMap pm, const float* __restrict__ src, int64_t P, float* __restrict__ dst) {
   const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= P) return;
   const int64_t r = pm.real_of(q);
@@ -627,7 +606,7 @@ __global__ void kmvp_pad_kernel(PadMap pm, const float* __restrict__ src, int64_
 }
 
 // grad[real(q)] += sum_w slab[w][q] in a fixed order (fp64); acc slots likewise
-__global__ void kmvp_reduce_kernel(PadMap pm, const float* __restrict__ gslab, int64_t n_waves, int64_t P,
+__global__ void kmvp_reduce_kernel(MlpPadMap pm, const float* __restrict__ gslab, int64_t n_waves, int64_t P,
                                    const float* __restrict__ aslab, float* __restrict__ grad,
                                    double* __restrict__ acc) {
   const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -658,7 +637,7 @@ int pad_dim(int d) { return d <= 2 ? 2 : (d <= 4 ? 4 : 8); }
 int pad_width(int w) { return w <= 8 ? 8 : (w <= 16 ? 16 : (w <= 20 ? 20 : (w <= 24 ? 24 : 28))); }
 
 struct PairPlan {
-  mlpp::PadMap pm;
+  MlpPadMap pm;
   int DP, WP;
   int64_t P, n_waves, items;
   size_t off_prm, off_gbar, off_scratch, off_gslab, off_aslab, total;  // bytes
