@@ -18,20 +18,19 @@
 // are staged together so every source plane is read once per tile.
 //
 // Per chunk (L = 2; deeper nets add the "middle" steps):
-//   L1f   h1, h1', h1'' planes                 VALU over [x | v] rows
-//   FWD   z2 streams = [h1, h1', h1''] K2                               E: tanh -> h2, z2', z2''
+//   FWD   z2 streams = [h1, h1', h1''] K2      A: layer 1 from the rows   E: tanh -> h2, z2', z2''
 //   OUT   y streams  = [h2, h2', h2''] Ko      A: h', h'' from planes   E: +bo, V' and V'' per row
 //   R1    a2 = (2y) Ko^T                                                E: store
 //   R1    a1 = (s1(h2) a2) K2^T                                         E: store
 //   g     g = (s1(z1) a1) K1^T                 VALU, one wave per row (layer-1 recompute)
 //   loss  (mlp.hip)  per-row terms, abar0 = 2 c1 g
-//   L1a   abar1 = s1(z1) (abar0 K1)             VALU
-//   F2    zetabar2 = abar1 K2                                            E: store
+//   F2    zetabar2 = abar1 K2                  A: abar1 = s1(z1) (abar0 K1) from the rows   E: store
 //   UB    ubar = (s1(h2) zetabar2) Ko                                   E: seeds ybar.., bo grad
 //   R2    hbar2 streams = ybar streams Ko^T                             E: act_bwd -> zbar2, b2 grad
 //   R2    hbar1 streams = zbar2 streams K2^T                            E: store
 //   L1    layer-1 act_bwd + K1 / b1 gradient   VALU, columns per thread, rows looped
-//   G     Ko += [h2..abar2]^T [ybar..u];  K2 += [h1..abar1]^T [zbar2..zeta2]
+//   G     Ko += [h2..abar2]^T [ybar..u];  K2 += [h1..abar1]^T [zbar2..zeta2] (layer-1 streams rebuilt
+//         from the rows in the A prologue: the h1 / abar1 planes never exist)
 #include <math.h>
 
 #include <algorithm>
@@ -71,7 +70,11 @@ __device__ __forceinline__ int xcd_linear(int b, int nb) {
   return x < r ? x * (q + 1) + l : r * (q + 1) + (x - r) * q + l;
 }
 
-enum { A_RAW1 = 0, A_FWD, A_S1MUL, A_U, A_S3 };
+enum { A_RAW1 = 0, A_FWD, A_S1MUL, A_U, A_S3, A_L1F, A_L1A };
+// A_L1F / A_L1A build the layer-1 streams in the prologue from the sample rows (no h1 planes):
+//   A_L1F: [h1, s1 z1', s2 z1'^2] with z1 = x K1 + b1, z1' = v K1      (the FWD operand)
+//   A_L1A: abar1 = s1(z1) (abar0 K1)                                      (the F2 operand)
+// One thread owns one row (x and v | abar0 in registers), K1^T and b1 sit in LDS (broadcast reads).
 enum { B_NN = 0, B_NT };
 enum { E_ACT_FWD = 0, E_OUT, E_STORE, E_STORE3, E_SEEDS, E_ACT_BWD };
 
@@ -87,7 +90,35 @@ struct GemmArgs {
   float4* terms;  // per row {V', V'', V, 0}
   float c2, c3, c0;
   float* part;
+  const float* xz;   // A_L1*: sample rows [x | v], stride ldxz
+  int64_t ldxz;
+  const float* ab0;  // A_L1A: abar0 [R x d]
+  const float* k1;   // A_L1*: K1 [d x K] (flax [in, out]) and b1 [K]
+  const float* b1;
 };
+
+template <int AM>
+constexpr bool a_is_l1() { return AM == A_L1F || AM == A_L1A; }
+template <int D>
+constexpr int k1_stride() { return (D + 1 + 3) & ~3; }  // K1^T row: d weights, b1, pad to 16 B
+
+// K1^T and b1 into LDS, row k = [K1[0][k] .. K1[d-1][k], b1[k], 0..]
+template <int D>
+__device__ __forceinline__ void stage_k1t(const float* __restrict__ k1, const float* __restrict__ b1, int K,
+                                          float* k1s) {
+  constexpr int SK = k1_stride<D>();
+  for (int e = threadIdx.x; e < K * SK; e += kT) {
+    const int k = e / SK, i = e - k * SK;
+    k1s[e] = i < D ? k1[i * K + k] : (i == D ? b1[k] : 0.f);
+  }
+}
+
+// layer-1 pre-activation z1 = x . K1[:, k] + b1[k] and the second projection y . K1[:, k]
+template <int D>
+__device__ __forceinline__ void l1_project(const float* x, const float* y, const float* kc, float& z, float& zy) {
+  z = kc[D] + dotd<D>(x, kc);
+  zy = dotd<D>(y, kc);
+}
 
 // ---- operand staging: global -> registers (issued one k-block ahead, in flight under the
 //      MFMAs of the current block) -> prologue math -> LDS (k-major) ----------------------
@@ -187,8 +218,10 @@ __device__ __forceinline__ void store_b(const GemmArgs& a, const float (&rb)[BK 
   }
 }
 
-template <int S, int BM, int BN, int WGM, int AM, int BMD, int EM>
+template <int S, int BM, int BN, int WGM, int AM, int BMD, int EM, int D = 0>
 __global__ __launch_bounds__(kT, 2) void fgemm(GemmArgs a) {
+  constexpr bool L1 = a_is_l1<AM>();
+  static_assert(!L1 || (D > 0 && kT % BM == 0), "layer-1 prologue: D and one row per thread");
   constexpr int WGN = 4 / WGM;
   constexpr int WM = BM / WGM, WN = BN / WGN, MI = WM / 32, NI = WN / 32;
   static_assert(MI >= 1 && NI >= 1 && MI * 32 == WM && NI * 32 == WN, "wave tile must be 32-multiples");
@@ -198,7 +231,9 @@ __global__ __launch_bounds__(kT, 2) void fgemm(GemmArgs a) {
   extern __shared__ float lds[];
   float* As = lds;                  // [S][BK][LDA]
   float* Bs = As + S * BK * LDA;    // [BK][LDB]
+  [[maybe_unused]] float* k1s = Bs + BK * LDB;  // L1 modes: [K][SK]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if constexpr (L1) stage_k1t<D>(a.k1, a.b1, a.K, k1s);  // visible after the k-loop's first barrier
   const int wm = wave / WGN, wn = wave - (wave / WGN) * WGN, l31 = lane & 31, hi = lane >> 5;
   const int gx = gridDim.x, gy = gridDim.y;
   const int lid = xcd_linear(blockIdx.x + blockIdx.y * gx, gx * gy);
@@ -220,17 +255,47 @@ __global__ __launch_bounds__(kT, 2) void fgemm(GemmArgs a) {
 #pragma unroll
           for (int q = 0; q < 16; ++q) acc[s][mi][ni][q] = 0.f;
 
-    ARegs<BM, AM> ra;
+    ARegs<BM, L1 ? A_RAW1 : AM> ra;
     float rb[BK * BN / kT];
-    load_a<BM, AM>(a, ra, r0, 0);
+    [[maybe_unused]] float rx[L1 ? D : 1], ry[L1 ? D : 1];  // L1 modes: the thread's row (x, v | abar0)
+    if constexpr (L1) {
+      const int64_t r = std::min<int64_t>(r0 + tid % BM, a.R - 1);
+#pragma unroll
+      for (int i = 0; i < D; ++i) {
+        rx[i] = a.xz[r * a.ldxz + i];
+        ry[i] = AM == A_L1F ? a.xz[r * a.ldxz + D + i] : a.ab0[r * D + i];
+      }
+    } else {
+      load_a<BM, AM>(a, ra, r0, 0);
+    }
     load_b<BN, BMD>(a, rb, 0, n0);
     for (int k0 = 0; k0 < a.K; k0 += BK) {
       __syncthreads();  // every wave is done reading the previous tile
-      store_a<S, BM, AM>(a, ra, As, r0, k0, r0 + BM <= a.R && k0 + BK <= a.K);
+      if constexpr (L1) {
+        const bool rok = r0 + tid % BM < a.R;
+#pragma unroll
+        for (int j = 0; j < BM * BK / kT; ++j) {
+          const int m = tid % BM, kk = tid / BM + (kT / BM) * j;
+          const bool ok = rok && k0 + kk < a.K;
+          const float* kc = k1s + (ok ? k0 + kk : 0) * k1_stride<D>();
+          float z, zy;
+          l1_project<D>(rx, ry, kc, z, zy);
+          const float h = ftanh(z), s1 = 1.f - h * h;
+          if constexpr (AM == A_L1F) {
+            As[kk * LDA + m] = ok ? h : 0.f;
+            As[(BK + kk) * LDA + m] = ok ? s1 * zy : 0.f;
+            As[(2 * BK + kk) * LDA + m] = ok ? -2.f * h * s1 * zy * zy : 0.f;
+          } else {
+            As[kk * LDA + m] = ok ? s1 * zy : 0.f;
+          }
+        }
+      } else {
+        store_a<S, BM, AM>(a, ra, As, r0, k0, r0 + BM <= a.R && k0 + BK <= a.K);
+      }
       store_b<BN, BMD>(a, rb, Bs, k0, n0, k0 + BK <= a.K && n0 + BN <= a.N);
       __syncthreads();
       if (k0 + BK < a.K) {  // next tile's global loads fly under this tile's MFMAs
-        load_a<BM, AM>(a, ra, r0, k0 + BK);
+        if constexpr (!L1) load_a<BM, AM>(a, ra, r0, k0 + BK);
         load_b<BN, BMD>(a, rb, k0 + BK, n0);
       }
 #pragma unroll
@@ -487,7 +552,10 @@ __global__ __launch_bounds__(kT) void l1_grad_kernel(const float* __restrict__ h
 }
 
 // ---- weight gradients -------------------------------------------------------------------
-enum { GA_RAW4 = 0, GA_PL };  // A streams: 4 stored planes | h, s1 z', s1 z'' + s2 z'^2, s1 zetabar
+// A streams: 4 stored planes | h, s1 z', s1 z'' + s2 z'^2, s1 zetabar | the layer-1 streams
+// [h1, s1 z1', s2 z1'^2, s1 (abar0 K1)] rebuilt from the sample rows (thread owns one feature, its
+// K1 column in registers; the 16 rows of a step staged in LDS one step ahead)
+enum { GA_RAW4 = 0, GA_PL, GA_L1 };
 enum { GB_PL = 0, GB_SM };    // B streams: zbar0..2, s1(h) a | ybar0..2, 2 y
 
 struct WgradArgs {
@@ -497,12 +565,23 @@ struct WgradArgs {
   const float *pa0, *pa1, *pa2, *pa3;        // A planes (ld n_in)
   const float *pb0, *pb1, *pb2, *pb3, *pb4;  // B planes (ld n_out): ZB0..2, H, A  |  YB0..2, Y0
   float* part;                               // [slices][n_in][n_out]
+  const float* xz;                           // GA_L1: rows [x | v] (ld ldxz), abar0 [R x d], K1, b1
+  int64_t ldxz;
+  const float* ab0;
+  const float* k1;
+  const float* b1;
 };
 
 // Offsets inside one chunk's planes fit in 32 bits (run_chunk checks Bc * W < 2^31), so the
 // loads use a uniform base + 32-bit lane offset.
-template <int BM, int BN, int GA, int GB>
+template <int D>
+constexpr int xrow_stride() { return (3 * D + 3) & ~3; }  // [x | v | abar0] padded to 16 B
+
+template <int BM, int BN, int GA, int GB, int D = 0>
 __global__ __launch_bounds__(kT) void fwgrad(WgradArgs a) {
+  static_assert(GA != GA_L1 || (D > 0 && kT % BM == 0), "GA_L1: D and one feature per thread");
+  constexpr int XS = GA == GA_L1 ? xrow_stride<D>() : 1;
+  constexpr int NX = GA == GA_L1 ? (BKG * XS + kT - 1) / kT : 1;
   constexpr int WM = BM / 2, WN = BN / 2, MI = WM / 32, NI = WN / 32;
   static_assert(MI >= 1 && NI >= 1, "tile");
   constexpr int LDA = BM + 4, LDB = BN + 4;
@@ -511,6 +590,7 @@ __global__ __launch_bounds__(kT) void fwgrad(WgradArgs a) {
   extern __shared__ float lds[];
   float* As = lds;                  // [4][BKG][LDA]  (k = sample row)
   float* Bs = As + 4 * BKG * LDA;   // [4][BKG][LDB]
+  [[maybe_unused]] float* xs = Bs + 4 * BKG * LDB;  // GA_L1: [2][BKG][XS]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1, l31 = lane & 31, hi = lane >> 5;
   const int tiles_n = (a.n_out + BN - 1) / BN;
@@ -528,10 +608,34 @@ __global__ __launch_bounds__(kT) void fwgrad(WgradArgs a) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[mi][ni][q] = 0.f;
 
-  float ra[NEA][4], rb[NEB][NVB];
+  float ra[GA == GA_L1 ? 1 : NEA][4], rb[NEB][NVB];
+  [[maybe_unused]] float kc[GA == GA_L1 ? D + 1 : 1], xr[NX];
+  if constexpr (GA == GA_L1) {
+    const int i = std::min(i0 + tid % BM, a.n_in - 1);
+#pragma unroll
+    for (int q = 0; q < D; ++q) kc[q] = a.k1[q * a.n_in + i];
+    kc[D] = a.b1[i];
+  }
+  auto load_x = [&](int rb0) {  // the step's sample rows -> registers (staged to LDS one step later)
+#pragma unroll
+    for (int t = 0; t < NX; ++t) {
+      const int e = tid + t * kT, rr = e / XS, cc = e - rr * XS, r = rb0 + rr;
+      float v = 0.f;
+      if (e < BKG * XS && r < rs1 && cc < 3 * D)
+        v = cc < 2 * D ? a.xz[(int64_t)r * a.ldxz + cc] : a.ab0[(int64_t)r * D + cc - 2 * D];
+      xr[t] = v;
+    }
+  };
+  auto stage_x = [&](int buf) {
+#pragma unroll
+    for (int t = 0; t < NX; ++t) {
+      const int e = tid + t * kT;
+      if (e < BKG * XS) xs[buf * BKG * XS + e] = xr[t];
+    }
+  };
   auto load = [&](int rb0) {
 #pragma unroll
-    for (int j = 0; j < NEA; ++j) {
+    for (int j = 0; j < (GA == GA_L1 ? 0 : NEA); ++j) {
       const int e = tid + j * kT, rr = e / BM, ii = e - rr * BM;
       const int r = rb0 + rr, i = i0 + ii;
       const bool ok = r < rs1 && i < a.n_in;
@@ -554,13 +658,24 @@ __global__ __launch_bounds__(kT) void fwgrad(WgradArgs a) {
       if constexpr (NVB > 4) rb[j][4] = ldo(a.pb4, o);
     }
   };
-  auto store = [&](int rb0) {
+  auto store = [&](int rb0, int buf) {
     const bool rows_full = rb0 + BKG <= rs1;
 #pragma unroll
     for (int j = 0; j < NEA; ++j) {
       const int e = tid + j * kT, rr = e / BM, ii = e - rr * BM;
       const bool ok = (rows_full || rb0 + rr < rs1) && i0 + ii < a.n_in;
-      float v0 = ra[j][0], v1 = ra[j][1], v2 = ra[j][2], v3 = ra[j][3];
+      float v0, v1, v2, v3;
+      if constexpr (GA == GA_L1) {
+        const float* xrow = xs + (buf * BKG + rr) * XS;
+        const float z = kc[D] + dotd<D>(xrow, kc), zd = dotd<D>(xrow + D, kc), zb = dotd<D>(xrow + 2 * D, kc);
+        const float h = ftanh(z), s1 = 1.f - h * h;
+        v0 = h;
+        v1 = s1 * zd;
+        v2 = -2.f * h * s1 * zd * zd;
+        v3 = s1 * zb;
+      } else {
+        v0 = ra[j][0]; v1 = ra[j][1]; v2 = ra[j][2]; v3 = ra[j][3];
+      }
       if constexpr (GA == GA_PL) {
         const float h = v0, zd = v1, zdd = v2, zeb = v3;
         const float s1 = 1.f - h * h, s2 = -2.f * h * s1;
@@ -591,12 +706,22 @@ __global__ __launch_bounds__(kT) void fwgrad(WgradArgs a) {
     }
   };
 
-  if (rs0 < rs1) load(rs0);
-  for (int rb0 = rs0; rb0 < rs1; rb0 += BKG) {
+  if (rs0 < rs1) {
+    load(rs0);
+    if constexpr (GA == GA_L1) {
+      load_x(rs0);
+      stage_x(0);
+      if (rs0 + BKG < rs1) load_x(rs0 + BKG);
+    }
+  }
+  for (int rb0 = rs0, it = 0; rb0 < rs1; rb0 += BKG, ++it) {
     __syncthreads();
-    store(rb0);
+    store(rb0, it & 1);
+    if constexpr (GA == GA_L1) stage_x((it & 1) ^ 1);  // next step's rows (buffer last read a step ago)
     __syncthreads();
     if (rb0 + BKG < rs1) load(rb0 + BKG);  // in flight under this block's MFMAs
+    if constexpr (GA == GA_L1)
+      if (rb0 + 2 * BKG < rs1) load_x(rb0 + 2 * BKG);
 #pragma unroll
     for (int p = 0; p < 4; ++p)
 #pragma unroll
@@ -625,66 +750,6 @@ __global__ __launch_bounds__(kT) void fwgrad(WgradArgs a) {
         if (i < a.n_in && n < a.n_out) out[(int64_t)i * a.n_out + n] = acc[mi][ni][q];
       }
     }
-}
-
-// ---- layer-1 streams stored once (VALU): thread owns columns, rows staged in LDS ------------
-//   fwd:  h1 = tanh(x K1 + b1), h1' = s1 (v K1), h1'' = s2 (v K1)^2      (the FWD A operand)
-//   adj:  abar1 = (1 - h1^2) (abar0 K1)                                  (the F2 A operand)
-template <int D, int W, bool ADJ>
-__global__ __launch_bounds__(kT) void l1_planes_kernel(const float* __restrict__ z, int64_t ldz,
-                                                       const float* __restrict__ abar0,
-                                                       const float* __restrict__ K1, const float* __restrict__ b1,
-                                                       int64_t R, int64_t rpb, float* __restrict__ o0,
-                                                       float* __restrict__ o1, float* __restrict__ o2) {
-  constexpr int CW = W < kT ? W : kT, CPT = W / CW, RPH = kT / CW;
-  constexpr int XW = ADJ ? D : 2 * D;
-  __shared__ float xs[kL1Rows * XW];
-  const int tid = threadIdx.x, c0 = tid % CW, ph = tid / CW;
-  float k1[CPT][D], bb[CPT];
-#pragma unroll
-  for (int j = 0; j < CPT; ++j) {
-    bb[j] = b1[c0 + CW * j];
-#pragma unroll
-    for (int i = 0; i < D; ++i) k1[j][i] = K1[i * W + c0 + CW * j];
-  }
-  const int64_t rs = (int64_t)blockIdx.x * rpb;
-  const int64_t re = rs + rpb < R ? rs + rpb : R;
-  for (int64_t rb = rs; rb < re; rb += kL1Rows) {
-    __syncthreads();
-    for (int e = tid; e < kL1Rows * XW; e += kT) {
-      const int m = e / XW, c = e - m * XW;
-      const int64_t r = rb + m;
-      xs[e] = r < re ? (ADJ ? abar0[r * D + c] : z[r * ldz + c]) : 0.f;
-    }
-    __syncthreads();
-    const int nr = (int)(re - rb < kL1Rows ? re - rb : kL1Rows);
-    for (int m = ph; m < nr; m += RPH) {
-      const float* x = xs + m * XW;
-      const int64_t rowo = (rb + m) * W;
-#pragma unroll
-      for (int j = 0; j < CPT; ++j) {
-        const int64_t o = rowo + c0 + CW * j;
-        if constexpr (ADJ) {
-          float zb = 0.f;
-#pragma unroll
-          for (int i = 0; i < D; ++i) zb = fmaf(x[i], k1[j][i], zb);
-          const float h = o1[o];  // h1 plane (read), abar1 -> o0
-          o0[o] = (1.f - h * h) * zb;
-        } else {
-          float zz = bb[j], zd = 0.f;
-#pragma unroll
-          for (int i = 0; i < D; ++i) {
-            zz = fmaf(x[i], k1[j][i], zz);
-            zd = fmaf(x[D + i], k1[j][i], zd);
-          }
-          const float h = ftanh(zz), s1 = 1.f - h * h;
-          o0[o] = h;
-          o1[o] = s1 * zd;
-          o2[o] = -2.f * h * s1 * zd * zd;
-        }
-      }
-    }
-  }
 }
 
 // Fixed-order slab sums: out[i] += sum_s part[s][i]. Many slabs are first folded in groups of
@@ -726,10 +791,11 @@ static int sum_slabs(const float* part, int S, int64_t n, float* out, float* scr
   return check_launch("kfp_mlp fused slab sum");
 }
 
-template <int S, int BM, int BN, int WGM, int AM, int BMD, int EM>
+template <int S, int BM, int BN, int WGM, int AM, int BMD, int EM, int D = 0>
 static int launch_gemm(GemmArgs a, hipStream_t st, int* grid_x_out = nullptr) {
-  const size_t bytes = ((size_t)S * BK * (BM + 4) + (size_t)BK * (BN + 4)) * sizeof(float);
-  auto kern = fgemm<S, BM, BN, WGM, AM, BMD, EM>;
+  const size_t k1f = a_is_l1<AM>() ? (size_t)a.K * k1_stride<D>() : 0;
+  const size_t bytes = ((size_t)S * BK * (BM + 4) + (size_t)BK * (BN + 4) + k1f) * sizeof(float);
+  auto kern = fgemm<S, BM, BN, WGM, AM, BMD, EM, D>;
   if (bytes > 64 * 1024)
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
   a.n_mblocks = mblocks(a.R, BM);
@@ -741,18 +807,19 @@ static int launch_gemm(GemmArgs a, hipStream_t st, int* grid_x_out = nullptr) {
 }
 
 // single-stream GEMM over N = W: full-width 256-column tiles when W allows (A built once per row)
-template <int AM, int BMD>
+template <int AM, int BMD, int D = 0>
 static int launch_gemm1(GemmArgs a, hipStream_t st) {
-  if (a.N % 256 == 0) return launch_gemm<1, 64, 256, 2, AM, BMD, E_STORE>(a, st);
-  if (a.N > 64) return launch_gemm<1, 64, 128, 2, AM, BMD, E_STORE>(a, st);
-  if (a.N > 32) return launch_gemm<1, 64, 64, 2, AM, BMD, E_STORE>(a, st);
-  return launch_gemm<1, 128, 32, 4, AM, BMD, E_STORE>(a, st);
+  if (a.N % 256 == 0) return launch_gemm<1, 64, 256, 2, AM, BMD, E_STORE, D>(a, st);
+  if (a.N > 64) return launch_gemm<1, 64, 128, 2, AM, BMD, E_STORE, D>(a, st);
+  if (a.N > 32) return launch_gemm<1, 64, 64, 2, AM, BMD, E_STORE, D>(a, st);
+  return launch_gemm<1, 128, 32, 4, AM, BMD, E_STORE, D>(a, st);
 }
 
-template <int BM, int BN, int GA, int GB>
+template <int BM, int BN, int GA, int GB, int D = 0>
 static int launch_wgrad(WgradArgs a, float* grad_out, float* scratch, hipStream_t st) {
-  const size_t bytes = ((size_t)4 * BKG * (BM + 4) + (size_t)4 * BKG * (BN + 4)) * sizeof(float);
-  auto kern = fwgrad<BM, BN, GA, GB>;
+  const size_t xf = GA == GA_L1 ? (size_t)2 * BKG * xrow_stride<D>() : 0;
+  const size_t bytes = ((size_t)4 * BKG * (BM + 4) + (size_t)4 * BKG * (BN + 4) + xf) * sizeof(float);
+  auto kern = fwgrad<BM, BN, GA, GB, D>;
   if (bytes > 64 * 1024)
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
   const int tiles = ((a.n_in + BM - 1) / BM) * ((a.n_out + BN - 1) / BN);
@@ -774,7 +841,7 @@ bool supported(int d, int L, int W, int O) {
 
 // workspace layout (floats), chunk of Bc rows
 struct Layout {
-  size_t layer0, layer_stride, h1, abar1, a1, hb1, ys, yb, terms, g, abar0, part, part2, total;
+  size_t layer0, layer_stride, a1, hb1, ys, yb, terms, g, abar0, part, part2, total;
 };
 enum { P_H = 0, P_ZD, P_ZDD, P_A, P_ZETABAR, P_ZB0, P_ZB1, P_ZB2, kPlanes };
 
@@ -792,8 +859,6 @@ static Layout layout(int d, int L, int W, int O, int64_t Bc) {
   const size_t plane = ((size_t)Bc * W + 63) & ~(size_t)63;
   y.layer_stride = plane * kPlanes;
   y.layer0 = take(y.layer_stride * (L - 1));
-  y.h1 = take(3 * plane);
-  y.abar1 = take(plane);
   y.a1 = take(plane);
   y.hb1 = take(3 * plane);
   y.ys = take((size_t)3 * Bc * O);
@@ -824,8 +889,6 @@ static int run_chunk_t(const Chunk& c, const LossHook& loss, hipStream_t st) {
   float* ws = c.ws;
   const size_t plane = ((size_t)c.Bc * W + 63) & ~(size_t)63;
   auto P = [&](int l, int k) { return ws + y.layer0 + y.layer_stride * (size_t)(l - 2) + plane * k; };
-  float* H1[3] = {ws + y.h1, ws + y.h1 + plane, ws + y.h1 + 2 * plane};
-  float* ABAR1 = ws + y.abar1;
   float* A1 = ws + y.a1;
   float* HB1[3] = {ws + y.hb1, ws + y.hb1 + plane, ws + y.hb1 + 2 * plane};
   float* Ys[3] = {ws + y.ys, ws + y.ys + (size_t)c.Bc * O, ws + y.ys + 2 * (size_t)c.Bc * O};
@@ -847,6 +910,11 @@ static int run_chunk_t(const Chunk& c, const LossHook& loss, hipStream_t st) {
   base.c3 = c.c3;
   base.c0 = c.c0;
   base.part = part;
+  base.xz = c.z;
+  base.ldxz = c.ldz;
+  base.ab0 = abar0;
+  base.k1 = Kw(1);
+  base.b1 = Bw(1);
   int rc = 0;
 #define RC(x)          \
   do {                 \
@@ -857,15 +925,11 @@ static int run_chunk_t(const Chunk& c, const LossHook& loss, hipStream_t st) {
   const int l1_blocks = (int)std::min<int64_t>((R + kL1Rows - 1) / kL1Rows, kRowGridCap);
   const int64_t l1_rpb = (R + l1_blocks - 1) / l1_blocks;
   // ---- F1 -------------------------------------------------------------------------------
-  hipLaunchKernelGGL((l1_planes_kernel<D, WB, false>), dim3(l1_blocks), dim3(kT), 0, st, c.z, c.ldz, nullptr, Kw(1),
-                     Bw(1), R, l1_rpb, H1[0], H1[1], H1[2]);
-  RC(check_launch("kfp_mlp fused layer-1 streams"));
-  {
+  {  // layer 1 in the prologue (h1 streams never stored), layer 2 on MFMA
     GemmArgs a = base;
     a.K = W; a.N = W; a.Bw = Kw(2); a.bias = Bw(2);
-    a.pa0 = H1[0]; a.pa1 = H1[1]; a.pa2 = H1[2];
     a.po0 = P(2, P_H); a.po1 = P(2, P_ZD); a.po2 = P(2, P_ZDD);
-    RC((launch_gemm<3, TM, TN, TG, A_S3, B_NN, E_ACT_FWD>(a, st)));
+    RC((launch_gemm<3, TM, TN, TG, A_L1F, B_NN, E_ACT_FWD, D>(a, st)));
   }
   for (int l = 3; l <= L; ++l) {
     GemmArgs a = base;
@@ -900,13 +964,10 @@ static int run_chunk_t(const Chunk& c, const LossHook& loss, hipStream_t st) {
   }
   RC(loss.fn(loss.ctx, G, terms, abar0, R, st));
   // ---- F2: forward adjoint ----------------------------------------------------------------
-  hipLaunchKernelGGL((l1_planes_kernel<D, WB, true>), dim3(l1_blocks), dim3(kT), 0, st, c.z, c.ldz, abar0, Kw(1),
-                     Bw(1), R, l1_rpb, ABAR1, H1[0], nullptr);
-  RC(check_launch("kfp_mlp fused layer-1 adjoint"));
-  {
+  {  // abar1 = s1(z1) (abar0 K1) in the prologue
     GemmArgs a = base;
-    a.K = W; a.N = W; a.Bw = Kw(2); a.pa0 = ABAR1; a.po0 = P(2, P_ZETABAR);
-    RC((launch_gemm1<A_RAW1, B_NN>(a, st)));
+    a.K = W; a.N = W; a.Bw = Kw(2); a.po0 = P(2, P_ZETABAR);
+    RC((launch_gemm1<A_L1A, B_NN, D>(a, st)));
   }
   for (int l = 3; l <= L; ++l) {
     GemmArgs a = base;
@@ -974,9 +1035,9 @@ static int run_chunk_t(const Chunk& c, const LossHook& loss, hipStream_t st) {
   {
     WgradArgs g{};
     g.R = R; g.n_in = W; g.n_out = W; g.part = part;
-    g.pa0 = H1[0]; g.pa1 = H1[1]; g.pa2 = H1[2]; g.pa3 = ABAR1;
+    g.xz = c.z; g.ldxz = c.ldz; g.ab0 = abar0; g.k1 = Kw(1); g.b1 = Bw(1);
     g.pb0 = P(2, P_ZB0); g.pb1 = P(2, P_ZB1); g.pb2 = P(2, P_ZB2); g.pb3 = P(2, P_H); g.pb4 = P(2, P_A);
-    RC((launch_wgrad<GW, GW, GA_RAW4, GB_PL>(g, c.grad + c.poff[1], part2, st)));
+    RC((launch_wgrad<GW, GW, GA_L1, GB_PL, D>(g, c.grad + c.poff[1], part2, st)));
   }
 #undef RC
   return 0;
