@@ -139,298 +139,247 @@ __global__ __launch_bounds__(kBlock) void realnvp_logdensity_kernel(NvpArgs a, c
 
 // ---------------------------------------------------------------------------------------------
 // Value and parameter gradient of the maximum-likelihood loss (log_density_estimation.py:47-58):
-// loss = -mean_i log p_{t_i}(x_i), replacing jax.value_and_grad(loss_fn). One thread per sample,
-// one 256-sample tile per block.
+// loss = -mean_i log p_{t_i}(x_i), replacing jax.value_and_grad(loss_fn).
+//
+// Matrix-core formulation (v_mfma_f32_16x16x4_f32, exact fp32). Samples go in tiles of 16; every
+// per-sample 16-vector (x, its gradient, the time embedding, each hidden layer) lives in the
+// MFMA accumulator layout: lane (g = lane / 16, s = lane % 16) holds components 4g .. 4g + 3 of
+// sample s. A dense layer out = W^T in is four MFMAs whose B operand at k-step j is register j of
+// that same layout — k-slot (j, g) stands for input component 4g + j, and the A operand (the
+// weights, read from LDS) is permuted to match — so layers chain with no data movement at all.
+// The input-gradient product W d uses the transposed read of the same LDS matrix. Weight
+// gradients sum_s a_s d_s^T take the samples as the reduction dimension: the two tiles go
+// through a per-wave LDS stage (one 16-byte write per lane, one read per k-step) into four MFMAs
+// whose accumulators (ΔW in the same layout, rows = inputs) stay in registers over the wave's
+// tiles. Bias and scaling-factor gradients are per-lane sums, wave-reduced at the flush.
+// All widths are padded to 16 (the net's first layer: 8 outputs; x: d <= 8 coordinates; time:
+// n_t <= 16 features) with zero weights, so padded components stay exactly 0.
 // * The backward pass walks the coupling layers in the opposite order of the likelihood pass and
-//   rebuilds each layer's input from its output by inverting the layer (x_in = x_out e^{-s} - tr;
-//   the masked coordinates, which feed s and tr, pass through unchanged and exact): no per-layer
-//   state is stored.
-// * Parameters are staged in LDS in a zero-padded canonical layout (x rows padded to DM, time rows
-//   to 16, output columns to DM, the time embedding to 16 x 16), so every per-sample loop has
-//   compile-time trip counts and no predicates: padded inputs are 0 and meet zero weights. Every
-//   lane reads the same weight (a broadcast ds_read).
-// * Each dense layer's weight gradient sum_samples a_i delta_o is formed per tile in LDS (rows of
-//   a and delta staged; items = (row i, 4 outputs) x sample slices; fixed-order slice combine)
-//   and written to the tile's row of a [tiles x (P + 1)] slab (column P = sum log p). A
-//   fixed-order fp64 column reduce (chunked over at most kNvpMaxRows tiles) gives
-//   grad = -1/n sum. No float atomics: bit-reproducible run to run.
-// Compiled for DM in {2, 4, 8} with the runtime dim d <= DM (padded coordinates are x = 0,
-// mask = 1, so they never move) and for the celu / elu activation (the flow of
-// log_density_estimation.py:103-114).
+//   rebuilds each layer's input by inverting the layer (x_in = x_out e^{-s} - tr; the masked
+//   coordinates, which feed s and tr, pass through unchanged and exact): no per-layer state.
+// * Per coupling layer the block flushes its four waves' partial gradients through LDS into its
+//   slab row (reference parameter order; column P = sum log p); a fixed-order fp64 column reduce
+//   gives grad = -1/n sum. No float atomics: bit-reproducible run to run.
+// Built for the celu / elu activation (the flow of log_density_estimation.py:103-114).
 // ---------------------------------------------------------------------------------------------
-constexpr int kNvpAst = 25;        // LDS row stride of a (<= 8 + 16 values; odd: conflict-free row writes)
-constexpr int kNvpGst = 17;        // LDS row stride of delta (<= 16 values)
-constexpr int kNvpMaxRows = 2048;  // tiles per slab chunk
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-// Activation derivative from the post-activation value h.
-template <int ACT>
-__device__ __forceinline__ float nvp_act_grad_h(float h) {
-  static_assert(ACT != PDEINV_ACT_SILU && ACT != PDEINV_ACT_GELU, "derivative needs the pre-activation");
-  if (ACT == PDEINV_ACT_CELU || ACT == PDEINV_ACT_ELU) return h > 0.f ? 1.f : h + 1.f;  // e^z = h + 1
-  if (ACT == PDEINV_ACT_RELU) return h > 0.f ? 1.f : 0.f;
-  if (ACT == PDEINV_ACT_TANH) return 1.f - h * h;
-  return 1.f - expf(-h);  // softplus: sigmoid(z) = 1 - e^{-h}
-}
+constexpr int kNvpMaxRows = 2048;  // slab rows (256-sample blocks) per reduce chunk
+constexpr int kNvT = 4;            // 16-sample tiles per wave (64 samples; 256 per block)
+constexpr int kNvWS = 20;          // LDS row stride of a padded 16 x 16 weight matrix
 
-// Canonical (padded) LDS layout of one BasicMLP and one coupling layer.
-template <int DM>
-struct NvpCanon {
-  static constexpr int W0x = 0, W0t = DM * 8, B0 = W0t + 16 * 8, W1 = B0 + 8, B1 = W1 + 8 * 16, W2 = B1 + 16,
-                       B2 = W2 + 16 * 16, W3 = B2 + 16, B3 = W3 + 16 * DM, MLP = B3 + DM;
-  static constexpr int SF = 0, SNET = DM, TNET = DM + MLP, LAYER = DM + 2 * MLP;
+// Activation derivative from the post-activation value h (celu / elu: e^z = h + 1).
+__device__ __forceinline__ float nvp_celu_grad_h(float h) { return h > 0.f ? 1.f : h + 1.f; }
+__device__ __forceinline__ float nvp_celu(float z) { return z > 0.f ? z : expm1f(z); }
+
+// Padded LDS layout of one BasicMLP (weights [in][out] with row stride kNvWS), one coupling layer
+// and the time embedding.
+struct NvM {
+  static constexpr int MAT = 16 * kNvWS;
+  static constexpr int W0T = 0, W0X = MAT, W1 = 2 * MAT, W2 = 3 * MAT, W3 = 4 * MAT, B0 = 5 * MAT, B1 = B0 + 16,
+                       B2 = B1 + 16, B3 = B2 + 16, NET = B3 + 16;
+  static constexpr int SF = 0, SNET = 16, TNET = 16 + NET, LAYER = 16 + 2 * NET;
+  static constexpr int E_W1 = 0, E_B1 = MAT, E_W2 = MAT + 16, E_B2 = 2 * MAT + 16, TEMB = 2 * MAT + 32;
 };
-constexpr int kTembCanon = 2 * (16 * 16 + 16);  // W1 [16x16], b1, W2 [16x16], b2
-
-struct NvpLds {
-  float a[kBlock * kNvpAst];
-  float g[kBlock * kNvpGst];
-  float part[kBlock * 4];
+// Per-wave partial-gradient block (flush layout, 16 x 16 matrices dense): per net W0t, W0x, W1, W2,
+// W3, b0..b3; the layer adds sf. The time embedding reuses the first 2 x 272 floats.
+struct NvR {
+  static constexpr int W0T = 0, W0X = 256, W1 = 512, W2 = 768, W3 = 1024, B0 = 1280, B1 = 1296, B2 = 1312,
+                       B3 = 1328, NET = 1344;
+  static constexpr int SNET = 0, TNET = NET, SF = 2 * NET, LAYER = 2 * NET + 16;
 };
 
-// row[off + r * n_out + o] = sum over the tile of a_r * g_o (r < n_in) and of g_o (the bias row
-// r = n_in). The caller has written its a row (L.a) after a barrier. All threads call.
-template <int NO>
-__device__ __forceinline__ void nvp_wgrad(NvpLds& L, const float (&g)[NO], int n_in, int n_out,
-                                          float* __restrict__ row, int64_t off) {
-  // Opaque copies: without them LICM hoists every call site's per-lane item / slice / address
-  // math out of the layer loop and keeps it live across the whole kernel (> 1 KB of spills).
-  int tid = threadIdx.x;
-  asm volatile("" : "+v"(tid));
-  asm volatile("" : "+s"(n_in), "+s"(n_out));
+struct NvLane {
+  int g, s;  // component group, sample within the tile
+};
+
+// out = W^T x + c : W [16 in][16 out] at stride kNvWS; x in the accumulator layout.
+__device__ __forceinline__ f32x4 nv_fwd(const float* W, const NvLane& ln, const f32x4& x, f32x4 c) {
 #pragma unroll
-  for (int o = 0; o < NO; ++o) L.g[tid * kNvpGst + o] = g[o];  // columns >= n_out are never stored
-  __syncthreads();
-  const int og_n = (n_out + 3) >> 2;
-  const int items = (n_in + 1) * og_n;
-  int S = 1;
-  while (S < 8 && 2 * S * items <= kBlock) S *= 2;
-  const int span = kBlock / S;
-  const int slice = tid / items, item = tid - slice * items;
-  const int r = item / og_n, o0 = (item - r * og_n) * 4;
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  if (slice < S) {
-    const int s0 = slice * span;
-    for (int s = s0; s < s0 + span; ++s) {
-      const float av = r < n_in ? L.a[s * kNvpAst + r] : 1.f;
-      const float* gs = L.g + s * kNvpGst + o0;
+  for (int j = 0; j < 4; ++j)
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(W[(4 * ln.g + j) * kNvWS + ln.s], x[j], c, 0, 0, 0);
+  return c;
+}
+// out = W d + c (input gradient of a layer).
+__device__ __forceinline__ f32x4 nv_bwd(const float* W, const NvLane& ln, const f32x4& d, f32x4 c) {
 #pragma unroll
-      for (int c = 0; c < 4; ++c) acc[c] = fmaf(av, gs[c], acc[c]);
-    }
+  for (int j = 0; j < 4; ++j)
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(W[ln.s * kNvWS + 4 * ln.g + j], d[j], c, 0, 0, 0);
+  return c;
+}
+__device__ __forceinline__ f32x4 nv_vec(const float* b, const NvLane& ln) {
+  return *reinterpret_cast<const f32x4*>(b + 4 * ln.g);
+}
+__device__ __forceinline__ f32x4 nv_celu4(f32x4 z) {
+  return f32x4{nvp_celu(z[0]), nvp_celu(z[1]), nvp_celu(z[2]), nvp_celu(z[3])};
+}
+__device__ __forceinline__ f32x4 nv_dact4(f32x4 d, f32x4 h) {
+  return f32x4{d[0] * nvp_celu_grad_h(h[0]), d[1] * nvp_celu_grad_h(h[1]), d[2] * nvp_celu_grad_h(h[2]),
+               d[3] * nvp_celu_grad_h(h[3])};
+}
+__device__ __forceinline__ void nv_wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+// acc += sum over the tile's samples of a_s d_s^T (rows = a components): per-wave LDS stage
+// [2][16 samples][kNvWS], one 16-byte write per lane, one read per operand and k-step.
+__device__ __forceinline__ f32x4 nv_wgrad(float* stage, const NvLane& ln, const f32x4& a, const f32x4& d,
+                                          f32x4 acc) {
+  nv_wave_sync();  // the previous reads of the stage are done
+  *reinterpret_cast<f32x4*>(stage + ln.s * kNvWS + 4 * ln.g) = a;
+  *reinterpret_cast<f32x4*>(stage + 16 * kNvWS + ln.s * kNvWS + 4 * ln.g) = d;
+  nv_wave_sync();
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int r = (4 * t + ln.g) * kNvWS + ln.s;
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(stage[r], stage[16 * kNvWS + r], acc, 0, 0, 0);
   }
-  if (S > 1) {
-    if (slice < S) {
-#pragma unroll
-      for (int c = 0; c < 4; ++c) L.part[(slice * items + item) * 4 + c] = acc[c];
-    }
-    __syncthreads();
-    if (tid < items) {
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        float v = 0.f;
-        for (int q = 0; q < S; ++q) v += L.part[(q * items + tid) * 4 + c];
-        acc[c] = v;
-      }
-    }
-  }
-  if (tid < items) {
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-      if (o0 + c < n_out) row[off + r * n_out + o0 + c] = acc[c];
-  }
+  return acc;
 }
 
-template <int NA>
-__device__ __forceinline__ void nvp_put_a(NvpLds& L, const float (&av)[NA]) {
-#pragma unroll
-  for (int i = 0; i < NA; ++i) L.a[threadIdx.x * kNvpAst + i] = av[i];  // slots >= n_in are never read
+// Gradient accumulators of one BasicMLP over the wave's tiles.
+struct NvNetAcc {
+  f32x4 w0t, w0x, w1, w2, w3, b0, b1, b2, b3;
+  __device__ void zero() { w0t = w0x = w1 = w2 = w3 = b0 = b1 = b2 = b3 = f32x4{0.f, 0.f, 0.f, 0.f}; }
+};
+
+struct NvAct {
+  f32x4 h0, h1, h2;
+};
+
+// BasicMLP (:97-111) forward: input [temb | xm], hidden 8 / 16 / 16, output d (all padded to 16).
+__device__ __forceinline__ f32x4 nv_mlp_fwd(const float* p, const NvLane& ln, const f32x4& temb, const f32x4& xm,
+                                            NvAct& h) {
+  h.h0 = nv_celu4(nv_fwd(p + NvM::W0X, ln, xm, nv_fwd(p + NvM::W0T, ln, temb, nv_vec(p + NvM::B0, ln))));
+  h.h1 = nv_celu4(nv_fwd(p + NvM::W1, ln, h.h0, nv_vec(p + NvM::B1, ln)));
+  h.h2 = nv_celu4(nv_fwd(p + NvM::W2, ln, h.h1, nv_vec(p + NvM::B2, ln)));
+  return nv_fwd(p + NvM::W3, ln, h.h2, nv_vec(p + NvM::B3, ln));
 }
 
-// Keeps the scheduler from hoisting whole weight matrices' LDS loads into VGPRs ahead of use
-// (without it the kernel spills > 1 KB per lane).
-#define NVP_ROW_FENCE() __builtin_amdgcn_sched_barrier(0)
-
-// BasicMLP (:97-111) forward on the canonical layout; keeps the post-activations.
-template <int DM, int ACT>
-__device__ __forceinline__ void nvp_mlp_fwd(const float* __restrict__ p, const float (&xm)[DM],
-                                            const float (&temb)[16], float (&h0)[8], float (&h1)[16],
-                                            float (&h2)[16], float (&out)[DM]) {
-  using C = NvpCanon<DM>;
-#pragma unroll
-  for (int o = 0; o < 8; ++o) h0[o] = p[C::B0 + o];
-#pragma unroll
-  for (int k = 0; k < DM; ++k) {
-    NVP_ROW_FENCE();
-#pragma unroll
-    for (int o = 0; o < 8; ++o) h0[o] = fmaf(xm[k], p[C::W0x + k * 8 + o], h0[o]);
-  }
-#pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    NVP_ROW_FENCE();
-#pragma unroll
-    for (int o = 0; o < 8; ++o) h0[o] = fmaf(temb[q], p[C::W0t + q * 8 + o], h0[o]);
-  }
-#pragma unroll
-  for (int o = 0; o < 8; ++o) h0[o] = nvp_act(ACT, h0[o]);
-#pragma unroll
-  for (int o = 0; o < 16; ++o) h1[o] = p[C::B1 + o];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    NVP_ROW_FENCE();
-#pragma unroll
-    for (int o = 0; o < 16; ++o) h1[o] = fmaf(h0[i], p[C::W1 + i * 16 + o], h1[o]);
-  }
-#pragma unroll
-  for (int o = 0; o < 16; ++o) h1[o] = nvp_act(ACT, h1[o]);
-#pragma unroll
-  for (int o = 0; o < 16; ++o) h2[o] = p[C::B2 + o];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    NVP_ROW_FENCE();
-#pragma unroll
-    for (int o = 0; o < 16; ++o) h2[o] = fmaf(h1[i], p[C::W2 + i * 16 + o], h2[o]);
-  }
-#pragma unroll
-  for (int o = 0; o < 16; ++o) h2[o] = nvp_act(ACT, h2[o]);
-#pragma unroll
-  for (int o = 0; o < DM; ++o) out[o] = p[C::B3 + o];
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    NVP_ROW_FENCE();
-#pragma unroll
-    for (int o = 0; o < DM; ++o) out[o] = fmaf(h2[j], p[C::W3 + j * DM + o], out[o]);
-  }
+// BasicMLP backward from d(out): parameter gradients into acc, input gradients added to gtemb
+// (time rows) and gx (x rows).
+__device__ __forceinline__ void nv_mlp_bwd(const float* p, const NvLane& ln, float* stage, const f32x4& temb,
+                                           const f32x4& xm, const NvAct& h, const f32x4& dout, NvNetAcc& acc,
+                                           f32x4& gtemb, f32x4& gx) {
+  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+  acc.w3 = nv_wgrad(stage, ln, h.h2, dout, acc.w3);
+  acc.b3 += dout;
+  const f32x4 d2 = nv_dact4(nv_bwd(p + NvM::W3, ln, dout, z4), h.h2);
+  acc.w2 = nv_wgrad(stage, ln, h.h1, d2, acc.w2);
+  acc.b2 += d2;
+  const f32x4 d1 = nv_dact4(nv_bwd(p + NvM::W2, ln, d2, z4), h.h1);
+  acc.w1 = nv_wgrad(stage, ln, h.h0, d1, acc.w1);
+  acc.b1 += d1;
+  const f32x4 d0 = nv_dact4(nv_bwd(p + NvM::W1, ln, d1, z4), h.h0);
+  acc.w0t = nv_wgrad(stage, ln, temb, d0, acc.w0t);
+  acc.w0x = nv_wgrad(stage, ln, xm, d0, acc.w0x);
+  acc.b0 += d0;
+  gtemb = nv_bwd(p + NvM::W0T, ln, d0, gtemb);
+  gx = nv_bwd(p + NvM::W0X, ln, d0, gx);
 }
 
-// BasicMLP backward: weight gradients into the tile's slab row at `off` (the net's first float
-// in the reference layout; n_in = d + n_t), input gradients added into gxm / gtemb.
-template <int DM, int ACT>
-__device__ __forceinline__ void nvp_mlp_bwd(NvpLds& L, const float* __restrict__ p, int64_t off, int d, int n_t,
-                                            const float (&xm)[DM], const float (&temb)[16], const float (&h0)[8],
-                                            const float (&h1)[16], const float (&h2)[16], const float (&dout)[DM],
-                                            float (&gxm)[DM], float (&gtemb)[16], float* __restrict__ row) {
-  using C = NvpCanon<DM>;
+// Sum of v over the 16 samples of each component group (xor shuffles inside 16-lane rows).
+__device__ __forceinline__ f32x4 nv_sum16(f32x4 v) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) v[i] += __shfl_xor(v[i], off, 64);
+  }
+  return v;
+}
+
+// A wave's partials into its LDS flush block: matrices in the accumulator layout (row 4g + i,
+// column s), vectors summed over samples.
+__device__ __forceinline__ void nv_put_mat(float* r, const NvLane& ln, const f32x4& m) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) r[(4 * ln.g + i) * 16 + ln.s] = m[i];
+}
+__device__ __forceinline__ void nv_put_vec(float* r, const NvLane& ln, const f32x4& v) {
+  const f32x4 t = nv_sum16(v);
+  if (ln.s == 0) *reinterpret_cast<f32x4*>(r + 4 * ln.g) = t;
+}
+__device__ __forceinline__ void nv_put_net(float* r, const NvLane& ln, const NvNetAcc& a) {
+  nv_put_mat(r + NvR::W0T, ln, a.w0t);
+  nv_put_mat(r + NvR::W0X, ln, a.w0x);
+  nv_put_mat(r + NvR::W1, ln, a.w1);
+  nv_put_mat(r + NvR::W2, ln, a.w2);
+  nv_put_mat(r + NvR::W3, ln, a.w3);
+  nv_put_vec(r + NvR::B0, ln, a.b0);
+  nv_put_vec(r + NvR::B1, ln, a.b1);
+  nv_put_vec(r + NvR::B2, ln, a.b2);
+  nv_put_vec(r + NvR::B3, ln, a.b3);
+}
+
+// Flat (reference-order) parameter f of one BasicMLP -> its index in the flush block, or -1.
+__device__ __forceinline__ int nv_net_src(int f, int d, int n_t) {
   const int n_in = d + n_t;
-  const int64_t o1 = (int64_t)n_in * 8 + 8, o2 = o1 + 8 * 16 + 16, o3 = o2 + 16 * 16 + 16;
-  __syncthreads();
-  nvp_put_a(L, h2);
-  nvp_wgrad(L, dout, 16, d, row, off + o3);
-  float d2[16];
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    NVP_ROW_FENCE();
-    float s = 0.f;
-#pragma unroll
-    for (int o = 0; o < DM; ++o) s = fmaf(p[C::W3 + j * DM + o], dout[o], s);
-    d2[j] = s * nvp_act_grad_h<ACT>(h2[j]);
+  if (f < n_in * 8) {
+    const int r = f / 8, o = f - r * 8;
+    return r < d ? NvR::W0X + r * 16 + o : NvR::W0T + (r - d) * 16 + o;
   }
-  __syncthreads();
-  nvp_put_a(L, h1);
-  nvp_wgrad(L, d2, 16, 16, row, off + o2);
-  float d1[16];
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    NVP_ROW_FENCE();
-    float s = 0.f;
-#pragma unroll
-    for (int o = 0; o < 16; ++o) s = fmaf(p[C::W2 + j * 16 + o], d2[o], s);
-    d1[j] = s * nvp_act_grad_h<ACT>(h1[j]);
-  }
-  __syncthreads();
-  nvp_put_a(L, h0);
-  nvp_wgrad(L, d1, 8, 16, row, off + o1);
-  float d0[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    NVP_ROW_FENCE();
-    float s = 0.f;
-#pragma unroll
-    for (int o = 0; o < 16; ++o) s = fmaf(p[C::W1 + j * 16 + o], d1[o], s);
-    d0[j] = s * nvp_act_grad_h<ACT>(h0[j]);
-  }
-  __syncthreads();
-  nvp_put_a(L, xm);  // reference row order: x rows 0..d-1, then the time rows
-#pragma unroll
-  for (int q = 0; q < 16; ++q) L.a[threadIdx.x * kNvpAst + d + q] = temb[q];
-  nvp_wgrad(L, d0, n_in, 8, row, off);
-#pragma unroll
-  for (int k = 0; k < DM; ++k) {
-    NVP_ROW_FENCE();
-#pragma unroll
-    for (int o = 0; o < 8; ++o) gxm[k] = fmaf(p[C::W0x + k * 8 + o], d0[o], gxm[k]);  // padded rows are 0
-  }
-#pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    NVP_ROW_FENCE();
-#pragma unroll
-    for (int o = 0; o < 8; ++o) gtemb[q] = fmaf(p[C::W0t + q * 8 + o], d0[o], gtemb[q]);
-  }
+  f -= n_in * 8;
+  if (f < 8) return NvR::B0 + f;
+  f -= 8;
+  if (f < 128) return NvR::W1 + (f / 16) * 16 + f % 16;
+  f -= 128;
+  if (f < 16) return NvR::B1 + f;
+  f -= 16;
+  if (f < 256) return NvR::W2 + f;
+  f -= 256;
+  if (f < 16) return NvR::B2 + f;
+  f -= 16;
+  if (f < 16 * d) return NvR::W3 + (f / d) * 16 + f % d;
+  f -= 16 * d;
+  return f < d ? NvR::B3 + f : -1;
 }
 
-// TimeEmbedding (:8-22) on the padded 16 x 16 copy: se = SinusoidalEmbedding(t) (:24-38) from the
-// per-slot (frequency, is_sin) table (0 past E), he = act(se W1 + b1), temb = he W2 + b2.
 template <int ACT>
-__device__ __forceinline__ void nvp_time_embed(const float* __restrict__ tw, const float* __restrict__ freq,
-                                               float t, float (&se)[16], float (&he)[16], float (&temb)[16]) {
-#pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const float e = t * freq[q];
-    se[q] = freq[16 + q] * sinf(e) + freq[32 + q] * cosf(e);
-  }
-#pragma unroll
-  for (int o = 0; o < 16; ++o) he[o] = tw[256 + o];
-#pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    NVP_ROW_FENCE();
-#pragma unroll
-    for (int o = 0; o < 16; ++o) he[o] = fmaf(se[q], tw[q * 16 + o], he[o]);
-  }
-#pragma unroll
-  for (int o = 0; o < 16; ++o) he[o] = nvp_act(ACT, he[o]);  // padded: act(0) = 0 (celu / elu)
-#pragma unroll
-  for (int o = 0; o < 16; ++o) temb[o] = tw[272 + 256 + o];
-#pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    NVP_ROW_FENCE();
-#pragma unroll
-    for (int o = 0; o < 16; ++o) temb[o] = fmaf(he[q], tw[272 + q * 16 + o], temb[o]);
-  }
-}
-
-template <int DM, int ACT>
-__global__ __launch_bounds__(kBlock) void realnvp_grad_kernel(NvpArgs a, int d, const float* __restrict__ params,
-                                                              const float* __restrict__ tv, int64_t t_stride,
-                                                              const float* __restrict__ xv, int64_t n, int64_t ld,
-                                                              int64_t layer_stride, int64_t n_params,
-                                                              int64_t tile0, float* __restrict__ slab,
-                                                              int64_t slab_ld) {
-  using C = NvpCanon<DM>;
-  __shared__ NvpLds L;
-  __shared__ float sW[C::LAYER];   // current coupling layer, canonical layout
-  __shared__ float sT[kTembCanon];  // time embedding, canonical layout
-  __shared__ float sF[48];          // sinusoid table: frequency, sin weight, cos weight (0 past E)
-  __shared__ float sM[PDEINV_REALNVP_MAX_LAYERS * DM];  // masks, padded with 1
-  __shared__ float sB[DM + DM * DM];                     // base mean, inverse covariance (0-padded)
+__global__ __launch_bounds__(kBlock, 2) void realnvp_grad_kernel(NvpArgs a, int d, const float* __restrict__ params,
+                                                                 const float* __restrict__ tv, int64_t t_stride,
+                                                                 const float* __restrict__ xv, int64_t n, int64_t ld,
+                                                                 int64_t layer_stride, int64_t n_params,
+                                                                 int64_t tile0, float* __restrict__ slab,
+                                                                 int64_t slab_ld) {
+  static_assert(ACT == PDEINV_ACT_CELU, "celu / elu flow");
+  __shared__ float sW[NvM::LAYER];                   // current coupling layer (padded)
+  __shared__ float sT[NvM::TEMB];                    // time embedding (padded)
+  __shared__ float sF[48];                           // sinusoid table: frequency, sin weight, cos weight
+  __shared__ float sM[PDEINV_REALNVP_MAX_LAYERS * 16];  // masks, padded with 1
+  __shared__ float sB[16 + 16 * 16];                 // base mean, inverse covariance (0-padded)
+  __shared__ float sStage[kWavesPerBlock][2 * 16 * kNvWS];
+  __shared__ float sRed[kWavesPerBlock][NvR::LAYER];
   const int E = a.E;
   const int n_in = a.in_dim, n_t = n_in - d;
   const int mlp_n = n_in * 8 + 8 + 8 * 16 + 16 + 16 * 16 + 16 + 16 * d + d;
   const int64_t temb_params = E > 0 ? 2 * ((int64_t)E * E + E) : 0;
   const float* layers = params + temb_params;
   const bool hard = !a.ignore_time && a.soft_init == 0.f;
-  const int tid = threadIdx.x;
-  // ---- per-block staging of the small tables ----
-  for (int q = tid; q < kTembCanon; q += kBlock) {
-    const int part = q / 272, r = q - part * 272;  // [W (16x16) | b (16)] x 2
-    float v = 0.f;
-    if (E > 0) {
-      const float* src = params + part * (E * E + E);
-      if (r < 256) {
-        const int i = r / 16, o = r % 16;
-        v = (i < E && o < E) ? src[i * E + o] : 0.f;
-      } else {
-        v = (r - 256 < E) ? src[E * E + (r - 256)] : 0.f;
-      }
+  const int tid = threadIdx.x, wave = tid >> 6;
+  NvLane ln;
+  {
+    int lane = tid & 63;
+    asm volatile("" : "+v"(lane));  // opaque: keeps per-use address math out of long-lived registers
+    ln.g = lane >> 4;
+    ln.s = lane & 15;
+  }
+  float* stage = sStage[wave];
+  float* red = sRed[wave];
+  // ---- per-block tables ----
+  auto put_mat = [&](float* dst, const float* src, int rows, int cols, int ld_src) {  // padded [16][kNvWS]
+    for (int q = tid; q < 16 * kNvWS; q += kBlock) {
+      const int r = q / kNvWS, c = q - r * kNvWS;
+      dst[q] = (r < rows && c < cols) ? src[r * ld_src + c] : 0.f;
     }
-    sT[q] = v;
+  };
+  auto put_vec = [&](float* dst, const float* src, int len) {
+    for (int q = tid; q < 16; q += kBlock) dst[q] = q < len ? src[q] : 0.f;
+  };
+  if (E > 0) {
+    put_mat(sT + NvM::E_W1, params, E, E, E);
+    put_vec(sT + NvM::E_B1, params + E * E, E);
+    put_mat(sT + NvM::E_W2, params + E * E + E, E, E, E);
+    put_vec(sT + NvM::E_B2, params + 2 * E * E + E, E);
   }
   if (tid < 16) {
     const int half = E / 2;
@@ -441,170 +390,215 @@ __global__ __launch_bounds__(kBlock) void realnvp_grad_kernel(NvpArgs a, int d, 
     sF[16 + tid] = on && is_sin ? 1.f : 0.f;
     sF[32 + tid] = on && !is_sin ? 1.f : 0.f;
   }
-  for (int q = tid; q < a.n_layers * DM; q += kBlock) {
-    const int l = q / DM, k = q % DM;
+  for (int q = tid; q < a.n_layers * 16; q += kBlock) {
+    const int l = q / 16, k = q % 16;
     sM[q] = k < d ? a.masks[l * d + k] : 1.f;
   }
-  for (int q = tid; q < DM + DM * DM; q += kBlock) {
+  for (int q = tid; q < 16 + 256; q += kBlock) {
     float v = 0.f;
-    if (q < DM) {
+    if (q < 16) {
       v = q < d ? a.mean[q] : 0.f;
     } else {
-      const int r = (q - DM) / DM, c = (q - DM) % DM;
+      const int r = (q - 16) / 16, c = (q - 16) % 16;
       v = (r < d && c < d) ? a.inv_cov[r * d + c] : 0.f;
     }
     sB[q] = v;
   }
-  // Stage layer l in the canonical layout (zero padding).
-  auto stage = [&](int l) {
+  auto stage_layer = [&](int l) {
     __syncthreads();
     const float* lp = layers + (int64_t)l * layer_stride;
-    for (int q = tid; q < C::LAYER; q += kBlock) {
-      float v = 0.f;
-      if (q < DM) {
-        v = q < d ? lp[q] : 0.f;
-      } else {
-        const int net = (q - DM) / C::MLP, r = (q - DM) - net * C::MLP;
-        const float* np = lp + d + net * mlp_n;
-        if (r < C::W0t) {
-          const int k = r / 8, o = r % 8;
-          v = k < d ? np[k * 8 + o] : 0.f;
-        } else if (r < C::B0) {
-          const int qq = (r - C::W0t) / 8, o = (r - C::W0t) % 8;
-          v = qq < n_t ? np[(d + qq) * 8 + o] : 0.f;
-        } else if (r < C::W3) {  // b0, W1, b1, W2, b2: same order and size as the reference
-          v = np[n_in * 8 + (r - C::B0)];
-        } else if (r < C::B3) {
-          const int j = (r - C::W3) / DM, o = (r - C::W3) % DM;
-          v = o < d ? np[n_in * 8 + (C::W3 - C::B0) + j * d + o] : 0.f;
-        } else {
-          const int o = r - C::B3;
-          v = o < d ? np[n_in * 8 + (C::W3 - C::B0) + 16 * d + o] : 0.f;
-        }
-      }
-      sW[q] = v;
+    put_vec(sW + NvM::SF, lp, d);
+#pragma unroll 1
+    for (int net = 0; net < 2; ++net) {
+      const float* np = lp + d + net * mlp_n;
+      float* w = sW + (net ? NvM::TNET : NvM::SNET);
+      put_mat(w + NvM::W0X, np, d, 8, 8);
+      put_mat(w + NvM::W0T, np + d * 8, n_t, 8, 8);
+      put_vec(w + NvM::B0, np + n_in * 8, 8);
+      const float* q = np + n_in * 8 + 8;
+      put_mat(w + NvM::W1, q, 8, 16, 16);
+      put_vec(w + NvM::B1, q + 128, 16);
+      put_mat(w + NvM::W2, q + 144, 16, 16, 16);
+      put_vec(w + NvM::B2, q + 400, 16);
+      put_mat(w + NvM::W3, q + 416, 16, d, d);
+      put_vec(w + NvM::B3, q + 416 + 16 * d, d);
     }
     __syncthreads();
   };
   float* row = slab + (int64_t)blockIdx.x * slab_ld;
-  const int64_t i = (tile0 + blockIdx.x) * kBlock + tid;
-  const bool active = i < n;
-  const float w = active ? 1.f : 0.f;
-  const float t = active ? tv[i * t_stride] : 0.f;
-  float x[DM];
-#pragma unroll
-  for (int k = 0; k < DM; ++k) x[k] = (active && k < d) ? xv[i * ld + k] : 0.f;
+  // write this block's reduced partials for the flat range [off, off + len): src(f) -> flush index
+  auto flush = [&](int64_t off, int len, auto src) {
+    __syncthreads();  // every wave's partials are in sRed
+    for (int f = tid; f < len; f += kBlock) {
+      const int k = src(f);
+      float v = 0.f;
+      if (k >= 0) v = ((sRed[0][k] + sRed[1][k]) + sRed[2][k]) + sRed[3][k];
+      row[off + f] = v;
+    }
+    __syncthreads();  // sRed free again
+  };
+
+  // ---- the wave's tiles ----
+  f32x4 x[kNvT], gx[kNvT], temb[kNvT], gtemb[kNvT];
+  float tt[kNvT], w[kNvT], ldj[kNvT];
+  const int64_t base = (tile0 + blockIdx.x) * kBlock + wave * 16 * kNvT;
   __syncthreads();
-  float temb[16];
-  {
-    float se[16], he[16];
-    nvp_time_embed<ACT>(sT, sF, t, se, he, temb);
-    if (E == 0) {
 #pragma unroll
-      for (int q = 0; q < 16; ++q) temb[q] = 0.f;
-      if (!a.ignore_time) temb[0] = t;  // the raw time appended (CouplingLayer :137)
+  for (int u = 0; u < kNvT; ++u) {
+    const int64_t i = base + 16 * u + ln.s;
+    const bool active = i < n;
+    w[u] = active ? 1.f : 0.f;
+    tt[u] = active ? tv[i * t_stride] : 0.f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int k = 4 * ln.g + c;
+      x[u][c] = (active && k < d) ? xv[i * ld + k] : 0.f;
+      gtemb[u][c] = 0.f;
+    }
+    ldj[u] = 0.f;
+    if (E > 0) {  // TimeEmbedding (:8-22): se = SinusoidalEmbedding(t) (:24-38), he = act(se W1 + b1)
+      f32x4 se;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int q = 4 * ln.g + c;
+        const float e = tt[u] * sF[q];
+        se[c] = sF[16 + q] * sinf(e) + sF[32 + q] * cosf(e);
+      }
+      const f32x4 he = nv_celu4(nv_fwd(sT + NvM::E_W1, ln, se, nv_vec(sT + NvM::E_B1, ln)));
+      temb[u] = nv_fwd(sT + NvM::E_W2, ln, he, nv_vec(sT + NvM::E_B2, ln));
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) temb[u][c] = (!a.ignore_time && ln.g == 0 && c == 0) ? tt[u] : 0.f;
     }
   }
   // ---- likelihood pass (layers L-1 .. 0): x <- (x + tr) e^s ----
-  float ldj = 0.f;
   for (int l = a.n_layers - 1; l >= 0; --l) {
-    stage(l);
-    float m[DM], xm[DM];
+    stage_layer(l);
+    const f32x4 m = nv_vec(sM + l * 16, ln), sfw = nv_vec(sW + NvM::SF, ln);
+#pragma unroll 1
+    for (int u = 0; u < kNvT; ++u) {
+      const f32x4 xm = x[u] * m;
+      NvAct h;
+      const f32x4 so = nv_mlp_fwd(sW + NvM::SNET, ln, temb[u], xm, h);
+      const f32x4 to = nv_mlp_fwd(sW + NvM::TNET, ln, temb[u], xm, h);
 #pragma unroll
-    for (int k = 0; k < DM; ++k) {
-      m[k] = sM[l * DM + k];
-      xm[k] = x[k] * m[k];
-    }
-    float h0[8], h1[16], h2[16], so[DM], to[DM];
-    nvp_mlp_fwd<DM, ACT>(sW + C::SNET, xm, temb, h0, h1, h2, so);
-    nvp_mlp_fwd<DM, ACT>(sW + C::TNET, xm, temb, h0, h1, h2, to);
-#pragma unroll
-    for (int k = 0; k < DM; ++k) {  // padded k: keep = 0, so x stays 0 and ldj is unchanged
-      const float keep = 1.f - m[k];
-      const float sf = expf(sW[C::SF + k]);
-      const float sk = tanhf((hard ? t * so[k] : so[k]) / sf) * sf * keep;
-      x[k] = (x[k] + (hard ? t * to[k] : to[k]) * keep) * expf(sk);
-      ldj += sk;
+      for (int c = 0; c < 4; ++c) {  // padded / masked k: keep = 0, x unchanged
+        const float keep = 1.f - m[c];
+        const float sf = expf(sfw[c]);
+        const float sk = tanhf((hard ? tt[u] * so[c] : so[c]) / sf) * sf * keep;
+        x[u][c] = (x[u][c] + (hard ? tt[u] * to[c] : to[c]) * keep) * expf(sk);
+        ldj[u] += sk;
+      }
     }
   }
-  // ---- base density log p0(x0) and its gradient ----
-  float gx[DM], diff[DM], quad = 0.f;
+  // ---- base density log p0(x0) and its gradient (per-wave stage holds the tile's x rows) ----
+  float lsum = 0.f;  // sum over the wave's samples of w log p (lane-partial)
+#pragma unroll 1
+  for (int u = 0; u < kNvT; ++u) {
+    const f32x4 diff = x[u] - nv_vec(sB, ln);
+    nv_wave_sync();
+    *reinterpret_cast<f32x4*>(stage + ln.s * kNvWS + 4 * ln.g) = diff;
+    nv_wave_sync();
+    float quad = 0.f;
 #pragma unroll
-  for (int c = 0; c < DM; ++c) diff[c] = x[c] - sB[c];  // padded: 0 - 0
-#pragma unroll
-  for (int r = 0; r < DM; ++r) {
-    float acc = 0.f;
-#pragma unroll
-    for (int c = 0; c < DM; ++c) acc = fmaf(sB[DM + r * DM + c], diff[c], acc);
-    quad = fmaf(diff[r], acc, quad);
-    gx[r] = -w * acc;
+    for (int c = 0; c < 4; ++c) {
+      const int r = 4 * ln.g + c;
+      float acc = 0.f;
+      for (int q = 0; q < d; ++q) acc = fmaf(sB[16 + r * 16 + q], stage[ln.s * kNvWS + q], acc);
+      quad = fmaf(diff[c], acc, quad);
+      gx[u][c] = -w[u] * acc;
+    }
+    float part = ldj[u] - 0.5f * quad;  // the four groups' parts sum to log p + 0.5 log_det
+    part += __shfl_xor(part, 16, 64);
+    part += __shfl_xor(part, 32, 64);
+    if (ln.g == 0) lsum += w[u] * (part - 0.5f * a.log_det);
   }
-  const float logp = -0.5f * (a.log_det + quad) + ldj;
   // ---- backward through layers 0 .. L-1, rebuilding each layer's input ----
-  float gtemb[16];
-#pragma unroll
-  for (int q = 0; q < 16; ++q) gtemb[q] = 0.f;
   for (int l = 0; l < a.n_layers; ++l) {
-    stage(l);
+    stage_layer(l);
     const int64_t loff = temb_params + (int64_t)l * layer_stride;
-    float m[DM], xm[DM];
+    const f32x4 m = nv_vec(sM + l * 16, ln), sfw = nv_vec(sW + NvM::SF, ln);
+    NvNetAcc as, at;
+    as.zero();
+    at.zero();
+    f32x4 galpha = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+    for (int u = 0; u < kNvT; ++u) {
+      const f32x4 xm = x[u] * m;
+      NvAct h;
+      const f32x4 out = nv_mlp_fwd(sW + NvM::SNET, ln, temb[u], xm, h);
+      f32x4 s, es, gso, gto;
 #pragma unroll
-    for (int k = 0; k < DM; ++k) {
-      m[k] = sM[l * DM + k];
-      xm[k] = x[k] * m[k];
-    }
-    float h0[8], h1[16], h2[16], out[DM];
-    nvp_mlp_fwd<DM, ACT>(sW + C::SNET, xm, temb, h0, h1, h2, out);
-    float s[DM], es[DM], gso[DM], gto[DM], galpha[DM], gacc[DM];
+      for (int c = 0; c < 4; ++c) {
+        const float keep = 1.f - m[c];
+        const float spre = hard ? tt[u] * out[c] : out[c];
+        const float sf = expf(sfw[c]);
+        const float th = tanhf(spre / sf);
+        s[c] = th * sf * keep;
+        es[c] = expf(s[c]);
+        const float gs = (gx[u][c] * x[u][c] + w[u]) * keep;  // d(log p0 + ldj)/ds via x_out and ldj
+        const float dth = 1.f - th * th;
+        galpha[c] += gs * (th * sf - dth * spre);              // d/d scaling_factor (sf = e^alpha)
+        gso[c] = (hard ? tt[u] : 1.f) * gs * dth;              // d/d scale_net output
+        gto[c] = (hard ? tt[u] : 1.f) * gx[u][c] * es[c] * keep;  // d/d translate_net output
+      }
+      f32x4 gacc = {0.f, 0.f, 0.f, 0.f};
+      nv_mlp_bwd(sW + NvM::SNET, ln, stage, temb[u], xm, h, gso, as, gtemb[u], gacc);
+      const f32x4 tro = nv_mlp_fwd(sW + NvM::TNET, ln, temb[u], xm, h);
+      nv_mlp_bwd(sW + NvM::TNET, ln, stage, temb[u], xm, h, gto, at, gtemb[u], gacc);
 #pragma unroll
-    for (int k = 0; k < DM; ++k) {
-      const float keep = 1.f - m[k];
-      const float spre = hard ? t * out[k] : out[k];
-      const float sf = expf(sW[C::SF + k]);
-      const float th = tanhf(spre / sf);
-      s[k] = th * sf * keep;
-      es[k] = expf(s[k]);
-      const float gs = (gx[k] * x[k] + w) * keep;         // d(log p0 + ldj)/ds via x_out and ldj
-      const float dth = 1.f - th * th;
-      galpha[k] = gs * (th * sf - dth * spre);            // d/d scaling_factor (sf = e^alpha)
-      gso[k] = (hard ? t : 1.f) * gs * dth;                // d/d scale_net output
-      gto[k] = (hard ? t : 1.f) * gx[k] * es[k] * keep;  // d/d translate_net output
-      gacc[k] = 0.f;
+      for (int c = 0; c < 4; ++c) {
+        const float tr = (hard ? tt[u] * tro[c] : tro[c]) * (1.f - m[c]);
+        x[u][c] = x[u][c] * expf(-s[c]) - tr;
+        gx[u][c] = gx[u][c] * es[c] + m[c] * gacc[c];
+      }
     }
-    __syncthreads();
-    nvp_wgrad(L, galpha, 0, d, row, loff);
-    nvp_mlp_bwd<DM, ACT>(L, sW + C::SNET, loff + d, d, n_t, xm, temb, h0, h1, h2, gso, gacc, gtemb, row);
-    nvp_mlp_fwd<DM, ACT>(sW + C::TNET, xm, temb, h0, h1, h2, out);
-    nvp_mlp_bwd<DM, ACT>(L, sW + C::TNET, loff + d + mlp_n, d, n_t, xm, temb, h0, h1, h2, gto, gacc, gtemb, row);
-#pragma unroll
-    for (int k = 0; k < DM; ++k) {
-      const float tr = (hard ? t * out[k] : out[k]) * (1.f - m[k]);
-      x[k] = x[k] * expf(-s[k]) - tr;
-      gx[k] = gx[k] * es[k] + m[k] * gacc[k];
-    }
+    nv_put_net(red + NvR::SNET, ln, as);
+    nv_put_net(red + NvR::TNET, ln, at);
+    nv_put_vec(red + NvR::SF, ln, galpha);
+    flush(loff, d, [&](int f) { return NvR::SF + f; });
+    flush(loff + d, 2 * mlp_n, [&](int f) {
+      const int net = f >= mlp_n;
+      const int k = nv_net_src(f - net * mlp_n, d, n_t);
+      return k < 0 ? -1 : k + (net ? NvR::TNET : NvR::SNET);
+    });
   }
-  // ---- time-embedding backward ----
+  // ---- time-embedding backward and the loss column ----
   if (E > 0) {
-    float se[16], he[16], temb2[16];
-    nvp_time_embed<ACT>(sT, sF, t, se, he, temb2);
-    __syncthreads();
-    nvp_put_a(L, he);
-    nvp_wgrad(L, gtemb, E, E, row, (int64_t)E * E + E);
-    float gz[16];
+    f32x4 w1 = {0.f, 0.f, 0.f, 0.f}, w2 = w1, b1 = w1, b2 = w1;
+#pragma unroll 1
+    for (int u = 0; u < kNvT; ++u) {
+      f32x4 se;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      float v = 0.f;
-#pragma unroll
-      for (int o = 0; o < 16; ++o) v = fmaf(sT[272 + q * 16 + o], gtemb[o], v);  // padded W2 is 0
-      gz[q] = v * nvp_act_grad_h<ACT>(he[q]);
+      for (int c = 0; c < 4; ++c) {
+        const int q = 4 * ln.g + c;
+        const float e = tt[u] * sF[q];
+        se[c] = sF[16 + q] * sinf(e) + sF[32 + q] * cosf(e);
+      }
+      const f32x4 he = nv_celu4(nv_fwd(sT + NvM::E_W1, ln, se, nv_vec(sT + NvM::E_B1, ln)));
+      w2 = nv_wgrad(stage, ln, he, gtemb[u], w2);
+      b2 += gtemb[u];
+      const f32x4 gz = nv_dact4(nv_bwd(sT + NvM::E_W2, ln, gtemb[u], f32x4{0.f, 0.f, 0.f, 0.f}), he);
+      w1 = nv_wgrad(stage, ln, se, gz, w1);
+      b1 += gz;
     }
-    __syncthreads();
-    nvp_put_a(L, se);
-    nvp_wgrad(L, gz, E, E, row, 0);
+    nv_put_mat(red + 0, ln, w1);
+    nv_put_vec(red + 256, ln, b1);
+    nv_put_mat(red + 272, ln, w2);
+    nv_put_vec(red + 528, ln, b2);
+    const int EE = E * E + E;
+    flush(0, 2 * EE, [&](int f) {
+      const int part = f >= EE, r = f - part * EE;
+      const int o = part * 272;
+      return r < E * E ? o + (r / E) * 16 + r % E : o + 256 + (r - E * E);
+    });
   }
-  float lw[1] = {w * logp};
-  __syncthreads();
-  nvp_wgrad(L, lw, 0, 1, row, n_params);
+  lsum += __shfl_xor(lsum, 1, 64);
+  lsum += __shfl_xor(lsum, 2, 64);
+  lsum += __shfl_xor(lsum, 4, 64);
+  lsum += __shfl_xor(lsum, 8, 64);
+  if (tid % 64 == 0) red[0] = lsum;
+  flush(n_params, 1, [&](int) { return 0; });
 }
 
 // acc[c] (+)= sum_r slab[r][c] over one chunk (fp64, fixed order: 4 row groups of a column, then
@@ -741,19 +735,12 @@ extern "C" int pdeinv_realnvp_value_and_grad(const pdeinv_realnvp_desc* d, const
   double* acc64 = (double*)((char*)workspace + (rows_max * (P + 1) * (int64_t)sizeof(float) + 15) / 16 * 16);
   hipStream_t st = (hipStream_t)stream;
   const int64_t tiles = (n + kBlock - 1) / kBlock;
-  // DM in {2, 4, 8} covers d = 1..8 (padded coordinates stay fixed); celu and elu are the same map.
+  // any d <= 8 (padded coordinates stay fixed); celu and elu are the same map.
   for (int64_t tile0 = 0; tile0 < tiles; tile0 += rows_max) {
     const int64_t rows = tiles - tile0 < rows_max ? tiles - tile0 : rows_max;
     const dim3 g((unsigned)rows);
-    if (D <= 2)
-      hipLaunchKernelGGL((realnvp_grad_kernel<2, PDEINV_ACT_CELU>), g, dim3(kBlock), 0, st, a, D, params, t,
-                         t_stride, x, n, ld, ls, P, tile0, slab, P + 1);
-    else if (D <= 4)
-      hipLaunchKernelGGL((realnvp_grad_kernel<4, PDEINV_ACT_CELU>), g, dim3(kBlock), 0, st, a, D, params, t,
-                         t_stride, x, n, ld, ls, P, tile0, slab, P + 1);
-    else
-      hipLaunchKernelGGL((realnvp_grad_kernel<8, PDEINV_ACT_CELU>), g, dim3(kBlock), 0, st, a, D, params, t,
-                         t_stride, x, n, ld, ls, P, tile0, slab, P + 1);
+    hipLaunchKernelGGL((realnvp_grad_kernel<PDEINV_ACT_CELU>), g, dim3(kBlock), 0, st, a, D, params, t, t_stride, x,
+                       n, ld, ls, P, tile0, slab, P + 1);
     int rc = check_launch("realnvp_grad_kernel");
     if (rc) return rc;
     hipLaunchKernelGGL(nvp_grad_reduce_kernel, dim3((unsigned)((P + 1 + 63) / 64)), dim3(kBlock), 0, st, slab,
