@@ -165,48 +165,43 @@ __global__ __launch_bounds__(kBlock) void realnvp_logdensity_kernel(NvpArgs a, c
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kNvpMaxRows = 2048;  // slab rows (256-sample blocks) per reduce chunk
-constexpr int kNvT = 4;            // 16-sample tiles per wave (64 samples; 256 per block)
+constexpr int kNvT = 2;            // 16-sample tiles per wave (32 samples; 128 per block)
+constexpr int kNvSPB = kWavesPerBlock * 16 * kNvT;  // samples per block = per slab row
 constexpr int kNvWS = 20;          // LDS row stride of a padded 16 x 16 weight matrix
+constexpr int kNvRaw = 8 + 2 * (24 * 8 + 8 + 128 + 16 + 256 + 16 + 16 * 8 + 8);  // one layer's params, d <= 8
+constexpr int kNvPre = (kNvRaw + kBlock - 1) / kBlock;
 
 // Activation derivative from the post-activation value h (celu / elu: e^z = h + 1).
 __device__ __forceinline__ float nvp_celu_grad_h(float h) { return h > 0.f ? 1.f : h + 1.f; }
-__device__ __forceinline__ float nvp_celu(float z) { return z > 0.f ? z : expm1f(z); }
+// hardware exp2 / rcp (v_exp_f32, v_rcp_f32: ~1 ulp; the grad kernel's transcendentals)
+__device__ __forceinline__ float nv_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
+__device__ __forceinline__ float nv_tanh(float x) { return 1.f - 2.f * __builtin_amdgcn_rcpf(nv_exp(2.f * x) + 1.f); }
+__device__ __forceinline__ float nvp_celu(float z) { return z > 0.f ? z : nv_exp(z) - 1.f; }
 
 // Padded LDS layout of one BasicMLP (weights [in][out] with row stride kNvWS), one coupling layer
 // and the time embedding.
+// Each matrix is also stored transposed (suffix T): the input-gradient product W d then reads it with
+// the same bank-conflict-free pattern as the forward (a transposed read of W itself is 4-way).
 struct NvM {
   static constexpr int MAT = 16 * kNvWS;
-  static constexpr int W0T = 0, W0X = MAT, W1 = 2 * MAT, W2 = 3 * MAT, W3 = 4 * MAT, B0 = 5 * MAT, B1 = B0 + 16,
-                       B2 = B1 + 16, B3 = B2 + 16, NET = B3 + 16;
+  static constexpr int W0T = 0, W0X = MAT, W1 = 2 * MAT, W2 = 3 * MAT, W3 = 4 * MAT, TR = 5 * MAT,  // W^T at +TR
+                       B0 = 10 * MAT, B1 = B0 + 16, B2 = B1 + 16, B3 = B2 + 16, NET = B3 + 16;
   static constexpr int SF = 0, SNET = 16, TNET = 16 + NET, LAYER = 16 + 2 * NET;
-  static constexpr int E_W1 = 0, E_B1 = MAT, E_W2 = MAT + 16, E_B2 = 2 * MAT + 16, TEMB = 2 * MAT + 32;
+  static constexpr int E_W1 = 0, E_B1 = MAT, E_W2 = MAT + 16, E_B2 = 2 * MAT + 16, E_W2T = 2 * MAT + 32,
+                       TEMB = 3 * MAT + 32;
 };
-// Per-wave partial-gradient block (flush layout, 16 x 16 matrices dense): per net W0t, W0x, W1, W2,
-// W3, b0..b3; the layer adds sf. The time embedding reuses the first 2 x 272 floats.
+// Per-wave partial-gradient block (flush layout, 16 x 16 matrices dense): one net's W0t, W0x, W1, W2,
+// W3, b0..b3 (the s-net flush adds sf). The time embedding reuses the first 2 x 272 floats.
 struct NvR {
   static constexpr int W0T = 0, W0X = 256, W1 = 512, W2 = 768, W3 = 1024, B0 = 1280, B1 = 1296, B2 = 1312,
                        B3 = 1328, NET = 1344;
-  static constexpr int SNET = 0, TNET = NET, SF = 2 * NET, LAYER = 2 * NET + 16;
+  static constexpr int SF = NET, SIZE = NET + 16;
 };
 
 struct NvLane {
   int g, s;  // component group, sample within the tile
 };
 
-// out = W^T x + c : W [16 in][16 out] at stride kNvWS; x in the accumulator layout.
-__device__ __forceinline__ f32x4 nv_fwd(const float* W, const NvLane& ln, const f32x4& x, f32x4 c) {
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-    c = __builtin_amdgcn_mfma_f32_16x16x4f32(W[(4 * ln.g + j) * kNvWS + ln.s], x[j], c, 0, 0, 0);
-  return c;
-}
-// out = W d + c (input gradient of a layer).
-__device__ __forceinline__ f32x4 nv_bwd(const float* W, const NvLane& ln, const f32x4& d, f32x4 c) {
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-    c = __builtin_amdgcn_mfma_f32_16x16x4f32(W[ln.s * kNvWS + 4 * ln.g + j], d[j], c, 0, 0, 0);
-  return c;
-}
 __device__ __forceinline__ f32x4 nv_vec(const float* b, const NvLane& ln) {
   return *reinterpret_cast<const f32x4*>(b + 4 * ln.g);
 }
@@ -217,24 +212,44 @@ __device__ __forceinline__ f32x4 nv_dact4(f32x4 d, f32x4 h) {
   return f32x4{d[0] * nvp_celu_grad_h(h[0]), d[1] * nvp_celu_grad_h(h[1]), d[2] * nvp_celu_grad_h(h[2]),
                d[3] * nvp_celu_grad_h(h[3])};
 }
-__device__ __forceinline__ void nv_wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+// Order the wave's own LDS stage accesses (a wave's LDS instructions execute in order, so a lane
+// reads what another lane of the same wave wrote before it) without fencing the MFMA / VALU
+// stream: a compiler memory barrier only, so independent matrix work still moves across it.
+__device__ __forceinline__ void nv_wave_sync() { asm volatile("" ::: "memory"); }
+// The wave's kNvT tiles go through every dense layer together: one A-operand (weight) read feeds
+// kNvT independent MFMAs, so the accumulation chains of the tiles interleave.
+typedef f32x4 NvV[kNvT];
+
+__device__ __forceinline__ void nv_fwdT(const float* W, const NvLane& ln, const NvV& x, NvV& c) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float av = W[(4 * ln.g + j) * kNvWS + ln.s];
+#pragma unroll
+    for (int u = 0; u < kNvT; ++u) c[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, x[u][j], c[u], 0, 0, 0);
+  }
 }
-// acc += sum over the tile's samples of a_s d_s^T (rows = a components): per-wave LDS stage
-// [2][16 samples][kNvWS], one 16-byte write per lane, one read per operand and k-step.
-__device__ __forceinline__ f32x4 nv_wgrad(float* stage, const NvLane& ln, const f32x4& a, const f32x4& d,
-                                          f32x4 acc) {
+__device__ __forceinline__ void nv_bcast(NvV& c, const f32x4& b) {
+#pragma unroll
+  for (int u = 0; u < kNvT; ++u) c[u] = b;
+}
+
+// acc += sum over the wave's samples of a_s d_s^T (rows = a components): per-wave LDS stage
+// [kNvT][2][16 samples][kNvWS], one 16-byte write per lane and tile, one read per operand and k-step.
+__device__ __forceinline__ f32x4 nv_wgrad(float* stage, const NvLane& ln, const NvV& a, const NvV& d, f32x4 acc) {
   nv_wave_sync();  // the previous reads of the stage are done
-  *reinterpret_cast<f32x4*>(stage + ln.s * kNvWS + 4 * ln.g) = a;
-  *reinterpret_cast<f32x4*>(stage + 16 * kNvWS + ln.s * kNvWS + 4 * ln.g) = d;
+#pragma unroll
+  for (int u = 0; u < kNvT; ++u) {
+    *reinterpret_cast<f32x4*>(stage + (2 * u) * 16 * kNvWS + ln.s * kNvWS + 4 * ln.g) = a[u];
+    *reinterpret_cast<f32x4*>(stage + (2 * u + 1) * 16 * kNvWS + ln.s * kNvWS + 4 * ln.g) = d[u];
+  }
   nv_wave_sync();
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int r = (4 * t + ln.g) * kNvWS + ln.s;
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(stage[r], stage[16 * kNvWS + r], acc, 0, 0, 0);
-  }
+  for (int u = 0; u < kNvT; ++u)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int r = (2 * u) * 16 * kNvWS + (4 * t + ln.g) * kNvWS + ln.s;
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(stage[r], stage[16 * kNvWS + r], acc, 0, 0, 0);
+    }
   return acc;
 }
 
@@ -245,46 +260,82 @@ struct NvNetAcc {
 };
 
 struct NvAct {
-  f32x4 h0, h1, h2;
+  NvV h0, h1, h2;
 };
 
 // BasicMLP (:97-111) forward: input [temb | xm], hidden 8 / 16 / 16, output d (all padded to 16).
-__device__ __forceinline__ f32x4 nv_mlp_fwd(const float* p, const NvLane& ln, const f32x4& temb, const f32x4& xm,
-                                            NvAct& h) {
-  h.h0 = nv_celu4(nv_fwd(p + NvM::W0X, ln, xm, nv_fwd(p + NvM::W0T, ln, temb, nv_vec(p + NvM::B0, ln))));
-  h.h1 = nv_celu4(nv_fwd(p + NvM::W1, ln, h.h0, nv_vec(p + NvM::B1, ln)));
-  h.h2 = nv_celu4(nv_fwd(p + NvM::W2, ln, h.h1, nv_vec(p + NvM::B2, ln)));
-  return nv_fwd(p + NvM::W3, ln, h.h2, nv_vec(p + NvM::B3, ln));
+__device__ __forceinline__ void nv_mlp_fwd(const float* p, const NvLane& ln, const NvV& temb, const NvV& xm,
+                                           NvAct& h, NvV& out) {
+  NvV z;
+  nv_bcast(z, nv_vec(p + NvM::B0, ln));
+  nv_fwdT(p + NvM::W0T, ln, temb, z);
+  nv_fwdT(p + NvM::W0X, ln, xm, z);
+#pragma unroll
+  for (int u = 0; u < kNvT; ++u) h.h0[u] = nv_celu4(z[u]);
+  nv_bcast(z, nv_vec(p + NvM::B1, ln));
+  nv_fwdT(p + NvM::W1, ln, h.h0, z);
+#pragma unroll
+  for (int u = 0; u < kNvT; ++u) h.h1[u] = nv_celu4(z[u]);
+  nv_bcast(z, nv_vec(p + NvM::B2, ln));
+  nv_fwdT(p + NvM::W2, ln, h.h1, z);
+#pragma unroll
+  for (int u = 0; u < kNvT; ++u) h.h2[u] = nv_celu4(z[u]);
+  nv_bcast(out, nv_vec(p + NvM::B3, ln));
+  nv_fwdT(p + NvM::W3, ln, h.h2, out);
 }
 
 // BasicMLP backward from d(out): parameter gradients into acc, input gradients added to gtemb
-// (time rows) and gx (x rows).
-__device__ __forceinline__ void nv_mlp_bwd(const float* p, const NvLane& ln, float* stage, const f32x4& temb,
-                                           const f32x4& xm, const NvAct& h, const f32x4& dout, NvNetAcc& acc,
-                                           f32x4& gtemb, f32x4& gx) {
+// (time rows) and gx (x rows). The input-gradient products W d read the transposed copies.
+__device__ __forceinline__ void nv_mlp_bwd(const float* p, const NvLane& ln, float* stage, const NvV& temb,
+                                           const NvV& xm, const NvAct& h, const NvV& dout, NvNetAcc& acc,
+                                           NvV& gtemb, NvV& gx) {
   const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+  NvV d, e;
   acc.w3 = nv_wgrad(stage, ln, h.h2, dout, acc.w3);
-  acc.b3 += dout;
-  const f32x4 d2 = nv_dact4(nv_bwd(p + NvM::W3, ln, dout, z4), h.h2);
-  acc.w2 = nv_wgrad(stage, ln, h.h1, d2, acc.w2);
-  acc.b2 += d2;
-  const f32x4 d1 = nv_dact4(nv_bwd(p + NvM::W2, ln, d2, z4), h.h1);
-  acc.w1 = nv_wgrad(stage, ln, h.h0, d1, acc.w1);
-  acc.b1 += d1;
-  const f32x4 d0 = nv_dact4(nv_bwd(p + NvM::W1, ln, d1, z4), h.h0);
-  acc.w0t = nv_wgrad(stage, ln, temb, d0, acc.w0t);
-  acc.w0x = nv_wgrad(stage, ln, xm, d0, acc.w0x);
-  acc.b0 += d0;
-  gtemb = nv_bwd(p + NvM::W0T, ln, d0, gtemb);
-  gx = nv_bwd(p + NvM::W0X, ln, d0, gx);
+  nv_bcast(e, z4);
+  nv_fwdT(p + NvM::TR + NvM::W3, ln, dout, e);
+#pragma unroll
+  for (int u = 0; u < kNvT; ++u) {
+    acc.b3 += dout[u];
+    d[u] = nv_dact4(e[u], h.h2[u]);
+  }
+  acc.w2 = nv_wgrad(stage, ln, h.h1, d, acc.w2);
+  nv_bcast(e, z4);
+  nv_fwdT(p + NvM::TR + NvM::W2, ln, d, e);
+#pragma unroll
+  for (int u = 0; u < kNvT; ++u) {
+    acc.b2 += d[u];
+    d[u] = nv_dact4(e[u], h.h1[u]);
+  }
+  acc.w1 = nv_wgrad(stage, ln, h.h0, d, acc.w1);
+  nv_bcast(e, z4);
+  nv_fwdT(p + NvM::TR + NvM::W1, ln, d, e);
+#pragma unroll
+  for (int u = 0; u < kNvT; ++u) {
+    acc.b1 += d[u];
+    d[u] = nv_dact4(e[u], h.h0[u]);
+  }
+  acc.w0t = nv_wgrad(stage, ln, temb, d, acc.w0t);
+  acc.w0x = nv_wgrad(stage, ln, xm, d, acc.w0x);
+#pragma unroll
+  for (int u = 0; u < kNvT; ++u) acc.b0 += d[u];
+  nv_fwdT(p + NvM::TR + NvM::W0T, ln, d, gtemb);
+  nv_fwdT(p + NvM::TR + NvM::W0X, ln, d, gx);
 }
 
-// Sum of v over the 16 samples of each component group (xor shuffles inside 16-lane rows).
+// Sum of v over the 16 samples of each component group: DPP inside 16-lane rows (quad_perm xor 1,
+// xor 2, row_half_mirror, row_mirror), every lane of the row ends with the row total.
+template <int CTRL>
+__device__ __forceinline__ float nv_dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
 __device__ __forceinline__ f32x4 nv_sum16(f32x4 v) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-#pragma unroll
-    for (int off = 1; off < 16; off <<= 1) v[i] += __shfl_xor(v[i], off, 64);
+    v[i] += nv_dpp<0xB1>(v[i]);
+    v[i] += nv_dpp<0x4E>(v[i]);
+    v[i] += nv_dpp<0x141>(v[i]);
+    v[i] += nv_dpp<0x140>(v[i]);
   }
   return v;
 }
@@ -347,8 +398,11 @@ __global__ __launch_bounds__(kBlock, 2) void realnvp_grad_kernel(NvpArgs a, int 
   __shared__ float sF[48];                           // sinusoid table: frequency, sin weight, cos weight
   __shared__ float sM[PDEINV_REALNVP_MAX_LAYERS * 16];  // masks, padded with 1
   __shared__ float sB[16 + 16 * 16];                 // base mean, inverse covariance (0-padded)
-  __shared__ float sStage[kWavesPerBlock][2 * 16 * kNvWS];
-  __shared__ float sRed[kWavesPerBlock][NvR::LAYER];
+  // per-wave wgrad stages during the tile math, per-wave flush blocks after it (a barrier between)
+  constexpr int kScr = NvR::SIZE > kNvT * 2 * 16 * kNvWS ? NvR::SIZE : kNvT * 2 * 16 * kNvWS;
+  __shared__ float sScr[kWavesPerBlock][kScr];
+  __shared__ float sRaw[kNvRaw];
+  __shared__ short sMap[2 * (24 * 8 + 8 + 128 + 16 + 256 + 16 + 16 * 8 + 8)];  // flat net param -> NvR index
   const int E = a.E;
   const int n_in = a.in_dim, n_t = n_in - d;
   const int mlp_n = n_in * 8 + 8 + 8 * 16 + 16 + 16 * 16 + 16 + 16 * d + d;
@@ -363,22 +417,23 @@ __global__ __launch_bounds__(kBlock, 2) void realnvp_grad_kernel(NvpArgs a, int 
     ln.g = lane >> 4;
     ln.s = lane & 15;
   }
-  float* stage = sStage[wave];
-  float* red = sRed[wave];
+  float* stage = sScr[wave];
+  float* red = sScr[wave];
   // ---- per-block tables ----
-  auto put_mat = [&](float* dst, const float* src, int rows, int cols, int ld_src) {  // padded [16][kNvWS]
-    for (int q = tid; q < 16 * kNvWS; q += kBlock) {
+  auto put_mat = [&](float* dst, float* dst_t, const float* src, int rows, int cols, int ld_src) {
+    for (int q = tid; q < 16 * kNvWS; q += kBlock) {  // padded [16][kNvWS], and its transpose
       const int r = q / kNvWS, c = q - r * kNvWS;
       dst[q] = (r < rows && c < cols) ? src[r * ld_src + c] : 0.f;
+      if (dst_t) dst_t[q] = (c < rows && r < cols) ? src[c * ld_src + r] : 0.f;
     }
   };
   auto put_vec = [&](float* dst, const float* src, int len) {
     for (int q = tid; q < 16; q += kBlock) dst[q] = q < len ? src[q] : 0.f;
   };
   if (E > 0) {
-    put_mat(sT + NvM::E_W1, params, E, E, E);
+    put_mat(sT + NvM::E_W1, nullptr, params, E, E, E);
     put_vec(sT + NvM::E_B1, params + E * E, E);
-    put_mat(sT + NvM::E_W2, params + E * E + E, E, E, E);
+    put_mat(sT + NvM::E_W2, sT + NvM::E_W2T, params + E * E + E, E, E, E);
     put_vec(sT + NvM::E_B2, params + 2 * E * E + E, E);
   }
   if (tid < 16) {
@@ -390,6 +445,7 @@ __global__ __launch_bounds__(kBlock, 2) void realnvp_grad_kernel(NvpArgs a, int 
     sF[16 + tid] = on && is_sin ? 1.f : 0.f;
     sF[32 + tid] = on && !is_sin ? 1.f : 0.f;
   }
+  for (int f = tid; f < mlp_n; f += kBlock) sMap[f] = (short)nv_net_src(f, d, n_t);
   for (int q = tid; q < a.n_layers * 16; q += kBlock) {
     const int l = q / 16, k = q % 16;
     sM[q] = k < d ? a.masks[l * d + k] : 1.f;
@@ -404,44 +460,66 @@ __global__ __launch_bounds__(kBlock, 2) void realnvp_grad_kernel(NvpArgs a, int 
     }
     sB[q] = v;
   }
+  // Layer parameters are prefetched one staged layer ahead into registers (one coalesced load per
+  // thread and slot, in flight under the previous layer's math), dropped into sRaw, then expanded
+  // LDS -> LDS into the padded / transposed layout. Staging order: L-1 .. 0 (likelihood), 0 .. L-1.
+  float pre[kNvPre];
+  auto prefetch = [&](int l) {
+    const float* lp = layers + (int64_t)l * layer_stride;
+#pragma unroll
+    for (int k = 0; k < kNvPre; ++k) {
+      const int q = tid + k * kBlock;
+      pre[k] = q < layer_stride ? lp[q] : 0.f;
+    }
+  };
+  int staged = 0;  // layers staged so far
   auto stage_layer = [&](int l) {
     __syncthreads();
-    const float* lp = layers + (int64_t)l * layer_stride;
+#pragma unroll
+    for (int k = 0; k < kNvPre; ++k) {
+      const int q = tid + k * kBlock;
+      if (q < layer_stride) sRaw[q] = pre[k];
+    }
+    __syncthreads();
+    ++staged;
+    if (staged < 2 * a.n_layers) prefetch(staged < a.n_layers ? a.n_layers - 1 - staged : staged - a.n_layers);
+    const float* lp = sRaw;
     put_vec(sW + NvM::SF, lp, d);
 #pragma unroll 1
     for (int net = 0; net < 2; ++net) {
       const float* np = lp + d + net * mlp_n;
       float* w = sW + (net ? NvM::TNET : NvM::SNET);
-      put_mat(w + NvM::W0X, np, d, 8, 8);
-      put_mat(w + NvM::W0T, np + d * 8, n_t, 8, 8);
+      put_mat(w + NvM::W0X, w + NvM::TR + NvM::W0X, np, d, 8, 8);
+      put_mat(w + NvM::W0T, w + NvM::TR + NvM::W0T, np + d * 8, n_t, 8, 8);
       put_vec(w + NvM::B0, np + n_in * 8, 8);
       const float* q = np + n_in * 8 + 8;
-      put_mat(w + NvM::W1, q, 8, 16, 16);
+      put_mat(w + NvM::W1, w + NvM::TR + NvM::W1, q, 8, 16, 16);
       put_vec(w + NvM::B1, q + 128, 16);
-      put_mat(w + NvM::W2, q + 144, 16, 16, 16);
+      put_mat(w + NvM::W2, w + NvM::TR + NvM::W2, q + 144, 16, 16, 16);
       put_vec(w + NvM::B2, q + 400, 16);
-      put_mat(w + NvM::W3, q + 416, 16, d, d);
+      put_mat(w + NvM::W3, w + NvM::TR + NvM::W3, q + 416, 16, d, d);
       put_vec(w + NvM::B3, q + 416 + 16 * d, d);
     }
     __syncthreads();
   };
+  prefetch(a.n_layers - 1);
   float* row = slab + (int64_t)blockIdx.x * slab_ld;
   // write this block's reduced partials for the flat range [off, off + len): src(f) -> flush index
   auto flush = [&](int64_t off, int len, auto src) {
-    __syncthreads();  // every wave's partials are in sRed
+    __syncthreads();  // every wave's partials are in its flush block
     for (int f = tid; f < len; f += kBlock) {
       const int k = src(f);
       float v = 0.f;
-      if (k >= 0) v = ((sRed[0][k] + sRed[1][k]) + sRed[2][k]) + sRed[3][k];
+      if (k >= 0) v = ((sScr[0][k] + sScr[1][k]) + sScr[2][k]) + sScr[3][k];
       row[off + f] = v;
     }
-    __syncthreads();  // sRed free again
+    __syncthreads();  // the flush blocks are free again
   };
 
   // ---- the wave's tiles ----
-  f32x4 x[kNvT], gx[kNvT], temb[kNvT], gtemb[kNvT];
+  NvV x, gx, temb, gtemb;
   float tt[kNvT], w[kNvT], ldj[kNvT];
-  const int64_t base = (tile0 + blockIdx.x) * kBlock + wave * 16 * kNvT;
+  const int64_t base = (tile0 + blockIdx.x) * kNvSPB + wave * 16 * kNvT;
   __syncthreads();
 #pragma unroll
   for (int u = 0; u < kNvT; ++u) {
@@ -456,44 +534,65 @@ __global__ __launch_bounds__(kBlock, 2) void realnvp_grad_kernel(NvpArgs a, int 
       gtemb[u][c] = 0.f;
     }
     ldj[u] = 0.f;
-    if (E > 0) {  // TimeEmbedding (:8-22): se = SinusoidalEmbedding(t) (:24-38), he = act(se W1 + b1)
-      f32x4 se;
+  }
+  // TimeEmbedding (:8-22): se = SinusoidalEmbedding(t) (:24-38), he = act(se W1 + b1), temb = he W2 + b2
+  auto sinusoid = [&](NvV& se) {
+#pragma unroll
+    for (int u = 0; u < kNvT; ++u)
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const int q = 4 * ln.g + c;
         const float e = tt[u] * sF[q];
-        se[c] = sF[16 + q] * sinf(e) + sF[32 + q] * cosf(e);
+        se[u][c] = sF[16 + q] * sinf(e) + sF[32 + q] * cosf(e);
       }
-      const f32x4 he = nv_celu4(nv_fwd(sT + NvM::E_W1, ln, se, nv_vec(sT + NvM::E_B1, ln)));
-      temb[u] = nv_fwd(sT + NvM::E_W2, ln, he, nv_vec(sT + NvM::E_B2, ln));
-    } else {
+  };
+  if (E > 0) {
+    NvV se, he;
+    sinusoid(se);
+    nv_bcast(he, nv_vec(sT + NvM::E_B1, ln));
+    nv_fwdT(sT + NvM::E_W1, ln, se, he);
+#pragma unroll
+    for (int u = 0; u < kNvT; ++u) he[u] = nv_celu4(he[u]);
+    nv_bcast(temb, nv_vec(sT + NvM::E_B2, ln));
+    nv_fwdT(sT + NvM::E_W2, ln, he, temb);
+  } else {
+#pragma unroll
+    for (int u = 0; u < kNvT; ++u)
 #pragma unroll
       for (int c = 0; c < 4; ++c) temb[u][c] = (!a.ignore_time && ln.g == 0 && c == 0) ? tt[u] : 0.f;
-    }
   }
   // ---- likelihood pass (layers L-1 .. 0): x <- (x + tr) e^s ----
   for (int l = a.n_layers - 1; l >= 0; --l) {
     stage_layer(l);
     const f32x4 m = nv_vec(sM + l * 16, ln), sfw = nv_vec(sW + NvM::SF, ln);
-#pragma unroll 1
-    for (int u = 0; u < kNvT; ++u) {
-      const f32x4 xm = x[u] * m;
+    f32x4 sf, isf;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      sf[c] = nv_exp(sfw[c]);
+      isf[c] = __builtin_amdgcn_rcpf(sf[c]);
+    }
+    NvV xm, so, to;
+#pragma unroll
+    for (int u = 0; u < kNvT; ++u) xm[u] = x[u] * m;
+    {
       NvAct h;
-      const f32x4 so = nv_mlp_fwd(sW + NvM::SNET, ln, temb[u], xm, h);
-      const f32x4 to = nv_mlp_fwd(sW + NvM::TNET, ln, temb[u], xm, h);
+      nv_mlp_fwd(sW + NvM::SNET, ln, temb, xm, h, so);
+      nv_mlp_fwd(sW + NvM::TNET, ln, temb, xm, h, to);
+    }
+#pragma unroll
+    for (int u = 0; u < kNvT; ++u) {
 #pragma unroll
       for (int c = 0; c < 4; ++c) {  // padded / masked k: keep = 0, x unchanged
         const float keep = 1.f - m[c];
-        const float sf = expf(sfw[c]);
-        const float sk = tanhf((hard ? tt[u] * so[c] : so[c]) / sf) * sf * keep;
-        x[u][c] = (x[u][c] + (hard ? tt[u] * to[c] : to[c]) * keep) * expf(sk);
+        const float sk = nv_tanh((hard ? tt[u] * so[u][c] : so[u][c]) * isf[c]) * sf[c] * keep;
+        x[u][c] = (x[u][c] + (hard ? tt[u] * to[u][c] : to[u][c]) * keep) * nv_exp(sk);
         ldj[u] += sk;
       }
     }
   }
   // ---- base density log p0(x0) and its gradient (per-wave stage holds the tile's x rows) ----
   float lsum = 0.f;  // sum over the wave's samples of w log p (lane-partial)
-#pragma unroll 1
+#pragma unroll
   for (int u = 0; u < kNvT; ++u) {
     const f32x4 diff = x[u] - nv_vec(sB, ln);
     nv_wave_sync();
@@ -518,70 +617,77 @@ __global__ __launch_bounds__(kBlock, 2) void realnvp_grad_kernel(NvpArgs a, int 
     stage_layer(l);
     const int64_t loff = temb_params + (int64_t)l * layer_stride;
     const f32x4 m = nv_vec(sM + l * 16, ln), sfw = nv_vec(sW + NvM::SF, ln);
+    f32x4 sfv, isf;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      sfv[c] = nv_exp(sfw[c]);
+      isf[c] = __builtin_amdgcn_rcpf(sfv[c]);
+    }
     NvNetAcc as, at;
     as.zero();
     at.zero();
     f32x4 galpha = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
+    NvV xm, out, s, es, gso, gto, gacc;
+    NvAct h;
+#pragma unroll
+    for (int u = 0; u < kNvT; ++u) xm[u] = x[u] * m;
+    nv_mlp_fwd(sW + NvM::SNET, ln, temb, xm, h, out);
+#pragma unroll
     for (int u = 0; u < kNvT; ++u) {
-      const f32x4 xm = x[u] * m;
-      NvAct h;
-      const f32x4 out = nv_mlp_fwd(sW + NvM::SNET, ln, temb[u], xm, h);
-      f32x4 s, es, gso, gto;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const float keep = 1.f - m[c];
-        const float spre = hard ? tt[u] * out[c] : out[c];
-        const float sf = expf(sfw[c]);
-        const float th = tanhf(spre / sf);
-        s[c] = th * sf * keep;
-        es[c] = expf(s[c]);
+        const float spre = hard ? tt[u] * out[u][c] : out[u][c];
+        const float sf = sfv[c];
+        const float th = nv_tanh(spre * isf[c]);
+        s[u][c] = th * sf * keep;
+        es[u][c] = nv_exp(s[u][c]);
         const float gs = (gx[u][c] * x[u][c] + w[u]) * keep;  // d(log p0 + ldj)/ds via x_out and ldj
         const float dth = 1.f - th * th;
         galpha[c] += gs * (th * sf - dth * spre);              // d/d scaling_factor (sf = e^alpha)
-        gso[c] = (hard ? tt[u] : 1.f) * gs * dth;              // d/d scale_net output
-        gto[c] = (hard ? tt[u] : 1.f) * gx[u][c] * es[c] * keep;  // d/d translate_net output
-      }
-      f32x4 gacc = {0.f, 0.f, 0.f, 0.f};
-      nv_mlp_bwd(sW + NvM::SNET, ln, stage, temb[u], xm, h, gso, as, gtemb[u], gacc);
-      const f32x4 tro = nv_mlp_fwd(sW + NvM::TNET, ln, temb[u], xm, h);
-      nv_mlp_bwd(sW + NvM::TNET, ln, stage, temb[u], xm, h, gto, at, gtemb[u], gacc);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const float tr = (hard ? tt[u] * tro[c] : tro[c]) * (1.f - m[c]);
-        x[u][c] = x[u][c] * expf(-s[c]) - tr;
-        gx[u][c] = gx[u][c] * es[c] + m[c] * gacc[c];
+        gso[u][c] = (hard ? tt[u] : 1.f) * gs * dth;           // d/d scale_net output
+        gto[u][c] = (hard ? tt[u] : 1.f) * gx[u][c] * es[u][c] * keep;  // d/d translate_net output
+        gacc[u][c] = 0.f;
       }
     }
-    nv_put_net(red + NvR::SNET, ln, as);
-    nv_put_net(red + NvR::TNET, ln, at);
+    nv_mlp_bwd(sW + NvM::SNET, ln, stage, temb, xm, h, gso, as, gtemb, gacc);
+    nv_mlp_fwd(sW + NvM::TNET, ln, temb, xm, h, out);
+    nv_mlp_bwd(sW + NvM::TNET, ln, stage, temb, xm, h, gto, at, gtemb, gacc);
+#pragma unroll
+    for (int u = 0; u < kNvT; ++u)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float tr = (hard ? tt[u] * out[u][c] : out[u][c]) * (1.f - m[c]);
+        x[u][c] = x[u][c] * __builtin_amdgcn_rcpf(es[u][c]) - tr;
+        gx[u][c] = gx[u][c] * es[u][c] + m[c] * gacc[u][c];
+      }
+    __syncthreads();  // every wave is done with its stage (the flush blocks alias it)
+    nv_put_net(red, ln, as);
     nv_put_vec(red + NvR::SF, ln, galpha);
-    flush(loff, d, [&](int f) { return NvR::SF + f; });
-    flush(loff + d, 2 * mlp_n, [&](int f) {
-      const int net = f >= mlp_n;
-      const int k = nv_net_src(f - net * mlp_n, d, n_t);
-      return k < 0 ? -1 : k + (net ? NvR::TNET : NvR::SNET);
-    });
+    flush(loff, d + mlp_n, [&](int f) { return f < d ? NvR::SF + f : (int)sMap[f - d]; });  // sf, s-net
+    nv_put_net(red, ln, at);
+    flush(loff + d + mlp_n, mlp_n, [&](int f) { return (int)sMap[f]; });  // t-net
   }
   // ---- time-embedding backward and the loss column ----
   if (E > 0) {
     f32x4 w1 = {0.f, 0.f, 0.f, 0.f}, w2 = w1, b1 = w1, b2 = w1;
-#pragma unroll 1
-    for (int u = 0; u < kNvT; ++u) {
-      f32x4 se;
+    NvV se, he, gz;
+    sinusoid(se);
+    nv_bcast(he, nv_vec(sT + NvM::E_B1, ln));
+    nv_fwdT(sT + NvM::E_W1, ln, se, he);
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const int q = 4 * ln.g + c;
-        const float e = tt[u] * sF[q];
-        se[c] = sF[16 + q] * sinf(e) + sF[32 + q] * cosf(e);
-      }
-      const f32x4 he = nv_celu4(nv_fwd(sT + NvM::E_W1, ln, se, nv_vec(sT + NvM::E_B1, ln)));
-      w2 = nv_wgrad(stage, ln, he, gtemb[u], w2);
+    for (int u = 0; u < kNvT; ++u) he[u] = nv_celu4(he[u]);
+    w2 = nv_wgrad(stage, ln, he, gtemb, w2);
+    nv_bcast(gz, f32x4{0.f, 0.f, 0.f, 0.f});
+    nv_fwdT(sT + NvM::E_W2T, ln, gtemb, gz);
+#pragma unroll
+    for (int u = 0; u < kNvT; ++u) {
       b2 += gtemb[u];
-      const f32x4 gz = nv_dact4(nv_bwd(sT + NvM::E_W2, ln, gtemb[u], f32x4{0.f, 0.f, 0.f, 0.f}), he);
-      w1 = nv_wgrad(stage, ln, se, gz, w1);
-      b1 += gz;
+      gz[u] = nv_dact4(gz[u], he[u]);
+      b1 += gz[u];
     }
+    w1 = nv_wgrad(stage, ln, se, gz, w1);
+    __syncthreads();  // stages done (flush blocks alias them)
     nv_put_mat(red + 0, ln, w1);
     nv_put_vec(red + 256, ln, b1);
     nv_put_mat(red + 272, ln, w2);
@@ -686,7 +792,7 @@ extern "C" int pdeinv_realnvp_logdensity(const pdeinv_realnvp_desc* d, const flo
 }
 
 static int64_t nvp_grad_rows(int64_t n) {
-  const int64_t tiles = (n + kBlock - 1) / kBlock;
+  const int64_t tiles = (n + kNvSPB - 1) / kNvSPB;
   return tiles < kNvpMaxRows ? tiles : kNvpMaxRows;
 }
 
@@ -734,7 +840,7 @@ extern "C" int pdeinv_realnvp_value_and_grad(const pdeinv_realnvp_desc* d, const
   float* slab = (float*)workspace;
   double* acc64 = (double*)((char*)workspace + (rows_max * (P + 1) * (int64_t)sizeof(float) + 15) / 16 * 16);
   hipStream_t st = (hipStream_t)stream;
-  const int64_t tiles = (n + kBlock - 1) / kBlock;
+  const int64_t tiles = (n + kNvSPB - 1) / kNvSPB;
   // any d <= 8 (padded coordinates stay fixed); celu and elu are the same map.
   for (int64_t tile0 = 0; tile0 < tiles; tile0 += rows_max) {
     const int64_t rows = tiles - tile0 < rows_max ? tiles - tile0 : rows_max;
