@@ -164,7 +164,7 @@ __global__ __launch_bounds__(kBlock) void realnvp_logdensity_kernel(NvpArgs a, c
 // ---------------------------------------------------------------------------------------------
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kNvpMaxRows = 2048;  // slab rows (256-sample blocks) per reduce chunk
+constexpr int kNvpMaxRows = 8192;  // slab rows (128-sample blocks) per launch + reduce chunk
 constexpr int kNvT = 2;            // 16-sample tiles per wave (32 samples; 128 per block)
 constexpr int kNvSPB = kWavesPerBlock * 16 * kNvT;  // samples per block = per slab row
 constexpr int kNvWS = 20;          // LDS row stride of a padded 16 x 16 weight matrix
@@ -707,23 +707,48 @@ __global__ __launch_bounds__(kBlock, 2) void realnvp_grad_kernel(NvpArgs a, int 
   flush(n_params, 1, [&](int) { return 0; });
 }
 
-// acc[c] (+)= sum_r slab[r][c] over one chunk (fp64, fixed order: 4 row groups of a column, then
-// the groups in order); on the last chunk grad[c] = scale * acc[c] (c < n_params), loss = ...[n_params].
-__global__ __launch_bounds__(kBlock) void nvp_grad_reduce_kernel(const float* __restrict__ slab, int rows,
-                                                                  int64_t ld, int64_t n_params, double* acc64,
-                                                                  int first, int last, double scale,
-                                                                  float* __restrict__ grad,
-                                                                  float* __restrict__ loss) {
+// Slab column sums in two fixed-order fp64 stages (bit-reproducible): kNvSplits row splits of the
+// chunk, each summed by 4 row phases of a 64-column block (4 independent loads in flight per
+// lane), then the splits in order. On the last chunk grad[c] = scale * acc[c] (c < n_params) and
+// loss = scale * acc[n_params].
+constexpr int kNvSplits = 16;
+__global__ __launch_bounds__(kBlock) void nvp_slab_split_kernel(const float* __restrict__ slab, int rows, int64_t ld,
+                                                                 int64_t n_cols, double* __restrict__ parts) {
   __shared__ double part[kBlock];
   const int64_t c = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
   const int g = threadIdx.x >> 6;
+  const int rps = (rows + kNvSplits - 1) / kNvSplits;
+  const int r0 = blockIdx.y * rps, r1 = r0 + rps < rows ? r0 + rps : rows;
   double acc = 0.0;
-  if (c <= n_params)
-    for (int r = g; r < rows; r += 4) acc += (double)slab[(int64_t)r * ld + c];
+  if (c < n_cols) {
+    int r = r0 + g;
+    for (; r + 12 < r1; r += 16) {
+      const float v0 = slab[(int64_t)r * ld + c], v1 = slab[(int64_t)(r + 4) * ld + c];
+      const float v2 = slab[(int64_t)(r + 8) * ld + c], v3 = slab[(int64_t)(r + 12) * ld + c];
+      acc += (double)v0;
+      acc += (double)v1;
+      acc += (double)v2;
+      acc += (double)v3;
+    }
+    for (; r < r1; r += 4) acc += (double)slab[(int64_t)r * ld + c];
+  }
   part[threadIdx.x] = acc;
   __syncthreads();
-  if (g == 0 && c <= n_params) {
-    double v = ((part[threadIdx.x] + part[threadIdx.x + 64]) + part[threadIdx.x + 128]) + part[threadIdx.x + 192];
+  if (g == 0 && c < n_cols)
+    parts[blockIdx.y * n_cols + c] =
+        ((part[threadIdx.x] + part[threadIdx.x + 64]) + part[threadIdx.x + 128]) + part[threadIdx.x + 192];
+}
+
+__global__ __launch_bounds__(kBlock) void nvp_grad_reduce_kernel(const double* __restrict__ parts,
+                                                                  int64_t n_params, double* acc64,
+                                                                  int first, int last, double scale,
+                                                                  float* __restrict__ grad,
+                                                                  float* __restrict__ loss) {
+  const int64_t c = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (c <= n_params) {
+    double v = 0.0;
+#pragma unroll
+    for (int q = 0; q < kNvSplits; ++q) v += parts[q * (n_params + 1) + c];
     if (!first) v += acc64[c];
     acc64[c] = v;
     if (last) {
@@ -800,7 +825,7 @@ extern "C" int64_t pdeinv_realnvp_grad_workspace(const pdeinv_realnvp_desc* d, i
   const int64_t P = pdeinv_realnvp_param_count(d);
   if (P < 0 || n < 0) return -1;
   const int64_t slab = (nvp_grad_rows(n) * (P + 1) * (int64_t)sizeof(float) + 15) / 16 * 16;
-  return slab + (P + 1) * (int64_t)sizeof(double);
+  return slab + (1 + kNvSplits) * (P + 1) * (int64_t)sizeof(double);
 }
 extern "C" int pdeinv_realnvp_value_and_grad(const pdeinv_realnvp_desc* d, const float* params, const float* t,
                                              int64_t t_stride, const float* x, int64_t n, int64_t ld, float* loss,
@@ -839,6 +864,7 @@ extern "C" int pdeinv_realnvp_value_and_grad(const pdeinv_realnvp_desc* d, const
   const int64_t rows_max = nvp_grad_rows(n);
   float* slab = (float*)workspace;
   double* acc64 = (double*)((char*)workspace + (rows_max * (P + 1) * (int64_t)sizeof(float) + 15) / 16 * 16);
+  double* parts = acc64 + (P + 1);
   hipStream_t st = (hipStream_t)stream;
   const int64_t tiles = (n + kNvSPB - 1) / kNvSPB;
   // any d <= 8 (padded coordinates stay fixed); celu and elu are the same map.
@@ -849,9 +875,13 @@ extern "C" int pdeinv_realnvp_value_and_grad(const pdeinv_realnvp_desc* d, const
                        n, ld, ls, P, tile0, slab, P + 1);
     int rc = check_launch("realnvp_grad_kernel");
     if (rc) return rc;
-    hipLaunchKernelGGL(nvp_grad_reduce_kernel, dim3((unsigned)((P + 1 + 63) / 64)), dim3(kBlock), 0, st, slab,
-                       (int)rows, P + 1, P, acc64, tile0 == 0 ? 1 : 0, tile0 + rows >= tiles ? 1 : 0,
-                       -1.0 / (double)n, grad, loss);
+    hipLaunchKernelGGL(nvp_slab_split_kernel, dim3((unsigned)((P + 1 + 63) / 64), kNvSplits), dim3(kBlock), 0, st,
+                       slab, (int)rows, P + 1, P + 1, parts);
+    rc = check_launch("nvp_slab_split_kernel");
+    if (rc) return rc;
+    hipLaunchKernelGGL(nvp_grad_reduce_kernel, dim3((unsigned)((P + 1 + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
+                       parts, P, acc64, tile0 == 0 ? 1 : 0, tile0 + rows >= tiles ? 1 : 0, -1.0 / (double)n, grad,
+                       loss);
     rc = check_launch("nvp_grad_reduce_kernel");
     if (rc) return rc;
   }
