@@ -1,0 +1,25 @@
+"""Per-residual HBM traffic of the C5 MLP residual from a tools/profile_r02.sh C5 run: the sum over every
+MLP-residual dispatch (mlpf::*, mlp_loss) of FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE, divided by
+the number of residual launches (mlp_loss dispatches / chunks per residual).
+    python tools/c5_traffic.py gpurun_out/prof_r02/C5 [chunks_per_residual=10]"""
+import csv
+import glob
+import os
+import sys
+
+root = sys.argv[1]
+chunks = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+tot, loss_calls = {}, {}
+for counter, sub, scale in (("FETCH_SIZE", "fetch", 2.0), ("WRITE_SIZE", "write", 1.0)):
+    s, n = 0.0, 0
+    for f in glob.glob(os.path.join(root, sub, "**", "*counter_collection.csv"), recursive=True):
+        for row in csv.DictReader(open(f)):
+            k = row["Kernel_Name"]
+            if row["Counter_Name"] != counter or not ("mlpf::" in k or "mlp_loss" in k):
+                continue
+            s += float(row["Counter_Value"]) * 1024 * scale
+            n += "mlp_loss" in k
+    tot[counter], loss_calls[counter] = s, n
+per = {c: tot[c] / (loss_calls[c] / chunks) for c in tot}
+print({"fetch_bytes_per_residual": per["FETCH_SIZE"], "write_bytes_per_residual": per["WRITE_SIZE"],
+       "traffic_bytes_per_residual": per["FETCH_SIZE"] + per["WRITE_SIZE"], "residuals": loss_calls})
