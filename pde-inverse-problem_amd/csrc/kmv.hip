@@ -106,11 +106,15 @@ __global__ __launch_bounds__(kBlock) void kmv_weights_kernel(float gamma, const 
 //    transpose (row stride 20 floats: conflict-free 16-byte row writes); the lane-private alternative
 //    (136 packed accumulators) left room for 2 waves per SIMD only;
 //  * the per-row quadratic forms of d_s log rho and d_s^2 log rho run as packed pairs over coefficient
-//    pairs (Gamma1_ij, Gamma2_ij) broadcast from LDS (as kernel SGPRs the 2 d^2 + 2 d coefficients spill);
+//    pairs (Gamma1_ij, Gamma2_ij) broadcast from LDS (as kernel SGPRs the 2 d^2 + 2 d coefficients spill),
+//    over the symmetrised upper triangle: d(d+1)/2 LDS reads and packed FMAs per row instead of d^2
+//    (this pass is bound by its per-row VALU / LDS work, not by HBM: 3.40 -> 2.81 ms at C4);
+//  * packed rows (ld == 2d): the wave's 64 rows are read as one contiguous block (2d/4 coalesced
+//    1 KiB loads) straight into the row stage, each lane then takes its own row back (3.80 -> 3.40 ms);
 //  * count, sum z and the weighted moments stay lane-private (wave / block reduction at the end).
 constexpr int kMwStride = 20;  // floats per staged row (16 features + pad)
 
-template <int D>
+template <int D, bool PACKED>
 __global__ __launch_bounds__(kBlock) void kmv_moments_weights_kernel(float gamma, const float* __restrict__ coef,
                                                                      const float* __restrict__ z, int64_t n_rows,
                                                                      int64_t set_stride, int64_t ld,
@@ -120,12 +124,24 @@ __global__ __launch_bounds__(kBlock) void kmv_moments_weights_kernel(float gamma
   const int t = blockIdx.y;
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
   const float* c = coef + (int64_t)t * NC;  // [m1 (D), a1, b1 (D), G1 (D*D), a2, b2 (D), G2 (D*D)]
-  __shared__ f32x2 cpair[D * D + D];        // (G1_ij, G2_ij) row-major, then (b1_i, b2_i)
+  constexpr int NT = D * (D + 1) / 2;       // upper triangle of the symmetrised (G1, G2)
+  __shared__ f32x2 cpair[NT + D];           // (G1_ij + G1_ji, G2_ij + G2_ji) for i < j, (G_ii) on the
+                                            // diagonal, row-major over i <= j; then (b1_i, b2_i)
   __shared__ float stage[kWavesPerBlock][kWave * kMwStride];
   __shared__ float gram[kWavesPerBlock][16 * 16];
-  for (int e = threadIdx.x; e < D * D + D; e += kBlock)
-    cpair[e] = e < D * D ? f32x2{c[2 * D + 1 + e], c[3 * D + 2 + D * D + e]}
-                         : f32x2{c[D + 1 + (e - D * D)], c[2 * D + 2 + D * D + (e - D * D)]};
+  for (int e = threadIdx.x; e < NT + D; e += kBlock) {
+    if (e < NT) {  // triangle index e -> (i, j), i <= j
+      int i = 0, rem = e;
+      while (rem >= D - i) { rem -= D - i; ++i; }
+      const int j = i + rem;
+      const float* G1 = c + 2 * D + 1;
+      const float* G2 = c + 3 * D + 2 + D * D;
+      cpair[e] = i == j ? f32x2{G1[i * D + i], G2[i * D + i]}
+                        : f32x2{G1[i * D + j] + G1[j * D + i], G2[i * D + j] + G2[j * D + i]};
+    } else {
+      cpair[e] = f32x2{c[D + 1 + (e - NT)], c[2 * D + 2 + D * D + (e - NT)]};
+    }
+  }
   float* srow = &stage[wave][lane * kMwStride];
 #pragma unroll
   for (int k = M; k < 16; ++k) srow[k] = 0.f;  // padding features read as 0 by the MFMA
@@ -142,6 +158,33 @@ __global__ __launch_bounds__(kBlock) void kmv_moments_weights_kernel(float gamma
   acc.zero();
   const float* base = z + (int64_t)t * set_stride;
   const bool vec4 = (M % 4 == 0) && (ld % 4 == 0) && (set_stride % 4 == 0) && (((uintptr_t)z & 15) == 0);
+  // Packed rows (ld == 2d): the wave's 64 rows are one contiguous 256·M-byte block, loaded with M/4
+  // fully coalesced 1 KiB dwordx4 instructions and transposed into the row stage through LDS (a
+  // lane-private row load spans 64 rows per instruction and touches every line M/4 times).
+  // PACKED (host-checked: 16-byte aligned, ld == 2d)
+  constexpr int NQ = M % 4 == 0 ? M / 4 : 1;
+  auto load_packed = [&](int64_t r0w, f32x4* q) {  // r0w: the wave's first row
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) {
+      const int p = k * 256 + lane * 4;  // float offset inside the wave's block
+      const int64_t r = r0w + p / M;
+      q[k] = r < n_rows ? __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(base + r0w * M + p))
+                        : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto stage_packed = [&](const f32x4* q, float* v) {
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) {
+      const int p = k * 256 + lane * 4;
+      *reinterpret_cast<f32x4*>(&stage[wave][(p / M) * kMwStride + p % M]) = q[k];
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int k = 0; k < M; k += 4) {
+      const f32x4 t4 = *reinterpret_cast<const f32x4*>(srow + k);
+      v[k] = t4[0]; v[k + 1] = t4[1]; v[k + 2] = t4[2]; v[k + 3] = t4[3];
+    }
+  };
   auto load = [&](int64_t r, float* v) {
     if (r < n_rows) {
       const float* row = base + r * ld;
@@ -163,19 +206,27 @@ __global__ __launch_bounds__(kBlock) void kmv_moments_weights_kernel(float gamma
   // wave-uniform trip count: every lane joins every MFMA (rows past the end are zeros, weight 0)
   const int64_t stride = (int64_t)gridDim.x * kBlock;
   int64_t r0 = (int64_t)blockIdx.x * kBlock + wave * kWave;
-  float vn[M];
-  load(r0 + lane, vn);
+  [[maybe_unused]] float vn[PACKED ? 1 : M];
+  [[maybe_unused]] f32x4 qn[PACKED ? NQ : 1];
+  if constexpr (PACKED) load_packed(r0, qn);
+  else load(r0 + lane, vn);
   for (; r0 < n_rows; r0 += stride) {
     const bool active = r0 + lane < n_rows;
     // keep the coefficient pairs in LDS: hoisted out of the loop they would take 2 d^2 + 2 d VGPRs
     asm volatile("" ::: "memory");
     float v[M];
+    if constexpr (PACKED) {
+      __builtin_amdgcn_wave_barrier();  // the previous iteration's stage reads are done
+      stage_packed(qn, v);               // stage the wave's rows (and take this lane's row back)
+      load_packed(r0 + stride, qn);      // software prefetch of the next block
+    } else {
 #pragma unroll
-    for (int k = 0; k < M; ++k) v[k] = vn[k];
-    load(r0 + stride + lane, vn);  // software prefetch of the next row
-    // stage the row, then the Gram of the wave's 64 rows on the matrix pipe
+      for (int k = 0; k < M; ++k) v[k] = vn[k];
+      load(r0 + stride + lane, vn);  // software prefetch of the next row
+      // stage the row, then the Gram of the wave's 64 rows on the matrix pipe
 #pragma unroll
-    for (int k = 0; k < M; k += 2) *reinterpret_cast<f32x2*>(srow + k) = f32x2{v[k], v[k + 1]};
+      for (int k = 0; k < M; k += 2) *reinterpret_cast<f32x2*>(srow + k) = f32x2{v[k], v[k + 1]};
+    }
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
@@ -191,11 +242,12 @@ __global__ __launch_bounds__(kBlock) void kmv_moments_weights_kernel(float gamma
 #pragma unroll
     for (int k = 0; k < D; ++k) rr[k] = m1[k] - v[k];
     f32x2 q = a12;
+    int o = 0;
 #pragma unroll
-    for (int i = 0; i < D; ++i) {
-      f32x2 g = cpair[D * D + i];
+    for (int i = 0; i < D; ++i) {  // q += r_i (b_i + sum_{j >= i} Gsym_ij r_j)
+      f32x2 g = cpair[NT + i];
 #pragma unroll
-      for (int j = 0; j < D; ++j) g = cpair[i * D + j] * f32x2{rr[j], rr[j]} + g;
+      for (int j = i; j < D; ++j, ++o) g = cpair[o] * f32x2{rr[j], rr[j]} + g;
       q = g * f32x2{rr[i], rr[i]} + q;
     }
     const float w = active ? q[1] + q[0] * q[0] + gamma * q[0] : 0.f;  // kinetic_mckean_vlasov.py:243-248
@@ -505,8 +557,18 @@ extern "C" int pdeinv_kmv_moments_weights(int32_t D, float gamma, const float* c
   float* p = (float*)ws;
   double* both = (double*)((char*)ws + kmv_mw_slab_bytes(cols, bx));
   const dim3 g(bx, (unsigned)n_sets);
+  // packed rows (ld == 2d, 16-byte aligned, even d): the coalesced block-load variant
+  const bool packed = (2 * D) % 4 == 0 && ld == 2 * D && set_stride % 4 == 0 && ((uintptr_t)z & 15) == 0;
   switch (D) {
-#define CASE(DD) case DD: hipLaunchKernelGGL(kmv_moments_weights_kernel<DD>, g, dim3(kBlock), 0, st, gamma, coef, z, n_rows, set_stride, ld, p); break;
+#define CASE(DD)                                                                                              \
+  case DD:                                                                                                    \
+    if (packed)                                                                                               \
+      hipLaunchKernelGGL((kmv_moments_weights_kernel<DD, (2 * DD) % 4 == 0>), g, dim3(kBlock), 0, st, gamma, coef, \
+                         z, n_rows, set_stride, ld, p);                                                       \
+    else                                                                                                      \
+      hipLaunchKernelGGL((kmv_moments_weights_kernel<DD, false>), g, dim3(kBlock), 0, st, gamma, coef, z, n_rows, \
+                         set_stride, ld, p);                                                                  \
+    break;
     CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
 #undef CASE
   }
