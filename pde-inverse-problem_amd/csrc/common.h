@@ -194,112 +194,178 @@ __device__ __forceinline__ float dotd(const float* a, const float* b) {
   }
 }
 
-// out[i] += s * a[i] (packed pairs for even d)
-template <int D>
-__device__ __forceinline__ void axpyd(float s, const float* a, float* out) {
-  if constexpr (D % 2 == 0) {
+// ---- GMM softmax and KFP-GMM residual, packed over centre pairs ---------------------------
+// A KM-slot GMM is held as KM/2 centre pairs: pair p keeps (mu_{2p,i}, mu_{2p+1,i}) for every
+// coordinate i and the two logit constants c_k = -l2s |mu_k|^2 / 2 (log2 units, l2s = log2 e / s^2;
+// -inf in empty slots, whose weight is then exactly 0 with no per-centre branch). Every per-centre
+// scalar of the softmax and of the residual adjoint is one half of a v_pk_* instruction, and the
+// d-term dots x . mu_k accumulate two centres at once with no horizontal add. (The previous layout
+// packed over coordinates and spent one scalar instruction per centre on every softmax / adjoint
+// scalar: 527 -> see DESIGN.md §4.4 for the instruction counts of the fused C3 step loop.)
+template <int D, int KM>
+struct GmmPairs {
+  static_assert(KM % 2 == 0, "GMM centre slots come in pairs");
+  static constexpr int KP = KM / 2;
+  f32x2 mu[KP][D];
+  f32x2 c[KP];
+  // slot k of a K-centre GMM (mus [K, D] row-major); empty slots: mu = 0, c = -inf. For an object in
+  // memory (LDS), one thread per slot: scalar stores, so the two threads of a pair never race.
+  __device__ __forceinline__ void set(int k, int K, const float* mus, float l2s) {
+    float n2 = 0.f;
 #pragma unroll
-    for (int p = 0; p < D / 2; ++p) {
-      const f32x2 r = f32x2{s, s} * f32x2{a[2 * p], a[2 * p + 1]} + f32x2{out[2 * p], out[2 * p + 1]};
-      out[2 * p] = r[0];
-      out[2 * p + 1] = r[1];
+    for (int i = 0; i < D; ++i) {
+      const float m = k < K ? mus[k * D + i] : 0.f;
+      reinterpret_cast<float*>(&mu[k / 2][i])[k % 2] = m;
+      n2 = fmaf(m, m, n2);
     }
-  } else {
+    reinterpret_cast<float*>(&c[k / 2])[k % 2] = k < K ? -0.5f * l2s * n2 : -INFINITY;
+  }
+};
+
+__device__ __forceinline__ f32x2 bc2(float s) { return f32x2{s, s}; }
+
+// E_k = 2^(a_k - max a) for a_k = l2s (x . mu_k) + c_k (the softmax logits of -|x - mu_k|^2 / (2 s^2)
+// up to the k-independent -|x|^2 / (2 s^2)); returns sum_k E_k.
+template <int D, int KM>
+__device__ __forceinline__ float gmm_exp_weights(const f32x2 (*mu)[D], const f32x2* c, float l2s, const float* x,
+                                                 f32x2* E) {
+  constexpr int KP = KM / 2;
+  float amax = -INFINITY;
 #pragma unroll
-    for (int i = 0; i < D; ++i) out[i] = fmaf(s, a[i], out[i]);
+  for (int p = 0; p < KP; ++p) {
+    f32x2 t = bc2(x[0]) * mu[p][0];
+#pragma unroll
+    for (int i = 1; i < D; ++i) t = bc2(x[i]) * mu[p][i] + t;
+    E[p] = t * bc2(l2s) + c[p];
+    amax = fmaxf(amax, fmaxf(E[p][0], E[p][1]));
+  }
+  f32x2 S = {0.f, 0.f};
+#pragma unroll
+  for (int p = 0; p < KP; ++p) {
+    const f32x2 a = E[p] - bc2(amax);
+    E[p] = f32x2{__builtin_amdgcn_exp2f(a[0]), __builtin_amdgcn_exp2f(a[1])};
+    S += E[p];
+  }
+  return S[0] + S[1];
+}
+
+// sum_k E_k mu_k[i] for every coordinate (two centre chains, added at the end)
+template <int D, int KM>
+__device__ __forceinline__ void gmm_mix(const f32x2 (*mu)[D], const f32x2* E, float* out) {
+  constexpr int KP = KM / 2;
+#pragma unroll
+  for (int i = 0; i < D; ++i) {
+    f32x2 s = E[0] * mu[0][i];
+#pragma unroll
+    for (int p = 1; p < KP; ++p) s = E[p] * mu[p][i] + s;
+    out[i] = s[0] + s[1];
   }
 }
 
+// grad of U = -logsumexp_k(-|q - mu_k|^2 / (2 s^2)) = (q - sum_k w_k mu_k) / s^2 (core/potential.py:32-37;
+// the softmax form of the commented analytic gradient :39-43).
 template <int D, int KM>
-__device__ __forceinline__ void gmm_softmax(const float* x, const float (*mu)[D], const float* nh, float l2s,
-                                            float* w, float* mbar, float* t) {
-  // unused centre slots carry nh = -inf: weight exactly 0, no per-centre branches
-  float amax = -INFINITY;
+__device__ __forceinline__ void gmm_grad(const f32x2 (*mu)[D], const f32x2* c, float l2s, float inv_s2,
+                                         const float* q, float* g) {
+  f32x2 E[KM / 2];
+  const float inv = __builtin_amdgcn_rcpf(gmm_exp_weights<D, KM>(mu, c, l2s, q, E));
+  float acc[D];
+  gmm_mix<D, KM>(mu, E, acc);
 #pragma unroll
-  for (int k = 0; k < KM; ++k) {
-    t[k] = dotd<D>(x, mu[k]);
-    w[k] = (t[k] + nh[k]) * l2s;
-    amax = fmaxf(amax, w[k]);
-  }
-  float den = 0.f;
-#pragma unroll
-  for (int k = 0; k < KM; ++k) {
-    w[k] = __builtin_amdgcn_exp2f(w[k] - amax);
-    den += w[k];
-  }
-  const float inv = __builtin_amdgcn_rcpf(den);
-#pragma unroll
-  for (int i = 0; i < D; ++i) mbar[i] = 0.f;
-#pragma unroll
-  for (int k = 0; k < KM; ++k) {
-    w[k] *= inv;
-    axpyd<D>(w[k], mu[k], mbar);
-  }
+  for (int i = 0; i < D; ++i) g[i] = inv_s2 * fmaf(-acc[i], inv, q[i]);
 }
+
+// Accumulators of the analytic mu-adjoint, per lane: G[p][i] = sum cw_k x_i + ce_k e_i + cv_k v_i over
+// the lane's samples and CW[p] = sum cw_k; the gradient is G_k - mu_k CW_k (gmm_adjoint_flat).
+template <int D, int KM>
+struct GmmAdjAcc {
+  static constexpr int KP = KM / 2;
+  f32x2 G[KP][D];
+  f32x2 CW[KP];
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int p = 0; p < KP; ++p) {
+      CW[p] = f32x2{0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < D; ++i) G[p][i] = f32x2{0.f, 0.f};
+    }
+  }
+};
 
 // One sample (x, v) of the KFP residual for the GMM model V_theta = -logsumexp_k(-|x-mu_k|^2/(2 s^2))
 // (kinetic_fokker_planck.py:33-50 per sample, …_GMM.py:214-234): returns grad V_theta = s2 (x - mbar) in g,
-// T1 = |g|^2, T2 = v^T Hess V_theta v, T3 = g . v, and adds the analytic adjoint of
-// c1 T1 + c2 T2 + c3 T3 with respect to mu (softmax chain rule; derivation and FD check:
-// oracle/numpy_ref.py kfp_gmm_grad_analytic) to gacc[K*D]. Shared by the standalone residual
-// (residual.hip kfp_gmm_kernel) and the simulator-fused one (sde.hip). The d-vector work runs on
-// packed pairs for even d; the per-centre scalars are folded so that each costs one or two FMAs.
+// T1 = |g|^2, T2 = v^T Hess V_theta v, T3 = g . v, and adds the analytic adjoint of c1 T1 + c2 T2 + c3 T3
+// with respect to mu (softmax chain rule; derivation and FD check: oracle/numpy_ref.py
+// kfp_gmm_grad_analytic) to `acc`. With w the softmax weights, p_k = mu_k . v, e = x - mbar,
+// em_k = e . mu_k, pbar = sum w p, A1 = -2 c1 s^4, A2 = -c2 s^4, A3 = -c3 s^2, B = A3 - 2 A2 pbar:
+//   F_k = A1 em_k + p_k (A2 p_k + B),   Fbar = sum w F,
+//   d/d mu_k = cw_k (x - mu_k) + ce_k e + cv_k v,  cw = w s2 (F - Fbar), ce = A1 w, cv = w (2 A2 p_k + B).
+// Shared by the standalone residual (residual.hip kfp_gmm_kernel) and the simulator-fused one (sde.hip).
 template <int D, int KM>
-__device__ __forceinline__ void gmm_residual_sample(const float (*mu)[D], const float* nh, float s2, float l2s,
+__device__ __forceinline__ void gmm_residual_sample(const f32x2 (*mu)[D], const f32x2* c, float s2, float l2s,
                                                     const float* x, const float* v, float c1, float c2, float c3,
-                                                    float* gacc, float* g, float& T1, float& T2, float& T3) {
-  float w[KM], mbar[D], xm[KM];
-  gmm_softmax<D, KM>(x, mu, nh, l2s, w, mbar, xm);
+                                                    GmmAdjAcc<D, KM>& acc, float* g, float& T1, float& T2,
+                                                    float& T3) {
+  constexpr int KP = KM / 2;
+  f32x2 W[KP];
+  const float inv = __builtin_amdgcn_rcpf(gmm_exp_weights<D, KM>(mu, c, l2s, x, W));
+#pragma unroll
+  for (int p = 0; p < KP; ++p) W[p] *= bc2(inv);
   float e[D];
+  gmm_mix<D, KM>(mu, W, e);
 #pragma unroll
   for (int i = 0; i < D; ++i) {
-    e[i] = x[i] - mbar[i];
+    e[i] = x[i] - e[i];
     g[i] = s2 * e[i];
   }
   const float ee = dotd<D>(e, e), ev = dotd<D>(e, v), vv = dotd<D>(v, v);
   T1 = s2 * s2 * ee;
   T3 = s2 * ev;
-  float pk[KM], em[KM], pbar = 0.f, wp2 = 0.f;
+  f32x2 PK[KP], EM[KP];
+  f32x2 pb = {0.f, 0.f}, wq = {0.f, 0.f};
 #pragma unroll
-  for (int k = 0; k < KM; ++k) {
-    pk[k] = dotd<D>(mu[k], v);
-    em[k] = dotd<D>(e, mu[k]);  // e.mu_k
-    pbar = fmaf(w[k], pk[k], pbar);
-    wp2 = fmaf(w[k] * pk[k], pk[k], wp2);
+  for (int p = 0; p < KP; ++p) {
+    PK[p] = bc2(v[0]) * mu[p][0];
+    EM[p] = bc2(e[0]) * mu[p][0];
+#pragma unroll
+    for (int i = 1; i < D; ++i) {
+      PK[p] = bc2(v[i]) * mu[p][i] + PK[p];
+      EM[p] = bc2(e[i]) * mu[p][i] + EM[p];
+    }
+    const f32x2 wp = W[p] * PK[p];
+    pb += wp;
+    wq = wp * PK[p] + wq;
   }
+  const float pbar = pb[0] + pb[1], wp2 = wq[0] + wq[1];
   const float s4 = s2 * s2;
   T2 = s2 * vv - s4 * (wp2 - pbar * pbar);  // v^T (I/s^2 - Cov_w(mu)/s^4) v
-  // adjoint: F_k = d f / d w_k = A1 em_k + pk_k (A2 (pk_k - 2 pbar) + A3), then the softmax chain rule
   const float A1 = -2.f * c1 * s4, A2 = -c2 * s4, A3 = -c3 * s2;
-  float Fk[KM], Fbar = 0.f;
+  const float B = fmaf(-2.f * A2, pbar, A3);
+  f32x2 F[KP], fb = {0.f, 0.f};
 #pragma unroll
-  for (int k = 0; k < KM; ++k) {
-    Fk[k] = fmaf(A1, em[k], pk[k] * fmaf(A2, pk[k] - 2.f * pbar, A3));
-    Fbar = fmaf(w[k], Fk[k], Fbar);
+  for (int p = 0; p < KP; ++p) {
+    F[p] = bc2(A1) * EM[p] + PK[p] * (bc2(A2) * PK[p] + bc2(B));
+    fb = W[p] * F[p] + fb;
   }
+  const float nsF = -s2 * (fb[0] + fb[1]);
 #pragma unroll
-  for (int k = 0; k < KM; ++k) {
-    // cw (x - mu_k) + ce e + cv v with cw = w (F_k - Fbar) s2, ce = A1 w, cv = w (2 A2 (pk_k - pbar) + A3)
-    const float cw = w[k] * s2 * (Fk[k] - Fbar);
-    const float ce = A1 * w[k];
-    const float cv = w[k] * fmaf(2.f * A2, pk[k] - pbar, A3);
-    float* gk = gacc + k * D;
-    if constexpr (D % 2 == 0) {
+  for (int p = 0; p < KP; ++p) {
+    const f32x2 cw = W[p] * (bc2(s2) * F[p] + bc2(nsF));
+    const f32x2 ce = bc2(A1) * W[p];
+    const f32x2 cv = W[p] * (bc2(2.f * A2) * PK[p] + bc2(B));
+    acc.CW[p] += cw;
 #pragma unroll
-      for (int p = 0; p < D / 2; ++p) {
-        const f32x2 xp = f32x2{x[2 * p], x[2 * p + 1]}, mp = f32x2{mu[k][2 * p], mu[k][2 * p + 1]};
-        f32x2 r = f32x2{gk[2 * p], gk[2 * p + 1]};
-        r = f32x2{cw, cw} * (xp - mp) + r;
-        r = f32x2{ce, ce} * f32x2{e[2 * p], e[2 * p + 1]} + r;
-        r = f32x2{cv, cv} * f32x2{v[2 * p], v[2 * p + 1]} + r;
-        gk[2 * p] = r[0];
-        gk[2 * p + 1] = r[1];
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < D; ++i) gk[i] += cw * (x[i] - mu[k][i]) + ce * e[i] + cv * v[i];
-    }
+    for (int i = 0; i < D; ++i) acc.G[p][i] = cv * bc2(v[i]) + (ce * bc2(e[i]) + (cw * bc2(x[i]) + acc.G[p][i]));
   }
+}
+
+// the lane's mu-gradient in the reference parameter order (k * D + i): G_k - mu_k CW_k
+template <int D, int KM>
+__device__ __forceinline__ void gmm_adjoint_flat(const GmmAdjAcc<D, KM>& acc, const f32x2 (*mu)[D], float* out) {
+#pragma unroll
+  for (int k = 0; k < KM; ++k)
+#pragma unroll
+    for (int i = 0; i < D; ++i) out[k * D + i] = fmaf(-mu[k / 2][i][k % 2], acc.CW[k / 2][k % 2], acc.G[k / 2][i][k % 2]);
 }
 
 // V_hypothesis parameters zero-padded to wider compiled shapes (exact: a padded hidden unit has zero

@@ -141,30 +141,22 @@ template <int D, int KM>
 __global__ __launch_bounds__(kBlock) void kfp_gmm_kernel(GmmResArgs a, const float* __restrict__ mus,
                                                          float* __restrict__ partials) {
   constexpr int NS = PDEINV_GMM_NACC;
-  // model and true centres pinned in VGPRs (as uniform SGPR values they overflow the scalar file
-  // and every use costs a v_readlane); empty slots: nh = -inf (softmax weight 0)
-  // Empty centre slots: nh = -inf (softmax weight exactly 0, no per-centre branches). Pinning the
-  // centres in VGPRs (as in the simulator) does not pay here: the K*d gradient accumulators already
-  // fill the register file (measured: occupancy 2 -> 1).
-  float mu[KM][D];
-  float mut[KM][D];
-  float nh[KM], nht[KM];
-#pragma unroll
-  for (int k = 0; k < KM; ++k) {
-    float n2 = 0.f, n2t = 0.f;
-#pragma unroll
-    for (int i = 0; i < D; ++i) {
-      mu[k][i] = (k < a.K) ? mus[k * D + i] : 0.f;
-      mut[k][i] = (k < a.KT) ? a.mus_true[k * D + i] : 0.f;
-      n2 = fmaf(mu[k][i], mu[k][i], n2);
-      n2t = fmaf(mut[k][i], mut[k][i], n2t);
-    }
-    nh[k] = (k < a.K) ? -0.5f * n2 : -INFINITY;
-    nht[k] = (k < a.KT) ? -0.5f * n2t : -INFINITY;
+  // model and true GMM in centre-pair layout (common.h GmmPairs) in LDS, read with wave-uniform
+  // broadcasts: pinned in VGPRs they took 2 (K d + K) registers beside the adjoint accumulators
+  // (155 VGPRs, occupancy 3)
+  __shared__ GmmPairs<D, KM> cen[2];
+  GmmPairs<D, KM>& cm = cen[0];
+  GmmPairs<D, KM>& ct = cen[1];
+  for (int k = threadIdx.x; k < KM; k += kBlock) {
+    cm.set(k, a.K, mus, a.l2s);
+    ct.set(k, a.KT, a.mus_true, a.l2st);
   }
-  float acc[NS + KM * D];
+  __syncthreads();
+  float acc[NS];
 #pragma unroll
-  for (int c = 0; c < NS + KM * D; ++c) acc[c] = 0.f;
+  for (int c = 0; c < NS; ++c) acc[c] = 0.f;
+  GmmAdjAcc<D, KM> adj;
+  adj.zero();
 
   const int64_t total = a.n0 + a.ni + a.nt;
   const int64_t stride = (int64_t)gridDim.x * kBlock;
@@ -186,6 +178,9 @@ __global__ __launch_bounds__(kBlock) void kfp_gmm_kernel(GmmResArgs a, const flo
     for (int i = 0; i < D; ++i) { xn[i] = row[i]; vn[i] = row[D + i]; }
   }
   for (; r < total; r += stride) {
+    // re-read the LDS centres every sample (hoisted out of the loop they take the registers the LDS
+    // layout exists to save)
+    asm volatile("" ::: "memory");
     const int set = set_n;
     float x[D], v[D];
 #pragma unroll
@@ -200,17 +195,16 @@ __global__ __launch_bounds__(kBlock) void kfp_gmm_kernel(GmmResArgs a, const flo
     const float c2 = set == 0 ? a.c_hess : 0.f;
     const float c3 = set == 0 ? a.c_fric : (set == 1 ? a.c_init : a.c_term);
     float g[D], T1, T2, T3;
-    gmm_residual_sample<D, KM>(mu, nh, s2, a.l2s, x, v, c1, c2, c3, acc + NS, g, T1, T2, T3);
+    gmm_residual_sample<D, KM>(cm.mu, cm.c, s2, a.l2s, x, v, c1, c2, c3, adj, g, T1, T2, T3);
     acc[PDEINV_GMM_ACC_LOSS] += c1 * T1 + c2 * T2 + c3 * T3;
     if (set == 0) {
-      float wt[KM], mbt[D], xmt[KM];
-      gmm_softmax<D, KM>(x, mut, nht, a.l2st, wt, mbt, xmt);
+      float gt[D];
+      gmm_grad<D, KM>(ct.mu, ct.c, a.l2st, a.s2t, x, gt);
       float Tt = 0.f, Tgt = 0.f;
 #pragma unroll
       for (int i = 0; i < D; ++i) {
-        const float gt = a.s2t * (x[i] - mbt[i]);
-        Tt = fmaf(gt, gt, Tt);
-        Tgt = fmaf(gt - g[i], gt - g[i], Tgt);
+        Tt = fmaf(gt[i], gt[i], Tt);
+        Tgt = fmaf(gt[i] - g[i], gt[i] - g[i], Tgt);
       }
       acc[PDEINV_GMM_ACC_LOSS] += a.c_true * Tt;
       acc[PDEINV_GMM_ACC_LOSS_GT] += a.c_true * Tgt;
@@ -224,8 +218,12 @@ __global__ __launch_bounds__(kBlock) void kfp_gmm_kernel(GmmResArgs a, const flo
       acc[PDEINV_GMM_ACC_TERMINAL] += a.inv_nt * T3;
     }
   }
+  float flat[NS + KM * D];
+#pragma unroll
+  for (int c = 0; c < NS; ++c) flat[c] = acc[c];
+  gmm_adjoint_flat<D, KM>(adj, cm.mu, flat + NS);
   __shared__ float lds[kWavesPerBlock * (NS + KM * D)];
-  block_reduce_to_slab(acc, NS + a.K * D, lds, partials, blockIdx.x, gridDim.x);
+  block_reduce_to_slab(flat, NS + a.K * D, lds, partials, blockIdx.x, gridDim.x);
 }
 
 __global__ void kfp_gmm_finalize_kernel(int n_grad, float gamma, const double* __restrict__ acc,

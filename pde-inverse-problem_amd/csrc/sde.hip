@@ -74,8 +74,7 @@ __device__ __forceinline__ void grad_quadratic(const SdeArgs& a, const float* q,
   }
 }
 
-// grad of U = -logsumexp_k(-|q-mu_k|^2/(2 s^2)) = (q - sum_k w_k mu_k) / s^2
-// (core/potential.py:32-37; the softmax form of the commented analytic gradient :39-43).
+// grad of U = -logsumexp_k(-|q-mu_k|^2/(2 s^2)): gmm_grad (common.h), packed over centre pairs.
 // Softmax logits are shift-invariant, so |q|^2 drops out: in log2 units
 // a_k = l2s (q . mu_k) + c_k, l2s = log2e / s^2, c_k = -l2s |mu_k|^2 / 2 — one d-term dot per
 // centre. The KM centres live in VGPRs for the whole kernel (pinned once: kept as kernel-argument
@@ -83,49 +82,21 @@ __device__ __forceinline__ void grad_quadratic(const SdeArgs& a, const float* q,
 // c_k = -inf, so the softmax needs no per-centre branches.
 template <int D, int KM>
 struct GmmCentres {
-  float mu[KM][D];
-  float c[KM];
+  GmmPairs<D, KM> g;
   __device__ __forceinline__ void load(const SdeArgs& a) {
 #pragma unroll
-    for (int k = 0; k < KM; ++k) {
+    for (int p = 0; p < KM / 2; ++p) {
 #pragma unroll
       for (int i = 0; i < D; ++i) {
-        mu[k][i] = k < a.K ? a.params[k * D + i] : 0.f;
-        asm volatile("" : "+v"(mu[k][i]));
+        g.mu[p][i] = f32x2{2 * p < a.K ? a.params[2 * p * D + i] : 0.f, 2 * p + 1 < a.K ? a.params[(2 * p + 1) * D + i] : 0.f};
+        asm volatile("" : "+v"(g.mu[p][i]));
       }
-      c[k] = k < a.K ? a.params[kMaxGmmK * D + k] : -INFINITY;
-      asm volatile("" : "+v"(c[k]));
+      g.c[p] = f32x2{2 * p < a.K ? a.params[kMaxGmmK * D + 2 * p] : -INFINITY,
+                     2 * p + 1 < a.K ? a.params[kMaxGmmK * D + 2 * p + 1] : -INFINITY};
+      asm volatile("" : "+v"(g.c[p]));
     }
   }
 };
-
-template <int D, int KM>
-__device__ __forceinline__ void grad_gmm(const SdeArgs& a, const float (*mu)[D], const float* cc, const float* q,
-                                         float* g) {
-  float al[KM];
-  float amax = -INFINITY;
-#pragma unroll
-  for (int k = 0; k < KM; ++k) {
-    float t = 0.f;
-#pragma unroll
-    for (int i = 0; i < D; ++i) t = fmaf(q[i], mu[k][i], t);
-    al[k] = fmaf(a.l2s, t, cc[k]);
-    amax = fmaxf(amax, al[k]);
-  }
-  float den = 0.f, acc[D];
-#pragma unroll
-  for (int i = 0; i < D; ++i) acc[i] = 0.f;
-#pragma unroll
-  for (int k = 0; k < KM; ++k) {
-    const float e = __builtin_amdgcn_exp2f(al[k] - amax);
-    den += e;
-#pragma unroll
-    for (int i = 0; i < D; ++i) acc[i] = fmaf(e, mu[k][i], acc[i]);
-  }
-  const float inv = __builtin_amdgcn_rcpf(den);
-#pragma unroll
-  for (int i = 0; i < D; ++i) g[i] = a.inv_s2 * fmaf(-acc[i], inv, q[i]);
-}
 
 // McKean–Vlasov drift with the mean path precomputed: grad U(q) = A (q - xbar_s), the same
 // operation order as the per-update exchange (mf_step_kernel) and the C oracle (y = q - xbar, then
@@ -282,7 +253,7 @@ __global__ __launch_bounds__(kBlock, MINW) void sde_simulate_kernel(SdeArgs a, c
   float z[M];
 #pragma unroll
   for (int k = 0; k < M; ++k) z[k] = z0[i * a.ld_z0 + k];
-  [[maybe_unused]] GmmCentres<D, KM> centres;
+  [[maybe_unused]] GmmCentres<D, (KM > 1 ? KM : 2)> centres;
   if constexpr (POT == PDEINV_POT_GMM && !RES) centres.load(a);
 
   __shared__ float lds[kWavesPerBlock * moment_len(M > 16 ? 2 : M)];
@@ -295,35 +266,26 @@ __global__ __launch_bounds__(kBlock, MINW) void sde_simulate_kernel(SdeArgs a, c
     block_reduce_to_slab(init.v, L, lds, partials, bid, nb);
   }
 
-  // fused GMM residual state: model centres (nh = -|mu|^2 / 2, empty slots -inf) and the accumulators
-  // With the residual fused, the true (simulated) and the model centres live in LDS and are read
-  // with wave-uniform broadcasts: in VGPRs they would take 2 (K d + K) registers and, beside the
-  // K d gradient accumulators, leave one wave per SIMD.
-  constexpr int NR = RES ? PDEINV_GMM_NACC + KM * D : 1;
-  struct LdsCentres {
-    float mu[KM][D];
-    float c[KM];
-  };
-  __shared__ LdsCentres lcen_s[RES ? 2 : 1];
-  [[maybe_unused]] LdsCentres& lcen = lcen_s[0];
-  [[maybe_unused]] LdsCentres& lmod = lcen_s[RES ? 1 : 0];
-  [[maybe_unused]] float racc[NR];
+  // fused GMM residual state: the true (simulated) and the model GMM in centre-pair layout (common.h
+  // GmmPairs) in LDS, read with wave-uniform broadcasts — in VGPRs they would take 2 (K d + K)
+  // registers and, beside the adjoint accumulators, leave one wave per SIMD.
+  __shared__ GmmPairs<D, (KM > 1 ? KM : 2)> lcen_s[RES ? 2 : 1];
+  [[maybe_unused]] auto& lcen = lcen_s[0];
+  [[maybe_unused]] auto& lmod = lcen_s[RES ? 1 : 0];
+  constexpr int KR = KM > 1 ? KM : 2;
+  [[maybe_unused]] float racc[PDEINV_GMM_NACC];
+  [[maybe_unused]] GmmAdjAcc<D, KR> radj;
   if constexpr (RES) {
-    for (int e = threadIdx.x; e < KM * (D + 1); e += kBlock) {
-      const int k = e / (D + 1), c = e % (D + 1);
-      if (c < D) {
-        lcen.mu[k][c] = k < a.K ? a.params[k * D + c] : 0.f;
-        lmod.mu[k][c] = k < rf.K ? rf.mus[k * D + c] : 0.f;
-      } else {
-        lcen.c[k] = k < a.K ? a.params[kMaxGmmK * D + k] : -INFINITY;
-        float n2 = 0.f;
-        for (int q = 0; q < D && k < rf.K; ++q) n2 = fmaf(rf.mus[k * D + q], rf.mus[k * D + q], n2);
-        lmod.c[k] = k < rf.K ? -0.5f * n2 : -INFINITY;
-      }
+    for (int k = threadIdx.x; k < KM; k += kBlock) {
+      // the simulator's packed constants (build_args) for the true GMM; the model's from its centres
+      lcen.set(k, a.K, a.params, a.l2s);
+      if (k < a.K) reinterpret_cast<float*>(&lcen.c[k / 2])[k % 2] = a.params[kMaxGmmK * D + k];
+      lmod.set(k, rf.K, rf.mus, rf.l2s);
     }
     __syncthreads();
 #pragma unroll
-    for (int c = 0; c < NR; ++c) racc[c] = 0.f;
+    for (int c = 0; c < PDEINV_GMM_NACC; ++c) racc[c] = 0.f;
+    radj.zero();
   }
   // set 0 = 0T (gt = grad V* at the row), 1 = initial, 2 = terminal; w = 0 for lanes past N
   [[maybe_unused]] auto res_add = [&](const float* zz, const float* gt, int set) {
@@ -332,8 +294,7 @@ __global__ __launch_bounds__(kBlock, MINW) void sde_simulate_kernel(SdeArgs a, c
       const float c2 = set == 0 ? w * rf.c_hess : 0.f;
       const float c3 = w * (set == 0 ? rf.c_fric : (set == 1 ? rf.c_init : rf.c_term));
       float gm[D], T1, T2, T3;
-      gmm_residual_sample<D, KM>(lmod.mu, lmod.c, rf.s2, rf.l2s, zz, zz + D, c1, c2, c3, racc + PDEINV_GMM_NACC,
-                                 gm, T1, T2, T3);
+      gmm_residual_sample<D, KR>(lmod.mu, lmod.c, rf.s2, rf.l2s, zz, zz + D, c1, c2, c3, radj, gm, T1, T2, T3);
       racc[PDEINV_GMM_ACC_LOSS] += c1 * T1 + c2 * T2 + c3 * T3;
       if (set == 0) {
         float Tt = 0.f, Tgt = 0.f;
@@ -384,8 +345,8 @@ __global__ __launch_bounds__(kBlock, MINW) void sde_simulate_kernel(SdeArgs a, c
     // registers this layout exists to save)
     if constexpr (RES) asm volatile("" ::: "memory");
     float g[D], xi[D];
-    if constexpr (POT == PDEINV_POT_GMM && RES) grad_gmm<D, KM>(a, lcen.mu, lcen.c, z, g);
-    else if constexpr (POT == PDEINV_POT_GMM) grad_gmm<D, KM>(a, centres.mu, centres.c, z, g);
+    if constexpr (POT == PDEINV_POT_GMM && RES) gmm_grad<D, KR>(lcen.mu, lcen.c, a.l2s, a.inv_s2, z, g);
+    else if constexpr (POT == PDEINV_POT_GMM) gmm_grad<D, KR>(centres.g.mu, centres.g.c, a.l2s, a.inv_s2, z, g);
     else if constexpr (POT == PDEINV_POT_MEANFIELD_QUADRATIC) grad_meanfield<D>(a, z, a.xbar + (int64_t)s * D, g);
     else grad_quadratic<D>(a, z, g);
     if constexpr (RES) {
@@ -423,8 +384,13 @@ __global__ __launch_bounds__(kBlock, MINW) void sde_simulate_kernel(SdeArgs a, c
   if (active && last) store_row<D, kStoreNT>(last + i * M, z);
   if constexpr (RES) {
     res_add(z, z, 2);  // last: the terminal set
+    constexpr int NR = PDEINV_GMM_NACC + KR * D;
+    float flat[NR];
+#pragma unroll
+    for (int c = 0; c < PDEINV_GMM_NACC; ++c) flat[c] = racc[c];
+    gmm_adjoint_flat<D, KR>(radj, lmod.mu, flat + PDEINV_GMM_NACC);
     __shared__ float rlds[kWavesPerBlock * NR];
-    block_reduce_to_slab(racc, PDEINV_GMM_NACC + rf.K * D, rlds, partials, bid, nb);
+    block_reduce_to_slab(flat, PDEINV_GMM_NACC + rf.K * D, rlds, partials, bid, nb);
   }
 
   if constexpr (MOM) {
