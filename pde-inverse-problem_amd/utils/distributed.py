@@ -16,8 +16,14 @@ import torch
 import torch.distributed as dist
 
 
+def _forced() -> bool:
+    """PDEINV_DIST_FORCE=1: take the distributed path (process group + every all-reduce call site) even
+    at world size 1 — lets a one-GPU box execute the RCCL data path (tests/test_gpu_multirank.py)."""
+    return os.environ.get("PDEINV_DIST_FORCE", "0") == "1"
+
+
 def is_distributed() -> bool:
-    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+    return dist.is_available() and dist.is_initialized() and (dist.get_world_size() > 1 or _forced())
 
 
 def rank() -> int:
@@ -31,7 +37,7 @@ def world_size() -> int:
 def init_from_env(backend: str = None) -> bool:
     """Initialise from torchrun's env (RANK/WORLD_SIZE/MASTER_ADDR/MASTER_PORT); no-op for one rank."""
     ws = int(os.environ.get("WORLD_SIZE", "1"))
-    if ws <= 1 or dist.is_initialized():
+    if (ws <= 1 and not _forced()) or dist.is_initialized():
         return dist.is_initialized()
     backend = os.environ.get("PDEINV_DIST_BACKEND", backend)  # test override (e.g. gloo on one GPU)
     if backend is None:

@@ -1,7 +1,8 @@
 """Worker for the multi-rank GPU tests (tests/test_gpu_multirank.py), launched by
 torch.distributed.run with PDEINV_DIST_BACKEND=gloo so that several ranks can share the one GPU
 of a test box (RCCL needs one GPU per rank; the data path and the all-reduce call sites are the
-same). Writes this rank's shard of the result to <out>/rank<r>.npz."""
+same), or as one rank over RCCL (PDEINV_DIST_FORCE=1, backend nccl). Writes this rank's shard of
+the result (and the backend that carried its all-reduces) to <out>/rank<r>.npz."""
 import os
 import sys
 
@@ -27,8 +28,9 @@ def mean_field(out_dir, exchange="fused", N=6000, n=30, d=8):
     pot = MeanFieldQuadraticPotential(nr.problem_constants(d))
     r = simulate_mean_field(torch.as_tensor(z0[off:off + cnt], device=dev), n, 0.02, PRNGKey(11), pot, 1.0,
                             particle_offset=off, counter_offset=3, exchange=exchange)
+    backend = torch.distributed.get_backend() if dist.is_distributed() else "none"
     np.savez(os.path.join(out_dir, f"rank{rank}.npz"), traj=r["traj"].cpu().numpy(), last=r["last"].cpu().numpy(),
-             xsum=r["xsum"].cpu().numpy(), off=off, world=world)
+             xsum=r["xsum"].cpu().numpy(), off=off, world=world, backend=backend)
 
 
 if __name__ == "__main__":

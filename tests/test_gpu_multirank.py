@@ -23,8 +23,13 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _launch(nproc, args, port, timeout=180):
-    env = dict(os.environ, PDEINV_DIST_BACKEND="gloo")
+def _launch(nproc, args, port, timeout=180, rccl=False):
+    env = dict(os.environ)
+    if rccl:  # one rank on the one GPU, over RCCL, with the distributed path forced at world size 1
+        env.pop("PDEINV_DIST_BACKEND", None)
+        env.update(PDEINV_DIST_FORCE="1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    else:
+        env["PDEINV_DIST_BACKEND"] = "gloo"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr=127.0.0.1", f"--master-port={port}"] + args
     return subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=timeout)
@@ -67,3 +72,35 @@ def test_bench_two_ranks(native):
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["value"] > 0 and out["config"]["particles_per_gpu"] == 65536
     assert abs(out["value"] * out["ms_per_step"] / 1e3 - 2 * 65536 * 101) < 1e-6 * out["value"]
+
+
+@pytest.mark.parametrize("exchange,port", [("fused", 29631), ("per_update", 29632)])
+def test_mean_field_over_rccl_world1(native, tmp_path, exchange, port):
+    """The RCCL data path executes: one rank under torch.distributed.run with the nccl backend and the
+    distributed path forced (PDEINV_DIST_FORCE=1), so every all-reduce call site of the McKean–Vlasov
+    drivers runs through RCCL; the result equals the plain single-process run (a one-rank all-reduce
+    is the identity, so bit-for-bit up to nothing)."""
+    worker = [os.path.join(ROOT, "tests", "mp_gpu_worker.py"), "mean_field"]
+    ref_dir, d = tmp_path / "plain", tmp_path / "rccl"
+    ref_dir.mkdir()
+    d.mkdir()
+    r = subprocess.run([sys.executable] + worker + [str(ref_dir), exchange],
+                       cwd=ROOT, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr[-3000:]
+    r = _launch(1, worker + [str(d), exchange], port, rccl=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert str(np.load(os.path.join(d, "rank0.npz"))["backend"]) == "nccl"
+    t1, l1, x1 = _gather(ref_dir, 1)
+    tr, lr, xr = _gather(d, 1)
+    assert np.array_equal(tr, t1) and np.array_equal(lr, l1) and np.array_equal(xr, x1)
+
+
+def test_bench_over_rccl_world1(native):
+    """bench.py's headline step with its residual all-reduce carried by RCCL (one rank, forced path)."""
+    r = _launch(1, [os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "3", "--warmup", "1",
+                    "--particles", "65536", "--no-cpu-baseline", "--no-recovery"], 29633, rccl=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 1 and out["value"] > 0 and np.isfinite(out["loss"])
