@@ -273,7 +273,15 @@ __global__ __launch_bounds__(kWavesPB * kWave) void kmvp_gbar_kernel(Args a) {
 // -------------------------------------------------------------------------------------------------
 // pass 2: d/dtheta of sum_ij [ u_i . grad Phi(y_ij) + c2 v_i^T Hess Phi(y_ij) v_i + c0_i Phi(y_ij) ]
 // -------------------------------------------------------------------------------------------------
-template <int D, int W>
+// Work units of pass 2: (item, block of kJB references) — finer than whole items, so the persistent
+// grid's waves get equal shares (5 000 items over 2 048 waves left 2 or 3 items of 79 tiles per wave).
+constexpr int kJB = 512;
+
+// LSLAB: the wave's weight-gradient slab lives in LDS for the whole kernel (every tile folds its 36
+// outer-product tiles there with ds_* read-modify-writes) and is copied to the wave's global slab row
+// once at the end; without it (nets whose padded parameter count does not fit) the folds go to the
+// global slab row directly.
+template <int D, int W, bool LSLAB>
 __global__ __launch_bounds__(kWavesPB * kWave) void kmvp_grad_kernel(Args a) {
   static_assert(W < 32 && D < 32, "a constant-1 input feature must fit the 32-wide MFMA tile");
   const int lane = threadIdx.x & (kWave - 1);
@@ -281,17 +289,26 @@ __global__ __launch_bounds__(kWavesPB * kWave) void kmvp_grad_kernel(Args a) {
   const int64_t wave = (int64_t)blockIdx.x * kWavesPB + wib;
   const int64_t n_waves = (int64_t)gridDim.x * kWavesPB;
   __shared__ float stage[kWavesPB][2][kWave * kSR];
+  extern __shared__ float lslab_all[];  // LSLAB: [kWavesPB][P]
   float* As = stage[wib][0];
   float* Bs = stage[wib][1];
   const Ring<W> ring{a.scratch + wave * (int64_t)5 * W * a.L * kWave, lane};
-  float* slab = a.gslab + wave * (int64_t)a.P;
+  float* gslab = a.gslab + wave * (int64_t)a.P;
+  float* slab = LSLAB ? lslab_all + wib * a.P : gslab;
+  if constexpr (LSLAB) {
+    for (int q = lane; q < a.P; q += kWave) slab[q] = 0.f;
+    wave_fence();
+  }
   cfloat* Ko = a.prm + kofs<D, W>(a.L);
   cfloat* bo = a.prm + bofs<D, W>(a.L, a.L, a.O);
   const int L = a.L, O = a.O;
   const float c2 = -2.f * a.s;
   float accs[3] = {0.f, 0.f, 0.f};  // LOSS, HESSIAN, FRICTION slot partials
-  for (int64_t it = wave; it < a.n_items; it += n_waves) {
+  const int64_t n_jb = (a.n + kJB - 1) / kJB;
+  for (int64_t u = wave; u < a.n_items * n_jb; u += n_waves) {
+    const int64_t it = u / n_jb, jb = u - it * n_jb;
     const int64_t t = it / a.n, i = it - t * a.n;
+    const int64_t j_end = (jb + 1) * kJB < a.n ? (jb + 1) * kJB : a.n;
     const float* zt = a.z + t * a.set_stride;
     float xi[D], vi[D], u0[D];
 #pragma unroll
@@ -302,9 +319,9 @@ __global__ __launch_bounds__(kWavesPB * kWave) void kmvp_grad_kernel(Args a) {
     }
     const float dsa = a.ds[it * 2], dsb = a.ds[it * 2 + 1];
     const float c0 = 2.f * a.s * (dsb + dsa * dsa + a.gamma * dsa);  // 2 s w_it (:84-89)
-    for (int64_t j0 = 0; j0 < a.n; j0 += kWave) {
+    for (int64_t j0 = jb * kJB; j0 < j_end; j0 += kWave) {
       const int64_t j = j0 + lane;
-      const bool active = j < a.n;
+      const bool active = j < j_end;
       float y[D];
 #pragma unroll
       for (int k = 0; k < D; ++k) y[k] = (active && k < a.Dr) ? xi[k] - zt[j * a.ld + k] : 0.f;
@@ -590,6 +607,10 @@ __global__ __launch_bounds__(kWavesPB * kWave) void kmvp_grad_kernel(Args a) {
       }
     }
   }
+  if constexpr (LSLAB) {
+    wave_fence();
+    for (int q = lane; q < a.P; q += kWave) gslab[q] = slab[q];
+  }
   float* as = a.aslab + wave * 8;
 #pragma unroll
   for (int q = 0; q < 3; ++q) {
@@ -674,10 +695,20 @@ PairPlan pair_plan(const pdeinv_kmv_mlp_desc* d) {
   return p;
 }
 
+constexpr size_t kLdsSlabMax = 64 * 1024;  // per block (the stage arrays take another 33 KB)
+
 template <int D, int W>
 void launch_pairs(const mlpp::Args& a, int64_t n_waves, hipStream_t st, bool pass2) {
   const dim3 g((unsigned)(n_waves / mlpp::kWavesPB)), b(mlpp::kWavesPB * kWave);
-  if (pass2) hipLaunchKernelGGL((mlpp::kmvp_grad_kernel<D, W>), g, b, 0, st, a);
+  const size_t lds = sizeof(float) * (size_t)mlpp::kWavesPB * a.P;
+  if (pass2 && lds <= kLdsSlabMax) {
+    static const bool attr = hipFuncSetAttribute((const void*)mlpp::kmvp_grad_kernel<D, W, true>,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 (int)kLdsSlabMax) == hipSuccess;
+    (void)attr;
+    hipLaunchKernelGGL((mlpp::kmvp_grad_kernel<D, W, true>), g, b, lds, st, a);
+  }
+  else if (pass2) hipLaunchKernelGGL((mlpp::kmvp_grad_kernel<D, W, false>), g, b, 0, st, a);
   else hipLaunchKernelGGL((mlpp::kmvp_gbar_kernel<D, W>), g, b, 0, st, a);
 }
 

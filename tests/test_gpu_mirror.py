@@ -53,14 +53,15 @@ def test_kmv_residual_vs_pairwise_restatement(native):
 @pytest.mark.parametrize("d,n,chunk,W,L,impl", [(2, 40, 1 << 18, 20, 3, 0), (4, 37, 300, 20, 3, 1),
                                                 (4, 37, 300, 20, 3, 2), (3, 70, 300, 10, 2, 2),
                                                 (2, 130, 300, 20, 8, 2), (8, 65, 300, 28, 2, 2),
-                                                (1, 66, 300, 16, 4, 2)])
+                                                (1, 66, 300, 16, 4, 2), (2, 530, 300, 20, 2, 2)])
 def test_kmv_general_phi_mlp_vs_pairwise_restatement(native, d, n, chunk, W, L, impl):
     """General Phi_theta = V_hypothesis (non-parametric KMV, kinetic_mckean_vlasov.py:11-120) == the
     literal pair-tensor restatement (loss, loss ground truth, terms) and its FD-checked analytic gradient
     (oracle kmv_mlp_grad_analytic), on both implementations: impl 2 / auto = the narrow-net pair kernels
     (pairs built in registers, MFMA weight gradients; odd widths / dims zero-padded; n not a multiple of
     the 64-pair tile), impl 1 = pair rows through rocBLAS (chunk = 300 forces partial i-blocks and
-    j-chunking). (2, 130, ..., 20, 8) is the reference's default net (MLP.yaml: width 20, 8 layers).
+    j-chunking). (2, 130, ..., 20, 8) is the reference's default net (MLP.yaml: width 20, 8 layers);
+    n = 530 spans two of pass 2's 512-reference work units (a partial second one).
     Tolerance 2e-4 relative (fp32)."""
     from example_problems.kinetic_mckean_vlasov_example_quadratic import KineticMcKeanVlasov
     from methods.consistency_instances import kinetic_mckean_vlasov as kmv
