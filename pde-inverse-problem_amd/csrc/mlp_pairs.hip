@@ -276,6 +276,7 @@ __global__ __launch_bounds__(kWavesPB * kWave) void kmvp_gbar_kernel(Args a) {
 // Work units of pass 2: (item, block of kJB references) — finer than whole items, so the persistent
 // grid's waves get equal shares (5 000 items over 2 048 waves left 2 or 3 items of 79 tiles per wave).
 constexpr int kJB = 512;
+constexpr int kRC = 4;  // checkpoint features loaded together in the reverse sweep
 
 // LSLAB: the wave's weight-gradient slab lives in LDS for the whole kernel (every tile folds its 36
 // outer-product tiles there with ds_* read-modify-writes) and is copied to the wave's global slab row
@@ -546,17 +547,31 @@ __global__ __launch_bounds__(kWavesPB * kWave) void kmvp_grad_kernel(Args a) {
       // ---- reverse sweep over the hidden layers (z-bars computed in place of the h-bars) ----
       for (int l = L - 1; l >= 0; --l) {
         float ze[W];
+        // the layer's five checkpoint rows in chunks of kRC features: 5 kRC loads in flight per wait
+        // (one wait per feature left every load's HBM latency exposed at one wave per SIMD)
+        static_assert(W % kRC == 0, "ring chunk");
 #pragma unroll
-        for (int k = 0; k < W; ++k) {
+        for (int k0 = 0; k0 < W; k0 += kRC) {
           __builtin_amdgcn_sched_barrier(0);
-          const float hn = *ring.at(l, 0, k), zd = *ring.at(l, 1, k), zdd = *ring.at(l, 2, k);
-          const float al = *ring.at(l, 3, k), zbar = *ring.at(l, 4, k);
-          const float s1 = 1.f - hn * hn, s2 = -2.f * hn * s1, s3 = -2.f * s1 * s1 - 2.f * hn * s2;
-          const float b0 = hb[0][k], b1 = hb[1][k], b2 = hb[2][k];
-          hb[0][k] = s1 * b0 + s2 * zd * b1 + fmaf(s2, zdd, s3 * zd * zd) * b2 + s2 * al * zbar;
-          hb[1][k] = s1 * b1 + 2.f * s2 * zd * b2;
-          hb[2][k] = s1 * b2;
-          ze[k] = s1 * al;
+          float hn[kRC], zd[kRC], zdd[kRC], al[kRC], zbar[kRC];
+#pragma unroll
+          for (int c = 0; c < kRC; ++c) {
+            hn[c] = *ring.at(l, 0, k0 + c);
+            zd[c] = *ring.at(l, 1, k0 + c);
+            zdd[c] = *ring.at(l, 2, k0 + c);
+            al[c] = *ring.at(l, 3, k0 + c);
+            zbar[c] = *ring.at(l, 4, k0 + c);
+          }
+#pragma unroll
+          for (int c = 0; c < kRC; ++c) {
+            const int k = k0 + c;
+            const float s1 = 1.f - hn[c] * hn[c], s2 = -2.f * hn[c] * s1, s3 = -2.f * s1 * s1 - 2.f * hn[c] * s2;
+            const float b0 = hb[0][k], b1 = hb[1][k], b2 = hb[2][k];
+            hb[0][k] = s1 * b0 + s2 * zd[c] * b1 + fmaf(s2, zdd[c], s3 * zd[c] * zd[c]) * b2 + s2 * al[c] * zbar[c];
+            hb[1][k] = s1 * b1 + 2.f * s2 * zd[c] * b2;
+            hb[2][k] = s1 * b2;
+            ze[k] = s1 * al[c];
+          }
         }
         // gK_l += [h, h', h'', abar]_{l-1}^T [zb, z'b, z''b, zeta]_l ; gb_l += zb (const-1 feature)
         auto outer = [&](auto tyc) {
