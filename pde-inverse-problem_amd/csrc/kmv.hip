@@ -7,15 +7,24 @@
 // stamp's moments, so the O(n^2) tensor becomes two streaming passes (moments, weights)
 // plus an O(n_time d^3) finalize — exact, not an approximation.
 #include <math.h>
+#include <stdlib.h>
 
 #include "common.h"
 
 namespace pdeinv {
 
-constexpr int kBatchedGridTarget = 2048;
+constexpr int kBatchedGridTarget = 3072;  // C4 KMV pass: 2.88 ms at 2048, 2.79 at 2304, 2.785 at 3072 (A/B on one box)
+
+static int64_t grid_target() {
+  static const int64_t t = [] {
+    const char* e = getenv("PDEINV_KMV_GRID");  // A/B experiments (tools)
+    return e ? (int64_t)atol(e) : (int64_t)kBatchedGridTarget;
+  }();
+  return t;
+}
 
 static int batched_bx(int64_t n_sets, int64_t n_rows) {
-  int64_t bx = (kBatchedGridTarget + n_sets - 1) / (n_sets > 0 ? n_sets : 1);
+  int64_t bx = (grid_target() + n_sets - 1) / (n_sets > 0 ? n_sets : 1);
   const int64_t need = (n_rows + kBlock - 1) / kBlock;
   if (bx > need) bx = need;
   if (bx < 1) bx = 1;
