@@ -232,7 +232,7 @@ def run_c2(a, rank, world, dev):
         out["drift_recovery"] = ("max |S - tilde_F|, S = K + K^T the exact residual minimiser from the EM moments, "
                                  "Richardson (8 S(n=400) - 6 S(n=200) + S(n=100)) / 3, "
                                  f"{passes * world * N} trajectories per level")
-    if rank == 0 and not a.no_cpu_baseline:
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:  # the CPU baseline: rank 0 at N = 1 only
         from oracle import cpu_baseline as cb
         ups1, secs1 = cb.single(F, d, n, T, gamma, a.cpu_particles)
         P = max(1, min(a.cpu_procs, os.cpu_count() or 1))
