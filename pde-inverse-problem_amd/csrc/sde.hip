@@ -11,6 +11,7 @@
 // terminal = last) that the parametric-quadratic residual needs, so the KFP residual
 // (kinetic_fokker_planck.py:33-58) costs no second pass over the trajectory.
 #include <math.h>
+#include <stddef.h>
 #include <stdlib.h>
 
 #include "common.h"
@@ -63,14 +64,36 @@ __device__ __forceinline__ void gen_normals(const SdeArgs& a, uint32_t plo, uint
 
 // grad U(q) = A (q - c) = A q - b, b = A c packed on the host (KOU: A = tilde_F, c = 0,
 // …_OU.py:130-138): the FMA chain starts at -b, so a centre costs no per-step instruction.
+typedef const __attribute__((address_space(4))) float kfloat;
+typedef const __attribute__((address_space(4))) char kchar;
+// SdeArgs::params in the kernel-argument segment (sde_simulate_kernel's first argument, offset 0), made
+// opaque per use: held across the step loop, d^2 + d uniform floats beyond ~32 overflow the scalar
+// register file and the spills come back as v_readlane on every update (d = 8: 46-66 per update).
+__device__ __forceinline__ kfloat* kernarg_params() {
+  kfloat* p = (kfloat*)((kchar*)__builtin_amdgcn_kernarg_segment_ptr() + offsetof(SdeArgs, params));
+  asm volatile("" : "+s"(p));
+  return p;
+}
+
 template <int D>
 __device__ __forceinline__ void grad_quadratic(const SdeArgs& a, const float* q, float* g) {
+  if constexpr (D * D + D > 32) {
+    kfloat* P = kernarg_params();
 #pragma unroll
-  for (int r = 0; r < D; ++r) {
-    float acc = -a.params[D * D + r];
+    for (int r = 0; r < D; ++r) {
+      float acc = -P[D * D + r];
 #pragma unroll
-    for (int c = 0; c < D; ++c) acc = fmaf(a.params[r * D + c], q[c], acc);
-    g[r] = acc;
+      for (int c = 0; c < D; ++c) acc = fmaf(P[r * D + c], q[c], acc);
+      g[r] = acc;
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < D; ++r) {
+      float acc = -a.params[D * D + r];
+#pragma unroll
+      for (int c = 0; c < D; ++c) acc = fmaf(a.params[r * D + c], q[c], acc);
+      g[r] = acc;
+    }
   }
 }
 
@@ -101,8 +124,12 @@ struct GmmCentres {
 // McKean–Vlasov drift with the mean path precomputed: grad U(q) = A (q - xbar_s), the same
 // operation order as the per-update exchange (mf_step_kernel) and the C oracle (y = q - xbar, then
 // A y). xbar_s is wave-uniform (scalar loads from a small device array, one row per update).
+// A is read from the kernel-argument segment with scalar loads at every update (kernarg_params): held
+// across the step loop, its d^2 SGPRs (64 at d = 8) overflowed the scalar file and the spills came back
+// as 46 v_readlane per update (C4 step loop 208 -> 162 VALU instructions per update).
 template <int D>
-__device__ __forceinline__ void grad_meanfield(const SdeArgs& a, const float* q, const float* xb, float* g) {
+__device__ __forceinline__ void grad_meanfield(const SdeArgs&, const float* q, const float* xb, float* g) {
+  kfloat* A = kernarg_params();
   float y[D];
 #pragma unroll
   for (int c = 0; c < D; ++c) y[c] = q[c] - xb[c];
@@ -110,7 +137,7 @@ __device__ __forceinline__ void grad_meanfield(const SdeArgs& a, const float* q,
   for (int r = 0; r < D; ++r) {
     float acc = 0.f;
 #pragma unroll
-    for (int c = 0; c < D; ++c) acc = fmaf(a.params[r * D + c], y[c], acc);
+    for (int c = 0; c < D; ++c) acc = fmaf(A[r * D + c], y[c], acc);
     g[r] = acc;
   }
 }
