@@ -24,6 +24,7 @@
 // Widths / dims between the compiled ones are zero-padded on the device (exact: padded units carry
 // z = 0, h = tanh 0 = 0 and zero outgoing weights).
 #include <math.h>
+#include <stdlib.h>
 
 #include <type_traits>
 
@@ -669,6 +670,15 @@ __global__ void kmvp_reduce_kernel(MlpPadMap pm, const float* __restrict__ gslab
 namespace {
 constexpr int kPairWaves = 2048;  // persistent grid: 2 waves per SIMD of 256 CUs
 
+int pair_waves() {
+  static const int w = [] {
+    const char* e = getenv("PDEINV_PAIR_WAVES");  // A/B experiments (tools)
+    const int v = e ? atoi(e) : kPairWaves;
+    return v >= 2 ? v & ~1 : kPairWaves;
+  }();
+  return w;
+}
+
 int pad_dim(int d) { return d <= 2 ? 2 : (d <= 4 ? 4 : 8); }
 int pad_width(int w) { return w <= 8 ? 8 : (w <= 16 ? 16 : (w <= 20 ? 20 : (w <= 24 ? 24 : 28))); }
 
@@ -698,7 +708,7 @@ PairPlan pair_plan(const pdeinv_kmv_mlp_desc* d) {
   }
   p.P = po;
   p.items = (int64_t)d->n_sets * d->n_rows;
-  p.n_waves = p.items < kPairWaves ? ((p.items + 1) / 2) * 2 : kPairWaves;
+  p.n_waves = p.items < pair_waves() ? ((p.items + 1) / 2) * 2 : pair_waves();
   size_t o = 0;
   auto take = [&](size_t bytes) { const size_t at = o; o += (bytes + 255) & ~(size_t)255; return at; };
   p.off_prm = take(sizeof(float) * p.P);
