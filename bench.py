@@ -60,6 +60,8 @@ def parse():
     p.add_argument("--recovery-passes", type=int, default=128,
                    help="ensembles per discretisation for the (untimed) drift recovery")
     p.add_argument("--cpu-particles", type=int, default=1 << 20)
+    p.add_argument("--chunk-rows", type=int, default=1 << 21,
+                   help="C5: MLP-residual rows per chunk (2^19 / 2^20 / 2^21: 114.5 / 113.7 / 113.4 ms; 7 / 14 / 28 GB workspace)")
     p.add_argument("--cpu-procs", type=int, default=16, help="CPU-baseline shard processes (the box's CPU share)")
     return p.parse_args()
 
@@ -437,7 +439,7 @@ def run_c5(a, rank, world, dev):
             sim_ev.append((e0, record[0]))
         acc, grad = native.residual_kfp_mlp(dims, flat, z0[:nb], r["last"][:nb], z0T, true_kind=native.POT_GMM,
                                             true_params=mus, gamma=gamma, total_time=T, world_scale=1.0 / world,
-                                            chunk_rows=1 << 19)
+                                            chunk_rows=a.chunk_rows)
         if record is not None:
             record[1].record()
         both = dist.allreduce_sum(torch.cat([acc, grad.double()]))
