@@ -260,6 +260,7 @@ struct GmmResFused {
   float c_nabla, c_hess, c_fric, c_true, c_init, c_term, inv_ni, inv_nt;
 };
 
+// SdeArgs must stay the FIRST parameter: kernarg_params() reads a.params at kernarg offset 0.
 template <int D, int POT, bool MOM, int STORE, int KM = 1, bool NOISE = false, int MINW = 1, bool RES = false>
 __global__ __launch_bounds__(kBlock, MINW) void sde_simulate_kernel(SdeArgs a, const float* __restrict__ z0,
                                                               float* __restrict__ traj,
