@@ -45,6 +45,24 @@ from utils import native  # noqa: E402
 
 METRIC = "particle-steps/sec + achieved HBM GB/s; recovered-drift L2 error"
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: dense fp32 (vector v_fma_f32 and MFMA alike)
+
+
+def gmm_sim_flops(d, K):
+    """Algorithmic fp32 FLOP of one particle-update of the GMM-potential simulator (FMA = 2):
+    logits x.mu_k + c_k (2K(d+1)), softmax shift / sum / normalise (3K), mixture mean (2Kd),
+    grad U = (x - mbar)/s^2 (2d), semi-implicit EM update of v and x (8d). Transcendentals
+    (K exp2, Box-Muller) and the Philox integer work are not counted."""
+    return 2 * K * (d + 1) + 3 * K + 2 * K * d + 2 * d + 8 * d
+
+
+def gmm_residual_flops(d, K):
+    """Algorithmic fp32 FLOP of one sample of the KFP-GMM residual value_and_grad (common.h
+    gmm_residual_sample): softmax + mixture mean as above (2K(d+1) + 3K + 2Kd), e and g (2d), the dots
+    e.e, e.v, v.v (6d), p_k = mu_k.v and em_k = e.mu_k (4Kd), pbar / sum w p^2 (4K), T terms (10),
+    F_k (6K), Fbar (2K), cw / ce / cv (7K), sum cw (K), the mu-adjoint sum cw x + ce e + cv v (6Kd)."""
+    return 2 * K * (d + 1) + 3 * K + 2 * K * d + 2 * d + 6 * d + 4 * K * d + 4 * K + 10 + 6 * K + 2 * K + 7 * K + K \
+        + 6 * K * d
 
 
 def parse():
@@ -62,7 +80,8 @@ def parse():
     p.add_argument("--cpu-particles", type=int, default=1 << 20)
     p.add_argument("--chunk-rows", type=int, default=1 << 21,
                    help="C5: MLP-residual rows per chunk (2^19 / 2^20 / 2^21: 114.5 / 113.7 / 113.4 ms; 7 / 14 / 28 GB workspace)")
-    p.add_argument("--cpu-procs", type=int, default=16, help="CPU-baseline shard processes (the box's CPU share)")
+    p.add_argument("--cpu-procs", type=int, default=0,
+                   help="CPU-baseline shard processes (0 = the per-GPU host share, os.cpu_count() // 8)")
     return p.parse_args()
 
 
@@ -135,17 +154,27 @@ def traffic_from_profiles(key):
         return None
 
 
-def base_record(a, world, value, ms, config, kern_ms, bytes_launch, kernel, traffic=None):
+def base_record(a, world, value, ms, config, kern_ms, bytes_launch, kernel, traffic=None, flops_launch=None):
+    """roofline: HBM-bound launches (the simulators) report algorithmic bytes / launch time against the
+    HBM peak; a VALU-bound launch (flops_launch given: C3's simulator with the fused GMM residual) reports
+    its algorithmic fp32 FLOP / launch time against the fp32 vector peak, the HBM figure kept beside it."""
     achieved = bytes_launch / (kern_ms / 1e3) / 1e9
+    if flops_launch is not None:
+        tf = flops_launch / (kern_ms / 1e3) / 1e12
+        roof = {"bound": "valu", "achieved": tf, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": tf / FP32_PEAK_TFLOPS, "traffic": traffic, "kernel": kernel, "kernel_ms": kern_ms,
+                "algorithmic_flops_per_launch": flops_launch, "algorithmic_bytes_per_launch": bytes_launch,
+                "hbm": {"achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS}}
+    else:
+        roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic, "kernel": kernel,
+                "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": bytes_launch}
     return {
         "metric": METRIC, "value": value, "unit": "particle-steps/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f32",
         "data": "synthetic: Philox Gaussian-init ensembles, fresh noise per step",
-        "config": config, "hbm_GBps": achieved,
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic, "kernel": kernel,
-                     "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": bytes_launch},
+        "config": config, "hbm_GBps": achieved, "roofline": roof,
     }
 
 
@@ -236,18 +265,26 @@ def run_c2(a, rank, world, dev):
                                  f"{passes * world * N} trajectories per level")
     if rank == 0 and world == 1 and not a.no_cpu_baseline:  # the CPU baseline: rank 0 at N = 1 only
         from oracle import cpu_baseline as cb
+        from example_problems.kinetic_fokker_planck_example_OU import problem_matrix as pm
         ups1, secs1 = cb.single(F, d, n, T, gamma, a.cpu_particles)
-        P = max(1, min(a.cpu_procs, os.cpu_count() or 1))
+        # the per-GPU share of the host: an 8-GPU node's cores / 8 (P = cores)
+        P = a.cpu_procs or max(1, (os.cpu_count() or 8) // 8)
+        P = max(1, min(P, os.cpu_count() or 1))
         n_per = max(1, a.cpu_particles // 4)
         upsP, secsP = cb.multi(F, d, n, T, gamma, n_per, P)
+        # C1 (BASELINE configs[0], scripts/run_KOU.sh): KOU d = 2, 4 096 particles, 100 steps, in full
+        ups_c1, secs_c1 = cb.single(pm(2), 2, n, T, gamma, 4096)
         what = (f"NumPy restatement of sampling_utils.py (oracle/cpu_baseline.py: update_step + moment pass), fp32, "
                 f"d={d}, {n + 1} updates")
         host = f"host {cpu_model()}, os.cpu_count()={os.cpu_count()}"
         out["cpu_baseline"] = {"value": upsP, "unit": "particle-steps/s", "cores": P, "kind": "port",
-                               "sample": f"{what}; {P} processes x {n_per} particles started together, "
-                                         f"{secsP:.1f} s wall; {host}"}
+                               "sample": f"{what}; {P} processes (os.cpu_count() // 8, the per-GPU host share) x "
+                                         f"{n_per} particles started together, {secsP:.1f} s wall; {host}"}
         out["cpu_baseline_1core"] = {"value": ups1, "unit": "particle-steps/s", "cores": 1, "kind": "port",
                                      "sample": f"{what}; one process, {a.cpu_particles} particles, {secs1:.1f} s"}
+        out["cpu_baseline_c1"] = {"value": ups_c1, "unit": "particle-steps/s", "cores": 1, "kind": "port",
+                                  "sample": f"C1 in full: KOU d=2, 4096 particles x {n + 1} updates (+ moment pass), "
+                                            f"one process, {secs_c1 * 1e3:.1f} ms"}
         out["gpu_over_cpu"] = value / upsP
     return out
 
@@ -292,9 +329,13 @@ def run_c3(a, rank, world, dev):
                        "residual value_and_grad over init/0T/terminal fused into the same launch",
            "dim": d, "n_centers": K, "n_steps": n, "particles_per_gpu": N, "total_time": T, "gamma": gamma,
            "parallelism": f"dp{world}"}
+    # VALU-bound: every particle-update runs the GMM simulator step and one residual sample (its 0T row;
+    # z0 / last add one sample per particle each)
+    flops = N * ((n + 1) * gmm_sim_flops(d, K) + (n + 2) * gmm_residual_flops(d, K))
     out = base_record(a, world, value, ms, cfg, kern_ms, sim_bytes(N, n, d),
                       "sde_simulate_kernel<4,GMM,staged,KM=8,fused KFP-GMM residual> (+ its slab reduce)",
-                      traffic_from_profiles("sde_simulate_C3_bytes_per_launch") if (N, n) == (1 << 22, 100) else None)
+                      traffic_from_profiles("sde_simulate_C3_bytes_per_launch") if (N, n) == (1 << 22, 100) else None,
+                      flops_launch=flops)
     out["loss"] = float(last_out[0][0][0].item())
 
     # untimed context: the same simulator without the residual, and the standalone residual kernel

@@ -141,7 +141,9 @@ int pdeinv_mf_step(const pdeinv_sde_desc* desc, int32_t s, const float* d_z, flo
  *                    [count, sum x0 (d), sum v0 (d), sum_i xi_{i,s} (d) for s = 0..n_steps]
  *                    over this call's particles (rank-local; all-reduce(sum) it across ranks);
  *   pdeinv_mf_mean_path: the all-reduced sums -> d_xbar [n_steps+1, d] fp32 (mean before update s)
- *                    and optionally d_xsum [n_steps+2, 1+d] fp64 = [count, count * xbar_s];
+ *                    and optionally d_xsum [n_steps+2, 1+d] fp64 = [count, count * xbar_s]
+ *                    (the closed-form path, a model quantity — not sums measured from the simulated
+ *                    fp32 states; take pdeinv_moments of the trajectory for those);
  *   pdeinv_sde_simulate(desc with d_meanfield = d_xbar): all n_steps+1 updates in registers.
  * The explicit-noise mode (d_noise) is honoured by pdeinv_mf_sums and the simulator alike. */
 int64_t pdeinv_mf_sums_len(const pdeinv_sde_desc* desc);

@@ -128,5 +128,59 @@ def main():
         print(f, os.path.getsize(os.path.join(OUT, f)))
 
 
+def kmv_mlp_large():
+    """General-Phi KMV (V_hypothesis interaction, the reference's default 20 x 8 net) at a size where the
+    pair kernels' persistent pass-1 grid (2 048 waves over n * n_time items, mlp_pairs.hip) iterates:
+    d = 2, n = 1 400 particles x 3 stamps = 4 200 items. The literal pair tensor (5.9 M pairs) is built
+    250 references at a time; loss terms and the analytic gradient (kmv_mlp_pairwise_loss /
+    kmv_mlp_grad_analytic, the same formulas) are sums over references, so the chunked evaluation is
+    exact. Writes tests/golden/kmv_mlp_pairs_1400.npz only (its own seed; the other fixtures untouched)."""
+    rng = np.random.default_rng(1400)
+    d, n, nt, W, L = 2, 1400, 3, 20, 8
+    F = nr.problem_constants(d)
+    cfg = nr.ou_configuration(F, gamma=1.0)
+    x = rng.standard_normal((n, nt, d)).astype(np.float32).astype(np.float64)
+    v = rng.standard_normal((n, nt, d)).astype(np.float32).astype(np.float64)
+    tau = np.array([0.3, 0.9, 1.6])
+    dims = [d] + [W] * L + [1]
+    flat = np.concatenate([np.concatenate([(rng.standard_normal((i, o)) / np.sqrt(i)).ravel(),
+                                           0.1 * rng.standard_normal(o)]) for i, o in zip(dims[:-1], dims[1:])])
+    flat = flat.astype(np.float32).astype(np.float64)
+    P = nr.mlp_unflat(flat, dims)
+    c = nr.kmv_value_weights(x, tau, cfg)
+    CH = 250
+    sg = np.zeros((n, nt, d)); sgt = np.zeros((n, nt, d)); sphi = np.zeros((n, nt)); shvv = np.zeros((n, nt))
+    for a0 in range(0, n, CH):
+        y = x[None] - x[a0:a0 + CH, None]                        # [a, b, T, d] = x_b - x_a
+        vv = np.broadcast_to(v[None], y.shape)
+        Phi, g, _, Hvv = nr.mlp_forward_terms(P, y.reshape(-1, d), vv.reshape(-1, d))
+        m = y.shape[0]
+        sphi += Phi.reshape(m, n, nt).sum(0); shvv += Hvv.reshape(m, n, nt).sum(0)
+        sg += g.reshape(m, n, nt, d).sum(0); sgt += (y @ F.T).sum(0)
+    gbar, gtrue = sg / n, sgt / n
+    parts = dict(nabla=np.mean(np.sum(gbar ** 2, -1)), hessian=np.mean(shvv / n), value=np.mean(sphi / n * c),
+                 nabla_true=np.mean(np.sum(gtrue ** 2, -1)))
+    loss = parts["nabla"] - 2 * parts["hessian"] + 2 * parts["value"] + parts["nabla_true"]
+    loss_gt = np.mean(np.sum((gtrue - gbar) ** 2, -1))
+    s = 1.0 / (n * n * nt)
+    grad = np.zeros_like(flat)
+    for a0 in range(0, n, CH):
+        y = x[None] - x[a0:a0 + CH, None]
+        m = y.shape[0]
+        rows = np.concatenate([y.reshape(-1, d), np.broadcast_to(v[None], y.shape).reshape(-1, d)], 1)
+        C = np.zeros((rows.shape[0], 4))
+        C[:, 1] = -2 * s
+        C[:, 3] = (2 * s * np.broadcast_to(c[None], (m, n, nt))).reshape(-1)
+        U = (2 * s * np.broadcast_to(gbar[None], y.shape)).reshape(-1, d)
+        grad += nr.mlp_flat(nr.mlp_grad_rows(P, rows, C, U))
+    np.savez_compressed(os.path.join(OUT, "kmv_mlp_pairs_1400.npz"), x=x.astype(np.float32), v=v.astype(np.float32),
+                        tau=tau, F=F, dims=np.asarray(dims), flat=flat.astype(np.float32), loss=loss, loss_gt=loss_gt,
+                        hessian=parts["hessian"], nabla=parts["nabla"], value=parts["value"], grad=grad)
+    print("kmv_mlp_pairs_1400.npz", os.path.getsize(os.path.join(OUT, "kmv_mlp_pairs_1400.npz")))
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "kmv_mlp_large":
+        kmv_mlp_large()
+    else:
+        main()

@@ -44,6 +44,13 @@ namespace mlpf {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int BK = 32;   // feature k-step of the row GEMMs
+// Row-GEMM LDS tiles are k-major with a row pitch of BM + 1 (A) / BN + 1 (B) floats. ds_write_b32
+// banks are (addr/4) mod 32 per 32-lane half: the transposing stores (A from row-major planes, B_NT
+// from row-major weights) put 32 consecutive k of one row in a half, i.e. a stride of one pitch;
+// a pitch = 1 (mod 32) maps them to 32 distinct banks (the old + 4 pitch made them 4-way
+// conflicts: SQ_LDS_BANK_CONFLICT > SQ_ACTIVE_INST_LDS in profiles/r02_c5_pmc_sq_v2.txt). The
+// MFMA operand reads (32 consecutive floats of one k row per half) are conflict-free at any pitch.
+constexpr int kPitchPad = 1;
 constexpr int BKG = 16;  // rows per weight-gradient step (4 pairs staged together)
 constexpr int kT = 256;
 
@@ -150,7 +157,7 @@ __device__ __forceinline__ void load_a(const GemmArgs& a, ARegs<BM, AM>& ra, int
 template <int S, int BM, int AM>
 __device__ __forceinline__ void store_a(const GemmArgs& a, const ARegs<BM, AM>& ra, float* As, int r0, int k0,
                                         bool full) {
-  constexpr int LDA = BM + 4;
+  constexpr int LDA = BM + kPitchPad;
 #pragma unroll
   for (int j = 0; j < ARegs<BM, AM>::NE; ++j) {
     const int e = threadIdx.x + j * kT;
@@ -208,7 +215,7 @@ __device__ __forceinline__ void load_b(const GemmArgs& a, float (&rb)[BK * BN / 
 template <int BN, int BMD>
 __device__ __forceinline__ void store_b(const GemmArgs& a, const float (&rb)[BK * BN / kT], float* Bs, int k0, int n0,
                                         bool full) {
-  constexpr int LDB = BN + 4;
+  constexpr int LDB = BN + kPitchPad;
 #pragma unroll
   for (int j = 0; j < BK * BN / kT; ++j) {
     int kk, nn;
@@ -226,7 +233,7 @@ __global__ __launch_bounds__(kT, 2) void fgemm(GemmArgs a) {
   constexpr int WM = BM / WGM, WN = BN / WGN, MI = WM / 32, NI = WN / 32;
   static_assert(MI >= 1 && NI >= 1 && MI * 32 == WM && NI * 32 == WN, "wave tile must be 32-multiples");
   static_assert(EM != E_OUT || WGN == 1, "E_OUT reduces each row inside one wave");
-  constexpr int LDA = BM + 4, LDB = BN + 4;
+  constexpr int LDA = BM + kPitchPad, LDB = BN + kPitchPad;
   constexpr int NP = (EM == E_SEEDS || EM == E_ACT_BWD) ? 1 : 0;
   extern __shared__ float lds[];
   float* As = lds;                  // [S][BK][LDA]
@@ -794,7 +801,7 @@ static int sum_slabs(const float* part, int S, int64_t n, float* out, float* scr
 template <int S, int BM, int BN, int WGM, int AM, int BMD, int EM, int D = 0>
 static int launch_gemm(GemmArgs a, hipStream_t st, int* grid_x_out = nullptr) {
   const size_t k1f = a_is_l1<AM>() ? (size_t)a.K * k1_stride<D>() : 0;
-  const size_t bytes = ((size_t)S * BK * (BM + 4) + (size_t)BK * (BN + 4) + k1f) * sizeof(float);
+  const size_t bytes = ((size_t)S * BK * (BM + kPitchPad) + (size_t)BK * (BN + kPitchPad) + k1f) * sizeof(float);
   auto kern = fgemm<S, BM, BN, WGM, AM, BMD, EM, D>;
   if (bytes > 64 * 1024)
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);

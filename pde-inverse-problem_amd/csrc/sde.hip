@@ -14,6 +14,8 @@
 #include <stddef.h>
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "common.h"
 
 namespace pdeinv {
@@ -431,6 +433,23 @@ __global__ __launch_bounds__(kBlock, MINW) void sde_simulate_kernel(SdeArgs a, c
     block_reduce_to_slab(term.v, L, lds, partials + (int64_t)2 * L * nb, bid, nb);
   }
 }
+
+// Compile-time guard of the kernarg_params() invariant: the kernel's first parameter is SdeArgs (so its
+// params field sits at kernarg offset offsetof(SdeArgs, params)), checked on a quadratic and a mean-field
+// instantiation; the struct must be standard-layout for offsetof to be that offset.
+template <typename F>
+struct first_param;
+template <typename R, typename A0, typename... As>
+struct first_param<R (*)(A0, As...)> {
+  using type = A0;
+};
+static_assert(std::is_standard_layout<SdeArgs>::value, "kernarg_params(): SdeArgs must be standard-layout");
+static_assert(std::is_same<first_param<decltype(&sde_simulate_kernel<4, PDEINV_POT_QUADRATIC, false, 2>)>::type,
+                           SdeArgs>::value &&
+                  std::is_same<first_param<decltype(&sde_simulate_kernel<8, PDEINV_POT_MEANFIELD_QUADRATIC, false, 2>)>::type,
+                               SdeArgs>::value,
+              "kernarg_params() reads SdeArgs::params at its kernarg offset: SdeArgs must stay the first parameter "
+              "of sde_simulate_kernel");
 
 // ---- McKean–Vlasov single update ---------------------------------------------------------
 // grad U(q_i) = A (q_i - xbar) with xbar = (sum x)/count of the ensemble BEFORE this update

@@ -21,7 +21,7 @@ import numpy as np
 import torch
 
 from core.model import get_model
-from methods.consistency_instances.kinetic_fokker_planck import resolve_model
+from methods.consistency_instances.kinetic_fokker_planck import grad_norm64, resolve_model, set_dp_grad_norm
 from utils import distributed as dist
 from utils import native, prng
 
@@ -36,11 +36,14 @@ def value_and_grad_fn(forward_fn, params, data, rng, pde_instance):
     T = float(pde_instance.total_evolving_time)
     acc, grad = native.residual_fp_mlp(model.dims(d), model.flat(params), data["initial"], data["terminal"],
                                        data["0T"], tilde_F=F, total_time=T, world_scale=1.0 / dist.world_size())
-    if dist.world_size() > 1:  # the pmap mean (trainer.py:52); per-set boundary means are not pre-scaled
-        both = dist.allreduce_sum(torch.cat([acc, grad.double()]))
-        acc, grad = both[: acc.numel()], both[acc.numel():].float()
-        acc[native.GMM_NACC - 2:native.GMM_NACC] /= dist.world_size()
+    W = dist.world_size()
+    if W > 1:  # the pmap mean (trainer.py:52); per-set boundary means are not pre-scaled
+        both = dist.allreduce_sum(torch.cat([acc, grad.double(), grad_norm64(grad, W)]))
+        acc, grad, gn = both[: acc.numel()], both[acc.numel():-1].float(), both[-1:] / W
+        acc[native.GMM_NACC - 2:native.GMM_NACC] /= W
     out = native.kfp_terms_finalize(acc, grad, 0.0)
+    if W > 1:
+        set_dp_grad_norm(out, gn)  # the mean over ranks of per-rank norms (trainer.py:44-53)
     return {"loss": out[native.KFP_SLOTS.index("loss")], "grad": model.unflat(grad, d),
             "grad_norm": out[native.KFP_SLOTS.index("grad_norm")],
             "loss ground truth": out[native.KFP_SLOTS.index("loss ground truth")]}

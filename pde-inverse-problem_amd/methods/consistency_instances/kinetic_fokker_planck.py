@@ -32,6 +32,19 @@ def resolve_model(forward_fn):
     return model
 
 
+def grad_norm64(grad: torch.Tensor, scale: float = 1.0) -> torch.Tensor:
+    """[1] fp64: scale * ||grad|| (compute_pytree_norm of one rank's gradient)."""
+    return (torch.linalg.vector_norm(grad.double()) * scale).reshape(1)
+
+
+def set_dp_grad_norm(out: torch.Tensor, gn: torch.Tensor) -> torch.Tensor:
+    """Data-parallel grad_norm as the reference reports it: under pmap every device returns the norm of
+    ITS OWN gradient and trainer.py:44-53 averages all outputs over devices, so grad_norm is the mean
+    over ranks of per-rank norms (not the norm of the mean gradient). gn: that mean, all-reduced."""
+    out[native.KFP_SLOTS.index("grad_norm")] = gn.to(out.dtype)
+    return out
+
+
 def _result(out: torch.Tensor, grad_tree) -> dict:
     return {"loss": out[native.KFP_SLOTS.index("loss")], "grad": grad_tree,
             "grad_norm": out[native.KFP_SLOTS.index("grad_norm")],
@@ -54,8 +67,18 @@ def value_and_grad_fn(forward_fn, params, data, rng, pde_instance):
     if model.residual_kind == "quadratic":
         if "tilde_F" not in ic:
             raise NotImplementedError("quadratic model needs a quadratic true potential (tilde_F)")
-        mom = dist.allreduce_sum(kfp_moments(data).contiguous())
-        out, grad = native.residual_kfp_quadratic(mom, model.flat(params), ic["tilde_F"], gamma, T)
+        theta = model.flat(params)
+        mom = kfp_moments(data).contiguous()
+        W = dist.world_size()
+        if W > 1:  # this rank's own gradient norm rides on the moment all-reduce
+            _, g_loc = native.residual_kfp_quadratic(mom, theta, ic["tilde_F"], gamma, T)
+            both = dist.allreduce_sum(torch.cat([mom.reshape(-1), grad_norm64(g_loc)]))
+            mom, gn = both[:-1].view_as(mom), both[-1:] / W
+        else:
+            mom = dist.allreduce_sum(mom)
+        out, grad = native.residual_kfp_quadratic(mom, theta, ic["tilde_F"], gamma, T)
+        if W > 1:
+            set_dp_grad_norm(out, gn)
         return _result(out, model.unflat(grad))
     if model.residual_kind == "gmm":
         mus_true = pde_instance.potential.mus
@@ -64,10 +87,22 @@ def value_and_grad_fn(forward_fn, params, data, rng, pde_instance):
                                    sigma=model.sigma, sigma_true=pde_instance.potential.sigma,
                                    world_scale=1.0 / dist.world_size())
         acc = native.residual_kfp_gmm(desc, data["initial"], data["terminal"], data["0T"], params["params"]["mus"])
-        acc = dist.allreduce_sum(acc)
-        if dist.world_size() > 1:  # the per-set means of the boundary terms are not pre-scaled
-            acc[native.GMM_NACC - 2:native.GMM_NACC] /= dist.world_size()
+        W = dist.world_size()
+        if W > 1:
+            # this rank's own finalize (its sums un-scaled, a world_scale = 1 descriptor) for its grad norm
+            loc = acc.clone()
+            loc[: native.GMM_NACC - 2] *= W
+            desc1 = native.kfp_gmm_desc(model.dim, model.n_Gaussians, mus_true, gamma, T, n_i, n_t, n_0,
+                                        sigma=model.sigma, sigma_true=pde_instance.potential.sigma, world_scale=1.0)
+            _, g_loc = native.residual_kfp_gmm_finalize(desc1, loc)
+            both = dist.allreduce_sum(torch.cat([acc, grad_norm64(g_loc)]))
+            acc, gn = both[:-1], both[-1:] / W
+            acc[native.GMM_NACC - 2:native.GMM_NACC] /= W  # the per-set means of the boundary terms are not pre-scaled
+        else:
+            acc = dist.allreduce_sum(acc)
         out, grad = native.residual_kfp_gmm_finalize(desc, acc)
+        if W > 1:
+            set_dp_grad_norm(out, gn)
         return _result(out, {"params": {"mus": grad}})
     if model.residual_kind == "mlp":
         d = pde_instance.dim
@@ -78,11 +113,14 @@ def value_and_grad_fn(forward_fn, params, data, rng, pde_instance):
         acc, grad = native.residual_kfp_mlp(model.dims(d), model.flat(params), data["initial"], data["terminal"],
                                             data["0T"], true_kind=true_kind, true_params=true_params, gamma=gamma,
                                             total_time=T, sigma_true=sigma_true, world_scale=1.0 / dist.world_size())
-        if dist.world_size() > 1:
-            both = dist.allreduce_sum(torch.cat([acc, grad.double()]))
-            acc, grad = both[: acc.numel()], both[acc.numel():].float()
-            acc[native.GMM_NACC - 2:native.GMM_NACC] /= dist.world_size()
+        W = dist.world_size()
+        if W > 1:  # grad is pre-scaled by 1/W: this rank's own gradient is W * grad
+            both = dist.allreduce_sum(torch.cat([acc, grad.double(), grad_norm64(grad, W)]))
+            acc, grad, gn = both[: acc.numel()], both[acc.numel():-1].float(), both[-1:] / W
+            acc[native.GMM_NACC - 2:native.GMM_NACC] /= W
         out = native.kfp_terms_finalize(acc, grad, gamma)
+        if W > 1:
+            set_dp_grad_norm(out, gn)
         return _result(out, model.unflat(grad, d))
     raise NotImplementedError(f"no native KFP residual for model kind '{model.residual_kind}'")
 

@@ -23,7 +23,7 @@ import numpy as np
 import torch
 
 from core.model import get_model
-from methods.consistency_instances.kinetic_fokker_planck import _result, resolve_model
+from methods.consistency_instances.kinetic_fokker_planck import _result, grad_norm64, resolve_model, set_dp_grad_norm
 from utils import distributed as dist
 from utils import native, prng
 
@@ -57,10 +57,17 @@ def value_and_grad_fn(forward_fn, params, data, rng, pde_instance):
     theta = model.flat(params)
     F = pde_instance.initial_configuration["tilde_F"]
     if data.get("shared_time", False):
-        both = dist.allreduce_sum(torch.cat([mom.reshape(-1), wst.reshape(-1)]))
-        mom = both[: mom.numel()].view_as(mom)
-        wst = both[mom.numel():].view_as(wst)
+        W = dist.world_size()
+        parts = [mom.reshape(-1), wst.reshape(-1)]
+        if W > 1:  # this rank's own gradient norm (the pmap mean of per-device norms, trainer.py:44-53)
+            parts.append(grad_norm64(native.residual_kmv(mom, wst, theta, F, gamma)[1]))
+        both = dist.allreduce_sum(torch.cat(parts))
+        nm = mom.numel()
+        mom = both[:nm].view_as(mom)
+        wst = both[nm:nm + wst.numel()].view_as(wst)
         out, grad = native.residual_kmv(mom, wst, theta, F, gamma)
+        if W > 1:
+            set_dp_grad_norm(out, both[-1:] / W)
     else:
         out, grad = native.residual_kmv(mom, wst, theta, F, gamma)
         if dist.world_size() > 1:

@@ -39,6 +39,10 @@ def init_from_env(backend: str = None) -> bool:
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     if (ws <= 1 and not _forced()) or dist.is_initialized():
         return dist.is_initialized()
+    if ws <= 1 and not all(k in os.environ for k in ("MASTER_ADDR", "MASTER_PORT")):
+        raise RuntimeError("PDEINV_DIST_FORCE=1 forces the distributed path at world size 1, which needs the "
+                           "torch.distributed.run rendezvous (MASTER_ADDR / MASTER_PORT); launch under "
+                           "torch.distributed.run or unset PDEINV_DIST_FORCE")
     backend = os.environ.get("PDEINV_DIST_BACKEND", backend)  # test override (e.g. gloo on one GPU)
     if backend is None:
         backend = "nccl" if torch.cuda.is_available() else "gloo"

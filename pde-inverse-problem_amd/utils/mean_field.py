@@ -54,7 +54,13 @@ def simulate_mean_field(q0_p0: torch.Tensor, n_steps: int, dt: float, key: Key, 
                         tau: bool = True, exchange: str = "fused", out: Optional[dict] = None) -> dict:
     """Returns {"last" [N, 2d], "xsum" [n+2, 1+d] fp64 ([count, sum x] before each update and after the
     last, global over ranks), "traj" [n, N, 2d] time-major, "tau" [n, N]}. `out` may hold preallocated
-    "traj" / "tau" / "last" buffers (fused path)."""
+    "traj" / "tau" / "last" buffers (fused path).
+
+    exchange="per_update": xsum holds the MEASURED sums, recomputed from the fp32 states after every
+    update (one all-reduce each). exchange="fused" (default): xsum = count * the closed-form fp64 mean
+    path of DESIGN.md §4.3 (also returned as "xbar"), the model quantity the drift uses — equal to the
+    measured ensemble mean in exact arithmetic and to fp32 rounding in practice (tested to 1e-6), but not
+    a measurement; take moments of "traj" / "last" for the measured means."""
     N, m = q0_p0.shape
     d = m // 2
     dev = q0_p0.device

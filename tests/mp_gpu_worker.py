@@ -33,9 +33,56 @@ def mean_field(out_dir, exchange="fused", N=6000, n=30, d=8):
              xsum=r["xsum"].cpu().numpy(), off=off, world=world, backend=backend)
 
 
+def _flat_grad(g):
+    if torch.is_tensor(g):
+        return g.reshape(-1)
+    if isinstance(g, dict):
+        return torch.cat([_flat_grad(g[k]) for k in g])
+    return torch.cat([_flat_grad(t) for t in g])
+
+
+def dp_residual(out_dir, shards="0", B=(3000, 2000, 40000)):
+    """The KFP residual (quadratic, GMM and MLP models) on this rank's shard of one fixed dataset.
+    World 1 with shards = W > 0: every shard r of the W-way split evaluated on its own (the reference's
+    per-device values under pmap); under torch.distributed.run: this rank's shard through the
+    data-parallel path (all-reduce). Saves loss / grad_norm / grad per model kind (and per shard)."""
+    from core.model import GMMModel, QuadraticModel, V_hypothesis
+    from methods.consistency_instances import kinetic_fokker_planck as kfp
+    from registry import get_pde_instance
+    from utils import config, prng
+    from utils import distributed as dist
+    W = int(shards)
+    rank, world = dist.rank(), dist.world_size()
+    dev = torch.device("cuda", dist.local_device())
+    rng = np.random.default_rng(5)
+    d = 4
+    full = {k: rng.standard_normal((b, 2 * d)).astype(np.float32) * 1.3 for k, b in zip(("initial", "terminal", "0T"), B)}
+    runs = [(r, W) for r in range(W)] if W > 0 else [(rank, world)]
+    res = {}
+    for pot in ("Quadratic", "GMM"):
+        cfg = config.compose("config", ["pde_instance=kinetic_fokker_planck", f"pde_instance.potential={pot}",
+                                        f"pde_instance.domain_dim={d}"])
+        pi = get_pde_instance(cfg)(cfg=cfg, rng=prng.PRNGKey(1))
+        models = [("mlp", V_hypothesis(output_dim=1, hidden_dims=[32, 32]))]
+        models.append(("quadratic", QuadraticModel(d)) if pot == "Quadratic" else ("gmm", GMMModel(d, 3)))
+        for name, net in models:
+            params = net.init(prng.PRNGKey(11), np.zeros(d), device=dev)
+            for r, ws in runs:
+                data = {}
+                for k, a in full.items():
+                    n = a.shape[0] // ws
+                    data[k] = torch.as_tensor(a[r * n:(r + 1) * n], device=dev)
+                out = kfp.value_and_grad_fn(net.apply, params, data, None, pi)
+                key = f"{pot}_{name}_{r}"
+                res[key + "_loss"] = float(out["loss"])
+                res[key + "_grad_norm"] = float(out["grad_norm"])
+                res[key + "_grad"] = _flat_grad(out["grad"]).double().cpu().numpy()
+    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), world=world, **res)
+
+
 if __name__ == "__main__":
     from utils import distributed as dist
     dist.init_from_env()
-    {"mean_field": mean_field}[sys.argv[1]](*sys.argv[2:])
+    {"mean_field": mean_field, "dp_residual": dp_residual}[sys.argv[1]](*sys.argv[2:])
     if dist.is_distributed():
         torch.distributed.destroy_process_group()

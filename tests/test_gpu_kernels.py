@@ -513,22 +513,25 @@ def test_realnvp_value_and_grad_vs_autograd(native, dim, mask_type, E, soft_init
 
 
 def test_realnvp_value_and_grad_chunks_and_errors(native):
-    """Past 2048 tiles the slab is reduced in chunks into an fp64 accumulator: the mean gradient over
-    n rows must equal the row-count-weighted mean of the gradients over two disjoint parts
-    (linearity, size-independent). Also: a broadcast t, the unsupported-activation and empty-batch
-    errors."""
+    """One launch covers kNvpMaxRows = 8192 slab rows of kNvSPB = 128 samples (realnvp.hip); past that
+    the epoch is split into launches whose slabs are reduced into one fp64 accumulator (first / last
+    flags of nvp_grad_reduce_kernel, the slab reused across launches, tile offsets). n is sized past
+    two launches: the mean gradient over n rows must equal the row-count-weighted mean of the gradients
+    over two disjoint parts (linearity, size-independent), with the split inside the second launch.
+    Also: a broadcast t, the unsupported-activation and empty-batch errors."""
     from core.distribution import Gaussian
     from core.normalizing_flow import MNF, RealNVP
     dim, E = 2, 10
     mnf = MNF(dim, 4, "loop", 1.0, False, "celu", E)
     flow = RealNVP(mnf, Gaussian(np.zeros(dim), np.eye(dim)).logdensity)
     flat = _t(nr.nvp_init(dim, mnf.n_layers, E, False, seed=5, scale=1.2, perturb=True))
-    n = 2048 * 256 + 777
+    per_launch = 8192 * 128  # kNvpMaxRows * kNvSPB
+    n = 2 * per_launch + 777  # three launches, the last one partial
     gen = torch.Generator(device=DEV).manual_seed(0)
     x = torch.randn((n, dim), device=DEV, generator=gen) * 1.5
     t = torch.rand(n, device=DEV, generator=gen) * 2
     loss, grad = flow.value_and_grad(flat, t, x)
-    n1 = 300_001
+    n1 = per_launch + 300_001  # part 1 spans two launches, part 2 ends in a partial one
     l1, g1 = flow.value_and_grad(flat, t[:n1], x[:n1])
     l2, g2 = flow.value_and_grad(flat, t[n1:], x[n1:])
     mix = (n1 * g1.double() + (n - n1) * g2.double()) / n

@@ -53,7 +53,8 @@ def test_kmv_residual_vs_pairwise_restatement(native):
 @pytest.mark.parametrize("d,n,chunk,W,L,impl", [(2, 40, 1 << 18, 20, 3, 0), (4, 37, 300, 20, 3, 1),
                                                 (4, 37, 300, 20, 3, 2), (3, 70, 300, 10, 2, 2),
                                                 (2, 130, 300, 20, 8, 2), (8, 65, 300, 28, 2, 2),
-                                                (1, 66, 300, 16, 4, 2), (2, 530, 300, 20, 2, 2)])
+                                                (1, 66, 300, 16, 4, 2), (2, 530, 300, 20, 2, 2),
+                                                (2, 70, 300, 28, 12, 2)])
 def test_kmv_general_phi_mlp_vs_pairwise_restatement(native, d, n, chunk, W, L, impl):
     """General Phi_theta = V_hypothesis (non-parametric KMV, kinetic_mckean_vlasov.py:11-120) == the
     literal pair-tensor restatement (loss, loss ground truth, terms) and its FD-checked analytic gradient
@@ -61,7 +62,9 @@ def test_kmv_general_phi_mlp_vs_pairwise_restatement(native, d, n, chunk, W, L, 
     (pairs built in registers, MFMA weight gradients; odd widths / dims zero-padded; n not a multiple of
     the 64-pair tile), impl 1 = pair rows through rocBLAS (chunk = 300 forces partial i-blocks and
     j-chunking). (2, 130, ..., 20, 8) is the reference's default net (MLP.yaml: width 20, 8 layers);
-    n = 530 spans two of pass 2's 512-reference work units (a partial second one).
+    n = 530 spans two of pass 2's 512-reference work units (a partial second one). (2, 70, ..., 28, 12)
+    pads to more than 8 192 parameters, so pass 2 takes its global-memory weight-gradient slab
+    (kmvp_grad_kernel<D, W, false>) instead of the LDS slab.
     Tolerance 2e-4 relative (fp32)."""
     from example_problems.kinetic_mckean_vlasov_example_quadratic import KineticMcKeanVlasov
     from methods.consistency_instances import kinetic_mckean_vlasov as kmv
@@ -100,6 +103,36 @@ def test_kmv_general_phi_mlp_vs_pairwise_restatement(native, d, n, chunk, W, L, 
     assert abs(got_gt - loss_gt) < 2e-4 * (1 + abs(loss_gt))
     g = g.double().cpu().numpy()
     assert np.abs(g - ga).max() < 2e-4 * (1 + np.abs(ga).max())
+
+
+def test_kmv_general_phi_pair_kernels_golden_1400(native):
+    """The pair kernels at a size where pass 1's persistent grid (2 048 waves over n * n_time items)
+    iterates: d = 2, n = 1 400, 3 stamps (4 200 items), the reference's default 20 x 8 net, against the
+    committed fp64 restatement (tests/golden/kmv_mlp_pairs_1400.npz, oracle/make_golden.py
+    kmv_mlp_large: the literal pair tensor of kinetic_mckean_vlasov.py:20-23, 74-97, evaluated 250
+    references at a time). Tolerance 2e-4 relative (fp32)."""
+    import os
+    from example_problems.kinetic_mckean_vlasov_example_quadratic import KineticMcKeanVlasov
+    from utils import native as nat, prng
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "kmv_mlp_pairs_1400.npz"))
+    x, v, tau, dims = g["x"], g["v"], g["tau"], [int(t) for t in g["dims"]]
+    n, n_t, d = x.shape
+    cfg = _cfg(["pde_instance=kinetic_mckean_vlasov", f"pde_instance.domain_dim={d}"])
+    pi = KineticMcKeanVlasov(cfg, prng.PRNGKey(0))
+    assert np.allclose(np.asarray(pi.initial_configuration["tilde_F"], np.float64), g["F"])
+    z = _t(np.concatenate([x, v], -1).reshape(-1, 2 * d))
+    coef = pi.coefficients(tau, z.device)
+    _, ds = nat.kmv_weights(d, 1.0, coef, z, n_t, n, 2 * d, n_t * 2 * d, want_ds=True)
+    acc, grad = nat.residual_kmv_mlp(dims, _t(g["flat"]), z, n_t, n, 2 * d, n_t * 2 * d, ds, g["F"], 1.0,
+                                     impl=nat.MLP_IMPL_FUSED)
+    out = nat.kfp_terms_finalize(acc, grad, 1.0).cpu().numpy()
+    for key, slot in (("loss", "loss"), ("loss_gt", "loss ground truth"), ("hessian", "loss_Hessian"),
+                      ("nabla", "loss_nabla")):
+        ref = float(g[key])
+        assert abs(out[nat.KFP_SLOTS.index(slot)] - ref) < 2e-4 * (1 + abs(ref)), (key, out[nat.KFP_SLOTS.index(slot)], ref)
+    ga = g["grad"]
+    gg = grad.double().cpu().numpy()
+    assert np.abs(gg - ga).max() < 2e-4 * (1 + np.abs(ga).max()), np.abs(gg - ga).max()
 
 
 def test_partial_s_log_density_kat(native):

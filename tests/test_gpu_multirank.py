@@ -9,7 +9,10 @@ GPU per rank, the call sites are the same).
   trajectory of the whole ensemble (up to the fp64 summation order of the partial sums: 2e-5 after 31
   updates).
 * bench.py --gpus 2 (the driver's scaling launch): one JSON line, n_gpus = 2, value = both ranks'
-  particle-updates / the max-over-ranks step time.
+  particle-updates / the max-over-ranks step time — for the headline C2 and for C4 / C5.
+* The data-parallel KFP residual reports what the reference's pmap branch reports (trainer.py:44-53:
+  every output averaged over devices): loss and grad the means of the per-shard values, and grad_norm
+  the MEAN OF PER-SHARD NORMS (not the norm of the mean gradient).
 """
 import json
 import os
@@ -72,6 +75,49 @@ def test_bench_two_ranks(native):
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["value"] > 0 and out["config"]["particles_per_gpu"] == 65536
     assert abs(out["value"] * out["ms_per_step"] / 1e3 - 2 * 65536 * 101) < 1e-6 * out["value"]
+
+
+@pytest.mark.parametrize("config,port,n", [("C4", 29615, 65536), ("C5", 29617, 65536)])
+def test_bench_two_ranks_c4_c5(native, config, port, n):
+    """The driver's 8-GPU scaling launch runs every config through the same code: world-2 bench.py
+    --config C4 (closed-form McKean-Vlasov: the mean-path and KMV all-reduces) and C5 (MLP residual +
+    its gradient all-reduce) print one line with both ranks' particle-updates."""
+    r = _launch(2, [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", config, "--steps", "2", "--warmup", "1",
+                    "--particles", str(n), "--no-cpu-baseline", "--no-recovery"], port, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["value"] > 0 and out["config"]["particles_per_gpu"] == n
+    assert abs(out["value"] * out["ms_per_step"] / 1e3 - 2 * n * 101) < 1e-6 * out["value"]
+
+
+def test_dp_residual_matches_pmap_mean_of_shards(native, tmp_path):
+    """2 ranks (gloo) vs the two shards evaluated one at a time: loss and grad = the shard means,
+    grad_norm = the mean of the shard gradients' norms (trainer.py:44-53), for the quadratic, GMM and
+    MLP models of the KFP residual. Tolerance 1e-5 relative (fp32 terms, fp64 all-reduce)."""
+    worker = [os.path.join(ROOT, "tests", "mp_gpu_worker.py"), "dp_residual"]
+    ref_dir, d2 = tmp_path / "shards", tmp_path / "w2"
+    ref_dir.mkdir()
+    d2.mkdir()
+    r = subprocess.run([sys.executable] + worker + [str(ref_dir), "2"], cwd=ROOT, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    r = _launch(2, worker + [str(d2), "0"], 29641, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    ref = dict(np.load(os.path.join(ref_dir, "rank0.npz")))
+    got = [dict(np.load(os.path.join(d2, f"rank{k}.npz"))) for k in range(2)]
+    kinds = ("Quadratic_mlp", "Quadratic_quadratic", "GMM_mlp", "GMM_gmm")
+    for kind in kinds:
+        loss = np.mean([ref[f"{kind}_{r}_loss"] for r in range(2)])
+        grad = np.mean([ref[f"{kind}_{r}_grad"] for r in range(2)], axis=0)
+        gnorm = np.mean([np.linalg.norm(ref[f"{kind}_{r}_grad"]) for r in range(2)])
+        assert abs(gnorm - np.linalg.norm(grad)) > 1e-4 * gnorm, kind  # the two definitions differ here
+        for k in range(2):  # both ranks return the same (all-reduced) values, each rank's own shard key
+            g = got[k]
+            assert abs(g[f"{kind}_{k}_loss"] - loss) < 1e-5 * (1 + abs(loss)), (kind, g[f"{kind}_{k}_loss"], loss)
+            assert abs(g[f"{kind}_{k}_grad_norm"] - gnorm) < 1e-5 * (1 + gnorm), (kind, g[f"{kind}_{k}_grad_norm"], gnorm)
+            assert np.abs(g[f"{kind}_{k}_grad"] - grad).max() < 1e-5 * (1 + np.abs(grad).max()), kind
 
 
 @pytest.mark.parametrize("exchange,port", [("fused", 29631), ("per_update", 29632)])
