@@ -33,6 +33,8 @@
 //         from the rows in the A prologue: the h1 / abar1 planes never exist)
 #include <math.h>
 
+#include <stdlib.h>
+
 #include <algorithm>
 #include <type_traits>
 
@@ -780,6 +782,431 @@ __global__ void sum_slabs_kernel(const float* __restrict__ part, int S, int64_t 
   out[i] += s;
 }
 
+// ---- B-resident row GEMMs and LDS-free weight gradients (W x W layers) -------------------
+// Measured limit of fgemm / fwgrad above (r02-r03 SQ passes): two barriers per 32-k tile with the
+// operand staging between them; the co-resident workgroup does not reliably cover that phase, so the
+// big GEMMs held the fp32 MFMA pipe at ~0.6-0.7. These two kernels have no barrier in the main loop:
+//
+// rgemm: one persistent 8-wave workgroup per CU owns 128 output columns for its whole life; their B
+//   slice (the whole K x 128 weight block, K <= 256: <= 129 KB) is staged into LDS ONCE. Each wave
+//   computes a 32-row x 64-column tile (1 x 2 v_mfma_f32_32x32x2_f32 tiles per stream, S streams) of
+//   row blocks of 128 rows; its A operand never touches LDS: lane (m = lane & 31, h = lane >> 5) owns
+//   row m and, within each 32-k tile, the 16 k's [16h, 16h + 16) (the MFMA k slot of a lane is any
+//   bijection shared by A and B), so it loads its 16 A values per plane as four 16-byte loads one tile
+//   ahead (register double buffer) and applies the prologue transform in registers; layer-1 modes
+//   rebuild A from the row's x / v | abar0 (registers) and K1^T (LDS, broadcast per half-wave).
+// wgrad2: C[i][n] = sum_r sum_p A_p[r][i] B_p[r][n]: the sample rows are the MFMA reduction dimension
+//   (lane (l = lane & 31, h) takes row 2s + h of step s), so every operand is one coalesced 128-byte
+//   row segment per half-wave, loaded straight into registers one step ahead — no LDS, no barrier. One
+//   8-wave workgroup per CU covers the whole [n_in x n_out] output for its slice of rows (waves 4 x 2,
+//   each 32 MI x 32 NI); the repeat reads of a row's planes by the other waves hit the CU's L1.
+constexpr int kRT = 512;            // 8 waves
+constexpr int kRBN = 128;          // block columns (B slice resident in LDS)
+constexpr int kRGridCap = 256;      // one workgroup per CU (LDS-bound)
+
+template <int AM>
+constexpr int rg_planes() {
+  return (AM == A_FWD || AM == A_S3) ? 3 : (AM == A_S1MUL ? 2 : ((AM == A_U || AM == A_RAW1) ? 1 : 0));
+}
+
+bool rgemm_shape(int K, int N) { return K % 64 == 0 && K <= 256 && N % kRBN == 0; }
+
+// V (schedule variant, A/B): 0 = Bt b128 reads, compiler schedule; 1 = + one fenced region per tile
+// (prefetch one tile ahead); 2 = + loads / layer-1 VALU interleaved one per MFMA; 3 = Bs[k][n] with one
+// ds_read_b32 per k-step and column tile, compiler schedule.
+template <int S, int NI, int AM, int BMD, int EM, int D = 0, int V = 0>
+__global__ __launch_bounds__(kRT, 1) void rgemm(GemmArgs a) {
+  constexpr int WGN = kRBN / (32 * NI), WGM = 8 / WGN, BMR = 32 * WGM;  // waves along N / M, block rows
+  static_assert((NI == 2 || NI == 4) && WGN * WGM == 8, "rgemm wave grid");
+  constexpr bool L1 = a_is_l1<AM>();
+  constexpr int NV = rg_planes<AM>();
+  constexpr int SK = L1 ? k1_stride<D>() : 1;
+  constexpr int NP = (EM == E_ACT_BWD) ? 1 : 0;
+  static_assert(!L1 || D > 0, "layer-1 modes need D");
+  static_assert(EM == E_ACT_FWD || EM == E_STORE || EM == E_STORE3 || EM == E_ACT_BWD, "rgemm epilogues");
+  extern __shared__ float lds[];
+  const int Kp = a.K + 4;                          // Bt row pitch: ds_read_b128 of 16 lanes' rows conflict-free
+  float* Bt = lds;                                 // [kRBN][Kp]: Bt[n][k] = B[k][n0 + n]  (V = 3: [K][kRBN + 1])
+  [[maybe_unused]] float* k1s = Bt + (V == 3 ? (size_t)a.K * (kRBN + 1) : (size_t)kRBN * Kp);  // L1: [K][SK]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WGN, wn = wave % WGN, l31 = lane & 31, hi = lane >> 5;
+  const int K = a.K, N = a.N;
+  const int ncb = N / kRBN;
+  const int lid = xcd_linear(blockIdx.x, gridDim.x);  // the column blocks of a row stream adjacent: same XCD
+  const int cb = lid % ncb, rs = lid / ncb, nrs = gridDim.x / ncb;
+  const int n0 = cb * kRBN;
+  for (int e = tid; e < K * kRBN; e += kRT) {
+    int k, n;
+    float v;
+    if constexpr (BMD == B_NN) {
+      k = e / kRBN;
+      n = e - k * kRBN;
+      v = a.Bw[(size_t)k * N + n0 + n];
+    } else {
+      n = e / K;
+      k = e - n * K;
+      v = a.Bw[(size_t)(n0 + n) * K + k];
+    }
+    if constexpr (V == 3) Bt[k * (kRBN + 1) + n] = v;
+    else Bt[n * Kp + k] = v;
+  }
+  if constexpr (L1) {
+    for (int e = tid; e < K * SK; e += kRT) {
+      const int k = e / SK, i = e - k * SK;
+      k1s[e] = i < D ? a.k1[i * K + k] : (i == D ? a.b1[k] : 0.f);
+    }
+  }
+  __syncthreads();
+  [[maybe_unused]] float pacc[NI] = {};
+  const int nk = K / 32;  // even: K % 64 == 0 (rgemm_shape)
+  // The row-block loop is software-pipelined too: the last tile of a row block prefetches tile 0 (and,
+  // layer-1 modes, the x / v | abar0 row) of the NEXT row block, so the epilogue and the next block's
+  // first tile never wait on HBM.
+  auto row_of = [&](int mb_) { return std::min<int64_t>((int64_t)mb_ * BMR + wm * 32 + l31, a.R - 1); };
+  const float* pl[3] = {a.pa0, a.pa1, a.pa2};
+  auto load_tile = [&](float (&t)[NV > 0 ? NV : 1][16], int kt, int64_t row) {
+#pragma unroll
+    for (int p = 0; p < NV; ++p) {
+      const f32x4* src = reinterpret_cast<const f32x4*>(pl[p] + row * K + kt * 32 + 16 * hi);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const f32x4 v = src[j];
+        t[p][4 * j] = v[0]; t[p][4 * j + 1] = v[1]; t[p][4 * j + 2] = v[2]; t[p][4 * j + 3] = v[3];
+      }
+    }
+  };
+  [[maybe_unused]] float rx[L1 ? D : 1], ry[L1 ? D : 1], rxn[L1 ? D : 1], ryn[L1 ? D : 1];
+  auto load_row = [&](float* x, float* y, int64_t row) {
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      x[i] = a.xz[row * a.ldxz + i];
+      y[i] = AM == A_L1F ? a.xz[row * a.ldxz + D + i] : a.ab0[row * D + i];
+    }
+  };
+  float t0[NV > 0 ? NV : 1][16], t1[NV > 0 ? NV : 1][16];
+  if (rs < a.n_mblocks) {
+    if constexpr (NV > 0) load_tile(t0, 0, row_of(rs));
+    if constexpr (L1) load_row(rx, ry, row_of(rs));
+  }
+  for (int mb = rs; mb < a.n_mblocks; mb += nrs) {
+    const int r0 = mb * BMR;
+    const int64_t mr = row_of(mb);  // clamped row (stores are guarded)
+    const int64_t mrn = mb + nrs < a.n_mblocks ? row_of(mb + nrs) : mr;
+    if constexpr (L1) load_row(rxn, ryn, mrn);
+    f32x16 acc[S][NI];
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[s][ni][q] = 0.f;
+    auto steps = [&](const float (&t)[NV > 0 ? NV : 1][16], int kt) {
+      float bt[NI][16];  // the lane's 16 k's of each B column: 4 ds_read_b128 per column tile
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+        for (int j = 0; j < (V == 3 ? 0 : 4); ++j) {
+          const f32x4 v = *reinterpret_cast<const f32x4*>(Bt + (wn * 32 * NI + ni * 32 + l31) * Kp + kt * 32 +
+                                                          16 * hi + 4 * j);
+          bt[ni][4 * j] = v[0]; bt[ni][4 * j + 1] = v[1]; bt[ni][4 * j + 2] = v[2]; bt[ni][4 * j + 3] = v[3];
+        }
+      // layer-1 modes: the tile's A values up front (the K1 columns are broadcast LDS reads), so their
+      // VALU work and LDS latency are independent of the MFMA chain and can interleave with it
+      [[maybe_unused]] float at[L1 ? S : 1][L1 ? 16 : 1];
+      if constexpr (L1) {
+#pragma unroll
+        for (int s = 0; s < 16; ++s) {
+          float z, zy;
+          l1_project<D>(rx, ry, k1s + (kt * 32 + 16 * hi + s) * SK, z, zy);
+          const float h = ftanh(z), s1 = 1.f - h * h;
+          if constexpr (AM == A_L1F) {
+            at[0][s] = h;
+            at[1][s] = s1 * zy;
+            at[2][s] = -2.f * h * s1 * zy * zy;
+          } else {
+            at[0][s] = s1 * zy;
+          }
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        float av[3];
+        if constexpr (L1) {
+#pragma unroll
+          for (int si = 0; si < S; ++si) av[si] = at[si][s];
+        } else if constexpr (AM == A_FWD) {
+          const float h = t[0][s], zd = t[1][s], zdd = t[2][s];
+          const float s1 = 1.f - h * h, s2 = -2.f * h * s1;
+          av[0] = h;
+          av[1] = s1 * zd;
+          av[2] = fmaf(s1, zdd, s2 * zd * zd);
+        } else if constexpr (AM == A_S1MUL) {
+          const float h = t[0][s];
+          av[0] = (1.f - h * h) * t[1][s];
+        } else if constexpr (AM == A_U) {
+          av[0] = 2.f * t[0][s];
+        } else if constexpr (AM == A_RAW1) {
+          av[0] = t[0][s];
+        } else {  // A_S3
+          av[0] = t[0][s];
+          av[1] = t[1][s];
+          av[2] = t[2][s];
+        }
+        if constexpr (V == 3) {
+#pragma unroll
+          for (int ni = 0; ni < NI; ++ni)
+            bt[ni][s] = Bt[(kt * 32 + 16 * hi + s) * (kRBN + 1) + wn * 32 * NI + ni * 32 + l31];
+        }
+#pragma unroll
+        for (int si = 0; si < S; ++si)
+#pragma unroll
+          for (int ni = 0; ni < NI; ++ni)
+            acc[si][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[si], bt[ni][s], acc[si][ni], 0, 0, 0);
+      }
+    };
+    // Register double buffer, loads UNCONDITIONAL (the last prefetch re-reads tile 0 and is dropped): a
+    // load under a branch makes the waitcnt pass merge the two paths and wait for the just-issued
+    // prefetch before the current tile's MFMAs (measured: vmcnt(2) instead of vmcnt(12) in wgrad2).
+    // One scheduling region per tile (sched_barrier around it): the B reads, the NEXT tile's A loads and
+    // this tile's MFMAs, with the loads spread one per MFMA (sched_group_barrier) so that no wave parks
+    // on a burst of 4 NV gathers in the memory pipeline, and layer-1 VALU spread between MFMAs. Without
+    // the region fence the machine scheduler sank each prefetch next to its first use (vmcnt(0) before
+    // every k-step) to save registers.
+    constexpr int NMF = 16 * S * NI, NLD = 4 * NV;
+    constexpr int VPM = AM == A_L1F ? 5 : (AM == A_L1A ? 6 : 1);  // layer-1 VALU per MFMA (~28 / 24 per k-step)
+    auto tile = [&](const float (&tc)[NV > 0 ? NV : 1][16], float (&tn)[NV > 0 ? NV : 1][16], int kt, int ktn,
+                    int64_t rown) {
+      if constexpr (NV > 0) load_tile(tn, ktn, rown);
+      steps(tc, kt);
+      if constexpr (V == 2) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 4 * NI + (L1 ? 48 : 0), 0);  // DS reads: B (+ K1 columns)
+        if constexpr (L1) __builtin_amdgcn_sched_group_barrier(0x002, 28, 0);      // the first k-step's A
+#pragma unroll
+        for (int i = 0; i < NMF; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          if (i < NLD) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+          if constexpr (L1) __builtin_amdgcn_sched_group_barrier(0x002, VPM, 0);
+        }
+      }
+      if constexpr (V == 1 || V == 2) __builtin_amdgcn_sched_barrier(0);
+    };
+    if constexpr (V == 1 || V == 2) __builtin_amdgcn_sched_barrier(0);
+    for (int kt = 0; kt < nk; kt += 2) {  // t0 holds tile kt on entry (the last pair fetches the next block's tile 0)
+      tile(t0, t1, kt, kt + 1, mr);
+      tile(t1, t0, kt + 1, kt + 2 < nk ? kt + 2 : 0, kt + 2 < nk ? mr : mrn);
+    }
+    // ---- epilogue: acc register q of tile ni is C[row][col], row = (q & 3) + 8 (q >> 2) + 4 hi, col = l31
+    const bool full = r0 + BMR <= a.R;
+    auto epilogue = [&](auto check) {
+      constexpr bool CHECK = decltype(check)::value;
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) {
+        const int n = n0 + wn * 32 * NI + ni * 32 + l31;
+        [[maybe_unused]] float bn = 0.f;
+        if constexpr (EM == E_ACT_FWD) bn = a.bias[n];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int r = r0 + wm * 32 + (q & 3) + 8 * (q >> 2) + 4 * hi;
+          const bool ok = !CHECK || r < a.R;
+          const uint32_t o = (uint32_t)(r * N + n);
+          if constexpr (EM == E_ACT_FWD) {
+            if (ok) {
+              sto(a.po0, o, ftanh(acc[0][ni][q] + bn));
+              sto(a.po1, o, acc[1][ni][q]);
+              sto(a.po2, o, acc[2][ni][q]);
+            }
+          } else if constexpr (EM == E_STORE) {
+            if (ok) sto(a.po0, o, acc[0][ni][q]);
+          } else if constexpr (EM == E_STORE3) {
+            if (ok) {
+              sto(a.po0, o, acc[0][ni][q]);
+              sto(a.po1, o, acc[1][ni][q]);
+              sto(a.po2, o, acc[2][ni][q]);
+            }
+          } else {  // E_ACT_BWD
+            if (ok) {
+              const float hb = acc[0][ni][q], hdb = acc[1][ni][q], hddb = acc[2][ni][q];
+              const float h = ldo(a.pe0, o), zd = ldo(a.pe1, o), zdd = ldo(a.pe2, o), aL = ldo(a.pe3, o),
+                          zb = ldo(a.pe4, o);
+              const float s1 = 1.f - h * h, s2 = -2.f * h * s1, s3 = -2.f * s1 * s1 - 2.f * h * s2;
+              const float zbar = s1 * hb + s2 * zd * hdb + (s2 * zdd + s3 * zd * zd) * hddb + s2 * aL * zb;
+              sto(a.po0, o, zbar);
+              sto(a.po1, o, s1 * hdb + 2.f * s2 * zd * hddb);
+              sto(a.po2, o, s1 * hddb);
+              pacc[ni] += zbar;
+            }
+          }
+        }
+      }
+    };
+    if (full) epilogue(std::false_type{});
+    else epilogue(std::true_type{});
+    if constexpr (L1) {
+#pragma unroll
+      for (int i = 0; i < D; ++i) {
+        rx[i] = rxn[i];
+        ry[i] = ryn[i];
+      }
+    }
+  }
+  if constexpr (NP > 0) {  // bias-gradient column sums: one slab row per row stream
+    __syncthreads();
+    float* red = lds;  // [WGM][kRBN] (Bt is dead)
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) {
+      const float v = pacc[ni] + __shfl_xor(pacc[ni], 32, 64);
+      if (hi == 0) red[wm * kRBN + wn * 32 * NI + ni * 32 + l31] = v;
+    }
+    __syncthreads();
+    for (int c = tid; c < kRBN; c += kRT) {
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < WGM; ++w) t += red[w * kRBN + c];
+      a.part[(int64_t)rs * N + n0 + c] = t;
+    }
+  }
+}
+
+template <int MI, int NI, int GA, int GB, int D = 0, int V = 0>
+__global__ __launch_bounds__(kRT, 1) void wgrad2(WgradArgs a) {
+  static_assert(GA != GA_L1 || D > 0, "GA_L1 needs D");
+  static_assert(GA != GA_RAW4, "wgrad2: A streams from planes (GA_PL) or rows (GA_L1)");
+  constexpr int NVA = GA == GA_PL ? 4 : 0;     // raw A planes per feature group
+  constexpr int NVB = GB == GB_PL ? 5 : 4;     // raw B planes per column group
+  constexpr int NX = GA == GA_L1 ? 3 * D : 1;  // the row's [x | v | abar0]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1, l31 = lane & 31, hi = lane >> 5;
+  const int slice = xcd_linear(blockIdx.x, gridDim.x);
+  const int64_t rs0 = (int64_t)slice * a.rows_per_slice;
+  const int64_t rs1 = std::min<int64_t>(rs0 + a.rows_per_slice, a.R);
+  const int i0 = wm * 32 * MI, nb0 = wn * 32 * NI;
+  f32x16 acc[MI][NI];
+#pragma unroll
+  for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[mi][ni][q] = 0.f;
+  [[maybe_unused]] float kc[GA == GA_L1 ? MI : 1][GA == GA_L1 ? D + 1 : 1];
+  if constexpr (GA == GA_L1) {
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi) {
+      const int i = i0 + mi * 32 + l31;
+#pragma unroll
+      for (int q = 0; q < D; ++q) kc[mi][q] = a.k1[q * a.n_in + i];
+      kc[mi][D] = a.b1[i];
+    }
+  }
+  struct Regs {
+    float ra[NVA > 0 ? MI : 1][NVA > 0 ? NVA : 1];
+    float rb[NI][NVB];
+    float x[NX];
+  };
+  const float* pa[4] = {a.pa0, a.pa1, a.pa2, a.pa3};
+  const float* pb[5] = {a.pb0, a.pb1, a.pb2, a.pb3, a.pb4};
+  auto load = [&](Regs& g, int64_t rb0) {
+    const int64_t r = std::min<int64_t>(rb0 + hi, a.R - 1);
+#pragma unroll
+    for (int mi = 0; mi < (NVA > 0 ? MI : 0); ++mi)
+#pragma unroll
+      for (int p = 0; p < NVA; ++p) g.ra[mi][p] = ldo(pa[p], (uint32_t)(r * a.n_in + i0 + mi * 32 + l31));
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+      for (int p = 0; p < NVB; ++p) g.rb[ni][p] = ldo(pb[p], (uint32_t)(r * a.n_out + nb0 + ni * 32 + l31));
+    if constexpr (GA == GA_L1) {
+#pragma unroll
+      for (int c = 0; c < 2 * D; ++c) g.x[c] = a.xz[r * a.ldxz + c];
+#pragma unroll
+      for (int c = 0; c < D; ++c) g.x[2 * D + c] = a.ab0[r * D + c];
+    }
+  };
+  auto step = [&](const Regs& g, int64_t rb0) {
+    const bool ok = rb0 + hi < rs1;
+    float av[MI][4], bv[NI][4];
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi) {
+      if constexpr (GA == GA_L1) {
+        const float z = kc[mi][D] + dotd<D>(g.x, kc[mi]), zd = dotd<D>(g.x + D, kc[mi]),
+                    zb = dotd<D>(g.x + 2 * D, kc[mi]);
+        const float h = ftanh(z), s1 = 1.f - h * h;
+        av[mi][0] = h;
+        av[mi][1] = s1 * zd;
+        av[mi][2] = -2.f * h * s1 * zd * zd;
+        av[mi][3] = s1 * zb;
+      } else {
+        const float h = g.ra[mi][0], zd = g.ra[mi][1], zdd = g.ra[mi][2], zeb = g.ra[mi][3];
+        const float s1 = 1.f - h * h, s2 = -2.f * h * s1;
+        av[mi][0] = h;
+        av[mi][1] = s1 * zd;
+        av[mi][2] = fmaf(s1, zdd, s2 * zd * zd);
+        av[mi][3] = s1 * zeb;
+      }
+#pragma unroll
+      for (int p = 0; p < 4; ++p) av[mi][p] = ok ? av[mi][p] : 0.f;  // rows past the slice add nothing
+    }
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) {
+      bv[ni][0] = g.rb[ni][0];
+      bv[ni][1] = g.rb[ni][1];
+      bv[ni][2] = g.rb[ni][2];
+      if constexpr (GB == GB_PL) {
+        const float h = g.rb[ni][3];
+        bv[ni][3] = (1.f - h * h) * g.rb[ni][4];
+      } else {
+        bv[ni][3] = 2.f * g.rb[ni][3];
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[mi][p], bv[ni][p], acc[mi][ni], 0, 0, 0);
+  };
+  // Two steps of 2 rows per iteration (register double buffer). Loads and steps are UNCONDITIONAL
+  // (clamped rows; the ok mask zeroes rows past the slice): a load under a branch makes the waitcnt
+  // pass merge both paths and wait for the just-issued prefetch (vmcnt(2)) before the MFMAs.
+  // One scheduling region per step: the next step's loads spread one per MFMA (sched_group_barrier),
+  // the operand transforms between them.
+  constexpr int NLD = (NVA > 0 ? MI * NVA : 0) + NI * NVB + (GA == GA_L1 ? 6 : 0);
+  constexpr int NMF = 4 * MI * NI;
+  auto region = [&](const Regs& gc, Regs& gn, int64_t rc, int64_t rn) {
+    load(gn, rn);
+    if constexpr (V == 1) __builtin_amdgcn_sched_barrier(0);
+    step(gc, rc);
+    if constexpr (V == 2) {
+#pragma unroll
+      for (int i = 0; i < NMF; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        if (i < NLD) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+      }
+    }
+    if constexpr (V >= 1) __builtin_amdgcn_sched_barrier(0);
+  };
+  Regs g0, g1;
+  load(g0, rs0);
+  if constexpr (V >= 1) __builtin_amdgcn_sched_barrier(0);
+  for (int64_t rb = rs0; rb < rs1; rb += 4) {
+    region(g0, g1, rb, rb + 2);
+    region(g1, g0, rb + 2, rb + 4);
+  }
+  float* out = a.part + (int64_t)slice * a.n_in * a.n_out;
+#pragma unroll
+  for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) {
+      const int n = nb0 + ni * 32 + l31;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int i = i0 + mi * 32 + (q & 3) + 8 * (q >> 2) + 4 * hi;
+        out[(int64_t)i * a.n_out + n] = acc[mi][ni][q];
+      }
+    }
+}
+
 // ---- host side ------------------------------------------------------------------------
 constexpr int kMaxWgradSlices = 256;
 constexpr int kRowGridCap = 1024;  // workgroups per row GEMM launch (persistent over row blocks)
@@ -841,6 +1268,62 @@ static int launch_wgrad(WgradArgs a, float* grad_out, float* scratch, hipStream_
   return sum_slabs(a.part, slices, (int64_t)a.n_in * a.n_out, grad_out, scratch, st);
 }
 
+// PDEINV_MLP_SCHED (A/B of the rgemm / wgrad2 schedules; 1 = fenced regions, the default, measured
+// best: profiles/r03_c5_sched_ab.txt): 0 = compiler schedule.
+static int sched_variant() {
+  static const int v = [] {
+    const char* e = getenv("PDEINV_MLP_SCHED");
+    return e ? (atoi(e) == 0 ? 0 : 1) : 1;
+  }();
+  return v;
+}
+
+// S = 1 streams take 32 x 128 wave tiles (4 MFMA tiles per A value: the A prologue is the per-k VALU
+// cost), S = 3 streams 32 x 64 (3 x 2 tiles, 96 accumulator registers).
+template <int S, int AM, int BMD, int EM, int D = 0>
+static int launch_rgemm(GemmArgs a, hipStream_t st, int* grid_x_out = nullptr) {
+  constexpr int NI = S == 1 ? 4 : 2;
+  constexpr int BMR = 32 * (8 / (kRBN / (32 * NI)));
+  if (!rgemm_shape(a.K, a.N)) return fail(PDEINV_ERR_INVALID, "kfp_mlp rgemm: K % 64 == 0, K <= 256, N % 128 == 0");
+  const int V = sched_variant();
+  const size_t bytes = ((V == 3 ? (size_t)a.K * (kRBN + 1) : (size_t)kRBN * (a.K + 4)) +
+                        (a_is_l1<AM>() ? (size_t)a.K * k1_stride<D>() : 0)) * sizeof(float);
+  auto kern = V == 1 ? rgemm<S, NI, AM, BMD, EM, D, 1> : rgemm<S, NI, AM, BMD, EM, D, 0>;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  a.n_mblocks = mblocks(a.R, BMR);
+  const int ncb = a.N / kRBN;
+  const int nrs = std::max(1, std::min(a.n_mblocks, kRGridCap / ncb));
+  if (grid_x_out) *grid_x_out = nrs;
+  hipLaunchKernelGGL(kern, dim3(ncb * nrs), dim3(kRT), bytes, st, a);
+  return check_launch("kfp_mlp fused B-resident row GEMM");
+}
+
+template <int MI, int NI, int GA, int GB, int D = 0>
+static int launch_wgrad2(WgradArgs a, float* grad_out, float* scratch, hipStream_t st) {
+  if (a.n_in != 128 * MI || a.n_out != 64 * NI) return fail(PDEINV_ERR_INVALID, "kfp_mlp wgrad2: tile / shape mismatch");
+  const int slices = (int)std::max<int64_t>(1, std::min<int64_t>(kMaxWgradSlices, (a.R + 63) / 64));
+  int64_t rps = (a.R + slices - 1) / slices;
+  rps = (rps + 1) & ~(int64_t)1;
+  const int used = (int)((a.R + rps - 1) / rps);
+  a.rows_per_slice = rps;
+  const int V = sched_variant();
+  auto kern = V == 1 ? wgrad2<MI, NI, GA, GB, D, 1> : wgrad2<MI, NI, GA, GB, D, 0>;
+  hipLaunchKernelGGL(kern, dim3(used), dim3(kRT), 0, st, a);
+  int rc = check_launch("kfp_mlp fused weight gradient (wgrad2)");
+  if (rc) return rc;
+  return sum_slabs(a.part, used, (int64_t)a.n_in * a.n_out, grad_out, scratch, st);
+}
+
+// B-resident row GEMMs / LDS-free weight gradients for W in {128, 256} (PDEINV_MLP_RGEMM=0: the
+// staged fgemm / fwgrad kernels, for A/B measurements)
+static bool use_rgemm(int W) {
+  static const bool off = [] {
+    const char* e = getenv("PDEINV_MLP_RGEMM");
+    return e && e[0] == '0';
+  }();
+  return !off && (W == 128 || W == 256);
+}
+
 bool supported(int d, int L, int W, int O) {
   return (d == 2 || d == 4 || d == 8 || d == 16) && L >= 2 && L <= 16 &&
          (W == 32 || W == 64 || W == 128 || W == 256 || W == 512) && O >= 1 && O <= 64;
@@ -893,6 +1376,7 @@ static int run_chunk_t(const Chunk& c, const LossHook& loss, hipStream_t st) {
   const int L = c.L, W = c.W, O = c.O;
   const int64_t R = c.R;
   const Layout y = layout(D, L, W, O, c.Bc);
+  const bool RG = use_rgemm(WB);
   float* ws = c.ws;
   const size_t plane = ((size_t)c.Bc * W + 63) & ~(size_t)63;
   auto P = [&](int l, int k) { return ws + y.layer0 + y.layer_stride * (size_t)(l - 2) + plane * k; };
@@ -936,14 +1420,16 @@ static int run_chunk_t(const Chunk& c, const LossHook& loss, hipStream_t st) {
     GemmArgs a = base;
     a.K = W; a.N = W; a.Bw = Kw(2); a.bias = Bw(2);
     a.po0 = P(2, P_H); a.po1 = P(2, P_ZD); a.po2 = P(2, P_ZDD);
-    RC((launch_gemm<3, TM, TN, TG, A_L1F, B_NN, E_ACT_FWD, D>(a, st)));
+    if (RG) RC((launch_rgemm<3, A_L1F, B_NN, E_ACT_FWD, D>(a, st)));
+    else RC((launch_gemm<3, TM, TN, TG, A_L1F, B_NN, E_ACT_FWD, D>(a, st)));
   }
   for (int l = 3; l <= L; ++l) {
     GemmArgs a = base;
     a.K = W; a.N = W; a.Bw = Kw(l); a.bias = Bw(l);
     a.pa0 = P(l - 1, P_H); a.pa1 = P(l - 1, P_ZD); a.pa2 = P(l - 1, P_ZDD);
     a.po0 = P(l, P_H); a.po1 = P(l, P_ZD); a.po2 = P(l, P_ZDD);
-    RC((launch_gemm<3, TM, TN, TG, A_FWD, B_NN, E_ACT_FWD>(a, st)));
+    if (RG) RC((launch_rgemm<3, A_FWD, B_NN, E_ACT_FWD>(a, st)));
+    else RC((launch_gemm<3, TM, TN, TG, A_FWD, B_NN, E_ACT_FWD>(a, st)));
   }
   {
     GemmArgs a = base;
@@ -962,7 +1448,8 @@ static int run_chunk_t(const Chunk& c, const LossHook& loss, hipStream_t st) {
     GemmArgs a = base;
     a.K = W; a.N = W; a.Bw = Kw(l); a.pa0 = P(l, P_H); a.pa1 = P(l, P_A);
     a.po0 = l > 2 ? P(l - 1, P_A) : A1;
-    RC((launch_gemm1<A_S1MUL, B_NT>(a, st)));
+    if (RG) RC((launch_rgemm<1, A_S1MUL, B_NT, E_STORE>(a, st)));
+    else RC((launch_gemm1<A_S1MUL, B_NT>(a, st)));
   }
   {
     const int blocks = (int)std::min<int64_t>((R + 3) / 4, 2048);
@@ -974,13 +1461,15 @@ static int run_chunk_t(const Chunk& c, const LossHook& loss, hipStream_t st) {
   {  // abar1 = s1(z1) (abar0 K1) in the prologue
     GemmArgs a = base;
     a.K = W; a.N = W; a.Bw = Kw(2); a.po0 = P(2, P_ZETABAR);
-    RC((launch_gemm1<A_L1A, B_NN, D>(a, st)));
+    if (RG) RC((launch_rgemm<1, A_L1A, B_NN, E_STORE, D>(a, st)));
+    else RC((launch_gemm1<A_L1A, B_NN, D>(a, st)));
   }
   for (int l = 3; l <= L; ++l) {
     GemmArgs a = base;
     a.K = W; a.N = W; a.Bw = Kw(l); a.pa0 = P(l - 1, P_H); a.pa1 = P(l - 1, P_ZETABAR);
     a.po0 = P(l, P_ZETABAR);
-    RC((launch_gemm1<A_S1MUL, B_NN>(a, st)));
+    if (RG) RC((launch_rgemm<1, A_S1MUL, B_NN, E_STORE>(a, st)));
+    else RC((launch_gemm1<A_S1MUL, B_NN>(a, st)));
   }
   {
     GemmArgs a = base;
@@ -1010,7 +1499,8 @@ static int run_chunk_t(const Chunk& c, const LossHook& loss, hipStream_t st) {
     a.pe4 = P(l - 1, P_ZETABAR);
     a.po0 = P(l - 1, P_ZB0); a.po1 = P(l - 1, P_ZB1); a.po2 = P(l - 1, P_ZB2);
     int gx = 0;
-    RC((launch_gemm<3, TM, TN, TG, A_S3, B_NT, E_ACT_BWD>(a, st, &gx)));
+    if (RG) RC((launch_rgemm<3, A_S3, B_NT, E_ACT_BWD>(a, st, &gx)));
+    else RC((launch_gemm<3, TM, TN, TG, A_S3, B_NT, E_ACT_BWD>(a, st, &gx)));
     RC(sum_slabs(part, gx, W, c.grad + c.boff[l - 2], part2, st));
   }
   {
@@ -1018,7 +1508,8 @@ static int run_chunk_t(const Chunk& c, const LossHook& loss, hipStream_t st) {
     a.K = W; a.N = W; a.Bw = Kw(2);
     a.pa0 = P(2, P_ZB0); a.pa1 = P(2, P_ZB1); a.pa2 = P(2, P_ZB2);
     a.po0 = HB1[0]; a.po1 = HB1[1]; a.po2 = HB1[2];
-    RC((launch_gemm<3, TM, TN, TG, A_S3, B_NT, E_STORE3>(a, st)));
+    if (RG) RC((launch_rgemm<3, A_S3, B_NT, E_STORE3>(a, st)));
+    else RC((launch_gemm<3, TM, TN, TG, A_S3, B_NT, E_STORE3>(a, st)));
     hipLaunchKernelGGL((l1_grad_kernel<D, WB>), dim3(l1_blocks), dim3(kT), 0, st, HB1[0], HB1[1], HB1[2], A1, c.z,
                        c.ldz, abar0, Kw(1), Bw(1), R, l1_rpb, part);
     RC(check_launch("kfp_mlp fused layer-1 gradient"));
@@ -1037,14 +1528,24 @@ static int run_chunk_t(const Chunk& c, const LossHook& loss, hipStream_t st) {
     g.R = R; g.n_in = W; g.n_out = W; g.part = part;
     g.pa0 = P(l - 1, P_H); g.pa1 = P(l - 1, P_ZD); g.pa2 = P(l - 1, P_ZDD); g.pa3 = P(l - 1, P_ZETABAR);
     g.pb0 = P(l, P_ZB0); g.pb1 = P(l, P_ZB1); g.pb2 = P(l, P_ZB2); g.pb3 = P(l, P_H); g.pb4 = P(l, P_A);
-    RC((launch_wgrad<GW, GW, GA_PL, GB_PL>(g, c.grad + c.poff[l - 1], part2, st)));
+    if constexpr (WB == 128 || WB == 256) {
+      if (RG) RC((launch_wgrad2<WB / 128, WB / 64, GA_PL, GB_PL>(g, c.grad + c.poff[l - 1], part2, st)));
+      else RC((launch_wgrad<GW, GW, GA_PL, GB_PL>(g, c.grad + c.poff[l - 1], part2, st)));
+    } else {
+      RC((launch_wgrad<GW, GW, GA_PL, GB_PL>(g, c.grad + c.poff[l - 1], part2, st)));
+    }
   }
   {
     WgradArgs g{};
     g.R = R; g.n_in = W; g.n_out = W; g.part = part;
     g.xz = c.z; g.ldxz = c.ldz; g.ab0 = abar0; g.k1 = Kw(1); g.b1 = Bw(1);
     g.pb0 = P(2, P_ZB0); g.pb1 = P(2, P_ZB1); g.pb2 = P(2, P_ZB2); g.pb3 = P(2, P_H); g.pb4 = P(2, P_A);
-    RC((launch_wgrad<GW, GW, GA_L1, GB_PL, D>(g, c.grad + c.poff[1], part2, st)));
+    if constexpr (WB == 128 || WB == 256) {
+      if (RG) RC((launch_wgrad2<WB / 128, WB / 64, GA_L1, GB_PL, D>(g, c.grad + c.poff[1], part2, st)));
+      else RC((launch_wgrad<GW, GW, GA_L1, GB_PL, D>(g, c.grad + c.poff[1], part2, st)));
+    } else {
+      RC((launch_wgrad<GW, GW, GA_L1, GB_PL, D>(g, c.grad + c.poff[1], part2, st)));
+    }
   }
 #undef RC
   return 0;

@@ -90,8 +90,8 @@ def value_and_grad_fn(forward_fn, params, data, rng, pde_instance):
         W = dist.world_size()
         if W > 1:
             # this rank's own finalize (its sums un-scaled, a world_scale = 1 descriptor) for its grad norm
-            loc = acc.clone()
-            loc[: native.GMM_NACC - 2] *= W
+            loc = acc * W  # c-weighted sums (loss slots and the mu adjoint) carry world_scale = 1/W ...
+            loc[native.GMM_NACC - 2:native.GMM_NACC] = acc[native.GMM_NACC - 2:native.GMM_NACC]  # ... the per-set means do not
             desc1 = native.kfp_gmm_desc(model.dim, model.n_Gaussians, mus_true, gamma, T, n_i, n_t, n_0,
                                         sigma=model.sigma, sigma_true=pde_instance.potential.sigma, world_scale=1.0)
             _, g_loc = native.residual_kfp_gmm_finalize(desc1, loc)

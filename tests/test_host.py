@@ -202,3 +202,45 @@ def test_loader_fails_loudly_without_gpu():
         pytest.skip("has a GPU")
     with pytest.raises(RuntimeError):
         native.sde_simulate(torch.zeros((4, 4)), 3, 0.1, 1.0, dict(kind=0, params=np.eye(2)), seed=1)
+
+
+def test_abi_argument_validation_without_gpu():
+    """The C ABI rejects bad descriptors before touching the HIP runtime (negative
+    status + thread-local pdeinv_last_error()), so these run on a GPU-less host: a null descriptor,
+    an unsupported dim, n_steps = 0, a non-finite dt, ld_z0 < 2d, a null RealNVP descriptor."""
+    import ctypes
+    from utils import native
+    L = native.lib()
+
+    def sde(**kw):
+        d = native.SdeDesc()
+        d.n_particles, d.dim, d.n_steps, d.dt, d.gamma, d.noise_scale = 16, 4, 10, 0.02, 1.0, 1.41
+        for k, v in kw.items():
+            setattr(d, k, v)
+        return L.pdeinv_sde_simulate(ctypes.byref(d), None, None, None, None, None, None, None)
+
+    assert L.pdeinv_sde_simulate(None, None, None, None, None, None, None, None) == native.PDEINV_ERR_INVALID
+    assert b"null descriptor" in L.pdeinv_last_error()
+    assert sde(dim=0) == native.PDEINV_ERR_UNSUPPORTED and b"dim" in L.pdeinv_last_error()
+    assert sde(dim=17) == native.PDEINV_ERR_UNSUPPORTED
+    assert sde(n_steps=0) == native.PDEINV_ERR_INVALID and b"n_steps" in L.pdeinv_last_error()
+    assert sde(dt=float("nan")) == native.PDEINV_ERR_INVALID
+    assert sde(n_particles=-1) == native.PDEINV_ERR_INVALID
+    assert sde(ld_z0=5) == native.PDEINV_ERR_INVALID and b"ld_z0" in L.pdeinv_last_error()
+    assert L.pdeinv_realnvp_value_and_grad(None, None, None, 0, None, 0, 0, None, None, None, 0, None) \
+        == native.PDEINV_ERR_INVALID
+    assert L.pdeinv_mlp_fused_supported(3, 2, 256, 40) == 0 and L.pdeinv_mlp_fused_supported(8, 2, 256, 40) == 1
+
+
+def test_oracle_under_asan():
+    """the host AddressSanitizer + UBSan build of the C oracle (oracle/Makefile `asan`,
+    oracle/asan_driver.c) runs every oracle entry point on ragged inputs and the Philox KATs clean."""
+    import shutil
+    import subprocess
+    if shutil.which(os.environ.get("CC", "gcc")) is None:
+        pytest.skip("no host C compiler")
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "asan"])
+    r = subprocess.run([os.path.join(ROOT, "oracle", "_build", "oracle_asan")], capture_output=True, text=True,
+                       timeout=300, env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0"))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "0 failed checks" in r.stdout
