@@ -892,7 +892,17 @@ __global__ __launch_bounds__(kRT, 1) void rgemm(GemmArgs a) {
     const int r0 = mb * BMR;
     const int64_t mr = row_of(mb);  // clamped row (stores are guarded)
     const int64_t mrn = mb + nrs < a.n_mblocks ? row_of(mb + nrs) : mr;
-    if constexpr (L1) load_row(rxn, ryn, mrn);
+    // layer-1 modes: the B operand of the pre-activation MFMAs, [x, 1, 0] / y by c-pairs (half h: c = 2 j + h)
+    [[maybe_unused]] float xsel[L1 ? (D + 2) / 2 : 1], ysel[L1 ? D / 2 : 1];
+    if constexpr (L1) {
+#pragma unroll
+      for (int j = 0; j < (D + 2) / 2; ++j) {
+        const float x0 = 2 * j < D ? rx[2 * j] : 1.f, x1 = 2 * j + 1 < D ? rx[2 * j + 1] : 0.f;
+        xsel[j] = hi ? x1 : x0;
+        if (j < D / 2) ysel[j] = hi ? ry[2 * j + 1] : ry[2 * j];
+      }
+      load_row(rxn, ryn, mrn);
+    }
     f32x16 acc[S][NI];
 #pragma unroll
     for (int s = 0; s < S; ++s)
@@ -906,25 +916,44 @@ __global__ __launch_bounds__(kRT, 1) void rgemm(GemmArgs a) {
       for (int ni = 0; ni < NI; ++ni)
 #pragma unroll
         for (int j = 0; j < (V == 3 ? 0 : 4); ++j) {
-          const f32x4 v = *reinterpret_cast<const f32x4*>(Bt + (wn * 32 * NI + ni * 32 + l31) * Kp + kt * 32 +
-                                                          16 * hi + 4 * j);
+          // plane modes: the lane's k's are [16 hi, 16 hi + 16); layer-1 modes: the 32x32 MFMA result rows
+          // (j & 3) + 8 (j >> 2) + 4 hi, i.e. 16-byte runs at 4 hi + 8 j
+          const int ko = L1 ? 4 * hi + 8 * j : 16 * hi + 4 * j;
+          const f32x4 v = *reinterpret_cast<const f32x4*>(Bt + (wn * 32 * NI + ni * 32 + l31) * Kp + kt * 32 + ko);
           bt[ni][4 * j] = v[0]; bt[ni][4 * j + 1] = v[1]; bt[ni][4 * j + 2] = v[2]; bt[ni][4 * j + 3] = v[3];
         }
-      // layer-1 modes: the tile's A values up front (the K1 columns are broadcast LDS reads), so their
-      // VALU work and LDS latency are independent of the MFMA chain and can interleave with it
+      // layer-1 modes: the pre-activations of the lane's row for the tile's 32 k on the matrix pipe,
+      //   Z^T[k][m] = sum_c [K1; b1][c][k] [x_m; 1][c],  Zy^T[k][m] = sum_c K1[c][k] y_m[c]
+      // (A = the K1^T row of k = lane & 31 from LDS, B = the lane's own row): the 32x32 result leaves lane
+      // (m, h) with k = (q & 3) + 8 (q >> 2) + 4 h for q < 16 — the lane's 16 A values of the tile, which
+      // is why the B reads above use that k order. 5 + 4 MFMAs (d = 8) replace ~20 VALU per A value:
+      // VALU in this kernel is not hidden under the MFMA pipe (profiles/r03_mfma_probe.txt).
       [[maybe_unused]] float at[L1 ? S : 1][L1 ? 16 : 1];
       if constexpr (L1) {
+        constexpr int NZ = (D + 2) / 2;  // c-pairs of [x, 1]
+        float kc[SK];
 #pragma unroll
-        for (int s = 0; s < 16; ++s) {
-          float z, zy;
-          l1_project<D>(rx, ry, k1s + (kt * 32 + 16 * hi + s) * SK, z, zy);
+        for (int j = 0; j < SK / 4; ++j) {
+          const f32x4 v = *reinterpret_cast<const f32x4*>(k1s + (kt * 32 + l31) * SK + 4 * j);
+          kc[4 * j] = v[0]; kc[4 * j + 1] = v[1]; kc[4 * j + 2] = v[2]; kc[4 * j + 3] = v[3];
+        }
+        f32x16 zt = {}, yt = {};
+#pragma unroll
+        for (int j = 0; j < NZ; ++j) {
+          const float ka = hi ? (2 * j + 1 < SK ? kc[2 * j + 1] : 0.f) : kc[2 * j];
+          zt = __builtin_amdgcn_mfma_f32_32x32x2f32(ka, xsel[j], zt, 0, 0, 0);
+          if (j < D / 2) yt = __builtin_amdgcn_mfma_f32_32x32x2f32(ka, ysel[j], yt, 0, 0, 0);
+        }
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const float z = zt[q], zy = yt[q];
           const float h = ftanh(z), s1 = 1.f - h * h;
           if constexpr (AM == A_L1F) {
-            at[0][s] = h;
-            at[1][s] = s1 * zy;
-            at[2][s] = -2.f * h * s1 * zy * zy;
+            at[0][q] = h;
+            at[1][q] = s1 * zy;
+            at[2][q] = -2.f * h * s1 * zy * zy;
           } else {
-            at[0][s] = s1 * zy;
+            at[0][q] = s1 * zy;
           }
         }
       }
