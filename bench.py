@@ -80,6 +80,12 @@ def parse():
     p.add_argument("--cpu-particles", type=int, default=1 << 20)
     p.add_argument("--chunk-rows", type=int, default=1 << 21,
                    help="C5: MLP-residual rows per chunk (2^19 / 2^20 / 2^21: 114.5 / 113.7 / 113.4 ms; 7 / 14 / 28 GB workspace)")
+    p.add_argument("--c4-serial", action="store_true",
+                   help="C4: one stream, steps back to back (default at world 1: the two-stream pipeline, simulate "
+                        "k+1 concurrent with the KMV residual of step k on a double-buffered trajectory)")
+    p.add_argument("--c4-separate-sums", action="store_true",
+                   help="C4: the next simulate's mean-path sums as their own launch (pdeinv_mf_sums) instead of "
+                        "inside the KMV pass (pdeinv_kmv_moments_weights_mf_sums), for A/B")
     p.add_argument("--cpu-procs", type=int, default=0,
                    help="CPU-baseline shard processes (0 = the per-GPU host share, os.cpu_count() // 8)")
     return p.parse_args()
@@ -393,6 +399,7 @@ def run_c4(a, rank, world, dev):
 
     coef_next = [host_coef(counter[0])]
     ev = {"sums": [], "res": []}
+    sums_next = [None]  # rank-local mean-path sums of the next simulate, from the previous step's KMV pass
 
     def step(record):
         coef = coef_next[0].to(dev, non_blocking=True)
@@ -401,7 +408,8 @@ def run_c4(a, rank, world, dev):
         e0 = torch.cuda.Event(enable_timing=True) if record is not None else None
         if e0 is not None:
             e0.record()
-        sums = dist.allreduce_sum(native.mf_sums(desc, z0))  # the one collective of the simulate
+        local = sums_next[0] if sums_next[0] is not None else native.mf_sums(desc, z0)
+        sums = dist.allreduce_sum(local)  # the one collective of the simulate
         xbar, _ = native.mf_mean_path(desc, sums, xsum=False)
         desc.d_meanfield = ctypes.c_void_p(xbar.data_ptr())
         if record is not None:
@@ -411,7 +419,14 @@ def run_c4(a, rank, world, dev):
             record[1].record()
         del keep
         counter[0] = (counter[0] + n + 1) & 0xFFFFFFFF
-        mom, wst = native.kmv_moments_weights(d, gamma, coef, bufs["traj"], n, N, N * 2 * d, 2 * d)
+        if a.c4_separate_sums:
+            mom, wst = native.kmv_moments_weights(d, gamma, coef, bufs["traj"], n, N, N * 2 * d, 2 * d)
+        else:  # steady state: the KMV pass also sums the next simulate's mean-path noise (same z0 ensemble)
+            desc_n, keep_n = native.mf_desc(N, d, n, T / n, gamma, A, seed=key.seed, counter_offset=counter[0],
+                                            particle_offset=poff)
+            mom, wst, sums_next[0] = native.kmv_moments_weights_mf_sums(d, gamma, coef, bufs["traj"], n, N,
+                                                                        N * 2 * d, 2 * d, desc_n, z0)
+            del keep_n
         if record is not None:
             e3 = torch.cuda.Event(enable_timing=True)
             e3.record()
@@ -420,6 +435,63 @@ def run_c4(a, rank, world, dev):
         both = dist.allreduce_sum(torch.cat([mom.reshape(-1), wst.reshape(-1)]))
         native.residual_kmv(both[: mom.numel()].view_as(mom), both[mom.numel():].view_as(wst), theta, A, gamma)
         coef_next[0] = host_coef(counter[0])
+
+    # Two-stream pipeline (world 1): the simulate of step k+1 depends on z0 and the noise stream only — not on
+    # step k's residual or parameters — so it runs on stream S while step k's KMV pass + residual run on
+    # stream R over the other half of a double-buffered trajectory: store-bound simulator, VALU-bound noise
+    # sums and read-bound KMV pass overlap. (Not at world > 1: two RCCL collectives in flight on two streams
+    # could meet in different orders on different GPUs.)
+    pipeline = not a.c4_serial and world == 1
+    if pipeline:
+        S, Rs = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
+        bsets = [bufs, {"traj": torch.empty((n, N, 2 * d), device=dev), "tau": torch.empty((n, N), device=dev),
+                        "last": torch.empty((N, 2 * d), device=dev)}]
+        sim_done = [torch.cuda.Event(), torch.cuda.Event()]
+        pass_done = [None, None]
+        kstep = [0]
+
+        def step(record):  # noqa: F811 - the pipelined step
+            k = kstep[0] % 2
+            kstep[0] += 1
+            b = bsets[k]
+            with torch.cuda.stream(S):
+                if pass_done[k] is not None:
+                    S.wait_event(pass_done[k])  # step k-2's pass has finished reading this buffer
+                desc, keep = native.mf_desc(N, d, n, T / n, gamma, A, seed=key.seed, counter_offset=counter[0],
+                                            particle_offset=poff)
+                e0 = torch.cuda.Event(enable_timing=True) if record is not None else None
+                if e0 is not None:
+                    e0.record()
+                sums = dist.allreduce_sum(native.mf_sums(desc, z0))
+                xbar, _ = native.mf_mean_path(desc, sums, xsum=False)
+                desc.d_meanfield = ctypes.c_void_p(xbar.data_ptr())
+                if record is not None:
+                    record[0].record()
+                native.sde_simulate_desc(desc, z0, b["traj"], b["tau"], b["last"])
+                if record is not None:
+                    record[1].record()
+                sim_done[k].record()
+                del keep
+            counter[0] = (counter[0] + n + 1) & 0xFFFFFFFF
+            with torch.cuda.stream(Rs):
+                Rs.wait_event(sim_done[k])
+                coef = coef_next[0].to(dev, non_blocking=True)
+                e2 = torch.cuda.Event(enable_timing=True) if record is not None else None
+                if e2 is not None:
+                    e2.record()
+                mom, wst = native.kmv_moments_weights(d, gamma, coef, b["traj"], n, N, N * 2 * d, 2 * d)
+                if record is not None:
+                    e3 = torch.cuda.Event(enable_timing=True)
+                    e3.record()
+                    ev["sums"].append((e0, record[0]))
+                    ev["res"].append((e2, e3))
+                both = dist.allreduce_sum(torch.cat([mom.reshape(-1), wst.reshape(-1)]))
+                native.residual_kmv(both[: mom.numel()].view_as(mom), both[mom.numel():].view_as(wst), theta, A,
+                                    gamma)
+                ev_done = torch.cuda.Event()
+                ev_done.record()
+                pass_done[k] = ev_done
+            coef_next[0] = host_coef(counter[0])
 
     ms, kern_ms = timed(step, a.steps, a.warmup, dev)
     value = world * N * (n + 1) / (ms / 1e3)
@@ -434,10 +506,22 @@ def run_c4(a, rank, world, dev):
     sums_ms = float(np.mean([s.elapsed_time(e) for s, e in ev["sums"]]))
     res_ms = float(np.mean([s.elapsed_time(e) for s, e in ev["res"]]))
     res_bytes = N * n * 8 * d
-    out["mean_path"] = {"kernel": "mf_sums_kernel<8> + slab reduce (+ all-reduce) + mf_path_kernel", "ms": sums_ms,
-                        "normals_per_s": N * (n + 1) * d / (sums_ms / 1e3)}
-    out["residual"] = {"kernel": "kmv_moments_weights_kernel<8> + slab reduce + split", "ms": res_ms,
-                       "algorithmic_bytes": res_bytes, "GBps": res_bytes / (res_ms / 1e3) / 1e9}
+    out["c4_schedule"] = ("two-stream pipeline: simulate k+1 (+ its mean-path sums) on one stream concurrent with "
+                          "the KMV pass + residual of step k on another, double-buffered trajectory" if pipeline else
+                          "serial" + (", mean-path sums of the next simulate inside the KMV pass"
+                                      if not a.c4_separate_sums else ", separate mean-path sums"))
+    if a.c4_separate_sums or pipeline:
+        out["mean_path"] = {"kernel": "mf_sums_kernel<8> + slab reduce (+ all-reduce) + mf_path_kernel",
+                            "ms": sums_ms, "normals_per_s": N * (n + 1) * d / (sums_ms / 1e3)}
+        out["residual"] = {"kernel": "kmv_moments_weights_kernel<8> + slab reduce + split", "ms": res_ms,
+                           "algorithmic_bytes": res_bytes, "GBps": res_bytes / (res_ms / 1e3) / 1e9}
+    else:
+        out["mean_path"] = {"kernel": "all-reduce of the sums the previous KMV pass produced + mf_path_kernel",
+                            "ms": sums_ms}
+        out["residual"] = {"kernel": "kmv_moments_weights_kernel<8, MF> (+ the next simulate's mean-path noise sums "
+                                     "of updates 0..n-1) + mf_sums tail (update n, z0) + slab reduces + split",
+                           "ms": res_ms, "algorithmic_bytes": res_bytes, "GBps": res_bytes / (res_ms / 1e3) / 1e9,
+                           "next_normals_per_s": N * (n + 1) * d / (res_ms / 1e3)}
     return out
 
 

@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define PDEINV_ABI_VERSION 6
+#define PDEINV_ABI_VERSION 7
 #define PDEINV_MAX_DIM 16          /* d (configuration-space dimension) */
 #define PDEINV_MAX_PARAMS 256      /* floats of potential parameters passed by value */
 
@@ -299,6 +299,21 @@ size_t pdeinv_kmv_moments_weights_workspace_bytes(int64_t n_sets, int64_t n_rows
 int pdeinv_kmv_moments_weights(int32_t dim, float gamma, const float* d_coef, const float* d_z, int64_t n_sets,
                                int64_t n_rows, int64_t set_stride, int64_t ld, void* d_workspace, double* d_mom,
                                double* d_wstats, void* stream);
+
+/* The same pass fused with the NEXT McKean–Vlasov simulate's mean-path input (the steady state of the
+ * KMV training loop, config C4): besides d_mom / d_wstats it writes d_sums_next =
+ * pdeinv_mf_sums(next, d_z0_next) — the noise sums of updates t < n_sets are generated inside the
+ * HBM-bound pass (stamp t's rows are the particles next->particle_offset + r, next->n_particles ==
+ * n_rows, dim equal, Philox noise only), the remaining updates and the [count, x0, v0] block by a
+ * tail launch. Equal to pdeinv_mf_sums up to the fp32 partial-sum order (different block tiling).
+ * Workspace: pdeinv_kmv_moments_weights_mf_sums_workspace_bytes(). */
+size_t pdeinv_kmv_moments_weights_mf_sums_workspace_bytes(int64_t n_sets, int64_t n_rows, int32_t dim,
+                                                          const pdeinv_sde_desc* next);
+int pdeinv_kmv_moments_weights_mf_sums(int32_t dim, float gamma, const float* d_coef, const float* d_z,
+                                       int64_t n_sets, int64_t n_rows, int64_t set_stride, int64_t ld,
+                                       void* d_workspace, double* d_mom, double* d_wstats,
+                                       const pdeinv_sde_desc* next, const float* d_z0_next, double* d_sums_next,
+                                       void* stream);
 
 /* KMV residual for Phi_theta(y) = y . Dense_d(y) (…_quadratic.py:205-216) from the per-time-stamp
  * moments of z (mom [n_sets][moment_len(2d)]) and weighted stats (wst [n_sets][moment_len(d)]):

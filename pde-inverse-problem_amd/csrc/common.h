@@ -60,6 +60,34 @@ __device__ __forceinline__ void box_muller(uint32_t a, uint32_t b, float& z0, fl
   z1 = r * __builtin_amdgcn_sinf(th);
 }
 
+// d standard normals of update counter `ctr` of particle (plo, phi): the simulator's noise stream
+// (include/pdeinv.h: Philox4x32-10 block j = (plo, phi, ctr, j), Box–Muller on each pair).
+template <int D>
+__device__ __forceinline__ void stream_normals(uint32_t k0, uint32_t k1, uint32_t ctr, uint32_t plo, uint32_t phi,
+                                               float* xi) {
+#pragma unroll
+  for (int j = 0; 4 * j < D; ++j) {
+    const uint4 r = philox4x32_10(make_uint4(plo, phi, ctr, (uint32_t)j), k0, k1);
+    float z[4];
+    box_muller(r.x, r.y, z[0], z[1]);
+    box_muller(r.z, r.w, z[2], z[3]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (4 * j + k < D) xi[4 * j + k] = z[k];
+  }
+}
+
+// The McKean–Vlasov mean-path noise stream of one simulate (pdeinv_mf_sums), for kernels that sum
+// it outside the simulator (the fused KMV pass, kmv.hip). Filled / validated by mf_noise_of (sde.hip).
+struct MfNoise {
+  uint32_t k0, k1, ctr_off;
+  int64_t poff;
+};
+int mf_noise_of(const pdeinv_sde_desc* d, int dim, int64_t n_particles, MfNoise& out);
+// pdeinv_mf_sums restricted to updates y0..n_steps and the [count, x0, v0] block: writes those columns of
+// `sums` (the columns of updates < y0 are left to the caller). Workspace: pdeinv_mf_sums_workspace_bytes.
+int mf_sums_tail(const pdeinv_sde_desc* d, const float* z0, int y0, void* ws, double* sums, hipStream_t st);
+
 // ---- wave / block reductions ------------------------------------------------------------
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -123,11 +123,17 @@ __global__ __launch_bounds__(kBlock) void kmv_weights_kernel(float gamma, const 
 //  * count, sum z and the weighted moments stay lane-private (wave / block reduction at the end).
 constexpr int kMwStride = 20;  // floats per staged row (16 features + pad)
 
-template <int D, bool PACKED>
+//  * MF (pdeinv_kmv_moments_weights_mf_sums): the pass also sums the NEXT McKean–Vlasov simulate's
+//    update-t noise over the stamp's particles (row r = particle poff + r), i.e. the mean-path input of
+//    pdeinv_mf_sums for updates t < n_sets: that kernel is pure Philox / Box–Muller VALU work and this
+//    pass is HBM-bound, so the RNG rides in the pass's idle issue slots instead of a separate launch.
+template <int D, bool PACKED, bool MF = false>
 __global__ __launch_bounds__(kBlock) void kmv_moments_weights_kernel(float gamma, const float* __restrict__ coef,
                                                                      const float* __restrict__ z, int64_t n_rows,
                                                                      int64_t set_stride, int64_t ld,
-                                                                     float* __restrict__ partials) {
+                                                                     float* __restrict__ partials,
+                                                                     MfNoise mf = MfNoise{},
+                                                                     float* __restrict__ mf_partials = nullptr) {
   constexpr int M = 2 * D, NC = 3 * D + 2 + 2 * D * D, LZ = moment_len(M), LW = moment_len(D);
   static_assert(M <= 16, "the 16x16 MFMA Gram holds 2d <= 16 features");
   const int t = blockIdx.y;
@@ -161,6 +167,7 @@ __global__ __launch_bounds__(kBlock) void kmv_moments_weights_kernel(float gamma
   const f32x2 a12 = f32x2{c[D], c[2 * D + 1 + D * D]};
 
   f32x4 g4 = {0.f, 0.f, 0.f, 0.f};
+  [[maybe_unused]] float xis[MF ? D : 1] = {};
   float zs[M] = {};
   float rows = 0.f;
   MomentAcc<D> acc;
@@ -261,6 +268,15 @@ __global__ __launch_bounds__(kBlock) void kmv_moments_weights_kernel(float gamma
     }
     const float w = active ? q[1] + q[0] * q[0] + gamma * q[0] : 0.f;  // kinetic_mckean_vlasov.py:243-248
     acc.add(v, w);
+    if constexpr (MF) {  // the next simulate's update-t normals of this lane's particle
+      if (active) {
+        const uint64_t gid = (uint64_t)(mf.poff + r0 + lane);
+        float xi[D];
+        stream_normals<D>(mf.k0, mf.k1, mf.ctr_off + (uint32_t)t, (uint32_t)gid, (uint32_t)(gid >> 32), xi);
+#pragma unroll
+        for (int k = 0; k < D; ++k) xis[k] += xi[k];
+      }
+    }
   }
   // the wave's 16 x 16 Gram: lane holds rows 4 (lane / 16) + i, column lane % 16 (symmetric, so the
   // row / column convention of the accumulator layout does not matter)
@@ -283,6 +299,10 @@ __global__ __launch_bounds__(kBlock) void kmv_moments_weights_kernel(float gamma
     slab[(int64_t)(1 + M + o) * gridDim.x + blockIdx.x] = s;
   }
   block_reduce_to_slab(acc.v, LW, lds, slab + (int64_t)LZ * gridDim.x, blockIdx.x, gridDim.x);
+  if constexpr (MF) {
+    __shared__ float lds2[kWavesPerBlock * D];
+    block_reduce_to_slab(xis, D, lds2, mf_partials + (int64_t)t * D * gridDim.x, blockIdx.x, gridDim.x);
+  }
 }
 
 // slab [n_sets][LZ + LW] (fp64, after slab_reduce) -> mom [n_sets][LZ], wst [n_sets][LW]
@@ -543,6 +563,46 @@ extern "C" int pdeinv_residual_kmv(const pdeinv_kmv_desc* d, const double* mom, 
 // fp32 partial slab, rounded up to 256 B so that the fp64 column sums behind it are aligned
 static size_t kmv_mw_slab_bytes(int64_t cols, int bx) { return ((size_t)cols * bx * sizeof(float) + 255) & ~(size_t)255; }
 
+static int kmv_mw_launch(int32_t D, float gamma, const float* coef, const float* z, int64_t n_sets, int64_t n_rows,
+                         int64_t set_stride, int64_t ld, void* ws, double* mom, double* wst, hipStream_t st,
+                         const MfNoise* mf, float* mf_partials) {
+  const int bx = batched_bx(n_sets, n_rows);
+  const int lz = moment_len(2 * D), lw = moment_len(D);
+  const int64_t cols = n_sets * (lz + lw);
+  float* p = (float*)ws;
+  double* both = (double*)((char*)ws + kmv_mw_slab_bytes(cols, bx));
+  const dim3 g(bx, (unsigned)n_sets);
+  // packed rows (ld == 2d, 16-byte aligned, even d): the coalesced block-load variant
+  const bool packed = (2 * D) % 4 == 0 && ld == 2 * D && set_stride % 4 == 0 && ((uintptr_t)z & 15) == 0;
+  const MfNoise m = mf ? *mf : MfNoise{};
+  switch (D) {
+#define CASE(DD)                                                                                              \
+  case DD:                                                                                                    \
+    if (mf && packed)                                                                                         \
+      hipLaunchKernelGGL((kmv_moments_weights_kernel<DD, (2 * DD) % 4 == 0, true>), g, dim3(kBlock), 0, st,    \
+                         gamma, coef, z, n_rows, set_stride, ld, p, m, mf_partials);                          \
+    else if (mf)                                                                                              \
+      hipLaunchKernelGGL((kmv_moments_weights_kernel<DD, false, true>), g, dim3(kBlock), 0, st, gamma, coef, z, \
+                         n_rows, set_stride, ld, p, m, mf_partials);                                          \
+    else if (packed)                                                                                          \
+      hipLaunchKernelGGL((kmv_moments_weights_kernel<DD, (2 * DD) % 4 == 0>), g, dim3(kBlock), 0, st, gamma, coef, \
+                         z, n_rows, set_stride, ld, p, MfNoise{}, nullptr);                                   \
+    else                                                                                                      \
+      hipLaunchKernelGGL((kmv_moments_weights_kernel<DD, false>), g, dim3(kBlock), 0, st, gamma, coef, z, n_rows, \
+                         set_stride, ld, p, MfNoise{}, nullptr);                                              \
+    break;
+    CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
+#undef CASE
+  }
+  int rc = check_launch("kmv_moments_weights_kernel");
+  if (rc) return rc;
+  launch_slab_reduce(p, bx, (int)cols, both, st);
+  rc = check_launch("slab_reduce_kernel");
+  if (rc) return rc;
+  hipLaunchKernelGGL(kmv_split_kernel, dim3(grid_for(cols)), dim3(kBlock), 0, st, both, n_sets, lz, lw, mom, wst);
+  return check_launch("kmv_split_kernel");
+}
+
 extern "C" size_t pdeinv_kmv_moments_weights_workspace_bytes(int64_t n_sets, int64_t n_rows, int32_t dim) {
   if (dim < 1 || dim > 8 || n_sets < 1 || n_rows < 0) return 0;
   const int64_t cols = n_sets * (moment_len(2 * dim) + moment_len(dim));
@@ -559,33 +619,45 @@ extern "C" int pdeinv_kmv_moments_weights(int32_t D, float gamma, const float* c
   PDEINV_REQUIRE(ld >= 2 * D && set_stride >= 0, PDEINV_ERR_INVALID, "kmv_moments_weights: bad strides");
   PDEINV_REQUIRE(coef && mom && wst && ws && (n_rows == 0 || z), PDEINV_ERR_INVALID,
                  "kmv_moments_weights: null pointer");
-  hipStream_t st = (hipStream_t)stream;
-  const int bx = batched_bx(n_sets, n_rows);
-  const int lz = moment_len(2 * D), lw = moment_len(D);
-  const int64_t cols = n_sets * (lz + lw);
-  float* p = (float*)ws;
-  double* both = (double*)((char*)ws + kmv_mw_slab_bytes(cols, bx));
-  const dim3 g(bx, (unsigned)n_sets);
-  // packed rows (ld == 2d, 16-byte aligned, even d): the coalesced block-load variant
-  const bool packed = (2 * D) % 4 == 0 && ld == 2 * D && set_stride % 4 == 0 && ((uintptr_t)z & 15) == 0;
-  switch (D) {
-#define CASE(DD)                                                                                              \
-  case DD:                                                                                                    \
-    if (packed)                                                                                               \
-      hipLaunchKernelGGL((kmv_moments_weights_kernel<DD, (2 * DD) % 4 == 0>), g, dim3(kBlock), 0, st, gamma, coef, \
-                         z, n_rows, set_stride, ld, p);                                                       \
-    else                                                                                                      \
-      hipLaunchKernelGGL((kmv_moments_weights_kernel<DD, false>), g, dim3(kBlock), 0, st, gamma, coef, z, n_rows, \
-                         set_stride, ld, p);                                                                  \
-    break;
-    CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
-#undef CASE
-  }
-  int rc = check_launch("kmv_moments_weights_kernel");
+  return kmv_mw_launch(D, gamma, coef, z, n_sets, n_rows, set_stride, ld, ws, mom, wst, (hipStream_t)stream,
+                       nullptr, nullptr);
+}
+
+extern "C" size_t pdeinv_kmv_moments_weights_mf_sums_workspace_bytes(int64_t n_sets, int64_t n_rows, int32_t dim,
+                                                                     const pdeinv_sde_desc* next) {
+  const size_t a = pdeinv_kmv_moments_weights_workspace_bytes(n_sets, n_rows, dim);
+  if (a == 0 || !next) return 0;
+  const size_t b = (size_t)n_sets * dim * batched_bx(n_sets, n_rows) * sizeof(float);
+  return ((a + 255) & ~(size_t)255) + ((b + 255) & ~(size_t)255) + pdeinv_mf_sums_workspace_bytes(next);
+}
+
+extern "C" int pdeinv_kmv_moments_weights_mf_sums(int32_t D, float gamma, const float* coef, const float* z,
+                                                  int64_t n_sets, int64_t n_rows, int64_t set_stride, int64_t ld,
+                                                  void* ws, double* mom, double* wst, const pdeinv_sde_desc* next,
+                                                  const float* z0_next, double* sums_next, void* stream) {
+  PDEINV_REQUIRE(D >= 1 && D <= 8, PDEINV_ERR_UNSUPPORTED, "kmv_moments_weights_mf_sums: dim must be in [1, 8]");
+  PDEINV_REQUIRE(n_sets >= 1 && n_sets <= 65535 && n_rows >= 1, PDEINV_ERR_INVALID,
+                 "kmv_moments_weights_mf_sums: need 1 <= n_sets <= 65535, n_rows >= 1");
+  if (ld == 0) ld = 2 * D;
+  PDEINV_REQUIRE(ld >= 2 * D && set_stride >= 0, PDEINV_ERR_INVALID, "kmv_moments_weights_mf_sums: bad strides");
+  PDEINV_REQUIRE(coef && mom && wst && ws && z && next && z0_next && sums_next, PDEINV_ERR_INVALID,
+                 "kmv_moments_weights_mf_sums: null pointer");
+  MfNoise mf;
+  int rc = mf_noise_of(next, D, n_rows, mf);
   if (rc) return rc;
-  launch_slab_reduce(p, bx, (int)cols, both, st);
+  PDEINV_REQUIRE(n_sets <= (int64_t)next->n_steps + 1, PDEINV_ERR_INVALID,
+                 "kmv_moments_weights_mf_sums: more stamps than updates of the next simulate");
+  hipStream_t st = (hipStream_t)stream;
+  const size_t a = (pdeinv_kmv_moments_weights_workspace_bytes(n_sets, n_rows, D) + 255) & ~(size_t)255;
+  const int bx = batched_bx(n_sets, n_rows);
+  const size_t b = ((size_t)n_sets * D * bx * sizeof(float) + 255) & ~(size_t)255;
+  float* mfp = (float*)((char*)ws + a);
+  rc = kmv_mw_launch(D, gamma, coef, z, n_sets, n_rows, set_stride, ld, ws, mom, wst, st, &mf, mfp);
+  if (rc) return rc;
+  // updates t < n_sets: the pass's slab -> sums columns 1 + 2D + t D + k
+  launch_slab_reduce(mfp, bx, (int)(n_sets * D), sums_next + 1 + 2 * D, st);
   rc = check_launch("slab_reduce_kernel");
   if (rc) return rc;
-  hipLaunchKernelGGL(kmv_split_kernel, dim3(grid_for(cols)), dim3(kBlock), 0, st, both, n_sets, lz, lw, mom, wst);
-  return check_launch("kmv_split_kernel");
+  // updates n_sets .. n_steps and [count, sum x0, sum v0] of the next simulate
+  return mf_sums_tail(next, z0_next, (int)n_sets, (char*)ws + a + b, sums_next, st);
 }

@@ -52,16 +52,7 @@ __device__ __forceinline__ void gen_normals(const SdeArgs& a, uint32_t plo, uint
     for (int k = 0; k < D; ++k) xi[k] = src[k];
     return;
   }
-#pragma unroll
-  for (int j = 0; 4 * j < D; ++j) {
-    const uint4 r = philox4x32_10(make_uint4(plo, phi, a.ctr_off + s, (uint32_t)j), a.k0, a.k1);
-    float z[4];
-    box_muller(r.x, r.y, z[0], z[1]);
-    box_muller(r.z, r.w, z[2], z[3]);
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (4 * j + k < D) xi[4 * j + k] = z[k];
-  }
+  stream_normals<D>(a.k0, a.k1, a.ctr_off + s, plo, phi, xi);
 }
 
 // grad U(q) = A (q - c) = A q - b, b = A c packed on the host (KOU: A = tilde_F, c = 0,
@@ -888,9 +879,9 @@ __host__ __device__ inline int64_t mf_sums_len(int D, int n_steps) { return 1 + 
 // noise, y = n_steps + 1 sums [count, x0, v0]. Slab columns: [count, x0 (D), v0 (D), xi_0 (D), ..., xi_n (D)].
 template <int D, bool EXPLICIT>
 __global__ __launch_bounds__(kBlock) void mf_sums_kernel(SdeArgs a, const float* __restrict__ z0,
-                                                         float* __restrict__ partials) {
+                                                         float* __restrict__ partials, int y0) {
   const int nb = gridDim.x, b = blockIdx.x;
-  const int y = blockIdx.y;
+  const int y = blockIdx.y + y0;  // y0 > 0: the tail after a fused KMV pass summed updates < y0
   const int64_t base = (int64_t)b * kBlock * kMfSumsPerThread + threadIdx.x;
   __shared__ float lds[kWavesPerBlock * (1 + 2 * D)];
   if (y == a.n_steps + 1) {
@@ -959,6 +950,9 @@ extern "C" size_t pdeinv_mf_sums_workspace_bytes(const pdeinv_sde_desc* d) {
   return (size_t)mf_sums_len(d->dim, d->n_steps) * mf_sums_grid(d->n_particles) * sizeof(float);
 }
 
+static int mf_sums_launch(const SdeArgs& a, const pdeinv_sde_desc* d, const float* z0, int y0, void* ws,
+                          double* sums, hipStream_t st);
+
 extern "C" int pdeinv_mf_sums(const pdeinv_sde_desc* d, const float* z0, void* ws, double* sums, void* stream) {
   SdeArgs a;
   int rc = build_args(d, a);
@@ -974,26 +968,65 @@ extern "C" int pdeinv_mf_sums(const pdeinv_sde_desc* d, const float* z0, void* w
       return fail(PDEINV_ERR_HIP, "mf_sums: hipMemsetAsync failed");
     return PDEINV_OK;
   }
+  return mf_sums_launch(a, d, z0, 0, ws, sums, st);
+}
+
+// grid.y over y0 .. n_steps + 1; slab-reduces the columns the launch wrote
+static int mf_sums_launch(const SdeArgs& a, const pdeinv_sde_desc* d, const float* z0, int y0, void* ws,
+                          double* sums, hipStream_t st) {
   PDEINV_REQUIRE(z0 && ws, PDEINV_ERR_INVALID, "mf_sums: null pointer");
   PDEINV_REQUIRE(d->n_steps + 2 <= 65535, PDEINV_ERR_UNSUPPORTED, "mf_sums: n_steps too large");
+  PDEINV_REQUIRE(y0 >= 0 && y0 <= d->n_steps + 1, PDEINV_ERR_INVALID, "mf_sums: bad first update");
+  const int D = d->dim;
+  const int64_t L = mf_sums_len(D, d->n_steps);
   const int nb = mf_sums_grid(a.N);
-  const dim3 g(nb, d->n_steps + 2);
+  const dim3 g(nb, d->n_steps + 2 - y0);
   float* p = (float*)ws;
   switch (D) {
 #define CASE(DD)                                                                                         \
   case DD:                                                                                               \
-    if (a.noise) hipLaunchKernelGGL((mf_sums_kernel<DD, true>), g, dim3(kBlock), 0, st, a, z0, p);       \
-    else hipLaunchKernelGGL((mf_sums_kernel<DD, false>), g, dim3(kBlock), 0, st, a, z0, p);              \
+    if (a.noise) hipLaunchKernelGGL((mf_sums_kernel<DD, true>), g, dim3(kBlock), 0, st, a, z0, p, y0);   \
+    else hipLaunchKernelGGL((mf_sums_kernel<DD, false>), g, dim3(kBlock), 0, st, a, z0, p, y0);          \
     break;
     CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) CASE(10) CASE(12) CASE(16)
 #undef CASE
     default:
       return fail(PDEINV_ERR_UNSUPPORTED, "mf_sums: dim must be one of 1-8, 10, 12, 16");
   }
-  rc = check_launch("mf_sums_kernel");
+  int rc = check_launch("mf_sums_kernel");
   if (rc) return rc;
-  launch_slab_reduce(p, nb, (int)L, sums, st);
+  if (y0 == 0) {
+    launch_slab_reduce(p, nb, (int)L, sums, st);
+  } else {  // [count, x0, v0] and the updates y0 .. n_steps
+    const int64_t c0 = 1 + 2 * D + (int64_t)y0 * D;
+    launch_slab_reduce(p, nb, 1 + 2 * D, sums, st);
+    if (L > c0) launch_slab_reduce(p + c0 * nb, nb, (int)(L - c0), sums + c0, st);
+  }
   return check_launch("slab_reduce_kernel");
+}
+
+int pdeinv::mf_sums_tail(const pdeinv_sde_desc* d, const float* z0, int y0, void* ws, double* sums, hipStream_t st) {
+  SdeArgs a;
+  int rc = build_args(d, a);
+  if (rc) return rc;
+  PDEINV_REQUIRE(d->potential.kind == PDEINV_POT_MEANFIELD_QUADRATIC, PDEINV_ERR_INVALID,
+                 "mf_sums: potential must be MEANFIELD_QUADRATIC");
+  PDEINV_REQUIRE(a.N > 0 && sums, PDEINV_ERR_INVALID, "mf_sums tail: empty ensemble or null sums");
+  return mf_sums_launch(a, d, z0, y0, ws, sums, st);
+}
+
+int pdeinv::mf_noise_of(const pdeinv_sde_desc* d, int dim, int64_t n_particles, MfNoise& out) {
+  SdeArgs a;
+  int rc = build_args(d, a);
+  if (rc) return rc;
+  PDEINV_REQUIRE(d->potential.kind == PDEINV_POT_MEANFIELD_QUADRATIC, PDEINV_ERR_INVALID,
+                 "fused mean-path sums: the next simulate must be MEANFIELD_QUADRATIC");
+  PDEINV_REQUIRE(d->dim == dim && d->n_particles == n_particles, PDEINV_ERR_INVALID,
+                 "fused mean-path sums: the next simulate's dim / n_particles must be the KMV pass's");
+  PDEINV_REQUIRE(d->d_noise == nullptr, PDEINV_ERR_UNSUPPORTED,
+                 "fused mean-path sums: Philox noise only (the explicit-noise mode runs pdeinv_mf_sums)");
+  out = MfNoise{a.k0, a.k1, a.ctr_off, a.poff};
+  return PDEINV_OK;
 }
 
 extern "C" int pdeinv_mf_mean_path(const pdeinv_sde_desc* d, const double* sums, float* xbar, double* xsum,

@@ -36,7 +36,7 @@ GMM_NACC = 8
 GMM_ACC_SLOTS = ("loss", "loss_gt", "nabla", "hessian", "friction", "nabla_true", "initial", "terminal")
 SQRT2 = math.sqrt(2.0)
 
-ABI_VERSION = 6  # PDEINV_ABI_VERSION of include/pdeinv.h this binding was written against
+ABI_VERSION = 7  # PDEINV_ABI_VERSION of include/pdeinv.h this binding was written against
 
 # Every exported symbol of include/pdeinv.h (tests check the library exports all of them).
 EXPORTED_SYMBOLS = (
@@ -57,6 +57,7 @@ EXPORTED_SYMBOLS = (
     "pdeinv_residual_kmv_mlp_workspace_bytes", "pdeinv_residual_kmv_mlp",
     "pdeinv_mf_sums_len", "pdeinv_mf_sums_workspace_bytes", "pdeinv_mf_sums", "pdeinv_mf_mean_path",
     "pdeinv_kmv_moments_weights_workspace_bytes", "pdeinv_kmv_moments_weights",
+    "pdeinv_kmv_moments_weights_mf_sums_workspace_bytes", "pdeinv_kmv_moments_weights_mf_sums",
     "pdeinv_sde_simulate_kfp_gmm_workspace_bytes", "pdeinv_sde_simulate_kfp_gmm",
 )
 
@@ -161,6 +162,8 @@ def lib():
         "pdeinv_mf_mean_path": (i32, [P, P, P, P, P]),
         "pdeinv_kmv_moments_weights_workspace_bytes": (ctypes.c_size_t, [i64, i64, i32]),
         "pdeinv_kmv_moments_weights": (i32, [i32, f32, P, P, i64, i64, i64, i64, P, P, P, P]),
+        "pdeinv_kmv_moments_weights_mf_sums_workspace_bytes": (ctypes.c_size_t, [i64, i64, i32, P]),
+        "pdeinv_kmv_moments_weights_mf_sums": (i32, [i32, f32, P, P, i64, i64, i64, i64, P, P, P, P, P, P, P]),
         "pdeinv_moments_workspace_bytes": (ctypes.c_size_t, [i64, i32]),
         "pdeinv_moments": (i32, [P, i64, i32, i64, P, P, P]),
         "pdeinv_residual_kfp_quadratic": (i32, [P, P, P, P, P, P]),
@@ -675,6 +678,35 @@ def kmv_moments_weights(d: int, gamma: float, coef: torch.Tensor, z: torch.Tenso
                                             _dev(wst, "wst", torch.float64), stream_handle()),
            "pdeinv_kmv_moments_weights")
     return mom, wst
+
+
+def kmv_moments_weights_mf_sums(d: int, gamma: float, coef: torch.Tensor, z: torch.Tensor, n_sets: int, n_rows: int,
+                                set_stride: int, ld: int, next_desc: SdeDesc, z0_next: torch.Tensor):
+    """kmv_moments_weights fused with the NEXT McKean-Vlasov simulate's mf_sums (the steady state of the KMV
+    loop): (mom, wst, sums_next) — sums_next equals mf_sums(next_desc, z0_next) up to the fp32 partial-sum
+    order (pdeinv_kmv_moments_weights_mf_sums)."""
+    _require_gpu()
+    if tuple(coef.shape) != (n_sets, kmv_ncoef(d)) or not coef.is_contiguous():
+        raise ValueError(f"coef must be contiguous [{n_sets}, {kmv_ncoef(d)}]")
+    _set_view(z, n_sets, n_rows, set_stride, ld, 2 * d)
+    if z0_next.dim() != 2 or z0_next.shape[0] != next_desc.n_particles or z0_next.shape[1] != 2 * d or \
+            z0_next.stride(1) != 1:
+        raise ValueError(f"z0_next must be [{next_desc.n_particles}, {2 * d}] with unit inner stride")
+    next_desc.ld_z0 = z0_next.stride(0) if z0_next.shape[0] > 1 else 2 * d
+    nbytes = lib().pdeinv_kmv_moments_weights_mf_sums_workspace_bytes(n_sets, n_rows, d, ctypes.byref(next_desc))
+    if nbytes == 0:
+        raise NotImplementedError(f"kmv_moments_weights_mf_sums: dim={d} unsupported (1..8)")
+    ws = torch.empty((nbytes + 3) // 4, device=z.device, dtype=torch.float32)
+    mom = torch.empty((n_sets, moment_len(2 * d)), device=z.device, dtype=torch.float64)
+    wst = torch.empty((n_sets, moment_len(d)), device=z.device, dtype=torch.float64)
+    sums = torch.empty(int(lib().pdeinv_mf_sums_len(ctypes.byref(next_desc))), device=z.device, dtype=torch.float64)
+    _check(lib().pdeinv_kmv_moments_weights_mf_sums(d, float(gamma), _dev(coef, "coef"), _dev(z, "z"), n_sets, n_rows,
+                                                    set_stride, ld, _dev(ws, "ws"), _dev(mom, "mom", torch.float64),
+                                                    _dev(wst, "wst", torch.float64), ctypes.byref(next_desc),
+                                                    _dev(z0_next, "z0_next"), _dev(sums, "sums", torch.float64),
+                                                    stream_handle()),
+           "pdeinv_kmv_moments_weights_mf_sums")
+    return mom, wst, sums
 
 
 def residual_kmv_mlp(dims, params_flat: torch.Tensor, z: torch.Tensor, n_sets: int, n_rows: int, set_stride: int,

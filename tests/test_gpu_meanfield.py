@@ -158,6 +158,34 @@ def test_kmv_moments_weights_fused_equals_separate(native, d, n_t, n):
         assert np.allclose(a, b, rtol=1e-5, atol=1e-5 * np.abs(b).max())
 
 
+@pytest.mark.parametrize("d,n_t,n,n_steps,poff", [(8, 100, 50_001, 100, 0), (8, 7, 4099, 30, 123_456_789_012),
+                                                  (2, 3, 999, 2, 5), (5, 4, 4096, 3, 0)])
+def test_kmv_pass_fused_with_next_mf_sums(native, d, n_t, n, n_steps, poff):
+    """pdeinv_kmv_moments_weights_mf_sums (the C4 steady state: the KMV pass also sums the NEXT simulate's
+    mean-path noise): mom / wst bit-identical to the plain pass (same kernel code), sums_next == mf_sums of
+    the next simulate to fp32 partial-sum reassociation (1e-6 relative of the term scale), incl. more updates
+    than stamps (the tail launch), particle ids past 2^32 and partial blocks."""
+    rng = np.random.default_rng(d + n)
+    tau = np.linspace(0.2, 1.8, n_t)
+    _, coef = _coef(d, tau)
+    z = _t(rng.standard_normal((n_t, n, 2 * d)) * 1.3 + 0.1)
+    z0n = _t(rng.standard_normal((n, 2 * d)) + 0.25)
+    A = nr.problem_constants(d)
+    desc, keep = native.mf_desc(n, d, n_steps, 0.02, 1.0, A, seed=0x5EED_0004, counter_offset=777,
+                                particle_offset=poff)
+    mom, wst = native.kmv_moments_weights(d, 1.0, coef, z, n_t, n, n * 2 * d, 2 * d)
+    mom2, wst2, sums = native.kmv_moments_weights_mf_sums(d, 1.0, coef, z, n_t, n, n * 2 * d, 2 * d, desc, z0n)
+    assert torch.equal(mom, mom2) and torch.equal(wst, wst2)
+    ref = native.mf_sums(desc, z0n).cpu().numpy()
+    got = sums.cpu().numpy()
+    assert got.shape == ref.shape
+    assert got[0] == ref[0] == n
+    assert np.allclose(got[1:1 + 2 * d], ref[1:1 + 2 * d], rtol=1e-6, atol=1e-6 * n)  # [x0, v0] sums
+    noise_scale = np.sqrt(n)  # |sum of n normals| ~ sqrt(n): absolute tolerance on that scale
+    assert np.max(np.abs(got[1 + 2 * d:] - ref[1 + 2 * d:])) < 1e-5 * noise_scale
+    del keep
+
+
 @pytest.mark.parametrize("name", ["kmv_pairwise_d8.npz", "kmv_pairwise_recipe.npz"])
 def test_kmv_residual_vs_pairwise_golden(native, name):
     """residual_kmv at the C4 dimension (d = 8, 2 time stamps) and on the reference's runnable recipe
