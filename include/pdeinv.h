@@ -401,9 +401,13 @@ typedef struct {
   float gamma;            /* friction (weights c = ds2 + ds^2 + gamma ds) */
   const float* tilde_F;   /* HOST [d*d]: Phi* = 0.5 y^T tilde_F y (…_quadratic.py:193-203) */
   int64_t chunk_rows;     /* pair rows per GEMM chunk (library path); 0 => 2^18 */
-  int32_t impl;           /* PDEINV_MLP_IMPL_*: AUTO / FUSED = the pair kernels (pairs built in registers,
-                             MFMA weight gradients; dim <= 8, width <= 28, n_layers <= 16, out <= 64),
-                             LIBRARY = pair rows through rocBLAS (any shape) */
+  int32_t impl;           /* PDEINV_MLP_IMPL_*: AUTO / FUSED = the hand-written paths — width <= 28: the
+                             pair kernels (pairs built in registers, MFMA weight gradients; dim <= 8,
+                             n_layers <= 16, out <= 64; workspace ~ 2048 waves x (5 W L x 64 + P) floats,
+                             ~0.4 GB for the default 20 x 8 net); width >= 32 (dim in {2, 4, 8},
+                             2 <= n_layers <= 16, width <= 512 zero-padded to 32/64/128/256/512, out <= 64):
+                             chunks of pair rows through the fused fp32-MFMA residual kernels of
+                             pdeinv_residual_kfp_mlp; LIBRARY = pair rows through rocBLAS (any shape) */
 } pdeinv_kmv_mlp_desc;
 size_t pdeinv_residual_kmv_mlp_workspace_bytes(const pdeinv_kmv_mlp_desc* desc);
 int pdeinv_residual_kmv_mlp(const pdeinv_kmv_mlp_desc* desc, const float* d_z, int64_t set_stride, int64_t ld,

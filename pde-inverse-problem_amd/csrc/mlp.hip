@@ -991,12 +991,148 @@ static bool kmv_use_pairs(const pdeinv_kmv_mlp_desc* d) {
   return d->impl != PDEINV_MLP_IMPL_LIBRARY && kmv_pairs_supported(d);
 }
 
+// ---- wide general-Phi nets (width >= 32): the pair rows through the fused fp32-MFMA path ------------
+// Pair rows [y_ij | v_i | u_i | w_it] are built chunk by chunk exactly as for the library path, then run
+// through mlpf::run_chunk (the C5 machinery: B-resident row GEMMs, LDS-free weight gradients) — pass 1 in
+// its grad-only mode (g = grad_x Phi per pair -> mean over j), pass 2 with the per-row value weight
+// w_it on c0 and the input-gradient seed u_i in the loss hook. Widths between the compiled ones are
+// zero-padded (exact, common.h MlpPadMap). No rocBLAS on this path.
+static pdeinv_kfp_mlp_desc kmv_as_kfp(const pdeinv_kmv_mlp_desc* d) {
+  pdeinv_kfp_mlp_desc m{};
+  m.dim = d->dim; m.n_layers = d->n_layers; m.width = d->width; m.out_features = d->out_features;
+  m.chunk_rows = d->chunk_rows > 0 ? d->chunk_rows : (1 << 18);
+  m.impl = d->impl;
+  return m;
+}
+
+static bool kmv_use_fused(const pdeinv_kmv_mlp_desc* d) {
+  if (d->impl == PDEINV_MLP_IMPL_LIBRARY || kmv_use_pairs(d)) return false;
+  if (d->dim != 2 && d->dim != 4 && d->dim != 8) return false;
+  const pdeinv_kfp_mlp_desc m = kmv_as_kfp(d);
+  return use_fused(&m) || fused_pad_width(&m) != 0;
+}
+
+namespace {
+struct KmvFusedPlan {
+  int Wf, WP;
+  int64_t Bc, ni, nj, PP;
+  MlpPadMap pm;
+  size_t fl, off_part, off_pbuf, off_gbuf, off_rows, off_gbar, off_spart, total;  // floats
+};
+
+KmvFusedPlan kmv_fused_plan(const pdeinv_kmv_mlp_desc* d) {
+  const pdeinv_kfp_mlp_desc m = kmv_as_kfp(d);
+  KmvFusedPlan k{};
+  k.WP = fused_pad_width(&m);
+  k.Wf = k.WP ? k.WP : d->width;
+  k.Bc = m.chunk_rows;
+  const int64_t n = d->n_rows;
+  k.nj = n <= k.Bc ? n : k.Bc;
+  k.ni = n <= k.Bc ? (k.Bc / n < n ? k.Bc / n : n) : 1;
+  if (k.WP) {
+    k.pm = width_pad_map(&m, k.WP);
+    k.PP = pad_param_count(k.pm);
+  }
+  size_t o = 0;
+  auto take = [&](size_t floats) { const size_t at = o; o += (floats + 63) & ~(size_t)63; return at; };
+  k.fl = take(mlpf::workspace_floats(d->dim, d->n_layers, k.Wf, d->out_features, k.Bc));
+  k.off_part = take((size_t)PDEINV_GMM_NACC * kLossGrid);
+  k.off_pbuf = take((size_t)k.PP);
+  k.off_gbuf = take((size_t)k.PP);
+  k.off_rows = take((size_t)k.Bc * (3 * d->dim + 1));
+  k.off_gbar = take((size_t)d->n_sets * n * d->dim);
+  k.off_spart = take((size_t)d->n_sets * 3 * 2);
+  k.total = o * sizeof(float);
+  return k;
+}
+}  // namespace
+
+template <int D>
+static int kmv_fused_run(const pdeinv_kmv_mlp_desc* d, const KmvFusedPlan& k, const float* z, int64_t set_stride,
+                         int64_t ld, const float* ds, const float* params, float* w, double* acc, float* grad,
+                         hipStream_t st) {
+  const int L = d->n_layers, O = d->out_features;
+  int64_t poff[18], boff[18];
+  param_offsets(D, k.Wf, O, L, poff, boff);
+  const float* fparams = params;
+  float* fgrad = grad;
+  if (k.WP) {
+    float* pbuf = w + k.off_pbuf;
+    fgrad = w + k.off_gbuf;
+    hipLaunchKernelGGL(mlp_pad_params_kernel, dim3((unsigned)((k.PP + 255) / 256)), dim3(256), 0, st, k.pm, params,
+                       k.PP, pbuf);
+    if (hipMemsetAsync(fgrad, 0, sizeof(float) * k.PP, st) != hipSuccess) return fail(PDEINV_ERR_HIP, "kmv_mlp: memset");
+    fparams = pbuf;
+  }
+  const int64_t n = d->n_rows, T = d->n_sets, rld = 3 * D + 1;
+  float* rows = w + k.off_rows;
+  float* gbar = w + k.off_gbar;
+  double* part = (double*)(w + k.off_spart);
+  const double s = 1.0 / ((double)n * (double)n * (double)T);
+  if (hipMemsetAsync(gbar, 0, sizeof(float) * (size_t)T * n * D, st) != hipSuccess)
+    return fail(PDEINV_ERR_HIP, "kmv_mlp: memset");
+  LossCtx lc{};
+  lc.la.d = D;
+  lc.la.set = 3;
+  lc.la.uw = 1;
+  lc.la.c2 = (float)(-2.0 * s);
+  lc.la.c0 = (float)(2.0 * s);
+  lc.part = w + k.off_part;
+  lc.acc = acc;
+  lc.D = D;
+  lc.zr = rows;
+  lc.ld = rld;
+  mlpf::Chunk c{};
+  c.d = D; c.L = L; c.W = k.Wf; c.O = O;
+  c.z = rows; c.ldz = rld;
+  c.params = fparams; c.grad = fgrad; c.poff = poff; c.boff = boff;
+  c.ws = w; c.Bc = k.Bc;
+  for (int pass = 0; pass < 2; ++pass) {
+    c.grad_only = pass == 0;
+    c.c2 = pass ? lc.la.c2 : 0.f;
+    c.c3 = 0.f;
+    c.c0 = pass ? lc.la.c0 : 0.f;
+    c.wrow = pass ? rows + 3 * D : nullptr;
+    c.ldw = rld;
+    for (int64_t t = 0; t < T; ++t) {
+      for (int64_t i0 = 0; i0 < n; i0 += k.ni) {
+        const int64_t ni = (n - i0) < k.ni ? (n - i0) : k.ni;
+        for (int64_t j0 = 0; j0 < n; j0 += k.nj) {
+          const int64_t nj = (n - j0) < k.nj ? (n - j0) : k.nj;
+          c.R = ni * nj;
+          hipLaunchKernelGGL(kmv_pair_rows_kernel<D>, dim3(grid_for(c.R)), dim3(kBlock), 0, st, z, set_stride, ld, t,
+                             i0, ni, j0, nj, n, pass ? gbar : nullptr, pass ? ds : nullptr, d->gamma,
+                             (float)(2.0 * s), rows);
+          const int rc = mlpf::run_chunk(c, mlpf::LossHook{fused_loss_hook, &lc}, st);
+          if (rc) return rc;
+          if (pass == 0)
+            hipLaunchKernelGGL(kmv_group_mean_kernel<D>, dim3((unsigned)ni), dim3(kBlock), 0, st, mlpf::grad_rows(c),
+                               nj, (float)(1.0 / (double)n), gbar + (t * n + i0) * D);
+        }
+      }
+    }
+    if (pass == 0) {
+      KmvTrueArgs ta{};
+      for (int q = 0; q < D * D; ++q) ta.F[q] = d->tilde_F[q];
+      hipLaunchKernelGGL(kmv_stamp_terms_kernel<D>, dim3((unsigned)T), dim3(kBlock), 0, st, ta, z, set_stride, ld, n,
+                         gbar, part);
+      hipLaunchKernelGGL(kmv_stamp_combine_kernel, dim3(1), dim3(64), 0, st, part, T, 1.0 / ((double)n * (double)T),
+                         acc);
+    }
+  }
+  if (k.WP)
+    hipLaunchKernelGGL(mlp_unpad_grad_kernel, dim3((unsigned)((k.PP + 255) / 256)), dim3(256), 0, st, k.pm, fgrad,
+                       k.PP, grad);
+  return check_launch("kmv_mlp fused kernels");
+}
+
 static size_t kmv_pairs_part_offset(const pdeinv_kmv_mlp_desc* d) { return (kmv_pairs_workspace_bytes(d) + 255) & ~(size_t)255; }
 
 extern "C" size_t pdeinv_residual_kmv_mlp_workspace_bytes(const pdeinv_kmv_mlp_desc* d) {
   if (!d || d->dim < 1 || d->n_layers < 1 || d->width < 1 || d->out_features < 1 || d->n_sets < 1 || d->n_rows < 1)
     return 0;
   if (kmv_use_pairs(d)) return kmv_pairs_part_offset(d) + sizeof(double) * (size_t)d->n_sets * 3;
+  if (kmv_use_fused(d)) return kmv_fused_plan(d).total;
   return kmv_plan(d).total;
 }
 
@@ -1036,8 +1172,17 @@ extern "C" int pdeinv_residual_kmv_mlp(const pdeinv_kmv_mlp_desc* d, const float
 #undef CASE
     }
   }
+  if (kmv_use_fused(d)) {
+    const KmvFusedPlan k = kmv_fused_plan(d);
+    switch (d->dim) {
+#define CASE(DD) case DD: return kmv_fused_run<DD>(d, k, z, set_stride, ld, ds, params, (float*)ws, acc, grad, st);
+      CASE(2) CASE(4) CASE(8)
+#undef CASE
+    }
+  }
   PDEINV_REQUIRE(d->impl != PDEINV_MLP_IMPL_FUSED, PDEINV_ERR_UNSUPPORTED,
-                 "kmv_mlp: the pair kernels need dim <= 8, width <= 28, n_layers <= 16, out_features <= 64");
+                 "kmv_mlp: the hand-written paths need dim <= 8 with width <= 28 (pair kernels), or dim in {2, 4, 8} "
+                 "with 2 <= n_layers <= 16, width <= 512, out_features <= 64 (fused MFMA path)");
   const KmvPlan k = kmv_plan(d);
   switch (d->dim) {
 #define CASE(DD) case DD: return kmv_mlp_run<DD>(d, k, z, set_stride, ld, ds, params, (float*)ws, acc, grad, st);

@@ -31,7 +31,15 @@ struct Chunk {
   float c2, c3, c0;          // loss weights of V'', V' and V for this set
   float* ws;                 // workspace_floats(..., Bc >= R)
   int64_t Bc;
+  // KMV pair rows (pdeinv_residual_kmv_mlp): per-row value weight w_r = wrow[r * ldw] multiplying c0
+  // (nullptr: 1), and grad_only = stop after g = grad_x V of every row (pass 1), left in grad_rows()
+  const float* wrow = nullptr;
+  int64_t ldw = 0;
+  bool grad_only = false;
 };
+
+// g = grad_x V [R x d] of the last run_chunk (workspace view)
+const float* grad_rows(const Chunk& c);
 
 int run_chunk(const Chunk& c, const LossHook& loss, hipStream_t st);
 

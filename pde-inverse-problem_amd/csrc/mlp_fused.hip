@@ -104,6 +104,8 @@ struct GemmArgs {
   const float* ab0;  // A_L1A: abar0 [R x d]
   const float* k1;   // A_L1*: K1 [d x K] (flax [in, out]) and b1 [K]
   const float* b1;
+  const float* wrow;  // E_SEEDS: per-row weight of c0 (KMV pair rows), stride ldw; nullptr = 1
+  int64_t ldw;
 };
 
 template <int AM>
@@ -375,7 +377,8 @@ __global__ __launch_bounds__(kT, 2) void fgemm(GemmArgs a) {
               if (ok) {
                 const float ub = acc[0][mi][ni][q];
                 const float y = ldo(a.pe0, o), yd = ldo(a.pe1, o), ydd = ldo(a.pe2, o);
-                const float yb = 2.f * a.c3 * yd + 2.f * a.c2 * ydd + 2.f * ub + 2.f * a.c0 * y;
+                const float c0r = a.wrow ? a.c0 * a.wrow[(int64_t)r * a.ldw] : a.c0;
+                const float yb = 2.f * a.c3 * yd + 2.f * a.c2 * ydd + 2.f * ub + 2.f * c0r * y;
                 sto(a.po0, o, yb);
                 sto(a.po1, o, 2.f * a.c3 * y + 4.f * a.c2 * yd);
                 sto(a.po2, o, 2.f * a.c2 * y);
@@ -1393,6 +1396,8 @@ static Layout layout(int d, int L, int W, int O, int64_t Bc) {
 
 size_t workspace_floats(int d, int L, int W, int O, int64_t Bc) { return layout(d, L, W, O, Bc).total; }
 
+const float* grad_rows(const Chunk& c) { return c.ws + layout(c.d, c.L, c.W, c.O, c.Bc).g; }
+
 template <int D, int WB>
 static int run_chunk_t(const Chunk& c, const LossHook& loss, hipStream_t st) {
   // hidden-width row-GEMM tiles: 64 x 128 (2 x 2 waves) for W >= 128; narrow nets get tiles no
@@ -1435,6 +1440,8 @@ static int run_chunk_t(const Chunk& c, const LossHook& loss, hipStream_t st) {
   base.ab0 = abar0;
   base.k1 = Kw(1);
   base.b1 = Bw(1);
+  base.wrow = c.wrow;
+  base.ldw = c.ldw;
   int rc = 0;
 #define RC(x)          \
   do {                 \
@@ -1485,6 +1492,7 @@ static int run_chunk_t(const Chunk& c, const LossHook& loss, hipStream_t st) {
     hipLaunchKernelGGL((l1_g_kernel<D, WB>), dim3(blocks), dim3(kT), 0, st, A1, c.z, c.ldz, Kw(1), Bw(1), R, G);
     RC(check_launch("kfp_mlp fused g"));
   }
+  if (c.grad_only) return 0;  // KMV pass 1: g of every row is all that is needed
   RC(loss.fn(loss.ctx, G, terms, abar0, R, st));
   // ---- F2: forward adjoint ----------------------------------------------------------------
   {  // abar1 = s1(z1) (abar0 K1) in the prologue

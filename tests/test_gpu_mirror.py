@@ -54,7 +54,9 @@ def test_kmv_residual_vs_pairwise_restatement(native):
                                                 (4, 37, 300, 20, 3, 2), (3, 70, 300, 10, 2, 2),
                                                 (2, 130, 300, 20, 8, 2), (8, 65, 300, 28, 2, 2),
                                                 (1, 66, 300, 16, 4, 2), (2, 530, 300, 20, 2, 2),
-                                                (2, 70, 300, 28, 12, 2)])
+                                                (2, 70, 300, 28, 12, 2), (2, 60, 300, 64, 2, 2),
+                                                (8, 40, 1 << 18, 256, 2, 0), (4, 45, 500, 100, 3, 2),
+                                                (4, 33, 256, 32, 2, 0)])
 def test_kmv_general_phi_mlp_vs_pairwise_restatement(native, d, n, chunk, W, L, impl):
     """General Phi_theta = V_hypothesis (non-parametric KMV, kinetic_mckean_vlasov.py:11-120) == the
     literal pair-tensor restatement (loss, loss ground truth, terms) and its FD-checked analytic gradient
@@ -64,7 +66,9 @@ def test_kmv_general_phi_mlp_vs_pairwise_restatement(native, d, n, chunk, W, L, 
     j-chunking). (2, 130, ..., 20, 8) is the reference's default net (MLP.yaml: width 20, 8 layers);
     n = 530 spans two of pass 2's 512-reference work units (a partial second one). (2, 70, ..., 28, 12)
     pads to more than 8 192 parameters, so pass 2 takes its global-memory weight-gradient slab
-    (kmvp_grad_kernel<D, W, false>) instead of the LDS slab.
+    (kmvp_grad_kernel<D, W, false>) instead of the LDS slab. Widths >= 32 (64, 256 = the C5 width, 100
+    zero-padded to 128, 32) run the pair rows through the fused fp32-MFMA residual kernels (no rocBLAS),
+    chunked (300 / 500 / 256 rows: partial i-blocks and j-chunks).
     Tolerance 2e-4 relative (fp32)."""
     from example_problems.kinetic_mckean_vlasov_example_quadratic import KineticMcKeanVlasov
     from methods.consistency_instances import kinetic_mckean_vlasov as kmv
