@@ -80,9 +80,10 @@ def parse():
     p.add_argument("--cpu-particles", type=int, default=1 << 20)
     p.add_argument("--chunk-rows", type=int, default=1 << 21,
                    help="C5: MLP-residual rows per chunk (2^19 / 2^20 / 2^21: 114.5 / 113.7 / 113.4 ms; 7 / 14 / 28 GB workspace)")
-    p.add_argument("--c4-serial", action="store_true",
-                   help="C4: one stream, steps back to back (default at world 1: the two-stream pipeline, simulate "
-                        "k+1 concurrent with the KMV residual of step k on a double-buffered trajectory)")
+    p.add_argument("--c4-pipeline", action="store_true",
+                   help="C4 at world 1: two streams, simulate k+1 concurrent with the KMV residual of step k on a "
+                        "double-buffered trajectory (measured 6.85 vs 6.25 ms/step serial: the step is HBM-bound, "
+                        "so overlap buys nothing and the fused next-simulate sums are lost); default serial")
     p.add_argument("--c4-separate-sums", action="store_true",
                    help="C4: the next simulate's mean-path sums as their own launch (pdeinv_mf_sums) instead of "
                         "inside the KMV pass (pdeinv_kmv_moments_weights_mf_sums), for A/B")
@@ -436,12 +437,12 @@ def run_c4(a, rank, world, dev):
         native.residual_kmv(both[: mom.numel()].view_as(mom), both[mom.numel():].view_as(wst), theta, A, gamma)
         coef_next[0] = host_coef(counter[0])
 
-    # Two-stream pipeline (world 1): the simulate of step k+1 depends on z0 and the noise stream only — not on
+    # Two-stream pipeline (world 1, --c4-pipeline; slower, kept for A/B): the simulate of step k+1 depends on z0 and the noise stream only — not on
     # step k's residual or parameters — so it runs on stream S while step k's KMV pass + residual run on
     # stream R over the other half of a double-buffered trajectory: store-bound simulator, VALU-bound noise
     # sums and read-bound KMV pass overlap. (Not at world > 1: two RCCL collectives in flight on two streams
     # could meet in different orders on different GPUs.)
-    pipeline = not a.c4_serial and world == 1
+    pipeline = a.c4_pipeline and world == 1
     if pipeline:
         S, Rs = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
         bsets = [bufs, {"traj": torch.empty((n, N, 2 * d), device=dev), "tau": torch.empty((n, N), device=dev),

@@ -165,7 +165,13 @@ __global__ __launch_bounds__(kBlock) void realnvp_logdensity_kernel(NvpArgs a, c
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kNvpMaxRows = 8192;  // slab rows (128-sample blocks) per launch + reduce chunk
-constexpr int kNvT = 2;            // 16-sample tiles per wave (32 samples; 128 per block)
+#ifndef PDEINV_NVT
+#define PDEINV_NVT 2
+#endif
+#ifndef PDEINV_NVW
+#define PDEINV_NVW 2
+#endif
+constexpr int kNvT = PDEINV_NVT;   // 16-sample tiles per wave (32 samples; 128 per block)
 constexpr int kNvSPB = kWavesPerBlock * 16 * kNvT;  // samples per block = per slab row
 constexpr int kNvWS = 20;          // LDS row stride of a padded 16 x 16 weight matrix
 constexpr int kNvRaw = 8 + 2 * (24 * 8 + 8 + 128 + 16 + 256 + 16 + 16 * 8 + 8);  // one layer's params, d <= 8
@@ -202,6 +208,30 @@ struct NvLane {
   int g, s;  // component group, sample within the tile
 };
 
+// Position of a component in the padded 16-vectors. Packed layout (PK: d <= 4, n_t <= 12): coordinate c
+// at 4c (register 0 of lane group c), time-embedding component e at 4(e / 3) + 1 + e % 3 (registers 1..3),
+// the first hidden layer's 8 units at 4(o / 2) + o % 2 (registers 0, 1). So [x | temb] is ONE 16-vector
+// with no data movement (register 0 from x, 1..3 from temb: the net's first layer is one 16 x 16 product,
+// not two), and the k-steps whose inputs are all padding are skipped: W1 reads 2 of 4, the input-gradient
+// products of W3 and W0 1 and 2 of 4. The matrices are permuted to match when a layer is staged (a
+// dense layer's output order is the A operand's row order, free to choose). Identity layout otherwise.
+template <bool PK> __device__ __forceinline__ int nv_xpos(int c) { return PK ? 4 * c : c; }
+template <bool PK> __device__ __forceinline__ int nv_tpos(int e) { return PK ? 4 * (e / 3) + 1 + e % 3 : e; }
+template <bool PK> __device__ __forceinline__ int nv_hpos(int o) { return PK ? 4 * (o / 2) + o % 2 : o; }
+// inverses: position -> component, or -1 (padding); n = the component count
+template <bool PK> __device__ __forceinline__ int nv_xinv(int p, int n) {
+  const int c = PK ? ((p & 3) == 0 ? p >> 2 : -1) : p;
+  return c < n ? c : -1;
+}
+template <bool PK> __device__ __forceinline__ int nv_tinv(int p, int n) {
+  const int e = PK ? ((p & 3) != 0 ? 3 * (p >> 2) + (p & 3) - 1 : -1) : p;
+  return e < n ? e : -1;
+}
+template <bool PK> __device__ __forceinline__ int nv_hinv(int p) {
+  const int o = PK ? ((p & 3) < 2 ? 2 * (p >> 2) + (p & 3) : -1) : p;
+  return o < 8 ? o : -1;
+}
+
 __device__ __forceinline__ f32x4 nv_vec(const float* b, const NvLane& ln) {
   return *reinterpret_cast<const f32x4*>(b + 4 * ln.g);
 }
@@ -220,9 +250,12 @@ __device__ __forceinline__ void nv_wave_sync() { asm volatile("" ::: "memory"); 
 // kNvT independent MFMAs, so the accumulation chains of the tiles interleave.
 typedef f32x4 NvV[kNvT];
 
+// k-steps j with JM bit j clear carry only padding inputs (all zero) and are skipped.
+template <int JM = 0xF>
 __device__ __forceinline__ void nv_fwdT(const float* W, const NvLane& ln, const NvV& x, NvV& c) {
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
+    if (!((JM >> j) & 1)) continue;
     const float av = W[(4 * ln.g + j) * kNvWS + ln.s];
 #pragma unroll
     for (int u = 0; u < kNvT; ++u) c[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, x[u][j], c[u], 0, 0, 0);
@@ -263,17 +296,31 @@ struct NvAct {
   NvV h0, h1, h2;
 };
 
+// Packed layout: the net input [xm | temb] as one vector (register 0 from xm, 1..3 from temb).
+__device__ __forceinline__ void nv_join(const NvV& xm, const NvV& temb, NvV& in) {
+#pragma unroll
+  for (int u = 0; u < kNvT; ++u) in[u] = f32x4{xm[u][0], temb[u][1], temb[u][2], temb[u][3]};
+}
+
 // BasicMLP (:97-111) forward: input [temb | xm], hidden 8 / 16 / 16, output d (all padded to 16).
+// Packed layout: the first layer is one product over the joined input, stored at W0T.
+template <bool PK>
 __device__ __forceinline__ void nv_mlp_fwd(const float* p, const NvLane& ln, const NvV& temb, const NvV& xm,
                                            NvAct& h, NvV& out) {
   NvV z;
   nv_bcast(z, nv_vec(p + NvM::B0, ln));
-  nv_fwdT(p + NvM::W0T, ln, temb, z);
-  nv_fwdT(p + NvM::W0X, ln, xm, z);
+  if constexpr (PK) {
+    NvV in;
+    nv_join(xm, temb, in);
+    nv_fwdT(p + NvM::W0T, ln, in, z);
+  } else {
+    nv_fwdT(p + NvM::W0T, ln, temb, z);
+    nv_fwdT(p + NvM::W0X, ln, xm, z);
+  }
 #pragma unroll
   for (int u = 0; u < kNvT; ++u) h.h0[u] = nv_celu4(z[u]);
   nv_bcast(z, nv_vec(p + NvM::B1, ln));
-  nv_fwdT(p + NvM::W1, ln, h.h0, z);
+  nv_fwdT<PK ? 0x3 : 0xF>(p + NvM::W1, ln, h.h0, z);
 #pragma unroll
   for (int u = 0; u < kNvT; ++u) h.h1[u] = nv_celu4(z[u]);
   nv_bcast(z, nv_vec(p + NvM::B2, ln));
@@ -286,6 +333,8 @@ __device__ __forceinline__ void nv_mlp_fwd(const float* p, const NvLane& ln, con
 
 // BasicMLP backward from d(out): parameter gradients into acc, input gradients added to gtemb
 // (time rows) and gx (x rows). The input-gradient products W d read the transposed copies.
+// Packed layout: acc.w0t holds the joined first-layer gradient (acc.w0x unused).
+template <bool PK>
 __device__ __forceinline__ void nv_mlp_bwd(const float* p, const NvLane& ln, float* stage, const NvV& temb,
                                            const NvV& xm, const NvAct& h, const NvV& dout, NvNetAcc& acc,
                                            NvV& gtemb, NvV& gx) {
@@ -293,7 +342,7 @@ __device__ __forceinline__ void nv_mlp_bwd(const float* p, const NvLane& ln, flo
   NvV d, e;
   acc.w3 = nv_wgrad(stage, ln, h.h2, dout, acc.w3);
   nv_bcast(e, z4);
-  nv_fwdT(p + NvM::TR + NvM::W3, ln, dout, e);
+  nv_fwdT<PK ? 0x1 : 0xF>(p + NvM::TR + NvM::W3, ln, dout, e);
 #pragma unroll
   for (int u = 0; u < kNvT; ++u) {
     acc.b3 += dout[u];
@@ -315,12 +364,28 @@ __device__ __forceinline__ void nv_mlp_bwd(const float* p, const NvLane& ln, flo
     acc.b1 += d[u];
     d[u] = nv_dact4(e[u], h.h0[u]);
   }
-  acc.w0t = nv_wgrad(stage, ln, temb, d, acc.w0t);
-  acc.w0x = nv_wgrad(stage, ln, xm, d, acc.w0x);
+  if constexpr (PK) {
+    NvV in;
+    nv_join(xm, temb, in);
+    acc.w0t = nv_wgrad(stage, ln, in, d, acc.w0t);
 #pragma unroll
-  for (int u = 0; u < kNvT; ++u) acc.b0 += d[u];
-  nv_fwdT(p + NvM::TR + NvM::W0T, ln, d, gtemb);
-  nv_fwdT(p + NvM::TR + NvM::W0X, ln, d, gx);
+    for (int u = 0; u < kNvT; ++u) acc.b0 += d[u];
+    nv_bcast(e, z4);
+    nv_fwdT<0x3>(p + NvM::TR + NvM::W0T, ln, d, e);
+#pragma unroll
+    for (int u = 0; u < kNvT; ++u) {
+      gx[u][0] += e[u][0];
+#pragma unroll
+      for (int c = 1; c < 4; ++c) gtemb[u][c] += e[u][c];
+    }
+  } else {
+    acc.w0t = nv_wgrad(stage, ln, temb, d, acc.w0t);
+    acc.w0x = nv_wgrad(stage, ln, xm, d, acc.w0x);
+#pragma unroll
+    for (int u = 0; u < kNvT; ++u) acc.b0 += d[u];
+    nv_fwdT(p + NvM::TR + NvM::W0T, ln, d, gtemb);
+    nv_fwdT(p + NvM::TR + NvM::W0X, ln, d, gx);
+  }
 }
 
 // Sum of v over the 16 samples of each component group: DPP inside 16-lane rows (quad_perm xor 1,
@@ -350,9 +415,10 @@ __device__ __forceinline__ void nv_put_vec(float* r, const NvLane& ln, const f32
   const f32x4 t = nv_sum16(v);
   if (ln.s == 0) *reinterpret_cast<f32x4*>(r + 4 * ln.g) = t;
 }
+template <bool PK>
 __device__ __forceinline__ void nv_put_net(float* r, const NvLane& ln, const NvNetAcc& a) {
   nv_put_mat(r + NvR::W0T, ln, a.w0t);
-  nv_put_mat(r + NvR::W0X, ln, a.w0x);
+  if constexpr (!PK) nv_put_mat(r + NvR::W0X, ln, a.w0x);
   nv_put_mat(r + NvR::W1, ln, a.w1);
   nv_put_mat(r + NvR::W2, ln, a.w2);
   nv_put_mat(r + NvR::W3, ln, a.w3);
@@ -363,16 +429,18 @@ __device__ __forceinline__ void nv_put_net(float* r, const NvLane& ln, const NvN
 }
 
 // Flat (reference-order) parameter f of one BasicMLP -> its index in the flush block, or -1.
+template <bool PK>
 __device__ __forceinline__ int nv_net_src(int f, int d, int n_t) {
   const int n_in = d + n_t;
   if (f < n_in * 8) {
-    const int r = f / 8, o = f - r * 8;
+    const int r = f / 8, o = nv_hpos<PK>(f - r * 8);
+    if (PK) return NvR::W0T + (r < d ? nv_xpos<PK>(r) : nv_tpos<PK>(r - d)) * 16 + o;
     return r < d ? NvR::W0X + r * 16 + o : NvR::W0T + (r - d) * 16 + o;
   }
   f -= n_in * 8;
-  if (f < 8) return NvR::B0 + f;
+  if (f < 8) return NvR::B0 + nv_hpos<PK>(f);
   f -= 8;
-  if (f < 128) return NvR::W1 + (f / 16) * 16 + f % 16;
+  if (f < 128) return NvR::W1 + nv_hpos<PK>(f / 16) * 16 + f % 16;
   f -= 128;
   if (f < 16) return NvR::B1 + f;
   f -= 16;
@@ -380,13 +448,49 @@ __device__ __forceinline__ int nv_net_src(int f, int d, int n_t) {
   f -= 256;
   if (f < 16) return NvR::B2 + f;
   f -= 16;
-  if (f < 16 * d) return NvR::W3 + (f / d) * 16 + f % d;
+  if (f < 16 * d) return NvR::W3 + (f / d) * 16 + nv_xpos<PK>(f % d);
   f -= 16 * d;
-  return f < d ? NvR::B3 + f : -1;
+  return f < d ? NvR::B3 + nv_xpos<PK>(f) : -1;
 }
 
-template <int ACT>
-__global__ __launch_bounds__(kBlock, 2) void realnvp_grad_kernel(NvpArgs a, int d, const float* __restrict__ params,
+// Raw coupling-layer parameter k (reference order: sf, s-net, t-net) -> its LDS position(s) in the padded layer
+// image: dst | dstT << 16 (the transposed copy of a matrix entry; 0xFFFF for vectors). Layer-invariant, so a
+// block computes it once and every staging is a scatter of the prefetched registers through this table.
+template <bool PK>
+__device__ __forceinline__ uint32_t nv_layer_dst(int k, int d, int n_t) {
+  const int n_in = d + n_t, mlp_n = n_in * 8 + 8 + 8 * 16 + 16 + 16 * 16 + 16 + 16 * d + d;
+  if (k < d) return (uint32_t)(NvM::SF + nv_xpos<PK>(k)) | 0xFFFF0000u;
+  k -= d;
+  const int net = k >= mlp_n ? 1 : 0;
+  int f = k - net * mlp_n;
+  const int base = net ? NvM::TNET : NvM::SNET;
+  auto mat = [&](int M, int pr, int pc) {
+    return (uint32_t)(base + M + pr * kNvWS + pc) | ((uint32_t)(base + NvM::TR + M + pc * kNvWS + pr) << 16);
+  };
+  auto vec = [&](int B, int p) { return (uint32_t)(base + B + p) | 0xFFFF0000u; };
+  if (f < n_in * 8) {
+    const int r = f / 8, o = f - r * 8;
+    if (PK) return mat(NvM::W0T, r < d ? nv_xpos<PK>(r) : nv_tpos<PK>(r - d), nv_hpos<PK>(o));
+    return r < d ? mat(NvM::W0X, r, o) : mat(NvM::W0T, r - d, o);
+  }
+  f -= n_in * 8;
+  if (f < 8) return vec(NvM::B0, nv_hpos<PK>(f));
+  f -= 8;
+  if (f < 128) return mat(NvM::W1, nv_hpos<PK>(f / 16), f % 16);
+  f -= 128;
+  if (f < 16) return vec(NvM::B1, f);
+  f -= 16;
+  if (f < 256) return mat(NvM::W2, f / 16, f % 16);
+  f -= 256;
+  if (f < 16) return vec(NvM::B2, f);
+  f -= 16;
+  if (f < 16 * d) return mat(NvM::W3, f / d, nv_xpos<PK>(f % d));
+  f -= 16 * d;
+  return vec(NvM::B3, nv_xpos<PK>(f));
+}
+
+template <int ACT, bool PK>
+__global__ __launch_bounds__(kBlock, PDEINV_NVW) void realnvp_grad_kernel(NvpArgs a, int d, const float* __restrict__ params,
                                                                  const float* __restrict__ tv, int64_t t_stride,
                                                                  const float* __restrict__ xv, int64_t n, int64_t ld,
                                                                  int64_t layer_stride, int64_t n_params,
@@ -401,7 +505,7 @@ __global__ __launch_bounds__(kBlock, 2) void realnvp_grad_kernel(NvpArgs a, int 
   // per-wave wgrad stages during the tile math, per-wave flush blocks after it (a barrier between)
   constexpr int kScr = NvR::SIZE > kNvT * 2 * 16 * kNvWS ? NvR::SIZE : kNvT * 2 * 16 * kNvWS;
   __shared__ float sScr[kWavesPerBlock][kScr];
-  __shared__ float sRaw[kNvRaw];
+  __shared__ uint32_t sDst[kNvRaw];                  // raw layer parameter -> LDS position(s), nv_layer_dst
   __shared__ short sMap[2 * (24 * 8 + 8 + 128 + 16 + 256 + 16 + 16 * 8 + 8)];  // flat net param -> NvR index
   const int E = a.E;
   const int n_in = a.in_dim, n_t = n_in - d;
@@ -420,21 +524,31 @@ __global__ __launch_bounds__(kBlock, 2) void realnvp_grad_kernel(NvpArgs a, int 
   float* stage = sScr[wave];
   float* red = sScr[wave];
   // ---- per-block tables ----
-  auto put_mat = [&](float* dst, float* dst_t, const float* src, int rows, int cols, int ld_src) {
-    for (int q = tid; q < 16 * kNvWS; q += kBlock) {  // padded [16][kNvWS], and its transpose
+  // padded [16][kNvWS] (and its transpose): position (r, c) <- src[rm(r)][cm(c)], 0 where a map gives -1
+  auto put_mat = [&](float* dst, float* dst_t, const float* src, int ld_src, auto rm, auto cm) {
+    for (int q = tid; q < 16 * kNvWS; q += kBlock) {
       const int r = q / kNvWS, c = q - r * kNvWS;
-      dst[q] = (r < rows && c < cols) ? src[r * ld_src + c] : 0.f;
-      if (dst_t) dst_t[q] = (c < rows && r < cols) ? src[c * ld_src + r] : 0.f;
+      const int sr = c < 16 ? rm(r) : -1, sc = c < 16 ? cm(c) : -1;
+      dst[q] = (sr >= 0 && sc >= 0) ? src[sr * ld_src + sc] : 0.f;
+      if (dst_t) {
+        const int tr = c < 16 ? rm(c) : -1, tc = c < 16 ? cm(r) : -1;
+        dst_t[q] = (tr >= 0 && tc >= 0) ? src[tr * ld_src + tc] : 0.f;
+      }
     }
   };
-  auto put_vec = [&](float* dst, const float* src, int len) {
-    for (int q = tid; q < 16; q += kBlock) dst[q] = q < len ? src[q] : 0.f;
+  auto put_vec = [&](float* dst, const float* src, auto m) {
+    for (int q = tid; q < 16; q += kBlock) {
+      const int k = m(q);
+      dst[q] = k >= 0 ? src[k] : 0.f;
+    }
   };
+  auto idn = [](int len) { return [len](int p) { return p < len ? p : -1; }; };
   if (E > 0) {
-    put_mat(sT + NvM::E_W1, nullptr, params, E, E, E);
-    put_vec(sT + NvM::E_B1, params + E * E, E);
-    put_mat(sT + NvM::E_W2, sT + NvM::E_W2T, params + E * E + E, E, E, E);
-    put_vec(sT + NvM::E_B2, params + 2 * E * E + E, E);
+    auto tmap = [E](int p) { return nv_tinv<PK>(p, E); };
+    put_mat(sT + NvM::E_W1, nullptr, params, E, idn(E), idn(E));
+    put_vec(sT + NvM::E_B1, params + E * E, idn(E));
+    put_mat(sT + NvM::E_W2, sT + NvM::E_W2T, params + E * E + E, E, idn(E), tmap);  // temb at its positions
+    put_vec(sT + NvM::E_B2, params + 2 * E * E + E, tmap);
   }
   if (tid < 16) {
     const int half = E / 2;
@@ -445,24 +559,27 @@ __global__ __launch_bounds__(kBlock, 2) void realnvp_grad_kernel(NvpArgs a, int 
     sF[16 + tid] = on && is_sin ? 1.f : 0.f;
     sF[32 + tid] = on && !is_sin ? 1.f : 0.f;
   }
-  for (int f = tid; f < mlp_n; f += kBlock) sMap[f] = (short)nv_net_src(f, d, n_t);
+  for (int f = tid; f < mlp_n; f += kBlock) sMap[f] = (short)nv_net_src<PK>(f, d, n_t);
+  for (int k = tid; k < layer_stride; k += kBlock) sDst[k] = nv_layer_dst<PK>(k, d, n_t);
+  for (int q = tid; q < NvM::LAYER; q += kBlock) sW[q] = 0.f;  // padding: never written again
   for (int q = tid; q < a.n_layers * 16; q += kBlock) {
-    const int l = q / 16, k = q % 16;
-    sM[q] = k < d ? a.masks[l * d + k] : 1.f;
+    const int l = q / 16, k = nv_xinv<PK>(q % 16, d);
+    sM[q] = k >= 0 ? a.masks[l * d + k] : 1.f;
   }
-  for (int q = tid; q < 16 + 256; q += kBlock) {
+  for (int q = tid; q < 16 + 256; q += kBlock) {  // mean at the x positions; inv_cov rows by position, columns by coordinate
     float v = 0.f;
     if (q < 16) {
-      v = q < d ? a.mean[q] : 0.f;
+      const int k = nv_xinv<PK>(q, d);
+      v = k >= 0 ? a.mean[k] : 0.f;
     } else {
-      const int r = (q - 16) / 16, c = (q - 16) % 16;
-      v = (r < d && c < d) ? a.inv_cov[r * d + c] : 0.f;
+      const int r = nv_xinv<PK>((q - 16) / 16, d), c = (q - 16) % 16;
+      v = (r >= 0 && c < d) ? a.inv_cov[r * d + c] : 0.f;
     }
     sB[q] = v;
   }
   // Layer parameters are prefetched one staged layer ahead into registers (one coalesced load per
-  // thread and slot, in flight under the previous layer's math), dropped into sRaw, then expanded
-  // LDS -> LDS into the padded / transposed layout. Staging order: L-1 .. 0 (likelihood), 0 .. L-1.
+  // thread and slot, in flight under the previous layer's math) and scattered into the padded /
+  // transposed layer image through the sDst table. Staging order: L-1 .. 0 (likelihood), 0 .. L-1.
   float pre[kNvPre];
   auto prefetch = [&](int l) {
     const float* lp = layers + (int64_t)l * layer_stride;
@@ -473,33 +590,19 @@ __global__ __launch_bounds__(kBlock, 2) void realnvp_grad_kernel(NvpArgs a, int 
     }
   };
   int staged = 0;  // layers staged so far
-  auto stage_layer = [&](int l) {
-    __syncthreads();
+  auto stage_layer = [&](int) {
+    __syncthreads();  // every wave is done with the previous layer
 #pragma unroll
     for (int k = 0; k < kNvPre; ++k) {
       const int q = tid + k * kBlock;
-      if (q < layer_stride) sRaw[q] = pre[k];
+      if (q < layer_stride) {
+        const uint32_t t = sDst[q];
+        sW[t & 0xFFFFu] = pre[k];
+        if ((t >> 16) != 0xFFFFu) sW[t >> 16] = pre[k];
+      }
     }
-    __syncthreads();
     ++staged;
     if (staged < 2 * a.n_layers) prefetch(staged < a.n_layers ? a.n_layers - 1 - staged : staged - a.n_layers);
-    const float* lp = sRaw;
-    put_vec(sW + NvM::SF, lp, d);
-#pragma unroll 1
-    for (int net = 0; net < 2; ++net) {
-      const float* np = lp + d + net * mlp_n;
-      float* w = sW + (net ? NvM::TNET : NvM::SNET);
-      put_mat(w + NvM::W0X, w + NvM::TR + NvM::W0X, np, d, 8, 8);
-      put_mat(w + NvM::W0T, w + NvM::TR + NvM::W0T, np + d * 8, n_t, 8, 8);
-      put_vec(w + NvM::B0, np + n_in * 8, 8);
-      const float* q = np + n_in * 8 + 8;
-      put_mat(w + NvM::W1, w + NvM::TR + NvM::W1, q, 8, 16, 16);
-      put_vec(w + NvM::B1, q + 128, 16);
-      put_mat(w + NvM::W2, w + NvM::TR + NvM::W2, q + 144, 16, 16, 16);
-      put_vec(w + NvM::B2, q + 400, 16);
-      put_mat(w + NvM::W3, w + NvM::TR + NvM::W3, q + 416, 16, d, d);
-      put_vec(w + NvM::B3, q + 416 + 16 * d, d);
-    }
     __syncthreads();
   };
   prefetch(a.n_layers - 1);
@@ -529,8 +632,8 @@ __global__ __launch_bounds__(kBlock, 2) void realnvp_grad_kernel(NvpArgs a, int 
     tt[u] = active ? tv[i * t_stride] : 0.f;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      const int k = 4 * ln.g + c;
-      x[u][c] = (active && k < d) ? xv[i * ld + k] : 0.f;
+      const int k = nv_xinv<PK>(4 * ln.g + c, d);
+      x[u][c] = (active && k >= 0) ? xv[i * ld + k] : 0.f;
       gtemb[u][c] = 0.f;
     }
     ldj[u] = 0.f;
@@ -559,7 +662,7 @@ __global__ __launch_bounds__(kBlock, 2) void realnvp_grad_kernel(NvpArgs a, int 
 #pragma unroll
     for (int u = 0; u < kNvT; ++u)
 #pragma unroll
-      for (int c = 0; c < 4; ++c) temb[u][c] = (!a.ignore_time && ln.g == 0 && c == 0) ? tt[u] : 0.f;
+      for (int c = 0; c < 4; ++c) temb[u][c] = (!a.ignore_time && 4 * ln.g + c == nv_tpos<PK>(0)) ? tt[u] : 0.f;
   }
   // ---- likelihood pass (layers L-1 .. 0): x <- (x + tr) e^s ----
   for (int l = a.n_layers - 1; l >= 0; --l) {
@@ -576,8 +679,8 @@ __global__ __launch_bounds__(kBlock, 2) void realnvp_grad_kernel(NvpArgs a, int 
     for (int u = 0; u < kNvT; ++u) xm[u] = x[u] * m;
     {
       NvAct h;
-      nv_mlp_fwd(sW + NvM::SNET, ln, temb, xm, h, so);
-      nv_mlp_fwd(sW + NvM::TNET, ln, temb, xm, h, to);
+      nv_mlp_fwd<PK>(sW + NvM::SNET, ln, temb, xm, h, so);
+      nv_mlp_fwd<PK>(sW + NvM::TNET, ln, temb, xm, h, to);
     }
 #pragma unroll
     for (int u = 0; u < kNvT; ++u) {
@@ -603,7 +706,7 @@ __global__ __launch_bounds__(kBlock, 2) void realnvp_grad_kernel(NvpArgs a, int 
     for (int c = 0; c < 4; ++c) {
       const int r = 4 * ln.g + c;
       float acc = 0.f;
-      for (int q = 0; q < d; ++q) acc = fmaf(sB[16 + r * 16 + q], stage[ln.s * kNvWS + q], acc);
+      for (int q = 0; q < d; ++q) acc = fmaf(sB[16 + r * 16 + q], stage[ln.s * kNvWS + nv_xpos<PK>(q)], acc);
       quad = fmaf(diff[c], acc, quad);
       gx[u][c] = -w[u] * acc;
     }
@@ -631,7 +734,7 @@ __global__ __launch_bounds__(kBlock, 2) void realnvp_grad_kernel(NvpArgs a, int 
     NvAct h;
 #pragma unroll
     for (int u = 0; u < kNvT; ++u) xm[u] = x[u] * m;
-    nv_mlp_fwd(sW + NvM::SNET, ln, temb, xm, h, out);
+    nv_mlp_fwd<PK>(sW + NvM::SNET, ln, temb, xm, h, out);
 #pragma unroll
     for (int u = 0; u < kNvT; ++u) {
 #pragma unroll
@@ -650,9 +753,9 @@ __global__ __launch_bounds__(kBlock, 2) void realnvp_grad_kernel(NvpArgs a, int 
         gacc[u][c] = 0.f;
       }
     }
-    nv_mlp_bwd(sW + NvM::SNET, ln, stage, temb, xm, h, gso, as, gtemb, gacc);
-    nv_mlp_fwd(sW + NvM::TNET, ln, temb, xm, h, out);
-    nv_mlp_bwd(sW + NvM::TNET, ln, stage, temb, xm, h, gto, at, gtemb, gacc);
+    nv_mlp_bwd<PK>(sW + NvM::SNET, ln, stage, temb, xm, h, gso, as, gtemb, gacc);
+    nv_mlp_fwd<PK>(sW + NvM::TNET, ln, temb, xm, h, out);
+    nv_mlp_bwd<PK>(sW + NvM::TNET, ln, stage, temb, xm, h, gto, at, gtemb, gacc);
 #pragma unroll
     for (int u = 0; u < kNvT; ++u)
 #pragma unroll
@@ -662,10 +765,10 @@ __global__ __launch_bounds__(kBlock, 2) void realnvp_grad_kernel(NvpArgs a, int 
         gx[u][c] = gx[u][c] * es[u][c] + m[c] * gacc[u][c];
       }
     __syncthreads();  // every wave is done with its stage (the flush blocks alias it)
-    nv_put_net(red, ln, as);
+    nv_put_net<PK>(red, ln, as);
     nv_put_vec(red + NvR::SF, ln, galpha);
-    flush(loff, d + mlp_n, [&](int f) { return f < d ? NvR::SF + f : (int)sMap[f - d]; });  // sf, s-net
-    nv_put_net(red, ln, at);
+    flush(loff, d + mlp_n, [&](int f) { return f < d ? NvR::SF + nv_xpos<PK>(f) : (int)sMap[f - d]; });  // sf, s-net
+    nv_put_net<PK>(red, ln, at);
     flush(loff + d + mlp_n, mlp_n, [&](int f) { return (int)sMap[f]; });  // t-net
   }
   // ---- time-embedding backward and the loss column ----
@@ -695,8 +798,9 @@ __global__ __launch_bounds__(kBlock, 2) void realnvp_grad_kernel(NvpArgs a, int 
     const int EE = E * E + E;
     flush(0, 2 * EE, [&](int f) {
       const int part = f >= EE, r = f - part * EE;
-      const int o = part * 272;
-      return r < E * E ? o + (r / E) * 16 + r % E : o + 256 + (r - E * E);
+      const int o = part * 272;  // W2 / b2 columns at the temb positions
+      if (r < E * E) return o + (r / E) * 16 + (part ? nv_tpos<PK>(r % E) : r % E);
+      return o + 256 + (part ? nv_tpos<PK>(r - E * E) : r - E * E);
     });
   }
   lsum += __shfl_xor(lsum, 1, 64);
@@ -867,12 +971,19 @@ extern "C" int pdeinv_realnvp_value_and_grad(const pdeinv_realnvp_desc* d, const
   double* parts = acc64 + (P + 1);
   hipStream_t st = (hipStream_t)stream;
   const int64_t tiles = (n + kNvSPB - 1) / kNvSPB;
-  // any d <= 8 (padded coordinates stay fixed); celu and elu are the same map.
+  // any d <= 8 (padded coordinates stay fixed); celu and elu are the same map. Packed layout where
+  // [x | temb] fits one 16-vector with x in register 0 (PDEINV_NVP_PACK=0 forces the identity layout, A/B).
+  static const bool pack_env = [] { const char* e = getenv("PDEINV_NVP_PACK"); return !(e && e[0] == '0'); }();
+  const bool packed = pack_env && D <= 4 && a.in_dim - D <= 12;
   for (int64_t tile0 = 0; tile0 < tiles; tile0 += rows_max) {
     const int64_t rows = tiles - tile0 < rows_max ? tiles - tile0 : rows_max;
     const dim3 g((unsigned)rows);
-    hipLaunchKernelGGL((realnvp_grad_kernel<PDEINV_ACT_CELU>), g, dim3(kBlock), 0, st, a, D, params, t, t_stride, x,
-                       n, ld, ls, P, tile0, slab, P + 1);
+    if (packed)
+      hipLaunchKernelGGL((realnvp_grad_kernel<PDEINV_ACT_CELU, true>), g, dim3(kBlock), 0, st, a, D, params, t,
+                         t_stride, x, n, ld, ls, P, tile0, slab, P + 1);
+    else
+      hipLaunchKernelGGL((realnvp_grad_kernel<PDEINV_ACT_CELU, false>), g, dim3(kBlock), 0, st, a, D, params, t,
+                         t_stride, x, n, ld, ls, P, tile0, slab, P + 1);
     int rc = check_launch("realnvp_grad_kernel");
     if (rc) return rc;
     hipLaunchKernelGGL(nvp_slab_split_kernel, dim3((unsigned)((P + 1 + 63) / 64), kNvSplits), dim3(kBlock), 0, st,
