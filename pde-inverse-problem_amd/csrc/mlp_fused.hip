@@ -817,40 +817,45 @@ bool rgemm_shape(int K, int N) { return K % 64 == 0 && K <= 256 && N % kRBN == 0
 // V (schedule variant, A/B): 0 = Bt b128 reads, compiler schedule; 1 = + one fenced region per tile
 // (prefetch one tile ahead); 2 = + loads / layer-1 VALU interleaved one per MFMA; 3 = Bs[k][n] with one
 // ds_read_b32 per k-step and column tile, compiler schedule.
-template <int S, int NI, int AM, int BMD, int EM, int D = 0, int V = 0>
+// BNC = block columns: 128 for the W x W layers; 64 for the output layer (N = out_features <= 64, one
+// column block, columns past N zero in the staged B and never stored; E_OUT reduces a row's outputs
+// inside one wave, E_SEEDS writes the seeds and the bias-gradient column sums).
+template <int S, int NI, int AM, int BMD, int EM, int D = 0, int V = 0, int BNC = kRBN>
 __global__ __launch_bounds__(kRT, 1) void rgemm(GemmArgs a) {
-  constexpr int WGN = kRBN / (32 * NI), WGM = 8 / WGN, BMR = 32 * WGM;  // waves along N / M, block rows
-  static_assert((NI == 2 || NI == 4) && WGN * WGM == 8, "rgemm wave grid");
+  constexpr int WGN = BNC / (32 * NI), WGM = 8 / WGN, BMR = 32 * WGM;  // waves along N / M, block rows
+  static_assert((NI == 2 || NI == 4) && WGN >= 1 && WGN * WGM == 8, "rgemm wave grid");
+  static_assert(EM != E_OUT || WGN == 1, "E_OUT reduces each row inside one wave");
   constexpr bool L1 = a_is_l1<AM>();
   constexpr int NV = rg_planes<AM>();
   constexpr int SK = L1 ? k1_stride<D>() : 1;
-  constexpr int NP = (EM == E_ACT_BWD) ? 1 : 0;
+  constexpr int NP = (EM == E_ACT_BWD || EM == E_SEEDS) ? 1 : 0;
   static_assert(!L1 || D > 0, "layer-1 modes need D");
-  static_assert(EM == E_ACT_FWD || EM == E_STORE || EM == E_STORE3 || EM == E_ACT_BWD, "rgemm epilogues");
+  static_assert(EM == E_ACT_FWD || EM == E_STORE || EM == E_STORE3 || EM == E_ACT_BWD || EM == E_OUT ||
+                    EM == E_SEEDS, "rgemm epilogues");
   extern __shared__ float lds[];
   const int Kp = a.K + 4;                          // Bt row pitch: ds_read_b128 of 16 lanes' rows conflict-free
-  float* Bt = lds;                                 // [kRBN][Kp]: Bt[n][k] = B[k][n0 + n]  (V = 3: [K][kRBN + 1])
-  [[maybe_unused]] float* k1s = Bt + (V == 3 ? (size_t)a.K * (kRBN + 1) : (size_t)kRBN * Kp);  // L1: [K][SK]
+  float* Bt = lds;                                 // [BNC][Kp]: Bt[n][k] = B[k][n0 + n]  (V = 3: [K][BNC + 1])
+  [[maybe_unused]] float* k1s = Bt + (V == 3 ? (size_t)a.K * (BNC + 1) : (size_t)BNC * Kp);  // L1: [K][SK]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WGN, wn = wave % WGN, l31 = lane & 31, hi = lane >> 5;
   const int K = a.K, N = a.N;
-  const int ncb = N / kRBN;
+  const int ncb = (N + BNC - 1) / BNC;
   const int lid = xcd_linear(blockIdx.x, gridDim.x);  // the column blocks of a row stream adjacent: same XCD
   const int cb = lid % ncb, rs = lid / ncb, nrs = gridDim.x / ncb;
-  const int n0 = cb * kRBN;
-  for (int e = tid; e < K * kRBN; e += kRT) {
+  const int n0 = cb * BNC;
+  for (int e = tid; e < K * BNC; e += kRT) {
     int k, n;
     float v;
     if constexpr (BMD == B_NN) {
-      k = e / kRBN;
-      n = e - k * kRBN;
-      v = a.Bw[(size_t)k * N + n0 + n];
+      k = e / BNC;
+      n = e - k * BNC;
+      v = n0 + n < N ? a.Bw[(size_t)k * N + n0 + n] : 0.f;
     } else {
       n = e / K;
       k = e - n * K;
-      v = a.Bw[(size_t)(n0 + n) * K + k];
+      v = n0 + n < N ? a.Bw[(size_t)(n0 + n) * K + k] : 0.f;
     }
-    if constexpr (V == 3) Bt[k * (kRBN + 1) + n] = v;
+    if constexpr (V == 3) Bt[k * (BNC + 1) + n] = v;
     else Bt[n * Kp + k] = v;
   }
   if constexpr (L1) {
@@ -923,6 +928,7 @@ __global__ __launch_bounds__(kRT, 1) void rgemm(GemmArgs a) {
           // (j & 3) + 8 (j >> 2) + 4 hi, i.e. 16-byte runs at 4 hi + 8 j
           const int ko = L1 ? 4 * hi + 8 * j : 16 * hi + 4 * j;
           const f32x4 v = *reinterpret_cast<const f32x4*>(Bt + (wn * 32 * NI + ni * 32 + l31) * Kp + kt * 32 + ko);
+          static_assert(V != 3 || BNC == kRBN, "V = 3 layout: 128 columns");
           bt[ni][4 * j] = v[0]; bt[ni][4 * j + 1] = v[1]; bt[ni][4 * j + 2] = v[2]; bt[ni][4 * j + 3] = v[3];
         }
       // layer-1 modes: the pre-activations of the lane's row for the tile's 32 k on the matrix pipe,
@@ -987,7 +993,7 @@ __global__ __launch_bounds__(kRT, 1) void rgemm(GemmArgs a) {
         if constexpr (V == 3) {
 #pragma unroll
           for (int ni = 0; ni < NI; ++ni)
-            bt[ni][s] = Bt[(kt * 32 + 16 * hi + s) * (kRBN + 1) + wn * 32 * NI + ni * 32 + l31];
+            bt[ni][s] = Bt[(kt * 32 + 16 * hi + s) * (BNC + 1) + wn * 32 * NI + ni * 32 + l31];
         }
 #pragma unroll
         for (int si = 0; si < S; ++si)
@@ -1031,15 +1037,21 @@ __global__ __launch_bounds__(kRT, 1) void rgemm(GemmArgs a) {
     const bool full = r0 + BMR <= a.R;
     auto epilogue = [&](auto check) {
       constexpr bool CHECK = decltype(check)::value;
+      [[maybe_unused]] float t0[16], t1[16], t2[16];  // E_OUT: the row's sum y^2, y y', y'^2 + y y''
+      if constexpr (EM == E_OUT) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) t0[q] = t1[q] = t2[q] = 0.f;
+      }
 #pragma unroll
       for (int ni = 0; ni < NI; ++ni) {
         const int n = n0 + wn * 32 * NI + ni * 32 + l31;
+        const bool nv = BNC == kRBN || n < N;  // output-layer blocks: columns past N are padding
         [[maybe_unused]] float bn = 0.f;
-        if constexpr (EM == E_ACT_FWD) bn = a.bias[n];
+        if constexpr (EM == E_ACT_FWD || EM == E_OUT) bn = a.bias[nv ? n : 0];
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
           const int r = r0 + wm * 32 + (q & 3) + 8 * (q >> 2) + 4 * hi;
-          const bool ok = !CHECK || r < a.R;
+          const bool ok = (!CHECK || r < a.R) && nv;
           const uint32_t o = (uint32_t)(r * N + n);
           if constexpr (EM == E_ACT_FWD) {
             if (ok) {
@@ -1054,6 +1066,27 @@ __global__ __launch_bounds__(kRT, 1) void rgemm(GemmArgs a) {
               sto(a.po0, o, acc[0][ni][q]);
               sto(a.po1, o, acc[1][ni][q]);
               sto(a.po2, o, acc[2][ni][q]);
+            }
+          } else if constexpr (EM == E_OUT) {
+            if (ok) {
+              const float y = acc[0][ni][q] + bn, yd = acc[1][ni][q], ydd = acc[2][ni][q];
+              sto(a.po0, o, y);
+              sto(a.po1, o, yd);
+              sto(a.po2, o, ydd);
+              t0[q] = fmaf(y, y, t0[q]);
+              t1[q] = fmaf(y, yd, t1[q]);
+              t2[q] = fmaf(yd, yd, fmaf(y, ydd, t2[q]));
+            }
+          } else if constexpr (EM == E_SEEDS) {
+            if (ok) {
+              const float ub = acc[0][ni][q];
+              const float y = ldo(a.pe0, o), yd = ldo(a.pe1, o), ydd = ldo(a.pe2, o);
+              const float c0r = a.wrow ? a.c0 * a.wrow[(int64_t)r * a.ldw] : a.c0;
+              const float yb = 2.f * a.c3 * yd + 2.f * a.c2 * ydd + 2.f * ub + 2.f * c0r * y;
+              sto(a.po0, o, yb);
+              sto(a.po1, o, 2.f * a.c3 * y + 4.f * a.c2 * yd);
+              sto(a.po2, o, 2.f * a.c2 * y);
+              pacc[ni] += yb;
             }
           } else {  // E_ACT_BWD
             if (ok) {
@@ -1070,6 +1103,20 @@ __global__ __launch_bounds__(kRT, 1) void rgemm(GemmArgs a) {
           }
         }
       }
+      if constexpr (EM == E_OUT) {  // per-row reductions over the 32 lanes of each half-wave
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          float p0 = t0[q], p1 = t1[q], p2 = t2[q];
+#pragma unroll
+          for (int off = 16; off > 0; off >>= 1) {
+            p0 += __shfl_xor(p0, off, 64);
+            p1 += __shfl_xor(p1, off, 64);
+            p2 += __shfl_xor(p2, off, 64);
+          }
+          const int r = r0 + wm * 32 + (q & 3) + 8 * (q >> 2) + 4 * hi;
+          if (l31 == 0 && r < a.R) a.terms[r] = make_float4(2.f * p1, 2.f * p2, p0, 0.f);
+        }
+      }
     };
     if (full) epilogue(std::false_type{});
     else epilogue(std::true_type{});
@@ -1083,18 +1130,18 @@ __global__ __launch_bounds__(kRT, 1) void rgemm(GemmArgs a) {
   }
   if constexpr (NP > 0) {  // bias-gradient column sums: one slab row per row stream
     __syncthreads();
-    float* red = lds;  // [WGM][kRBN] (Bt is dead)
+    float* red = lds;  // [WGM][BNC] (Bt is dead)
 #pragma unroll
     for (int ni = 0; ni < NI; ++ni) {
       const float v = pacc[ni] + __shfl_xor(pacc[ni], 32, 64);
-      if (hi == 0) red[wm * kRBN + wn * 32 * NI + ni * 32 + l31] = v;
+      if (hi == 0) red[wm * BNC + wn * 32 * NI + ni * 32 + l31] = v;
     }
     __syncthreads();
-    for (int c = tid; c < kRBN; c += kRT) {
+    for (int c = tid; c < BNC; c += kRT) {
       float t = 0.f;
 #pragma unroll
-      for (int w = 0; w < WGM; ++w) t += red[w * kRBN + c];
-      a.part[(int64_t)rs * N + n0 + c] = t;
+      for (int w = 0; w < WGM; ++w) t += red[w * BNC + c];
+      if (n0 + c < N) a.part[(int64_t)rs * N + n0 + c] = t;
     }
   }
 }
@@ -1348,6 +1395,30 @@ static int launch_wgrad2(WgradArgs a, float* grad_out, float* scratch, hipStream
 
 // B-resident row GEMMs / LDS-free weight gradients for W in {128, 256} (PDEINV_MLP_RGEMM=0: the
 // staged fgemm / fwgrad kernels, for A/B measurements)
+// The output layer (K = W, N = out_features <= 64) on the B-resident kernel: one 64-column block, 8 waves
+// of 32 rows x 64 columns (NI = 2), row blocks of 256.
+template <int S, int AM, int EM>
+static int launch_rgemm_out(GemmArgs a, hipStream_t st, int* grid_x_out = nullptr) {
+  constexpr int NI = 2, BNC = 64, BMR = 256;
+  if (!(a.K % 64 == 0 && a.K <= 256 && a.N >= 1 && a.N <= BNC))
+    return fail(PDEINV_ERR_INVALID, "kfp_mlp rgemm (output layer): K % 64 == 0, K <= 256, N <= 64");
+  const int V = sched_variant();
+  const size_t bytes = (size_t)BNC * (a.K + 4) * sizeof(float);
+  auto kern = V == 1 ? rgemm<S, NI, AM, B_NN, EM, 0, 1, BNC> : rgemm<S, NI, AM, B_NN, EM, 0, 0, BNC>;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  a.n_mblocks = mblocks(a.R, BMR);
+  const int nrs = std::max(1, std::min(a.n_mblocks, kRGridCap));
+  if (grid_x_out) *grid_x_out = nrs;
+  hipLaunchKernelGGL(kern, dim3(nrs), dim3(kRT), bytes, st, a);
+  return check_launch("kfp_mlp fused B-resident output-layer GEMM");
+}
+
+// PDEINV_MLP_RGEMM_OUT=0: the output-layer products on fgemm (A/B)
+static bool use_rgemm_out() {
+  static const bool on = [] { const char* e = getenv("PDEINV_MLP_RGEMM_OUT"); return !(e && e[0] == '0'); }();
+  return on;
+}
+
 static bool use_rgemm(int W) {
   static const bool off = [] {
     const char* e = getenv("PDEINV_MLP_RGEMM");
@@ -1472,7 +1543,8 @@ static int run_chunk_t(const Chunk& c, const LossHook& loss, hipStream_t st) {
     a.K = W; a.N = O; a.Bw = Ko; a.bias = bo;
     a.pa0 = P(L, P_H); a.pa1 = P(L, P_ZD); a.pa2 = P(L, P_ZDD);
     a.po0 = Ys[0]; a.po1 = Ys[1]; a.po2 = Ys[2]; a.terms = terms;
-    RC((launch_gemm<3, 128, 64, 4, A_FWD, B_NN, E_OUT>(a, st)));
+    if (RG && use_rgemm_out() && O <= 64) RC((launch_rgemm_out<3, A_FWD, E_OUT>(a, st)));
+    else RC((launch_gemm<3, 128, 64, 4, A_FWD, B_NN, E_OUT>(a, st)));
   }
   // ---- R1: grad_x chain -------------------------------------------------------------------
   {
@@ -1514,7 +1586,8 @@ static int run_chunk_t(const Chunk& c, const LossHook& loss, hipStream_t st) {
     a.pe0 = Ys[0]; a.pe1 = Ys[1]; a.pe2 = Ys[2];
     a.po0 = YB[0]; a.po1 = YB[1]; a.po2 = YB[2];
     int gx = 0;
-    RC((launch_gemm<1, 128, 64, 4, A_S1MUL, B_NN, E_SEEDS>(a, st, &gx)));
+    if (RG && use_rgemm_out() && O <= 64) RC((launch_rgemm_out<1, A_S1MUL, E_SEEDS>(a, st, &gx)));
+    else RC((launch_gemm<1, 128, 64, 4, A_S1MUL, B_NN, E_SEEDS>(a, st, &gx)));
     RC(sum_slabs(part, gx, O, c.grad + c.boff[L], part2, st));
   }
   // ---- R2: reverse over the forward streams -------------------------------------------------
