@@ -1,0 +1,911 @@
+// mlp_pairs_mfma.hip — the general-Phi KMV residual for the reference's narrow hypothesis nets on
+// the matrix pipe: 16-pair tiles, every product a v_mfma_f32_16x16x4_f32 (gfx950).
+//
+// Same contract as the register-ring pair kernels of mlp_pairs.hip (which stay for the shapes this
+// file does not cover): for methods/consistency_instances/kinetic_mckean_vlasov.py:11-120 with a
+// non-parametric Phi_theta = V_hypothesis (core/model.py:32-62: tanh layers, Dense(40), sum of
+// squares), every pair (i, j) of a time stamp's particles, y_ij = x_i - x_j (x_minus_ref, :20-23),
+// contributes grad Phi(y_ij) (pass 1: gbar_i = mean_j grad Phi), and pass 2 differentiates
+//     l_ij = u_i . grad Phi(y_ij) + c2 v_i^T Hess Phi(y_ij) v_i + c0_i Phi(y_ij)
+// (u_i = 2 s gbar_i, c2 = -2 s, c0_i = 2 s w_it; s = 1 / (n^2 n_sets); loss assembly :74-97) with
+// respect to theta. Covered: dim <= 8, width <= 20 (zero-padded to 20), 1 <= n_layers <= 8,
+// out_features <= 48 — the reference default is 2 -> 20 x 8 -> 40 (configurations/neural_network/
+// MLP.yaml:4-5, model.py:45-47).
+//
+// Layout. A wave owns 16 pairs (i, j..j+15) of one particle i. Every activation tile is the C/D
+// fragment of a 16x16x4 MFMA: the pair on lane & 15 (the MFMA's N), the feature on (lane >> 4,
+// register) — "P layout". A width-20 layer output is two 16-row M blocks; its 20 real features sit in
+// 5 "compact slots" (registers 0..3 of block 0, register 0 of block 1: block-1 row r = 4g + s holds
+// feature 16 + 4s + g), and because an MFMA's K index is lane >> 4 within a k-step, slot k of the
+// P layout is directly the B operand of k-step k of the next product: layers chain in registers, no
+// LDS, no lane movement (the weights are the A operand, permuted once on the host side of the image).
+//
+// Pass 2 streams (Taylor mode, tanh layers): primal h, first order along u (z'_u), first and second
+// order along v (z'_v, z''_v). Per tanh layer the four pre-activation streams (h, z'_u, z'_v, z''_v)
+// are the whole checkpoint — 20 registers for a 16-pair tile — kept in VGPRs through the reverse sweep
+// (8 layers: 145 VGPRs). Reverse: the four adjoints z-bar from the output seeds; weight gradients
+// sum outer products over pairs, i.e. a contraction over the pair index, which the P layout cannot feed
+// (pairs sit on the MFMA's N lanes): each stream's z-bar and layer input go through a per-wave LDS image
+// [feature][pair] (pitch 24 floats: conflict-free 16-B reads, 2-way-free 4-B writes) and are read back
+// with the pair on the K lanes ("F layout"); the bias gradient rides a constant-1 input row. Tile sums
+// fold into the block's LDS gradient slab (ds_add_f32), copied to a per-block global slab at the end;
+// a fixed-order fp64 reduction over blocks gives the gradient.
+//
+// Weights: one image per call (kmvq_image_kernel), lane-linear A-operand fragments of every product
+// (forward: K^T with rows = outputs; backward: K with rows = inputs), staged once per persistent block
+// into LDS and read as 16-B fragments.
+#include <math.h>
+#include <stdlib.h>
+
+#include <type_traits>
+
+#include "common.h"
+
+namespace pdeinv {
+namespace mlpq {
+
+constexpr int kW = 20;       // padded hidden width
+constexpr int kNS = 5;       // compact slots of a hidden stream
+constexpr int kLMax = 8;     // hidden (tanh) layers
+constexpr int kWaves = 8;    // waves per block of pass 1 (two blocks per CU)
+constexpr int kWaves2 = 4;   // waves per block of pass 2: one per SIMD (512 registers: the checkpoints stay in registers)
+constexpr int kChunk = 256;  // references per work unit (16 tiles)
+constexpr int kPS = 24;      // LDS image row pitch (floats)
+constexpr int kRowsA = 48, kRowsB = 32;
+constexpr int kTImg = (kRowsA + kRowsB) * kPS;  // floats per wave
+
+// feature carried by compact slot k in lane group g, for a stream of ns slots
+__host__ __device__ inline int slot_feat(int ns, int k, int g) {
+  const int fm = ns / 4;
+  return k < 4 * fm ? 16 * (k >> 2) + 4 * g + (k & 3) : 16 * fm + 4 * (k - 4 * fm) + g;
+}
+// feature of M row r of block mb (-1: a padding row)
+__host__ __device__ inline int row_feat(int ns, int mb, int r) {
+  const int fm = ns / 4;
+  if (mb < fm) return 16 * mb + r;
+  return (r & 3) < ns % 4 ? 16 * fm + 4 * (r & 3) + (r >> 2) : -1;
+}
+
+struct Args {
+  int L, D, n_ch;
+  int64_t n, n_items, n_units, set_stride, ld;
+  const float* z;
+  const float* ds;
+  float gamma, s, inv_n;
+  const float* img;       // weight image (device), img_floats (multiple of 4)
+  int img_floats;
+  int fwd[kLMax + 1], bwd[kLMax + 1], bias[kLMax + 1];  // unit offsets (fwd / bwd), float offsets (bias)
+  int qoff[kLMax + 1];                                  // gradient-slab offsets (padded layout)
+  int fwd_out, bwd_out, bias_out, qoff_out;             // the output layer's (index L: scalar kernel args)
+  int P;                                                // padded parameter count
+  const float* gbar;      // pass 2: [n_items][D]
+  float* gpart;           // pass 1: [n_units][D]
+  float* gslab;           // pass 2: [n_blocks][P]
+  float* aslab;           // pass 2: [n_waves][8]
+};
+
+__device__ __forceinline__ float ftanh(float z) {
+  const float e = __builtin_amdgcn_exp2f(2.8853900817779268f * z);
+  return 1.f - 2.f * __builtin_amdgcn_rcpf(e + 1.f);
+}
+
+__device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// N consecutive 64-lane units of the image starting at unit u0 (u0 % 4 == 0): 16-B reads
+template <int N>
+__device__ __forceinline__ void load_units(const float* img, int u0, int lane, float (&w)[N]) {
+  static_assert(N % 4 == 0, "units come in fours");
+  const f32x4* q = reinterpret_cast<const f32x4*>(img) + (u0 >> 2) * 64 + lane;
+#pragma unroll
+  for (int c = 0; c < N / 4; ++c) {
+    const f32x4 v = q[c * 64];
+    w[4 * c] = v[0]; w[4 * c + 1] = v[1]; w[4 * c + 2] = v[2]; w[4 * c + 3] = v[3];
+  }
+}
+
+__device__ __forceinline__ int pos_of(int p) { return 4 * (p & 3) + (p >> 2); }
+
+// P layout -> image rows (row = feature): slot k of lane (p, g) holds feature slot_feat(NS, k, g)
+template <int NS>
+__device__ __forceinline__ void put_slots(float* T, const float (&v)[NS], int p, int g) {
+  const int pp = pos_of(p);
+#pragma unroll
+  for (int k = 0; k < NS; ++k) T[slot_feat(NS, k, g) * kPS + pp] = v[k];
+}
+// F layout read: rows 16 blk + (lane & 15), the pairs (lane >> 4) + 4 ks of k-steps ks = 0..3
+__device__ __forceinline__ f32x4 get_rows(const float* T, int blk, int p, int g) {
+  return *reinterpret_cast<const f32x4*>(T + (16 * blk + p) * kPS + 4 * g);
+}
+
+// slab[qoff + in * pout + out] += G[mb][nb] (in == pin is the bias row)
+template <int MBN, int NBN>
+__device__ __forceinline__ void fold(float* slab, int qoff, int pout, int pin, const f32x4 (&G)[MBN][NBN], int p,
+                                     int g) {
+#pragma unroll
+  for (int mb = 0; mb < MBN; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < NBN; ++nb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int out = 16 * mb + 4 * g + r, in = 16 * nb + p;
+        if (out < pout && in <= pin) atomicAdd(&slab[qoff + in * pout + out], G[mb][nb][r]);
+      }
+}
+
+// the four forward streams entering the next layer from a layer's checkpoint (h, z'_u, z'_v, z''_v)
+__device__ __forceinline__ void streams_of(const float (&h)[kNS], const float (&zu)[kNS], const float (&zv)[kNS],
+                                           const float (&zw)[kNS], float (&H)[4][kNS]) {
+#pragma unroll
+  for (int k = 0; k < kNS; ++k) {
+    const float s1 = 1.f - h[k] * h[k], s2 = -2.f * h[k] * s1;
+    H[0][k] = h[k];
+    H[1][k] = s1 * zu[k];
+    H[2][k] = s1 * zv[k];
+    H[3][k] = fmaf(s1, zw[k], s2 * zv[k] * zv[k]);
+  }
+}
+template <int S>
+__device__ __forceinline__ void stream_of(const float (&h)[kNS], const float (&zu)[kNS], const float (&zv)[kNS],
+                                          const float (&zw)[kNS], float (&H)[kNS]) {
+#pragma unroll
+  for (int k = 0; k < kNS; ++k) {
+    const float s1 = 1.f - h[k] * h[k];
+    if constexpr (S == 0) H[k] = h[k];
+    else if constexpr (S == 1) H[k] = s1 * zu[k];
+    else if constexpr (S == 2) H[k] = s1 * zv[k];
+    else H[k] = fmaf(s1, zw[k], -2.f * h[k] * s1 * zv[k] * zv[k]);
+  }
+}
+
+// bias-initialised accumulators of a width-20 layer (slots 0..4 -> blocks 0 / 1)
+__device__ __forceinline__ void bias_hidden(const float* img, int boff, int g, f32x4 (&A)[2]) {
+  const float* b = img + boff;
+  A[0] = f32x4{b[4 * g], b[4 * g + 1], b[4 * g + 2], b[4 * g + 3]};
+  A[1] = f32x4{b[16 + g], 0.f, 0.f, 0.f};
+}
+__device__ __forceinline__ void compact_hidden(const f32x4 (&A)[2], float (&z)[kNS]) {
+  z[0] = A[0][0]; z[1] = A[0][1]; z[2] = A[0][2]; z[3] = A[0][3]; z[4] = A[1][0];
+}
+
+// layer-0 lane values: dimension k = 4 kk + g of the lane's group (0 past D)
+template <int KD>
+__device__ __forceinline__ void lane_dims(const float* row, int D, int g, float (&x)[KD]) {
+#pragma unroll
+  for (int kk = 0; kk < KD; ++kk) {
+    const int k = 4 * kk + g;
+    x[kk] = k < D ? row[k] : 0.f;
+  }
+}
+
+// -------------------------------------------------------------------------------------------------
+// pass 2: d/dtheta of sum_ij l_ij (and the loss slots), 16-pair tiles
+// -------------------------------------------------------------------------------------------------
+template <int KD, int OS>
+__global__ __launch_bounds__(kWaves2 * kWave, 1) void kmvq_grad_kernel(Args a) {
+  constexpr int OMB = (OS + 3) / 4;  // output M blocks
+  static_assert(OMB <= 3 && 16 * OMB <= kRowsA, "output rows");
+  extern __shared__ f32x4 lds4[];
+  float* lds = reinterpret_cast<float*>(lds4);
+  float* img = lds;
+  const int slab_f = (a.P + 3) & ~3;
+  float* slab = lds + a.img_floats;
+  const int lane0 = threadIdx.x & (kWave - 1), p = lane0 & 15, g = lane0 >> 4;
+  const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  float* tA = lds + a.img_floats + slab_f + wib * kTImg;
+  float* tB = tA + kRowsA * kPS;
+  for (int q = threadIdx.x; q < a.img_floats / 4; q += blockDim.x) lds4[q] = reinterpret_cast<const f32x4*>(a.img)[q];
+  for (int q = threadIdx.x; q < slab_f + kWaves2 * kTImg; q += blockDim.x) lds[a.img_floats + q] = 0.f;
+  __syncthreads();
+
+  const int64_t wave = (int64_t)blockIdx.x * kWaves2 + wib;
+  const int64_t n_waves = (int64_t)gridDim.x * kWaves2;
+  const int L = a.L, D = a.D;
+  const float c2 = -2.f * a.s;
+  float accs[3] = {0.f, 0.f, 0.f};  // LOSS, HESSIAN, FRICTION slot partials
+
+  for (int64_t unit = wave; unit < a.n_units; unit += n_waves) {
+    const int64_t it = unit / a.n_ch, ch = unit - it * a.n_ch;
+    const int64_t t = it / a.n, i = it - t * a.n;
+    const int64_t j_end = (ch + 1) * kChunk < a.n ? (ch + 1) * kChunk : a.n;
+    const float* zt = a.z + t * a.set_stride;
+    float xi[KD], vi[KD], ui[KD];
+    lane_dims<KD>(zt + i * a.ld, D, g, xi);
+    lane_dims<KD>(zt + i * a.ld + D, D, g, vi);
+    lane_dims<KD>(a.gbar + it * D, D, g, ui);
+#pragma unroll
+    for (int kk = 0; kk < KD; ++kk) ui[kk] *= 2.f * a.s;
+    const float dsa = a.ds[it * 2], dsb = a.ds[it * 2 + 1];
+    const float c0 = 2.f * a.s * (dsb + dsa * dsa + a.gamma * dsa);  // 2 s w_it (:84-89)
+
+    // layer-0 tangents along u and v: the same for every pair of the item
+    float w0[4];
+    load_units<4>(img, a.fwd[0], lane0, w0);  // unit kk * 2 + mb
+    float zu0[kNS], zv0[kNS], zw0[kNS];
+    {
+      f32x4 Au[2] = {}, Av[2] = {};
+#pragma unroll
+      for (int kk = 0; kk < KD; ++kk)
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb) {
+          Au[mb] = mfma(w0[kk * 2 + mb], ui[kk], Au[mb]);
+          Av[mb] = mfma(w0[kk * 2 + mb], vi[kk], Av[mb]);
+        }
+      compact_hidden(Au, zu0);
+      compact_hidden(Av, zv0);
+#pragma unroll
+      for (int k = 0; k < kNS; ++k) zw0[k] = 0.f;
+    }
+
+    float xn[KD];  // next tile's reference coordinates (prefetched)
+    {
+      const int64_t j = ch * kChunk + p;
+#pragma unroll
+      for (int kk = 0; kk < KD; ++kk) {
+        const int k = 4 * kk + g;
+        xn[kk] = (j < j_end && k < D) ? zt[j * a.ld + k] : 0.f;
+      }
+    }
+    for (int64_t j0 = ch * kChunk; j0 < j_end; j0 += 16) {
+      // the weight fragments are the same for every tile: an opaque lane index keeps the compiler from
+      // hoisting all of them out of the tile loop (hundreds of VGPRs)
+      int lane = lane0;
+      asm volatile("" : "+v"(lane));
+      // (opaque too: every lane-dependent LDS address — hoisted, they held ~150 VGPRs)
+      const int pq = lane & 15, gq = lane >> 4, ppq = pos_of(pq);
+      const bool active = j0 + p < j_end;
+      float yb[KD];
+#pragma unroll
+      for (int kk = 0; kk < KD; ++kk) yb[kk] = (active && 4 * kk + gq < D) ? xi[kk] - xn[kk] : 0.f;
+      {
+        const int64_t j = j0 + 16 + p;
+#pragma unroll
+        for (int kk = 0; kk < KD; ++kk) {
+          const int k = 4 * kk + gq;
+          xn[kk] = (j < j_end && k < D) ? zt[j * a.ld + k] : 0.f;
+        }
+      }
+      // ---- forward ----
+      float ckh[kLMax][kNS], cku[kLMax][kNS], ckv[kLMax][kNS], ckw[kLMax][kNS];
+      float H[4][kNS];
+      {
+        f32x4 A[2];
+        bias_hidden(img, a.bias[0], gq, A);
+#pragma unroll
+        for (int kk = 0; kk < KD; ++kk)
+#pragma unroll
+          for (int mb = 0; mb < 2; ++mb) A[mb] = mfma(w0[kk * 2 + mb], yb[kk], A[mb]);
+        float z[kNS];
+        compact_hidden(A, z);
+#pragma unroll
+        for (int k = 0; k < kNS; ++k) ckh[0][k] = ftanh(z[k]);
+        streams_of(ckh[0], zu0, zv0, zw0, H);
+      }
+#pragma unroll
+      for (int l = 1; l < kLMax; ++l) {
+        if (l < L) {
+          float w[12];
+          load_units<12>(img, a.fwd[l], lane, w);  // unit kk * 2 + mb
+          f32x4 A[4][2] = {};
+          bias_hidden(img, a.bias[l], gq, A[0]);
+#pragma unroll
+          for (int kk = 0; kk < kNS; ++kk)
+#pragma unroll
+            for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+              for (int s = 0; s < 4; ++s) A[s][mb] = mfma(w[kk * 2 + mb], H[s][kk], A[s][mb]);
+          float z0[kNS];
+          compact_hidden(A[0], z0);
+          compact_hidden(A[1], cku[l]);
+          compact_hidden(A[2], ckv[l]);
+          compact_hidden(A[3], ckw[l]);
+#pragma unroll
+          for (int k = 0; k < kNS; ++k) ckh[l][k] = ftanh(z0[k]);
+          streams_of(ckh[l], cku[l], ckv[l], ckw[l], H);
+        }
+      }
+      // ---- output layer: o, o'_u, o'_v, o''_v ----
+      float ob[4][OS];
+      {
+        float w[16];
+        load_units<16>(img, a.fwd_out, lane, w);  // unit kk * 3 + mb
+        f32x4 O[4][3] = {};
+        {
+          const float* b = img + a.bias_out;
+#pragma unroll
+          for (int mb = 0; mb < 3; ++mb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) O[0][mb][r] = 4 * mb + r < OS ? b[slot_feat(OS, 4 * mb + r, gq)] : 0.f;
+        }
+#pragma unroll
+        for (int kk = 0; kk < kNS; ++kk)
+#pragma unroll
+          for (int mb = 0; mb < OMB; ++mb)
+#pragma unroll
+            for (int s = 0; s < 4; ++s) O[s][mb] = mfma(w[kk * 3 + mb], H[s][kk], O[s][mb]);
+        float T0 = 0.f, T2 = 0.f;
+#pragma unroll
+        for (int k = 0; k < OS; ++k) {
+          const float o = O[0][k >> 2][k & 3], ou = O[1][k >> 2][k & 3], ov = O[2][k >> 2][k & 3],
+                      ow = O[3][k >> 2][k & 3];
+          T0 = fmaf(o, o, T0);
+          T2 = fmaf(ov, ov, fmaf(o, ow, T2));
+          // seeds: l = 2 sum o o'_u + 2 c2 sum (o'_v^2 + o o''_v) + c0 sum o^2
+          ob[0][k] = active ? 2.f * ou + 2.f * c2 * ow + 2.f * c0 * o : 0.f;
+          ob[1][k] = active ? 2.f * o : 0.f;
+          ob[2][k] = active ? 4.f * c2 * ov : 0.f;
+          ob[3][k] = active ? 2.f * c2 * o : 0.f;
+        }
+        T2 *= 2.f;
+        if (active) {
+          accs[0] += c2 * T2 + c0 * T0;
+          accs[1] += -0.5f * c2 * T2;
+          accs[2] += c0 * T0;
+        }
+      }
+      // ---- output-layer weight gradient: [h_{L-1} streams | 1]^T x seeds ----
+      {
+        f32x4 G[3][2] = {};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          put_slots<OS>(tA, ob[s], pq, gq);
+          put_slots<kNS>(tB, H[s], pq, gq);
+          if (gq == 0) tB[kW * kPS + ppq] = s == 0 ? 1.f : 0.f;
+          f32x4 fa[3], fb[2];
+#pragma unroll
+          for (int mb = 0; mb < OMB; ++mb) fa[mb] = get_rows(tA, mb, pq, gq);
+#pragma unroll
+          for (int nb = 0; nb < 2; ++nb) fb[nb] = get_rows(tB, nb, pq, gq);
+#pragma unroll
+          for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+            for (int mb = 0; mb < OMB; ++mb)
+#pragma unroll
+              for (int nb = 0; nb < 2; ++nb) G[mb][nb] = mfma(fa[mb][ks], fb[nb][ks], G[mb][nb]);
+        }
+        fold<3, 2>(slab, a.qoff_out, 4 * OS, kW, G, pq, gq);
+      }
+      // ---- back through the output layer: hbar = K_L obar ----
+      float hb[4][kNS];
+      {
+        float w[2 * OS];
+        load_units<2 * OS>(img, a.bwd_out, lane, w);  // unit kk * 2 + mb
+        f32x4 B[4][2] = {};
+#pragma unroll
+        for (int kk = 0; kk < OS; ++kk)
+#pragma unroll
+          for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+            for (int s = 0; s < 4; ++s) B[s][mb] = mfma(w[kk * 2 + mb], ob[s][kk], B[s][mb]);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) compact_hidden(B[s], hb[s]);
+      }
+      // ---- reverse sweep over the tanh layers ----
+      auto zbar_of = [&](const float (&h)[kNS], const float (&zu)[kNS], const float (&zv)[kNS],
+                         const float (&zw)[kNS], float (&zb)[4][kNS]) {
+#pragma unroll
+        for (int k = 0; k < kNS; ++k) {
+          const float s1 = 1.f - h[k] * h[k], s2 = -2.f * h[k] * s1, s3 = -2.f * s1 * s1 - 2.f * h[k] * s2;
+          const float b0 = hb[0][k], b1 = hb[1][k], b2 = hb[2][k], b3 = hb[3][k];
+          zb[3][k] = s1 * b3;
+          zb[2][k] = fmaf(s1, b2, 2.f * s2 * zv[k] * b3);
+          zb[1][k] = s1 * b1;
+          zb[0][k] = fmaf(s1, b0, fmaf(s2, fmaf(zu[k], b1, zv[k] * b2), fmaf(s2, zw[k], s3 * zv[k] * zv[k]) * b3));
+        }
+      };
+#pragma unroll
+      for (int l = kLMax - 1; l >= 1; --l) {
+        if (l < L) {
+          float zb[4][kNS];
+          zbar_of(ckh[l], cku[l], ckv[l], ckw[l], zb);
+          const float(&ph)[kNS] = ckh[l - 1];
+          const float(&pu)[kNS] = l - 1 == 0 ? zu0 : cku[l - 1];
+          const float(&pv)[kNS] = l - 1 == 0 ? zv0 : ckv[l - 1];
+          const float(&pw)[kNS] = l - 1 == 0 ? zw0 : ckw[l - 1];
+          f32x4 G[2][2] = {};
+          auto outer = [&](auto sc) {
+            constexpr int s = decltype(sc)::value;
+            float Hp[kNS];
+            stream_of<s>(ph, pu, pv, pw, Hp);
+            put_slots<kNS>(tA, zb[s], pq, gq);
+            put_slots<kNS>(tB, Hp, pq, gq);
+            if (gq == 0) tB[kW * kPS + ppq] = s == 0 ? 1.f : 0.f;
+            f32x4 fa[2], fb[2];
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+              fa[b] = get_rows(tA, b, pq, gq);
+              fb[b] = get_rows(tB, b, pq, gq);
+            }
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+              for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb) G[mb][nb] = mfma(fa[mb][ks], fb[nb][ks], G[mb][nb]);
+          };
+          outer(std::integral_constant<int, 0>{});
+          outer(std::integral_constant<int, 1>{});
+          outer(std::integral_constant<int, 2>{});
+          outer(std::integral_constant<int, 3>{});
+          fold<2, 2>(slab, a.qoff[l], kW, kW, G, pq, gq);
+          float w[12];
+          load_units<12>(img, a.bwd[l], lane, w);  // unit kk * 2 + mb
+          f32x4 B[4][2] = {};
+#pragma unroll
+          for (int kk = 0; kk < kNS; ++kk)
+#pragma unroll
+            for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+              for (int s = 0; s < 4; ++s) B[s][mb] = mfma(w[kk * 2 + mb], zb[s][kk], B[s][mb]);
+#pragma unroll
+          for (int s = 0; s < 4; ++s) compact_hidden(B[s], hb[s]);
+        }
+      }
+      // layer 0: inputs y (per pair), u, v (per item), 0 (second order)
+      {
+        float zb[4][kNS];
+        zbar_of(ckh[0], zu0, zv0, zw0, zb);
+        f32x4 G[2][1] = {};
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {
+          put_slots<kNS>(tA, zb[s], pq, gq);
+#pragma unroll
+          for (int kk = 0; kk < KD; ++kk) {
+            const int k = 4 * kk + gq;
+            if (k < D) tB[k * kPS + ppq] = s == 0 ? yb[kk] : (s == 1 ? ui[kk] : vi[kk]);
+          }
+          if (gq == 0) tB[D * kPS + ppq] = s == 0 ? 1.f : 0.f;
+          f32x4 fa[2], fb;
+#pragma unroll
+          for (int b = 0; b < 2; ++b) fa[b] = get_rows(tA, b, pq, gq);
+          fb = get_rows(tB, 0, pq, gq);
+#pragma unroll
+          for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+            for (int mb = 0; mb < 2; ++mb) G[mb][0] = mfma(fa[mb][ks], fb[ks], G[mb][0]);
+        }
+        fold<2, 1>(slab, a.qoff[0], kW, D, G, pq, gq);
+      }
+    }
+  }
+  float* as = a.aslab + wave * 8;
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const float v = wave_sum(accs[q]);
+    if (lane0 == 0) as[q] = v;
+  }
+  __syncthreads();
+  float* gs = a.gslab + (int64_t)blockIdx.x * a.P;
+  for (int q = threadIdx.x; q < a.P; q += blockDim.x) gs[q] = slab[q];
+}
+
+// -------------------------------------------------------------------------------------------------
+// pass 1: gbar partials per (item, chunk of references): sum_j grad_y Phi(x_i - x_j)
+// -------------------------------------------------------------------------------------------------
+template <int KD, int OS>
+__global__ __launch_bounds__(kWaves * kWave, 2) void kmvq_gbar_kernel(Args a) {
+  constexpr int OMB = (OS + 3) / 4;
+  extern __shared__ f32x4 lds4[];
+  float* img = reinterpret_cast<float*>(lds4);
+  for (int q = threadIdx.x; q < a.img_floats / 4; q += blockDim.x) lds4[q] = reinterpret_cast<const f32x4*>(a.img)[q];
+  __syncthreads();
+  const int lane0 = threadIdx.x & (kWave - 1), p = lane0 & 15, g = lane0 >> 4;
+  const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const int64_t wave = (int64_t)blockIdx.x * kWaves + wib;
+  const int64_t n_waves = (int64_t)gridDim.x * kWaves;
+  const int L = a.L, D = a.D;
+  for (int64_t unit = wave; unit < a.n_units; unit += n_waves) {
+    const int64_t it = unit / a.n_ch, ch = unit - it * a.n_ch;
+    const int64_t t = it / a.n, i = it - t * a.n;
+    const int64_t j_end = (ch + 1) * kChunk < a.n ? (ch + 1) * kChunk : a.n;
+    const float* zt = a.z + t * a.set_stride;
+    float xi[KD];
+    lane_dims<KD>(zt + i * a.ld, D, g, xi);
+    float w0[4];
+    load_units<4>(img, a.fwd[0], lane0, w0);
+    f32x4 gacc = {};
+    float xn[KD];
+    {
+      const int64_t j = ch * kChunk + p;
+#pragma unroll
+      for (int kk = 0; kk < KD; ++kk) {
+        const int k = 4 * kk + g;
+        xn[kk] = (j < j_end && k < D) ? zt[j * a.ld + k] : 0.f;
+      }
+    }
+    for (int64_t j0 = ch * kChunk; j0 < j_end; j0 += 16) {
+      // the weight fragments are the same for every tile: an opaque lane index keeps the compiler from
+      // hoisting all of them out of the tile loop (hundreds of VGPRs)
+      int lane = lane0;
+      asm volatile("" : "+v"(lane));
+      const int gq = lane >> 4;  // (opaque too: the bias reads)
+      const bool active = j0 + p < j_end;
+      float yb[KD];
+#pragma unroll
+      for (int kk = 0; kk < KD; ++kk) yb[kk] = (active && 4 * kk + g < D) ? xi[kk] - xn[kk] : 0.f;
+      {
+        const int64_t j = j0 + 16 + p;
+#pragma unroll
+        for (int kk = 0; kk < KD; ++kk) {
+          const int k = 4 * kk + g;
+          xn[kk] = (j < j_end && k < D) ? zt[j * a.ld + k] : 0.f;
+        }
+      }
+      float ckh[kLMax][kNS];
+      {
+        f32x4 A[2];
+        bias_hidden(img, a.bias[0], gq, A);
+#pragma unroll
+        for (int kk = 0; kk < KD; ++kk)
+#pragma unroll
+          for (int mb = 0; mb < 2; ++mb) A[mb] = mfma(w0[kk * 2 + mb], yb[kk], A[mb]);
+        float z[kNS];
+        compact_hidden(A, z);
+#pragma unroll
+        for (int k = 0; k < kNS; ++k) ckh[0][k] = ftanh(z[k]);
+      }
+      float h[kNS];
+#pragma unroll
+      for (int k = 0; k < kNS; ++k) h[k] = ckh[0][k];
+#pragma unroll
+      for (int l = 1; l < kLMax; ++l) {
+        if (l < L) {
+          float w[12];
+          load_units<12>(img, a.fwd[l], lane, w);
+          f32x4 A[2];
+          bias_hidden(img, a.bias[l], gq, A);
+#pragma unroll
+          for (int kk = 0; kk < kNS; ++kk)
+#pragma unroll
+            for (int mb = 0; mb < 2; ++mb) A[mb] = mfma(w[kk * 2 + mb], h[kk], A[mb]);
+          float z[kNS];
+          compact_hidden(A, z);
+#pragma unroll
+          for (int k = 0; k < kNS; ++k) h[k] = ckh[l][k] = ftanh(z[k]);
+        }
+      }
+      float ob[OS];
+      {
+        float w[16];
+        load_units<16>(img, a.fwd_out, lane, w);
+        f32x4 O[3];
+        const float* b = img + a.bias_out;
+#pragma unroll
+        for (int mb = 0; mb < 3; ++mb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) O[mb][r] = 4 * mb + r < OS ? b[slot_feat(OS, 4 * mb + r, gq)] : 0.f;
+#pragma unroll
+        for (int kk = 0; kk < kNS; ++kk)
+#pragma unroll
+          for (int mb = 0; mb < OMB; ++mb) O[mb] = mfma(w[kk * 3 + mb], h[kk], O[mb]);
+#pragma unroll
+        for (int k = 0; k < OS; ++k) ob[k] = active ? 2.f * O[k >> 2][k & 3] : 0.f;  // d Phi / d o
+      }
+      float hb[kNS];
+      {
+        float w[2 * OS];
+        load_units<2 * OS>(img, a.bwd_out, lane, w);
+        f32x4 B[2] = {};
+#pragma unroll
+        for (int kk = 0; kk < OS; ++kk)
+#pragma unroll
+          for (int mb = 0; mb < 2; ++mb) B[mb] = mfma(w[kk * 2 + mb], ob[kk], B[mb]);
+        compact_hidden(B, hb);
+      }
+#pragma unroll
+      for (int l = kLMax - 1; l >= 1; --l) {
+        if (l < L) {
+          float zb[kNS];
+#pragma unroll
+          for (int k = 0; k < kNS; ++k) zb[k] = (1.f - ckh[l][k] * ckh[l][k]) * hb[k];
+          float w[12];
+          load_units<12>(img, a.bwd[l], lane, w);
+          f32x4 B[2] = {};
+#pragma unroll
+          for (int kk = 0; kk < kNS; ++kk)
+#pragma unroll
+            for (int mb = 0; mb < 2; ++mb) B[mb] = mfma(w[kk * 2 + mb], zb[kk], B[mb]);
+          compact_hidden(B, hb);
+        }
+      }
+      {
+        float zb[kNS];
+#pragma unroll
+        for (int k = 0; k < kNS; ++k) zb[k] = (1.f - ckh[0][k] * ckh[0][k]) * hb[k];
+        float w[8];
+        load_units<8>(img, a.bwd[0], lane, w);  // unit kk (one M block: rows = input dims)
+#pragma unroll
+        for (int kk = 0; kk < kNS; ++kk) gacc = mfma(w[kk], zb[kk], gacc);
+      }
+    }
+    // sum over the 16 pairs of the lane row, dims 4 g + r
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float v = gacc[r];
+#pragma unroll
+      for (int off = 8; off > 0; off >>= 1) v += __shfl_xor(v, off, 16);
+      const int k = 4 * g + r;
+      if (p == 0 && k < D) a.gpart[unit * D + k] = v;
+    }
+  }
+}
+
+// gbar[it][k] = inv_n sum_ch gpart[it][ch][k] (fixed order, fp64)
+__global__ void kmvq_gbar_reduce_kernel(const float* __restrict__ gpart, int64_t n_items, int n_ch, int D, float inv_n,
+                                        float* __restrict__ gbar) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= n_items * D) return;
+  const int64_t it = q / D;
+  const int k = (int)(q - it * D);
+  double s = 0.0;
+  for (int c = 0; c < n_ch; ++c) s += (double)gpart[(it * n_ch + c) * D + k];
+  gbar[q] = (float)(s * inv_n);
+}
+
+// -------------------------------------------------------------------------------------------------
+// weight image: lane-linear A-operand fragments, unit u of a section at ((u >> 2) * 64 + lane) * 4 + (u & 3)
+// -------------------------------------------------------------------------------------------------
+constexpr int kMaxSec = 2 * (kLMax + 1);
+struct ImageArgs {
+  int L, D, W, O, OS, KD;
+  int nsec;
+  int sec_layer[kMaxSec], sec_bwd[kMaxSec], sec_mb[kMaxSec], sec_u0[kMaxSec], sec_units[kMaxSec];
+  int64_t roff[kLMax + 1];
+  int bias_off[kLMax + 1];
+  int units_total, img_floats;
+};
+
+__global__ void kmvq_image_kernel(ImageArgs ia, const float* __restrict__ prm, float* __restrict__ img) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= ia.img_floats) return;
+  const int L = ia.L;
+  const int64_t unit_floats = (int64_t)ia.units_total * 64;
+  if (q >= unit_floats) {  // biases (padded raw vectors), zero elsewhere
+    float v = 0.f;
+    for (int l = 0; l <= L; ++l) {
+      const int pout = l == L ? 4 * ia.OS : kW, dout = l == L ? ia.O : ia.W, din = l == 0 ? ia.D : ia.W;
+      const int o = (int)q - ia.bias_off[l];  // bias_off: absolute float offsets
+      if (o >= 0 && o < pout) {
+        v = o < dout ? prm[ia.roff[l] + (int64_t)din * dout + o] : 0.f;
+        break;
+      }
+    }
+    img[q] = v;
+    return;
+  }
+  const int u = (int)(q / 256), lane = (int)((q / 4) % 64), uu = 4 * u + (int)(q % 4);
+  float v = 0.f;
+  for (int s = 0; s < ia.nsec; ++s) {
+    const int lu = uu - ia.sec_u0[s];
+    if (lu < 0 || lu >= ia.sec_units[s]) continue;
+    const int l = ia.sec_layer[s], MB = ia.sec_mb[s];
+    const int kk = lu / MB, mb = lu % MB;
+    const int g = lane >> 4, m = lane & 15;
+    const int din = l == 0 ? ia.D : ia.W, dout = l == L ? ia.O : ia.W;
+    int in, out;
+    if (!ia.sec_bwd[s]) {  // forward: A[m = out row][k = in slot]
+      in = l == 0 ? 4 * kk + g : slot_feat(kNS, kk, g);
+      out = l == L ? row_feat(ia.OS, mb, m) : row_feat(kNS, mb, m);
+    } else {  // backward: A[m = in row][k = out slot]
+      in = l == 0 ? m : row_feat(kNS, mb, m);
+      out = l == L ? slot_feat(ia.OS, kk, g) : slot_feat(kNS, kk, g);
+    }
+    if (in >= 0 && in < din && out >= 0 && out < dout) v = prm[ia.roff[l] + (int64_t)in * dout + out];
+    break;
+  }
+  img[q] = v;
+}
+
+// grad[real(q)] += sum_b slab[b][q] (fixed order, fp64); loss slots from the per-wave partials
+__global__ void kmvq_reduce_kernel(MlpPadMap pm, const float* __restrict__ gslab, int n_blocks, int64_t P,
+                                   const float* __restrict__ aslab, int64_t n_waves, float* __restrict__ grad,
+                                   double* __restrict__ acc) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q < P) {
+    const int64_t r = pm.real_of(q);
+    if (r >= 0) {
+      double s = 0.0;
+      for (int b = 0; b < n_blocks; ++b) s += (double)gslab[(int64_t)b * P + q];
+      grad[r] += (float)s;
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x < 3) {
+    double s = 0.0;
+    for (int64_t w = 0; w < n_waves; ++w) s += (double)aslab[w * 8 + threadIdx.x];
+    const int slot = threadIdx.x == 0 ? PDEINV_GMM_ACC_LOSS
+                                      : (threadIdx.x == 1 ? PDEINV_GMM_ACC_HESSIAN : PDEINV_GMM_ACC_FRICTION);
+    acc[slot] += s;
+  }
+}
+
+}  // namespace mlpq
+
+// ---- host driver ------------------------------------------------------------------------------
+namespace {
+
+int device_cus() {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                              hipSuccess || cus <= 0)
+    cus = 256;
+  return cus;
+}
+
+struct QPlan {
+  mlpq::ImageArgs ia;
+  MlpPadMap pm;
+  int OS, KD, n_ch, n_blocks2, n_blocks1;
+  int64_t items, n_units, P;
+  int fwd[mlpq::kLMax + 1], bwd[mlpq::kLMax + 1];
+  size_t lds2, lds1;                                                    // bytes
+  size_t off_img, off_gbar, off_gpart, off_gslab, off_aslab, total;  // bytes
+};
+
+QPlan q_plan(const pdeinv_kmv_mlp_desc* d) {
+  QPlan p{};
+  const int L = d->n_layers;
+  p.OS = d->out_features <= 40 ? 10 : 12;
+  p.KD = d->dim <= 4 ? 1 : 2;
+  mlpq::ImageArgs& ia = p.ia;
+  ia.L = L; ia.D = d->dim; ia.W = d->width; ia.O = d->out_features; ia.OS = p.OS; ia.KD = p.KD;
+  // image sections: per layer forward then backward, each rounded to 4 units
+  int u = 0, ns = 0;
+  auto sec = [&](int l, int bwd, int ks, int mb) {
+    ia.sec_layer[ns] = l; ia.sec_bwd[ns] = bwd; ia.sec_mb[ns] = mb; ia.sec_u0[ns] = u;
+    ia.sec_units[ns] = ks * mb;
+    ++ns;
+    const int at = u;
+    u += (ks * mb + 3) & ~3;
+    return at;
+  };
+  for (int l = 0; l <= L; ++l) {
+    p.fwd[l] = sec(l, 0, l == 0 ? 2 : mlpq::kNS, l == L ? 3 : 2);  // layer 0: KD <= 2 k-steps (zeros past KD)
+    p.bwd[l] = sec(l, 1, l == L ? p.OS : mlpq::kNS, l == 0 ? 1 : 2);
+  }
+  ia.nsec = ns;
+  ia.units_total = u;
+  int bf = u * 64;
+  for (int l = 0; l <= L; ++l) {
+    ia.bias_off[l] = bf;
+    bf += ((l == L ? 4 * p.OS : mlpq::kW) + 3) & ~3;
+  }
+  ia.img_floats = (bf + 3) & ~3;
+  // padded parameter layout of the gradient slab: K [pin][pout] then b [pout]
+  p.pm.L = L;
+  int64_t ro = 0, po = 0;
+  for (int l = 0; l <= L; ++l) {
+    p.pm.din[l] = l == 0 ? d->dim : d->width;
+    p.pm.dout[l] = l == L ? d->out_features : d->width;
+    p.pm.pin[l] = l == 0 ? d->dim : mlpq::kW;
+    p.pm.pout[l] = l == L ? 4 * p.OS : mlpq::kW;
+    p.pm.roff[l] = ro;
+    p.pm.poff[l] = po;
+    ia.roff[l] = ro;
+    ro += (int64_t)p.pm.din[l] * p.pm.dout[l] + p.pm.dout[l];
+    po += (int64_t)p.pm.pin[l] * p.pm.pout[l] + p.pm.pout[l];
+  }
+  p.P = po;
+  p.items = (int64_t)d->n_sets * d->n_rows;
+  p.n_ch = (int)((d->n_rows + mlpq::kChunk - 1) / mlpq::kChunk);
+  p.n_units = p.items * p.n_ch;
+  const int cus = device_cus();
+  const int64_t need1 = (p.n_units + mlpq::kWaves - 1) / mlpq::kWaves;
+  const int64_t need2 = (p.n_units + mlpq::kWaves2 - 1) / mlpq::kWaves2;
+  p.n_blocks2 = (int)(need2 < cus ? need2 : cus);
+  p.n_blocks1 = (int)(need1 < 2 * cus ? need1 : 2 * cus);
+  p.lds1 = sizeof(float) * (size_t)ia.img_floats;
+  p.lds2 = sizeof(float) * ((size_t)ia.img_floats + (((size_t)p.P + 3) & ~(size_t)3) +
+                            (size_t)mlpq::kWaves2 * mlpq::kTImg);
+  size_t o = 0;
+  auto take = [&](size_t bytes) { const size_t at = o; o += (bytes + 255) & ~(size_t)255; return at; };
+  p.off_img = take(sizeof(float) * (size_t)ia.img_floats);
+  p.off_gbar = take(sizeof(float) * (size_t)p.items * d->dim);
+  p.off_gpart = take(sizeof(float) * (size_t)p.n_units * d->dim);
+  p.off_gslab = take(sizeof(float) * (size_t)cus * p.P);
+  p.off_aslab = take(sizeof(float) * (size_t)cus * mlpq::kWaves2 * 8);
+  p.total = o;
+  return p;
+}
+
+bool q_forced_off() {
+  const char* e = getenv("PDEINV_PAIRS_IMPL");  // "ring": the register-ring kernels (A/B experiments)
+  return e && e[0] == 'r';
+}
+
+template <int KD, int OS>
+int q_launch(const mlpq::Args& a, const QPlan& p, hipStream_t st, int pass) {
+  if (pass == 0) {
+    static const bool attr = hipFuncSetAttribute((const void*)mlpq::kmvq_gbar_kernel<KD, OS>,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+    (void)attr;
+    hipLaunchKernelGGL((mlpq::kmvq_gbar_kernel<KD, OS>), dim3((unsigned)p.n_blocks1), dim3(mlpq::kWaves * kWave),
+                       p.lds1, st, a);
+    return check_launch("kmvq_gbar_kernel");
+  }
+  static const bool attr = hipFuncSetAttribute((const void*)mlpq::kmvq_grad_kernel<KD, OS>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+  (void)attr;
+  hipLaunchKernelGGL((mlpq::kmvq_grad_kernel<KD, OS>), dim3((unsigned)p.n_blocks2), dim3(mlpq::kWaves2 * kWave), p.lds2,
+                     st, a);
+  return check_launch("kmvq_grad_kernel");
+}
+
+}  // namespace
+
+bool kmvq_supported(const pdeinv_kmv_mlp_desc* d) {
+  if (q_forced_off()) return false;
+  if (!(d->dim >= 1 && d->dim <= 8 && d->width >= 1 && d->width <= mlpq::kW && d->n_layers >= 1 &&
+        d->n_layers <= mlpq::kLMax && d->out_features >= 1 && d->out_features <= 48))
+    return false;
+  return q_plan(d).lds2 <= 160 * 1024;
+}
+
+size_t kmvq_workspace_bytes(const pdeinv_kmv_mlp_desc* d) { return q_plan(d).total; }
+
+// pass 0: weight image + gbar (returned through gbar_out); pass 1: the gradient (grad, acc accumulate +=)
+int kmvq_run(const pdeinv_kmv_mlp_desc* d, const float* z, int64_t set_stride, int64_t ld, const float* ds,
+             const float* params, void* ws, double* acc, float* grad, float** gbar_out, int pass, hipStream_t st) {
+  const QPlan p = q_plan(d);
+  char* w = (char*)ws;
+  mlpq::Args a{};
+  a.L = d->n_layers;
+  a.D = d->dim;
+  a.n_ch = p.n_ch;
+  a.n = d->n_rows;
+  a.n_items = p.items;
+  a.n_units = p.n_units;
+  a.set_stride = set_stride;
+  a.ld = ld;
+  a.z = z;
+  a.ds = ds;
+  a.gamma = d->gamma;
+  a.s = (float)(1.0 / ((double)d->n_rows * (double)d->n_rows * (double)d->n_sets));
+  a.inv_n = (float)(1.0 / (double)d->n_rows);
+  a.img = (const float*)(w + p.off_img);
+  a.img_floats = p.ia.img_floats;
+  for (int l = 0; l <= d->n_layers; ++l) {
+    a.fwd[l] = p.fwd[l];
+    a.bwd[l] = p.bwd[l];
+    a.bias[l] = p.ia.bias_off[l];
+    a.qoff[l] = (int)p.pm.poff[l];
+  }
+  a.fwd_out = p.fwd[d->n_layers];
+  a.bwd_out = p.bwd[d->n_layers];
+  a.bias_out = p.ia.bias_off[d->n_layers];
+  a.qoff_out = (int)p.pm.poff[d->n_layers];
+  a.P = (int)p.P;
+  float* gbar = (float*)(w + p.off_gbar);
+  a.gbar = gbar;
+  a.gpart = (float*)(w + p.off_gpart);
+  a.gslab = (float*)(w + p.off_gslab);
+  a.aslab = (float*)(w + p.off_aslab);
+  if (gbar_out) *gbar_out = gbar;
+  int rc = PDEINV_OK;
+  if (pass == 0) {
+    hipLaunchKernelGGL(mlpq::kmvq_image_kernel, dim3((unsigned)((p.ia.img_floats + 255) / 256)), dim3(256), 0, st,
+                       p.ia, params, (float*)(w + p.off_img));
+    rc = check_launch("kmvq_image_kernel");
+    if (rc) return rc;
+  }
+  const int key = p.KD * 100 + p.OS;
+  switch (key) {
+    case 110: rc = q_launch<1, 10>(a, p, st, pass); break;
+    case 112: rc = q_launch<1, 12>(a, p, st, pass); break;
+    case 210: rc = q_launch<2, 10>(a, p, st, pass); break;
+    case 212: rc = q_launch<2, 12>(a, p, st, pass); break;
+    default: return fail(PDEINV_ERR_UNSUPPORTED, "kmv_mlp mfma pairs: shape");
+  }
+  if (rc) return rc;
+  if (pass == 0) {
+    const int64_t nq = p.items * d->dim;
+    hipLaunchKernelGGL(mlpq::kmvq_gbar_reduce_kernel, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, st, a.gpart,
+                       p.items, p.n_ch, d->dim, a.inv_n, gbar);
+    return check_launch("kmvq_gbar_reduce_kernel");
+  }
+  hipLaunchKernelGGL(mlpq::kmvq_reduce_kernel, dim3((unsigned)((p.P + 255) / 256)), dim3(256), 0, st, p.pm, a.gslab,
+                     p.n_blocks2, p.P, a.aslab, (int64_t)p.n_blocks2 * mlpq::kWaves2, grad, acc);
+  return check_launch("kmvq_reduce_kernel");
+}
+
+}  // namespace pdeinv
