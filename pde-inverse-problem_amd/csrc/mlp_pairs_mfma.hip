@@ -52,7 +52,7 @@ constexpr int kWaves2 = 4;   // waves per block of pass 2: one per SIMD (512 reg
 constexpr int kChunk = 256;  // references per work unit (16 tiles)
 constexpr int kPS = 24;      // LDS image row pitch (floats)
 constexpr int kRowsA = 48, kRowsB = 32;
-constexpr int kTImg = (kRowsA + kRowsB) * kPS;  // floats per wave
+constexpr int kTImg = (kRowsA + kRowsB) * kPS;  // floats per wave: the [A | B] transpose images
 
 // feature carried by compact slot k in lane group g, for a stream of ns slots
 __host__ __device__ inline int slot_feat(int ns, int k, int g) {
@@ -107,6 +107,15 @@ __device__ __forceinline__ void load_units(const float* img, int u0, int lane, f
 
 __device__ __forceinline__ int pos_of(int p) { return 4 * (p & 3) + (p >> 2); }
 
+// Opaque copy: the reverse sweep recomputes s1, s2 and the layer-input streams from the checkpoint;
+// without this the compiler CSEs them with the forward's values and keeps those live across the whole
+// tile (~64 VGPRs per layer instead of the 20 of the checkpoint).
+template <int N>
+__device__ __forceinline__ void launder(float (&v)[N]) {
+#pragma unroll
+  for (int k = 0; k < N; ++k) asm volatile("" : "+v"(v[k]));
+}
+
 // P layout -> image rows (row = feature): slot k of lane (p, g) holds feature slot_feat(NS, k, g)
 template <int NS>
 __device__ __forceinline__ void put_slots(float* T, const float (&v)[NS], int p, int g) {
@@ -119,19 +128,31 @@ __device__ __forceinline__ f32x4 get_rows(const float* T, int blk, int p, int g)
   return *reinterpret_cast<const f32x4*>(T + (16 * blk + p) * kPS + 4 * g);
 }
 
-// slab[qoff + in * pout + out] += G[mb][nb] (in == pin is the bias row)
-template <int MBN, int NBN>
-__device__ __forceinline__ void fold(float* slab, int qoff, int pout, int pin, const f32x4 (&G)[MBN][NBN], int p,
-                                     int g) {
+// The wave's private gradient slab (LDS, no atomics: deterministic): slab[qoff + in * pitch + out] +=
+// G[ib][ob], the tile of rows in = 16 ib + 4 g + r (in == pin is the bias row), columns out = 16 ob + p.
+// Row-major with pitch = 20 / 44 puts lane groups g = 0 / 1 on the two halves of the 32 banks
+// (4 pitch = 16 mod 32): conflict-free read-modify-writes. Padding entries go to the lane's own dump word.
+template <int IBN, int OBN>
+__device__ __forceinline__ void fold(float* slab, int qoff, int pitch, int nout, int pin, const f32x4 (&G)[IBN][OBN],
+                                     int p, int g, float* dump) {
+  float* dst[IBN][OBN][4];
+  float v[IBN][OBN][4];
 #pragma unroll
-  for (int mb = 0; mb < MBN; ++mb)
+  for (int ib = 0; ib < IBN; ++ib)
 #pragma unroll
-    for (int nb = 0; nb < NBN; ++nb)
+    for (int ob = 0; ob < OBN; ++ob)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int out = 16 * mb + 4 * g + r, in = 16 * nb + p;
-        if (out < pout && in <= pin) atomicAdd(&slab[qoff + in * pout + out], G[mb][nb][r]);
+        const int in = 16 * ib + 4 * g + r, out = 16 * ob + p;
+        dst[ib][ob][r] = (out < nout && in <= pin) ? slab + qoff + in * pitch + out : dump;
+        v[ib][ob][r] = *dst[ib][ob][r];
       }
+#pragma unroll
+  for (int ib = 0; ib < IBN; ++ib)
+#pragma unroll
+    for (int ob = 0; ob < OBN; ++ob)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) *dst[ib][ob][r] = v[ib][ob][r] + G[ib][ob][r];
 }
 
 // the four forward streams entering the next layer from a layer's checkpoint (h, z'_u, z'_v, z''_v)
@@ -190,13 +211,15 @@ __global__ __launch_bounds__(kWaves2 * kWave, 1) void kmvq_grad_kernel(Args a) {
   float* lds = reinterpret_cast<float*>(lds4);
   float* img = lds;
   const int slab_f = (a.P + 3) & ~3;
-  float* slab = lds + a.img_floats;
   const int lane0 = threadIdx.x & (kWave - 1), p = lane0 & 15, g = lane0 >> 4;
   const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  float* tA = lds + a.img_floats + slab_f + wib * kTImg;
-  float* tB = tA + kRowsA * kPS;
+  float* slab = lds + a.img_floats + wib * slab_f;  // this wave's private gradient slab
+  float* tA0 = lds + a.img_floats + kWaves2 * slab_f + wib * kTImg;
+  float* tB0 = tA0 + kRowsA * kPS;
+  float* tA1 = tA0;
+  float* tB1 = tB0;
   for (int q = threadIdx.x; q < a.img_floats / 4; q += blockDim.x) lds4[q] = reinterpret_cast<const f32x4*>(a.img)[q];
-  for (int q = threadIdx.x; q < slab_f + kWaves2 * kTImg; q += blockDim.x) lds[a.img_floats + q] = 0.f;
+  for (int q = threadIdx.x; q < kWaves2 * (slab_f + kTImg); q += blockDim.x) lds[a.img_floats + q] = 0.f;
   __syncthreads();
 
   const int64_t wave = (int64_t)blockIdx.x * kWaves2 + wib;
@@ -244,7 +267,8 @@ __global__ __launch_bounds__(kWaves2 * kWave, 1) void kmvq_grad_kernel(Args a) {
 #pragma unroll
       for (int kk = 0; kk < KD; ++kk) {
         const int k = 4 * kk + g;
-        xn[kk] = (j < j_end && k < D) ? zt[j * a.ld + k] : 0.f;
+        const float v = zt[(j < j_end ? j : j_end - 1) * a.ld + (k < D ? k : D - 1)];  // unconditional load
+        xn[kk] = (j < j_end && k < D) ? v : 0.f;
       }
     }
     for (int64_t j0 = ch * kChunk; j0 < j_end; j0 += 16) {
@@ -254,6 +278,7 @@ __global__ __launch_bounds__(kWaves2 * kWave, 1) void kmvq_grad_kernel(Args a) {
       asm volatile("" : "+v"(lane));
       // (opaque too: every lane-dependent LDS address — hoisted, they held ~150 VGPRs)
       const int pq = lane & 15, gq = lane >> 4, ppq = pos_of(pq);
+      float* dump = tB0 + 24 * kPS + lane;  // fold's padding entries: rows 24..26 of image B0 (unread)
       const bool active = j0 + p < j_end;
       float yb[KD];
 #pragma unroll
@@ -263,7 +288,8 @@ __global__ __launch_bounds__(kWaves2 * kWave, 1) void kmvq_grad_kernel(Args a) {
 #pragma unroll
         for (int kk = 0; kk < KD; ++kk) {
           const int k = 4 * kk + gq;
-          xn[kk] = (j < j_end && k < D) ? zt[j * a.ld + k] : 0.f;
+          const float v = zt[(j < j_end ? j : j_end - 1) * a.ld + (k < D ? k : D - 1)];  // unconditional load
+        xn[kk] = (j < j_end && k < D) ? v : 0.f;
         }
       }
       // ---- forward ----
@@ -290,11 +316,11 @@ __global__ __launch_bounds__(kWaves2 * kWave, 1) void kmvq_grad_kernel(Args a) {
           f32x4 A[4][2] = {};
           bias_hidden(img, a.bias[l], gq, A[0]);
 #pragma unroll
-          for (int kk = 0; kk < kNS; ++kk)
+          for (int s = 0; s < 4; ++s)  // stream-major: the primal's tanh overlaps the tangents' MFMAs
 #pragma unroll
-            for (int mb = 0; mb < 2; ++mb)
+            for (int kk = 0; kk < kNS; ++kk)
 #pragma unroll
-              for (int s = 0; s < 4; ++s) A[s][mb] = mfma(w[kk * 2 + mb], H[s][kk], A[s][mb]);
+              for (int mb = 0; mb < 2; ++mb) A[s][mb] = mfma(w[kk * 2 + mb], H[s][kk], A[s][mb]);
           float z0[kNS];
           compact_hidden(A[0], z0);
           compact_hidden(A[1], cku[l]);
@@ -302,6 +328,8 @@ __global__ __launch_bounds__(kWaves2 * kWave, 1) void kmvq_grad_kernel(Args a) {
           compact_hidden(A[3], ckw[l]);
 #pragma unroll
           for (int k = 0; k < kNS; ++k) ckh[l][k] = ftanh(z0[k]);
+          // copied out of the accumulator tuples now (block 1 holds one live value in four registers)
+          launder(cku[l]); launder(ckv[l]); launder(ckw[l]); launder(ckh[l]);
           streams_of(ckh[l], cku[l], ckv[l], ckw[l], H);
         }
       }
@@ -319,11 +347,11 @@ __global__ __launch_bounds__(kWaves2 * kWave, 1) void kmvq_grad_kernel(Args a) {
             for (int r = 0; r < 4; ++r) O[0][mb][r] = 4 * mb + r < OS ? b[slot_feat(OS, 4 * mb + r, gq)] : 0.f;
         }
 #pragma unroll
-        for (int kk = 0; kk < kNS; ++kk)
+        for (int s = 0; s < 4; ++s)
 #pragma unroll
-          for (int mb = 0; mb < OMB; ++mb)
+          for (int kk = 0; kk < kNS; ++kk)
 #pragma unroll
-            for (int s = 0; s < 4; ++s) O[s][mb] = mfma(w[kk * 3 + mb], H[s][kk], O[s][mb]);
+            for (int mb = 0; mb < OMB; ++mb) O[s][mb] = mfma(w[kk * 3 + mb], H[s][kk], O[s][mb]);
         float T0 = 0.f, T2 = 0.f;
 #pragma unroll
         for (int k = 0; k < OS; ++k) {
@@ -338,46 +366,45 @@ __global__ __launch_bounds__(kWaves2 * kWave, 1) void kmvq_grad_kernel(Args a) {
           ob[3][k] = active ? 2.f * c2 * o : 0.f;
         }
         T2 *= 2.f;
-        if (active) {
-          accs[0] += c2 * T2 + c0 * T0;
-          accs[1] += -0.5f * c2 * T2;
-          accs[2] += c0 * T0;
-        }
+        accs[0] += active ? c2 * T2 + c0 * T0 : 0.f;
+        accs[1] += active ? -0.5f * c2 * T2 : 0.f;
+        accs[2] += active ? c0 * T0 : 0.f;
       }
-      // ---- output-layer weight gradient: [h_{L-1} streams | 1]^T x seeds ----
+      // ---- output layer, per stream: weight gradient ([h_{L-1} streams | 1]^T x seeds, through the
+      // transpose images) interleaved with the backward product hbar = K_L obar (registers only) ----
+      float hb[4][kNS];
       {
-        f32x4 G[3][2] = {};
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
+        float w[2 * OS];
+        load_units<2 * OS>(img, a.bwd_out, lane, w);  // unit kk * 2 + mb
+        f32x4 G[2][3] = {}, B[4][2] = {};
+        auto step = [&](auto sc) {
+          constexpr int s = decltype(sc)::value;
+          float* tA = s & 1 ? tA1 : tA0;
+          float* tB = s & 1 ? tB1 : tB0;
           put_slots<OS>(tA, ob[s], pq, gq);
           put_slots<kNS>(tB, H[s], pq, gq);
-          if (gq == 0) tB[kW * kPS + ppq] = s == 0 ? 1.f : 0.f;
+          *(gq == 0 ? tB + kW * kPS + ppq : dump) = s == 0 ? 1.f : 0.f;
           f32x4 fa[3], fb[2];
 #pragma unroll
           for (int mb = 0; mb < OMB; ++mb) fa[mb] = get_rows(tA, mb, pq, gq);
 #pragma unroll
           for (int nb = 0; nb < 2; ++nb) fb[nb] = get_rows(tB, nb, pq, gq);
 #pragma unroll
+          for (int kk = 0; kk < OS; ++kk)
+#pragma unroll
+            for (int mb = 0; mb < 2; ++mb) B[s][mb] = mfma(w[kk * 2 + mb], ob[s][kk], B[s][mb]);
+#pragma unroll
           for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
-            for (int mb = 0; mb < OMB; ++mb)
+            for (int ib = 0; ib < 2; ++ib)
 #pragma unroll
-              for (int nb = 0; nb < 2; ++nb) G[mb][nb] = mfma(fa[mb][ks], fb[nb][ks], G[mb][nb]);
-        }
-        fold<3, 2>(slab, a.qoff_out, 4 * OS, kW, G, pq, gq);
-      }
-      // ---- back through the output layer: hbar = K_L obar ----
-      float hb[4][kNS];
-      {
-        float w[2 * OS];
-        load_units<2 * OS>(img, a.bwd_out, lane, w);  // unit kk * 2 + mb
-        f32x4 B[4][2] = {};
-#pragma unroll
-        for (int kk = 0; kk < OS; ++kk)
-#pragma unroll
-          for (int mb = 0; mb < 2; ++mb)
-#pragma unroll
-            for (int s = 0; s < 4; ++s) B[s][mb] = mfma(w[kk * 2 + mb], ob[s][kk], B[s][mb]);
+              for (int ob = 0; ob < OMB; ++ob) G[ib][ob] = mfma(fb[ib][ks], fa[ob][ks], G[ib][ob]);
+        };
+        step(std::integral_constant<int, 0>{});
+        step(std::integral_constant<int, 1>{});
+        step(std::integral_constant<int, 2>{});
+        step(std::integral_constant<int, 3>{});
+        fold<2, 3>(slab, a.qoff_out, 4 * OS + 4, 4 * OS, kW, G, pq, gq, dump);  // pitch 44 / 52
 #pragma unroll
         for (int s = 0; s < 4; ++s) compact_hidden(B[s], hb[s]);
       }
@@ -397,65 +424,71 @@ __global__ __launch_bounds__(kWaves2 * kWave, 1) void kmvq_grad_kernel(Args a) {
 #pragma unroll
       for (int l = kLMax - 1; l >= 1; --l) {
         if (l < L) {
+          launder(ckh[l]); launder(cku[l]); launder(ckv[l]); launder(ckw[l]);
+          launder(ckh[l - 1]);
+          if (l - 1 > 0) { launder(cku[l - 1]); launder(ckv[l - 1]); launder(ckw[l - 1]); }
           float zb[4][kNS];
           zbar_of(ckh[l], cku[l], ckv[l], ckw[l], zb);
           const float(&ph)[kNS] = ckh[l - 1];
           const float(&pu)[kNS] = l - 1 == 0 ? zu0 : cku[l - 1];
           const float(&pv)[kNS] = l - 1 == 0 ? zv0 : ckv[l - 1];
           const float(&pw)[kNS] = l - 1 == 0 ? zw0 : ckw[l - 1];
-          f32x4 G[2][2] = {};
-          auto outer = [&](auto sc) {
+          float w[12];
+          load_units<12>(img, a.bwd[l], lane, w);  // unit kk * 2 + mb
+          f32x4 G[2][2] = {}, B[4][2] = {};
+          auto step = [&](auto sc) {
             constexpr int s = decltype(sc)::value;
+            float* tA = s & 1 ? tA1 : tA0;
+            float* tB = s & 1 ? tB1 : tB0;
             float Hp[kNS];
             stream_of<s>(ph, pu, pv, pw, Hp);
             put_slots<kNS>(tA, zb[s], pq, gq);
             put_slots<kNS>(tB, Hp, pq, gq);
-            if (gq == 0) tB[kW * kPS + ppq] = s == 0 ? 1.f : 0.f;
+            *(gq == 0 ? tB + kW * kPS + ppq : dump) = s == 0 ? 1.f : 0.f;
             f32x4 fa[2], fb[2];
 #pragma unroll
             for (int b = 0; b < 2; ++b) {
               fa[b] = get_rows(tA, b, pq, gq);
               fb[b] = get_rows(tB, b, pq, gq);
             }
+            // the backward product of this stream needs no LDS: it covers the images' round trip
+#pragma unroll
+            for (int kk = 0; kk < kNS; ++kk)
+#pragma unroll
+              for (int mb = 0; mb < 2; ++mb) B[s][mb] = mfma(w[kk * 2 + mb], zb[s][kk], B[s][mb]);
 #pragma unroll
             for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
-              for (int mb = 0; mb < 2; ++mb)
+              for (int ib = 0; ib < 2; ++ib)
 #pragma unroll
-                for (int nb = 0; nb < 2; ++nb) G[mb][nb] = mfma(fa[mb][ks], fb[nb][ks], G[mb][nb]);
+                for (int ob = 0; ob < 2; ++ob) G[ib][ob] = mfma(fb[ib][ks], fa[ob][ks], G[ib][ob]);
           };
-          outer(std::integral_constant<int, 0>{});
-          outer(std::integral_constant<int, 1>{});
-          outer(std::integral_constant<int, 2>{});
-          outer(std::integral_constant<int, 3>{});
-          fold<2, 2>(slab, a.qoff[l], kW, kW, G, pq, gq);
-          float w[12];
-          load_units<12>(img, a.bwd[l], lane, w);  // unit kk * 2 + mb
-          f32x4 B[4][2] = {};
-#pragma unroll
-          for (int kk = 0; kk < kNS; ++kk)
-#pragma unroll
-            for (int mb = 0; mb < 2; ++mb)
-#pragma unroll
-              for (int s = 0; s < 4; ++s) B[s][mb] = mfma(w[kk * 2 + mb], zb[s][kk], B[s][mb]);
+          step(std::integral_constant<int, 0>{});
+          step(std::integral_constant<int, 1>{});
+          step(std::integral_constant<int, 2>{});
+          step(std::integral_constant<int, 3>{});
+          fold<2, 2>(slab, a.qoff[l], kW, kW, kW, G, pq, gq, dump);
 #pragma unroll
           for (int s = 0; s < 4; ++s) compact_hidden(B[s], hb[s]);
         }
       }
       // layer 0: inputs y (per pair), u, v (per item), 0 (second order)
       {
+        launder(ckh[0]); launder(zu0); launder(zv0);
         float zb[4][kNS];
         zbar_of(ckh[0], zu0, zv0, zw0, zb);
-        f32x4 G[2][1] = {};
+        f32x4 G[1][2] = {};
 #pragma unroll
         for (int s = 0; s < 3; ++s) {
+          float* tA = s & 1 ? tA1 : tA0;
+          float* tB = s & 1 ? tB1 : tB0;
           put_slots<kNS>(tA, zb[s], pq, gq);
 #pragma unroll
           for (int kk = 0; kk < KD; ++kk) {
-            const int k = 4 * kk + gq;
-            if (k < D) tB[k * kPS + ppq] = s == 0 ? yb[kk] : (s == 1 ? ui[kk] : vi[kk]);
+            const int k = 4 * kk + gq;  // rows past D go to row 15 (a column no layer-0 output reads)
+            tB[(k < D ? k : 15) * kPS + ppq] = s == 0 ? yb[kk] : (s == 1 ? ui[kk] : vi[kk]);
           }
-          if (gq == 0) tB[D * kPS + ppq] = s == 0 ? 1.f : 0.f;
+          *(gq == 0 ? tB + D * kPS + ppq : dump) = s == 0 ? 1.f : 0.f;
           f32x4 fa[2], fb;
 #pragma unroll
           for (int b = 0; b < 2; ++b) fa[b] = get_rows(tA, b, pq, gq);
@@ -463,9 +496,9 @@ __global__ __launch_bounds__(kWaves2 * kWave, 1) void kmvq_grad_kernel(Args a) {
 #pragma unroll
           for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
-            for (int mb = 0; mb < 2; ++mb) G[mb][0] = mfma(fa[mb][ks], fb[ks], G[mb][0]);
+            for (int ob = 0; ob < 2; ++ob) G[0][ob] = mfma(fb[ks], fa[ob][ks], G[0][ob]);
         }
-        fold<2, 1>(slab, a.qoff[0], kW, D, G, pq, gq);
+        fold<1, 2>(slab, a.qoff[0], kW, kW, D, G, pq, gq, dump);
       }
     }
   }
@@ -475,9 +508,8 @@ __global__ __launch_bounds__(kWaves2 * kWave, 1) void kmvq_grad_kernel(Args a) {
     const float v = wave_sum(accs[q]);
     if (lane0 == 0) as[q] = v;
   }
-  __syncthreads();
-  float* gs = a.gslab + (int64_t)blockIdx.x * a.P;
-  for (int q = threadIdx.x; q < a.P; q += blockDim.x) gs[q] = slab[q];
+  float* gs = a.gslab + wave * a.P;
+  for (int q = lane0; q < a.P; q += kWave) gs[q] = slab[q];
 }
 
 // -------------------------------------------------------------------------------------------------
@@ -511,7 +543,8 @@ __global__ __launch_bounds__(kWaves * kWave, 2) void kmvq_gbar_kernel(Args a) {
 #pragma unroll
       for (int kk = 0; kk < KD; ++kk) {
         const int k = 4 * kk + g;
-        xn[kk] = (j < j_end && k < D) ? zt[j * a.ld + k] : 0.f;
+        const float v = zt[(j < j_end ? j : j_end - 1) * a.ld + (k < D ? k : D - 1)];  // unconditional load
+        xn[kk] = (j < j_end && k < D) ? v : 0.f;
       }
     }
     for (int64_t j0 = ch * kChunk; j0 < j_end; j0 += 16) {
@@ -529,7 +562,8 @@ __global__ __launch_bounds__(kWaves * kWave, 2) void kmvq_gbar_kernel(Args a) {
 #pragma unroll
         for (int kk = 0; kk < KD; ++kk) {
           const int k = 4 * kk + g;
-          xn[kk] = (j < j_end && k < D) ? zt[j * a.ld + k] : 0.f;
+          const float v = zt[(j < j_end ? j : j_end - 1) * a.ld + (k < D ? k : D - 1)];  // unconditional load
+        xn[kk] = (j < j_end && k < D) ? v : 0.f;
         }
       }
       float ckh[kLMax][kNS];
@@ -778,7 +812,7 @@ QPlan q_plan(const pdeinv_kmv_mlp_desc* d) {
     p.pm.din[l] = l == 0 ? d->dim : d->width;
     p.pm.dout[l] = l == L ? d->out_features : d->width;
     p.pm.pin[l] = l == 0 ? d->dim : mlpq::kW;
-    p.pm.pout[l] = l == L ? 4 * p.OS : mlpq::kW;
+    p.pm.pout[l] = l == L ? 4 * p.OS + 4 : mlpq::kW;  // slab row pitch (4 pitch = 16 mod 32)
     p.pm.roff[l] = ro;
     p.pm.poff[l] = po;
     ia.roff[l] = ro;
@@ -795,14 +829,14 @@ QPlan q_plan(const pdeinv_kmv_mlp_desc* d) {
   p.n_blocks2 = (int)(need2 < cus ? need2 : cus);
   p.n_blocks1 = (int)(need1 < 2 * cus ? need1 : 2 * cus);
   p.lds1 = sizeof(float) * (size_t)ia.img_floats;
-  p.lds2 = sizeof(float) * ((size_t)ia.img_floats + (((size_t)p.P + 3) & ~(size_t)3) +
-                            (size_t)mlpq::kWaves2 * mlpq::kTImg);
+  p.lds2 = sizeof(float) * ((size_t)ia.img_floats +
+                            (size_t)mlpq::kWaves2 * ((((size_t)p.P + 3) & ~(size_t)3) + mlpq::kTImg));
   size_t o = 0;
   auto take = [&](size_t bytes) { const size_t at = o; o += (bytes + 255) & ~(size_t)255; return at; };
   p.off_img = take(sizeof(float) * (size_t)ia.img_floats);
   p.off_gbar = take(sizeof(float) * (size_t)p.items * d->dim);
   p.off_gpart = take(sizeof(float) * (size_t)p.n_units * d->dim);
-  p.off_gslab = take(sizeof(float) * (size_t)cus * p.P);
+  p.off_gslab = take(sizeof(float) * (size_t)cus * mlpq::kWaves2 * p.P);
   p.off_aslab = take(sizeof(float) * (size_t)cus * mlpq::kWaves2 * 8);
   p.total = o;
   return p;
@@ -904,7 +938,7 @@ int kmvq_run(const pdeinv_kmv_mlp_desc* d, const float* z, int64_t set_stride, i
     return check_launch("kmvq_gbar_reduce_kernel");
   }
   hipLaunchKernelGGL(mlpq::kmvq_reduce_kernel, dim3((unsigned)((p.P + 255) / 256)), dim3(256), 0, st, p.pm, a.gslab,
-                     p.n_blocks2, p.P, a.aslab, (int64_t)p.n_blocks2 * mlpq::kWaves2, grad, acc);
+                     p.n_blocks2 * mlpq::kWaves2, p.P, a.aslab, (int64_t)p.n_blocks2 * mlpq::kWaves2, grad, acc);
   return check_launch("kmvq_reduce_kernel");
 }
 
