@@ -56,7 +56,8 @@ def test_kmv_residual_vs_pairwise_restatement(native):
                                                 (1, 66, 300, 16, 4, 2), (2, 530, 300, 20, 2, 2),
                                                 (2, 70, 300, 28, 12, 2), (2, 60, 300, 64, 2, 2),
                                                 (8, 40, 1 << 18, 256, 2, 0), (4, 45, 500, 100, 3, 2),
-                                                (4, 33, 256, 32, 2, 0)])
+                                                (4, 33, 256, 32, 2, 0), (8, 45, 300, 20, 3, -2), (3, 70, 300, 10, 2, -2),
+                                                (2, 300, 300, 20, 3, -2)])
 def test_kmv_general_phi_mlp_vs_pairwise_restatement(native, d, n, chunk, W, L, impl):
     """General Phi_theta = V_hypothesis (non-parametric KMV, kinetic_mckean_vlasov.py:11-120) == the
     literal pair-tensor restatement (loss, loss ground truth, terms) and its FD-checked analytic gradient
@@ -69,11 +70,15 @@ def test_kmv_general_phi_mlp_vs_pairwise_restatement(native, d, n, chunk, W, L, 
     (kmvp_grad_kernel<D, W, false>) instead of the LDS slab. Widths >= 32 (64, 256 = the C5 width, 100
     zero-padded to 128, 32) run the pair rows through the fused fp32-MFMA residual kernels (no rocBLAS),
     chunked (300 / 500 / 256 rows: partial i-blocks and j-chunks).
+    impl = -2: impl 2 with every parameter perturbed by 0.15 N(0, 1) (non-zero biases: the initialiser's
+    are zero), on the MFMA pair-tile kernels (widths <= 20: mlp_pairs_mfma.hip).
     Tolerance 2e-4 relative (fp32)."""
     from example_problems.kinetic_mckean_vlasov_example_quadratic import KineticMcKeanVlasov
     from methods.consistency_instances import kinetic_mckean_vlasov as kmv
     from core.model import V_hypothesis
     from utils import native as nat, prng
+    perturb = impl < 0
+    impl = abs(impl)
     n_t = 3
     cfg = _cfg(["pde_instance=kinetic_mckean_vlasov", f"pde_instance.domain_dim={d}"])
     pi = KineticMcKeanVlasov(cfg, prng.PRNGKey(0))
@@ -84,6 +89,8 @@ def test_kmv_general_phi_mlp_vs_pairwise_restatement(native, d, n, chunk, W, L, 
     params = net.init(prng.PRNGKey(11), np.zeros(d), device=DEV)
     dims = net.dims(d)
     flat = net.flat(params)
+    if perturb:
+        flat = flat + torch.as_tensor(0.15 * rng.standard_normal(flat.numel()), dtype=flat.dtype, device=flat.device)
     P = nr.mlp_unflat(flat.double().cpu().numpy(), dims)
     cfg_np = nr.ou_configuration(pi.initial_configuration["tilde_F"], gamma=1.0)
     loss, loss_gt, parts = nr.kmv_mlp_pairwise_loss(P, x, v, tau, cfg_np)
