@@ -92,6 +92,32 @@ __device__ __forceinline__ float ftanh(float z) {
 __device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
+// v_mfma_f32_4x4x1_16b_f32: 16 independent 4 x 4 outer products; lane 4b + j, register i of the result
+// is block b's A[lane 4b + i] * B[lane 4b + j] (tools/mfma4_probe.hip; ~0.7 of the 16x16x4 issue rate)
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, c, 0, 0, 0);
+}
+
+// Hidden-layer weight gradient dK[in][out] (+ the bias row in = 20) of one 16-pair tile: the 16 x 16
+// core (in, out < 16) on 16x16x4 (every row and column real), the 164 edge entries (in 16..20 x out 0..19,
+// in 0..15 x out 16..19) as 14 of the 16 blocks of one 4x4x1 MFMA per pair-stream — 4 + 16 MFMAs per
+// stream instead of 16 16x16x4 over a 32 x 32 tile of which 21 x 20 is real. Block b of the edge MFMA:
+// b < 8: in 16 + 4 (b >> 2) + i x out 4 (b & 3) + j;  b < 12: in 4 (b - 8) + i x out 16 + j;
+// b < 14: in 16 + 4 (b - 12) + i x out 16 + j  (i: the A lane of the block, j: the B lane).
+struct EdgeMap {
+  int ra, rb;  // image rows read by this lane: hprev feature (A), zbar feature (B)
+  int in0, out0;
+  bool live;
+  __device__ __forceinline__ explicit EdgeMap(int lane) {
+    const int b = lane >> 2, i = lane & 3;
+    if (b < 8) { in0 = 16 + 4 * (b >> 2); out0 = 4 * (b & 3); }
+    else if (b < 12) { in0 = 4 * (b - 8); out0 = 16; }
+    else { in0 = 16 + 4 * (b - 12); out0 = 16; }
+    live = b < 14;
+    ra = in0 + i;   // <= 23: rows 21..23 of the input image are never folded
+    rb = out0 + i;  // <= 19
+  }
+};
 
 // N consecutive 64-lane units of the image starting at unit u0 (u0 % 4 == 0): 16-B reads
 template <int N>
@@ -435,7 +461,8 @@ __global__ __launch_bounds__(kWaves2 * kWave, 1) void kmvq_grad_kernel(Args a) {
           const float(&pw)[kNS] = l - 1 == 0 ? zw0 : ckw[l - 1];
           float w[12];
           load_units<12>(img, a.bwd[l], lane, w);  // unit kk * 2 + mb
-          f32x4 G[2][2] = {}, B[4][2] = {};
+          f32x4 G0 = {}, E = {}, B[4][2] = {};
+          const EdgeMap em(lane);
           auto step = [&](auto sc) {
             constexpr int s = decltype(sc)::value;
             float* tA = s & 1 ? tA1 : tA0;
@@ -445,11 +472,12 @@ __global__ __launch_bounds__(kWaves2 * kWave, 1) void kmvq_grad_kernel(Args a) {
             put_slots<kNS>(tA, zb[s], pq, gq);
             put_slots<kNS>(tB, Hp, pq, gq);
             *(gq == 0 ? tB + kW * kPS + ppq : dump) = s == 0 ? 1.f : 0.f;
-            f32x4 fa[2], fb[2];
+            const f32x4 fa = get_rows(tA, 0, pq, gq), fb = get_rows(tB, 0, pq, gq);
+            f32x4 ea[4], eb[4];  // edge operands: 4 pairs per 16-byte read (pairs q + 4 ks)
 #pragma unroll
-            for (int b = 0; b < 2; ++b) {
-              fa[b] = get_rows(tA, b, pq, gq);
-              fb[b] = get_rows(tB, b, pq, gq);
+            for (int q = 0; q < 4; ++q) {
+              ea[q] = *reinterpret_cast<const f32x4*>(tB + em.ra * kPS + 4 * q);
+              eb[q] = *reinterpret_cast<const f32x4*>(tA + em.rb * kPS + 4 * q);
             }
             // the backward product of this stream needs no LDS: it covers the images' round trip
 #pragma unroll
@@ -457,17 +485,35 @@ __global__ __launch_bounds__(kWaves2 * kWave, 1) void kmvq_grad_kernel(Args a) {
 #pragma unroll
               for (int mb = 0; mb < 2; ++mb) B[s][mb] = mfma(w[kk * 2 + mb], zb[s][kk], B[s][mb]);
 #pragma unroll
-            for (int ks = 0; ks < 4; ++ks)
+            for (int ks = 0; ks < 4; ++ks) G0 = mfma(fb[ks], fa[ks], G0);
 #pragma unroll
-              for (int ib = 0; ib < 2; ++ib)
+            for (int q = 0; q < 4; ++q)
 #pragma unroll
-                for (int ob = 0; ob < 2; ++ob) G[ib][ob] = mfma(fb[ib][ks], fa[ob][ks], G[ib][ob]);
+              for (int ks = 0; ks < 4; ++ks) E = mfma4(ea[q][ks], eb[q][ks], E);
           };
           step(std::integral_constant<int, 0>{});
           step(std::integral_constant<int, 1>{});
           step(std::integral_constant<int, 2>{});
           step(std::integral_constant<int, 3>{});
-          fold<2, 2>(slab, a.qoff[l], kW, kW, kW, G, pq, gq, dump);
+          {  // core: in 4 g + r, out p; edge: lane 4 b + j holds in in0 + i (register i), out out0 + j
+            float* sl = slab + a.qoff[l];
+            float* dc[4];
+            float* de[4];
+            float vc[4], ve[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              dc[r] = sl + (4 * gq + r) * kW + pq;
+              const int in = em.in0 + r, out = em.out0 + (lane & 3);
+              de[r] = (em.live && in <= kW && out < kW) ? sl + in * kW + out : dump;
+              vc[r] = *dc[r];
+              ve[r] = *de[r];
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              *dc[r] = vc[r] + G0[r];
+              *de[r] = ve[r] + E[r];
+            }
+          }
 #pragma unroll
           for (int s = 0; s < 4; ++s) compact_hidden(B[s], hb[s]);
         }
