@@ -76,7 +76,7 @@ struct Args {
   int img_floats;
   int fwd[kLMax + 1], bwd[kLMax + 1], bias[kLMax + 1];  // unit offsets (fwd / bwd), float offsets (bias)
   int qoff[kLMax + 1];                                  // gradient-slab offsets (padded layout)
-  int fwd_out, bwd_out, bias_out, qoff_out;             // the output layer's (index L: scalar kernel args)
+  int fwd_out, bias_out, qoff_out;                      // the output layer's (index L: scalar kernel args)
   int P;                                                // padded parameter count
   const float* gbar;      // pass 2: [n_items][D]
   float* gpart;           // pass 1: [n_units][D]
@@ -98,26 +98,6 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, c, 0, 0, 0);
 }
 
-// Hidden-layer weight gradient dK[in][out] (+ the bias row in = 20) of one 16-pair tile: the 16 x 16
-// core (in, out < 16) on 16x16x4 (every row and column real), the 164 edge entries (in 16..20 x out 0..19,
-// in 0..15 x out 16..19) as 14 of the 16 blocks of one 4x4x1 MFMA per pair-stream — 4 + 16 MFMAs per
-// stream instead of 16 16x16x4 over a 32 x 32 tile of which 21 x 20 is real. Block b of the edge MFMA:
-// b < 8: in 16 + 4 (b >> 2) + i x out 4 (b & 3) + j;  b < 12: in 4 (b - 8) + i x out 16 + j;
-// b < 14: in 16 + 4 (b - 12) + i x out 16 + j  (i: the A lane of the block, j: the B lane).
-struct EdgeMap {
-  int ra, rb;  // image rows read by this lane: hprev feature (A), zbar feature (B)
-  int in0, out0;
-  bool live;
-  __device__ __forceinline__ explicit EdgeMap(int lane) {
-    const int b = lane >> 2, i = lane & 3;
-    if (b < 8) { in0 = 16 + 4 * (b >> 2); out0 = 4 * (b & 3); }
-    else if (b < 12) { in0 = 4 * (b - 8); out0 = 16; }
-    else { in0 = 16 + 4 * (b - 12); out0 = 16; }
-    live = b < 14;
-    ra = in0 + i;   // <= 23: rows 21..23 of the input image are never folded
-    rb = out0 + i;  // <= 19
-  }
-};
 
 // N consecutive 64-lane units of the image starting at unit u0 (u0 % 4 == 0): 16-B reads
 template <int N>
@@ -152,6 +132,76 @@ __device__ __forceinline__ void put_slots(float* T, const float (&v)[NS], int p,
 // F layout read: rows 16 blk + (lane & 15), the pairs (lane >> 4) + 4 ks of k-steps ks = 0..3
 __device__ __forceinline__ f32x4 get_rows(const float* T, int blk, int p, int g) {
   return *reinterpret_cast<const f32x4*>(T + (16 * blk + p) * kPS + 4 * g);
+}
+
+// Hidden-layer weight gradient dK[in][out] (+ the bias row in = 20) of one 16-pair tile: the 16 x 16
+// core (in, out < 16) on 16x16x4 (every row and column real), the 164 edge entries (in 16..20 x out 0..19,
+// in 0..15 x out 16..19) as 14 of the 16 blocks of one 4x4x1 MFMA per pair-stream — 4 + 16 MFMAs per
+// stream instead of 16 16x16x4 over a 32 x 32 tile of which 21 x 20 is real. Block b of the edge MFMA:
+// b < 8: in 16 + 4 (b >> 2) + i x out 4 (b & 3) + j;  b < 12: in 4 (b - 8) + i x out 16 + j;
+// b < 14: in 16 + 4 (b - 12) + i x out 16 + j  (i: the A lane of the block, j: the B lane).
+struct EdgeMap;
+__device__ __forceinline__ void fold_ce(float* sl, const f32x4& G0, const f32x4& E, const EdgeMap& em, int pq, int gq,
+                                        int lane, float* dump);
+struct EdgeMap {
+  int ra, rb;  // image rows read by this lane: hprev feature (A), zbar feature (B)
+  int in0, out0;
+  bool live;
+  __device__ __forceinline__ explicit EdgeMap(int lane) {
+    const int b = lane >> 2, i = lane & 3;
+    if (b < 8) { in0 = 16 + 4 * (b >> 2); out0 = 4 * (b & 3); }
+    else if (b < 12) { in0 = 4 * (b - 8); out0 = 16; }
+    else { in0 = 16 + 4 * (b - 12); out0 = 16; }
+    live = b < 14;
+    ra = in0 + i;   // <= 23: rows 21..23 of the input image are never folded
+    rb = out0 + i;  // <= 19
+  }
+};
+
+// Fold one tile's width-20 weight gradient into the wave's slab region sl (row-major [21][20], row 20 =
+// the bias): core register r = [in 4 g + r][out p]; edge register i of lane 4 b + j = [in0 + i][out0 + j].
+__device__ __forceinline__ void fold_ce(float* sl, const f32x4& G0, const f32x4& E, const EdgeMap& em, int pq, int gq,
+                                        int lane, float* dump) {
+  float* dc[4];
+  float* de[4];
+  float vc[4], ve[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    dc[r] = sl + (4 * gq + r) * kW + pq;
+    const int in = em.in0 + r, out = em.out0 + (lane & 3);
+    de[r] = (em.live && in <= kW && out < kW) ? sl + in * kW + out : dump;
+    vc[r] = *dc[r];
+    ve[r] = *de[r];
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    *dc[r] = vc[r] + G0[r];
+    *de[r] = ve[r] + E[r];
+  }
+}
+
+// One outer-product stream of a width-20 weight gradient, sum over the tile's pairs of av (x) bv (av: the
+// layer input, rows = in, plus the constant bias_row at in = 20; bv: rows = out), through the transpose
+// images: the 16 x 16 core on 16x16x4, the edge blocks on 4x4x1.
+__device__ __forceinline__ void outer_stream(float* tA, float* tB, const float (&bv)[kNS], const float (&av)[kNS],
+                                             float bias_row, int pq, int gq, int ppq, float* dump, const EdgeMap& em,
+                                             f32x4& G0, f32x4& E) {
+  put_slots<kNS>(tA, bv, pq, gq);
+  put_slots<kNS>(tB, av, pq, gq);
+  *(gq == 0 ? tB + kW * kPS + ppq : dump) = bias_row;
+  const f32x4 fa = get_rows(tA, 0, pq, gq), fb = get_rows(tB, 0, pq, gq);
+  f32x4 ea[4], eb[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    ea[q] = *reinterpret_cast<const f32x4*>(tB + em.ra * kPS + 4 * q);
+    eb[q] = *reinterpret_cast<const f32x4*>(tA + em.rb * kPS + 4 * q);
+  }
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) G0 = mfma(fb[ks], fa[ks], G0);
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) E = mfma4(ea[q][ks], eb[q][ks], E);
 }
 
 // The wave's private gradient slab (LDS, no atomics: deterministic): slab[qoff + in * pitch + out] +=
@@ -229,10 +279,8 @@ __device__ __forceinline__ void lane_dims(const float* row, int D, int g, float 
 // -------------------------------------------------------------------------------------------------
 // pass 2: d/dtheta of sum_ij l_ij (and the loss slots), 16-pair tiles
 // -------------------------------------------------------------------------------------------------
-template <int KD, int OS>
+template <int KD>
 __global__ __launch_bounds__(kWaves2 * kWave, 1) void kmvq_grad_kernel(Args a) {
-  constexpr int OMB = (OS + 3) / 4;  // output M blocks
-  static_assert(OMB <= 3 && 16 * OMB <= kRowsA, "output rows");
   extern __shared__ f32x4 lds4[];
   float* lds = reinterpret_cast<float*>(lds4);
   float* img = lds;
@@ -253,6 +301,7 @@ __global__ __launch_bounds__(kWaves2 * kWave, 1) void kmvq_grad_kernel(Args a) {
   const int L = a.L, D = a.D;
   const float c2 = -2.f * a.s;
   float accs[3] = {0.f, 0.f, 0.f};  // LOSS, HESSIAN, FRICTION slot partials
+  float cs[kNS] = {}, c0sum = 0.f;   // sum c0 h (the dl/dc remainder), sum c0 (dl/db's |b|^2 term)
 
   for (int64_t unit = wave; unit < a.n_units; unit += n_waves) {
     const int64_t it = unit / a.n_ch, ch = unit - it * a.n_ch;
@@ -359,80 +408,57 @@ __global__ __launch_bounds__(kWaves2 * kWave, 1) void kmvq_grad_kernel(Args a) {
           streams_of(ckh[l], cku[l], ckv[l], ckw[l], H);
         }
       }
-      // ---- output layer: o, o'_u, o'_v, o''_v ----
-      float ob[4][OS];
+      // ---- output layer as a quadratic form: Phi = |K_L^T h + b|^2 = h^T M h + 2 c^T h + |b|^2 with
+      // M = K_L K_L^T (20 x 20), c = K_L b (kmvq_image_kernel). The four streams' M-products give every
+      // output-side term: T0 = Phi, T2 = v^T Hess Phi v, the adjoints of the four h streams (no backward
+      // product through K_L), and dl/dM, dl/dc as two outer products over the pairs (the K_L / b gradient
+      // follows once per call, kmvq_out_post_kernel). 40 + 8 + 32 (4x4x1) MFMAs replace 60 + 80 + 96. ----
+      float hb[4][kNS];
       {
-        float w[16];
-        load_units<16>(img, a.fwd_out, lane, w);  // unit kk * 3 + mb
-        f32x4 O[4][3] = {};
-        {
-          const float* b = img + a.bias_out;
-#pragma unroll
-          for (int mb = 0; mb < 3; ++mb)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) O[0][mb][r] = 4 * mb + r < OS ? b[slot_feat(OS, 4 * mb + r, gq)] : 0.f;
-        }
+        float w[12];
+        load_units<12>(img, a.fwd_out, lane, w);  // M, unit kk * 2 + mb
+        f32x4 Mh[4][2] = {};
 #pragma unroll
         for (int s = 0; s < 4; ++s)
 #pragma unroll
           for (int kk = 0; kk < kNS; ++kk)
 #pragma unroll
-            for (int mb = 0; mb < OMB; ++mb) O[s][mb] = mfma(w[kk * 3 + mb], H[s][kk], O[s][mb]);
-        float T0 = 0.f, T2 = 0.f;
+            for (int mb = 0; mb < 2; ++mb) Mh[s][mb] = mfma(w[kk * 2 + mb], H[s][kk], Mh[s][mb]);
+        float m[4][kNS], cv[kNS];
 #pragma unroll
-        for (int k = 0; k < OS; ++k) {
-          const float o = O[0][k >> 2][k & 3], ou = O[1][k >> 2][k & 3], ov = O[2][k >> 2][k & 3],
-                      ow = O[3][k >> 2][k & 3];
-          T0 = fmaf(o, o, T0);
-          T2 = fmaf(ov, ov, fmaf(o, ow, T2));
-          // seeds: l = 2 sum o o'_u + 2 c2 sum (o'_v^2 + o o''_v) + c0 sum o^2
-          ob[0][k] = active ? 2.f * ou + 2.f * c2 * ow + 2.f * c0 * o : 0.f;
-          ob[1][k] = active ? 2.f * o : 0.f;
-          ob[2][k] = active ? 4.f * c2 * ov : 0.f;
-          ob[3][k] = active ? 2.f * c2 * o : 0.f;
+        for (int s = 0; s < 4; ++s) compact_hidden(Mh[s], m[s]);
+        const float* cb = img + a.bias_out;  // c[20], |b|^2
+#pragma unroll
+        for (int k = 0; k < 4; ++k) cv[k] = cb[4 * gq + k];
+        cv[4] = cb[16 + gq];
+        float T0 = gq == 0 ? cb[kW] : 0.f, T2 = 0.f;  // |b|^2 once per pair (lane group 0)
+        float q1[kNS], q2[kNS];
+#pragma unroll
+        for (int k = 0; k < kNS; ++k) {
+          const float m0 = m[0][k] + cv[k];  // M h + c
+          T0 = fmaf(H[0][k], m0 + cv[k], T0);
+          T2 = fmaf(H[2][k], m[2][k], fmaf(H[0][k], m[3][k], fmaf(cv[k], H[3][k], T2)));
+          // l = 2 (h^T M h'_u + c^T h'_u) + c2 T2 + c0 T0
+          hb[0][k] = active ? 2.f * m[1][k] + 2.f * c2 * m[3][k] + 2.f * c0 * m0 : 0.f;
+          hb[1][k] = active ? 2.f * m0 : 0.f;
+          hb[2][k] = active ? 4.f * c2 * m[2][k] : 0.f;
+          hb[3][k] = active ? 2.f * c2 * m0 : 0.f;
+          // dl/dM = sum h (x) (2 h'_u + 2 c2 h''_v + c0 h) + h'_v (x) 2 c2 h'_v; dl/dc = that first factor
+          // summed (the bias row) + c0 sum h (cs, a per-lane accumulator over the whole launch)
+          q1[k] = active ? 2.f * H[1][k] + 2.f * c2 * H[3][k] + c0 * H[0][k] : 0.f;
+          q2[k] = active ? 2.f * c2 * H[2][k] : 0.f;
+          cs[k] += active ? c0 * H[0][k] : 0.f;
         }
         T2 *= 2.f;
         accs[0] += active ? c2 * T2 + c0 * T0 : 0.f;
         accs[1] += active ? -0.5f * c2 * T2 : 0.f;
         accs[2] += active ? c0 * T0 : 0.f;
-      }
-      // ---- output layer, per stream: weight gradient ([h_{L-1} streams | 1]^T x seeds, through the
-      // transpose images) interleaved with the backward product hbar = K_L obar (registers only) ----
-      float hb[4][kNS];
-      {
-        float w[2 * OS];
-        load_units<2 * OS>(img, a.bwd_out, lane, w);  // unit kk * 2 + mb
-        f32x4 G[2][3] = {}, B[4][2] = {};
-        auto step = [&](auto sc) {
-          constexpr int s = decltype(sc)::value;
-          float* tA = s & 1 ? tA1 : tA0;
-          float* tB = s & 1 ? tB1 : tB0;
-          put_slots<OS>(tA, ob[s], pq, gq);
-          put_slots<kNS>(tB, H[s], pq, gq);
-          *(gq == 0 ? tB + kW * kPS + ppq : dump) = s == 0 ? 1.f : 0.f;
-          f32x4 fa[3], fb[2];
-#pragma unroll
-          for (int mb = 0; mb < OMB; ++mb) fa[mb] = get_rows(tA, mb, pq, gq);
-#pragma unroll
-          for (int nb = 0; nb < 2; ++nb) fb[nb] = get_rows(tB, nb, pq, gq);
-#pragma unroll
-          for (int kk = 0; kk < OS; ++kk)
-#pragma unroll
-            for (int mb = 0; mb < 2; ++mb) B[s][mb] = mfma(w[kk * 2 + mb], ob[s][kk], B[s][mb]);
-#pragma unroll
-          for (int ks = 0; ks < 4; ++ks)
-#pragma unroll
-            for (int ib = 0; ib < 2; ++ib)
-#pragma unroll
-              for (int ob = 0; ob < OMB; ++ob) G[ib][ob] = mfma(fb[ib][ks], fa[ob][ks], G[ib][ob]);
-        };
-        step(std::integral_constant<int, 0>{});
-        step(std::integral_constant<int, 1>{});
-        step(std::integral_constant<int, 2>{});
-        step(std::integral_constant<int, 3>{});
-        fold<2, 3>(slab, a.qoff_out, 4 * OS + 4, 4 * OS, kW, G, pq, gq, dump);  // pitch 44 / 52
-#pragma unroll
-        for (int s = 0; s < 4; ++s) compact_hidden(B[s], hb[s]);
+        c0sum += (active && gq == 0) ? c0 : 0.f;
+        const EdgeMap em(lane);
+        f32x4 G0 = {}, E = {};
+        outer_stream(tA0, tB0, q1, H[0], 1.f, pq, gq, ppq, dump, em, G0, E);
+        outer_stream(tA1, tB1, q2, H[2], 0.f, pq, gq, ppq, dump, em, G0, E);
+        fold_ce(slab + a.qoff_out, G0, E, em, pq, gq, lane, dump);
       }
       // ---- reverse sweep over the tanh layers ----
       auto zbar_of = [&](const float (&h)[kNS], const float (&zu)[kNS], const float (&zv)[kNS],
@@ -495,25 +521,7 @@ __global__ __launch_bounds__(kWaves2 * kWave, 1) void kmvq_grad_kernel(Args a) {
           step(std::integral_constant<int, 1>{});
           step(std::integral_constant<int, 2>{});
           step(std::integral_constant<int, 3>{});
-          {  // core: in 4 g + r, out p; edge: lane 4 b + j holds in in0 + i (register i), out out0 + j
-            float* sl = slab + a.qoff[l];
-            float* dc[4];
-            float* de[4];
-            float vc[4], ve[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              dc[r] = sl + (4 * gq + r) * kW + pq;
-              const int in = em.in0 + r, out = em.out0 + (lane & 3);
-              de[r] = (em.live && in <= kW && out < kW) ? sl + in * kW + out : dump;
-              vc[r] = *dc[r];
-              ve[r] = *de[r];
-            }
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              *dc[r] = vc[r] + G0[r];
-              *de[r] = ve[r] + E[r];
-            }
-          }
+          fold_ce(slab + a.qoff[l], G0, E, em, pq, gq, lane, dump);
 #pragma unroll
           for (int s = 0; s < 4; ++s) compact_hidden(B[s], hb[s]);
         }
@@ -554,6 +562,18 @@ __global__ __launch_bounds__(kWaves2 * kWave, 1) void kmvq_grad_kernel(Args a) {
     const float v = wave_sum(accs[q]);
     if (lane0 == 0) as[q] = v;
   }
+  {  // the output region's tail: [21 x 20] | c0 sum h [20] | sum c0
+    float* tail = slab + a.qoff_out + (kW + 1) * kW;
+#pragma unroll
+    for (int k = 0; k < kNS; ++k) {
+      float v = cs[k];
+#pragma unroll
+      for (int off = 8; off > 0; off >>= 1) v += __shfl_xor(v, off, 16);
+      if (p == 0) tail[slot_feat(kNS, k, g)] += v;
+    }
+    const float v = wave_sum(c0sum);
+    if (lane0 == 0) tail[kW] += v;
+  }
   float* gs = a.gslab + wave * a.P;
   for (int q = lane0; q < a.P; q += kWave) gs[q] = slab[q];
 }
@@ -561,9 +581,8 @@ __global__ __launch_bounds__(kWaves2 * kWave, 1) void kmvq_grad_kernel(Args a) {
 // -------------------------------------------------------------------------------------------------
 // pass 1: gbar partials per (item, chunk of references): sum_j grad_y Phi(x_i - x_j)
 // -------------------------------------------------------------------------------------------------
-template <int KD, int OS>
+template <int KD>
 __global__ __launch_bounds__(kWaves * kWave, 2) void kmvq_gbar_kernel(Args a) {
-  constexpr int OMB = (OS + 3) / 4;
   extern __shared__ f32x4 lds4[];
   float* img = reinterpret_cast<float*>(lds4);
   for (int q = threadIdx.x; q < a.img_floats / 4; q += blockDim.x) lds4[q] = reinterpret_cast<const f32x4*>(a.img)[q];
@@ -645,33 +664,23 @@ __global__ __launch_bounds__(kWaves * kWave, 2) void kmvq_gbar_kernel(Args a) {
           for (int k = 0; k < kNS; ++k) h[k] = ckh[l][k] = ftanh(z[k]);
         }
       }
-      float ob[OS];
-      {
-        float w[16];
-        load_units<16>(img, a.fwd_out, lane, w);
-        f32x4 O[3];
-        const float* b = img + a.bias_out;
-#pragma unroll
-        for (int mb = 0; mb < 3; ++mb)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) O[mb][r] = 4 * mb + r < OS ? b[slot_feat(OS, 4 * mb + r, gq)] : 0.f;
+      float hb[kNS];
+      {  // dPhi/dh = 2 (M h + c): the output layer as a quadratic form (see the gradient kernel)
+        float w[12];
+        load_units<12>(img, a.fwd_out, lane, w);
+        f32x4 Mh[2] = {};
 #pragma unroll
         for (int kk = 0; kk < kNS; ++kk)
 #pragma unroll
-          for (int mb = 0; mb < OMB; ++mb) O[mb] = mfma(w[kk * 3 + mb], h[kk], O[mb]);
+          for (int mb = 0; mb < 2; ++mb) Mh[mb] = mfma(w[kk * 2 + mb], h[kk], Mh[mb]);
+        float m[kNS];
+        compact_hidden(Mh, m);
+        const float* cb = img + a.bias_out;
 #pragma unroll
-        for (int k = 0; k < OS; ++k) ob[k] = active ? 2.f * O[k >> 2][k & 3] : 0.f;  // d Phi / d o
-      }
-      float hb[kNS];
-      {
-        float w[2 * OS];
-        load_units<2 * OS>(img, a.bwd_out, lane, w);
-        f32x4 B[2] = {};
-#pragma unroll
-        for (int kk = 0; kk < OS; ++kk)
-#pragma unroll
-          for (int mb = 0; mb < 2; ++mb) B[mb] = mfma(w[kk * 2 + mb], ob[kk], B[mb]);
-        compact_hidden(B, hb);
+        for (int k = 0; k < kNS; ++k) {
+          const float c = k < 4 ? cb[4 * gq + k] : cb[16 + gq];
+          hb[k] = active ? 2.f * (m[k] + c) : 0.f;
+        }
       }
 #pragma unroll
       for (int l = kLMax - 1; l >= 1; --l) {
@@ -727,8 +736,9 @@ __global__ void kmvq_gbar_reduce_kernel(const float* __restrict__ gpart, int64_t
 // weight image: lane-linear A-operand fragments, unit u of a section at ((u >> 2) * 64 + lane) * 4 + (u & 3)
 // -------------------------------------------------------------------------------------------------
 constexpr int kMaxSec = 2 * (kLMax + 1);
+constexpr int kOutRegion = (kW + 1) * kW + kW + 4;  // slab of the folded output layer: [21][20] | c0 sum h | sum c0
 struct ImageArgs {
-  int L, D, W, O, OS, KD;
+  int L, D, W, O, KD;
   int nsec;
   int sec_layer[kMaxSec], sec_bwd[kMaxSec], sec_mb[kMaxSec], sec_u0[kMaxSec], sec_units[kMaxSec];
   int64_t roff[kLMax + 1];
@@ -736,20 +746,34 @@ struct ImageArgs {
   int units_total, img_floats;
 };
 
+// The image: for each tanh layer l the forward (K_l^T, rows = outputs) and backward (K_l, rows = inputs)
+// A-operand fragments and the raw bias vector; for the output layer the fragments of M = K_L K_L^T
+// (symmetric: one orientation) and [c = K_L b, |b|^2] in its bias slot (the quadratic-form fold).
 __global__ void kmvq_image_kernel(ImageArgs ia, const float* __restrict__ prm, float* __restrict__ img) {
   const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= ia.img_floats) return;
-  const int L = ia.L;
+  const int L = ia.L, W = ia.W, O = ia.O;
+  const float* KL = prm + ia.roff[L];  // [W][O], then b [O]
+  const float* bL = KL + (int64_t)W * O;
   const int64_t unit_floats = (int64_t)ia.units_total * 64;
   if (q >= unit_floats) {  // biases (padded raw vectors), zero elsewhere
     float v = 0.f;
     for (int l = 0; l <= L; ++l) {
-      const int pout = l == L ? 4 * ia.OS : kW, dout = l == L ? ia.O : ia.W, din = l == 0 ? ia.D : ia.W;
       const int o = (int)q - ia.bias_off[l];  // bias_off: absolute float offsets
-      if (o >= 0 && o < pout) {
-        v = o < dout ? prm[ia.roff[l] + (int64_t)din * dout + o] : 0.f;
-        break;
+      if (o < 0 || o >= kW + 4) continue;
+      if (l < L) {
+        const int din = l == 0 ? ia.D : W;
+        v = o < W ? prm[ia.roff[l] + (int64_t)din * W + o] : 0.f;
+      } else if (o < W) {  // c = K_L b
+        float c = 0.f;
+        for (int k = 0; k < O; ++k) c = fmaf(KL[(int64_t)o * O + k], bL[k], c);
+        v = c;
+      } else if (o == kW) {  // |b|^2
+        float bb = 0.f;
+        for (int k = 0; k < O; ++k) bb = fmaf(bL[k], bL[k], bb);
+        v = bb;
       }
+      break;
     }
     img[q] = v;
     return;
@@ -762,23 +786,32 @@ __global__ void kmvq_image_kernel(ImageArgs ia, const float* __restrict__ prm, f
     const int l = ia.sec_layer[s], MB = ia.sec_mb[s];
     const int kk = lu / MB, mb = lu % MB;
     const int g = lane >> 4, m = lane & 15;
-    const int din = l == 0 ? ia.D : ia.W, dout = l == L ? ia.O : ia.W;
+    const int din = l == 0 ? ia.D : W;
     int in, out;
     if (!ia.sec_bwd[s]) {  // forward: A[m = out row][k = in slot]
       in = l == 0 ? 4 * kk + g : slot_feat(kNS, kk, g);
-      out = l == L ? row_feat(ia.OS, mb, m) : row_feat(kNS, mb, m);
+      out = row_feat(kNS, mb, m);
     } else {  // backward: A[m = in row][k = out slot]
       in = l == 0 ? m : row_feat(kNS, mb, m);
-      out = l == L ? slot_feat(ia.OS, kk, g) : slot_feat(kNS, kk, g);
+      out = slot_feat(kNS, kk, g);
     }
-    if (in >= 0 && in < din && out >= 0 && out < dout) v = prm[ia.roff[l] + (int64_t)in * dout + out];
+    if (l == L) {  // M[in][out] = sum_k K_L[in][k] K_L[out][k]
+      if (in >= 0 && in < W && out >= 0 && out < W) {
+        float mm = 0.f;
+        for (int k = 0; k < O; ++k) mm = fmaf(KL[(int64_t)in * O + k], KL[(int64_t)out * O + k], mm);
+        v = mm;
+      }
+    } else if (in >= 0 && in < din && out >= 0 && out < W) {
+      v = prm[ia.roff[l] + (int64_t)in * W + out];
+    }
     break;
   }
   img[q] = v;
 }
 
-// grad[real(q)] += sum_b slab[b][q] (fixed order, fp64); loss slots from the per-wave partials
-__global__ void kmvq_reduce_kernel(MlpPadMap pm, const float* __restrict__ gslab, int n_blocks, int64_t P,
+// grad[real(q)] += sum_w slab[w][q] (fixed order, fp64) for the tanh layers; loss slots from the
+// per-wave partials. The folded output layer's region is reduced by kmvq_out_post_kernel.
+__global__ void kmvq_reduce_kernel(MlpPadMap pm, const float* __restrict__ gslab, int n_slabs, int64_t P,
                                    const float* __restrict__ aslab, int64_t n_waves, float* __restrict__ grad,
                                    double* __restrict__ acc) {
   const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -786,7 +819,7 @@ __global__ void kmvq_reduce_kernel(MlpPadMap pm, const float* __restrict__ gslab
     const int64_t r = pm.real_of(q);
     if (r >= 0) {
       double s = 0.0;
-      for (int b = 0; b < n_blocks; ++b) s += (double)gslab[(int64_t)b * P + q];
+      for (int b = 0; b < n_slabs; ++b) s += (double)gslab[(int64_t)b * P + q];
       grad[r] += (float)s;
     }
   }
@@ -796,6 +829,36 @@ __global__ void kmvq_reduce_kernel(MlpPadMap pm, const float* __restrict__ gslab
     const int slot = threadIdx.x == 0 ? PDEINV_GMM_ACC_LOSS
                                       : (threadIdx.x == 1 ? PDEINV_GMM_ACC_HESSIAN : PDEINV_GMM_ACC_FRICTION);
     acc[slot] += s;
+  }
+}
+
+// Output layer from the folded sums (fixed order, fp64): with G_M = dl/dM, G_c = dl/dc, C0 = sum c0,
+//   dl/dK_L = (G_M + G_M^T) K_L + G_c b^T,   dl/db = K_L^T G_c + 2 C0 b.
+__global__ __launch_bounds__(256) void kmvq_out_post_kernel(const float* __restrict__ gslab, int n_slabs, int64_t P,
+                                                            int qoff, int W, int O, const float* __restrict__ KL,
+                                                            float* __restrict__ gL) {
+  __shared__ double red[kOutRegion];
+  for (int e = threadIdx.x; e < kOutRegion; e += blockDim.x) {
+    double s = 0.0;
+    for (int b = 0; b < n_slabs; ++b) s += (double)gslab[(int64_t)b * P + qoff + e];
+    red[e] = s;
+  }
+  __syncthreads();
+  const double* GM = red;                      // [20][20]
+  const double* Gc1 = red + kW * kW;           // bias row: sum (2 h'_u + 2 c2 h''_v + c0 h)
+  const double* Gc2 = red + (kW + 1) * kW;     // c0 sum h
+  const double C0 = red[(kW + 1) * kW + kW];
+  const float* b = KL + (int64_t)W * O;
+  for (int e = threadIdx.x; e < W * O; e += blockDim.x) {
+    const int f = e / O, o = e - f * O;
+    double s = (Gc1[f] + Gc2[f]) * (double)b[o];
+    for (int f2 = 0; f2 < W; ++f2) s += (GM[f * kW + f2] + GM[f2 * kW + f]) * (double)KL[(int64_t)f2 * O + o];
+    gL[e] += (float)s;
+  }
+  for (int o = threadIdx.x; o < O; o += blockDim.x) {
+    double s = 2.0 * C0 * (double)b[o];
+    for (int f = 0; f < W; ++f) s += (double)KL[(int64_t)f * O + o] * (Gc1[f] + Gc2[f]);
+    gL[(int64_t)W * O + o] += (float)s;
   }
 }
 
@@ -815,7 +878,7 @@ int device_cus() {
 struct QPlan {
   mlpq::ImageArgs ia;
   MlpPadMap pm;
-  int OS, KD, n_ch, n_blocks2, n_blocks1;
+  int KD, n_ch, n_blocks2, n_blocks1;
   int64_t items, n_units, P;
   int fwd[mlpq::kLMax + 1], bwd[mlpq::kLMax + 1];
   size_t lds2, lds1;                                                    // bytes
@@ -825,10 +888,9 @@ struct QPlan {
 QPlan q_plan(const pdeinv_kmv_mlp_desc* d) {
   QPlan p{};
   const int L = d->n_layers;
-  p.OS = d->out_features <= 40 ? 10 : 12;
   p.KD = d->dim <= 4 ? 1 : 2;
   mlpq::ImageArgs& ia = p.ia;
-  ia.L = L; ia.D = d->dim; ia.W = d->width; ia.O = d->out_features; ia.OS = p.OS; ia.KD = p.KD;
+  ia.L = L; ia.D = d->dim; ia.W = d->width; ia.O = d->out_features; ia.KD = p.KD;
   // image sections: per layer forward then backward, each rounded to 4 units
   int u = 0, ns = 0;
   auto sec = [&](int l, int bwd, int ks, int mb) {
@@ -840,30 +902,38 @@ QPlan q_plan(const pdeinv_kmv_mlp_desc* d) {
     return at;
   };
   for (int l = 0; l <= L; ++l) {
-    p.fwd[l] = sec(l, 0, l == 0 ? 2 : mlpq::kNS, l == L ? 3 : 2);  // layer 0: KD <= 2 k-steps (zeros past KD)
-    p.bwd[l] = sec(l, 1, l == L ? p.OS : mlpq::kNS, l == 0 ? 1 : 2);
+    p.fwd[l] = sec(l, 0, l == 0 ? 2 : mlpq::kNS, 2);  // layer 0: KD <= 2 k-steps (zeros past KD); layer L: M
+    p.bwd[l] = l < L ? sec(l, 1, mlpq::kNS, l == 0 ? 1 : 2) : 0;
   }
   ia.nsec = ns;
   ia.units_total = u;
   int bf = u * 64;
   for (int l = 0; l <= L; ++l) {
     ia.bias_off[l] = bf;
-    bf += ((l == L ? 4 * p.OS : mlpq::kW) + 3) & ~3;
+    bf += mlpq::kW + 4;  // layer L: c [20], |b|^2
   }
   ia.img_floats = (bf + 3) & ~3;
-  // padded parameter layout of the gradient slab: K [pin][pout] then b [pout]
-  p.pm.L = L;
+  // padded parameter layout of the gradient slab: K [pin][20] then b [20] for the tanh layers (row
+  // pitch 20: 4 pitch = 16 mod 32), then the folded output layer's region (kOutRegion floats). The
+  // pad map covers the tanh layers only (pm.L = L - 1); the output region goes through kmvq_out_post_kernel.
+  p.pm.L = L - 1;
   int64_t ro = 0, po = 0;
   for (int l = 0; l <= L; ++l) {
-    p.pm.din[l] = l == 0 ? d->dim : d->width;
-    p.pm.dout[l] = l == L ? d->out_features : d->width;
-    p.pm.pin[l] = l == 0 ? d->dim : mlpq::kW;
-    p.pm.pout[l] = l == L ? 4 * p.OS + 4 : mlpq::kW;  // slab row pitch (4 pitch = 16 mod 32)
+    const int din = l == 0 ? d->dim : d->width, dout = l == L ? d->out_features : d->width;
+    ia.roff[l] = ro;
     p.pm.roff[l] = ro;
     p.pm.poff[l] = po;
-    ia.roff[l] = ro;
-    ro += (int64_t)p.pm.din[l] * p.pm.dout[l] + p.pm.dout[l];
-    po += (int64_t)p.pm.pin[l] * p.pm.pout[l] + p.pm.pout[l];
+    if (l < L) {  // rows: layer 0 its D inputs, the others the padded width (the kernels' bias row is 20)
+      const int pin = l == 0 ? d->dim : mlpq::kW;
+      p.pm.din[l] = din;
+      p.pm.dout[l] = dout;
+      p.pm.pin[l] = pin;
+      p.pm.pout[l] = mlpq::kW;
+      po += (int64_t)pin * mlpq::kW + mlpq::kW;
+    } else {
+      po += mlpq::kOutRegion;
+    }
+    ro += (int64_t)din * dout + dout;
   }
   p.P = po;
   p.items = (int64_t)d->n_sets * d->n_rows;
@@ -893,20 +963,20 @@ bool q_forced_off() {
   return e && e[0] == 'r';
 }
 
-template <int KD, int OS>
+template <int KD>
 int q_launch(const mlpq::Args& a, const QPlan& p, hipStream_t st, int pass) {
   if (pass == 0) {
-    static const bool attr = hipFuncSetAttribute((const void*)mlpq::kmvq_gbar_kernel<KD, OS>,
+    static const bool attr = hipFuncSetAttribute((const void*)mlpq::kmvq_gbar_kernel<KD>,
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
     (void)attr;
-    hipLaunchKernelGGL((mlpq::kmvq_gbar_kernel<KD, OS>), dim3((unsigned)p.n_blocks1), dim3(mlpq::kWaves * kWave),
+    hipLaunchKernelGGL((mlpq::kmvq_gbar_kernel<KD>), dim3((unsigned)p.n_blocks1), dim3(mlpq::kWaves * kWave),
                        p.lds1, st, a);
     return check_launch("kmvq_gbar_kernel");
   }
-  static const bool attr = hipFuncSetAttribute((const void*)mlpq::kmvq_grad_kernel<KD, OS>,
+  static const bool attr = hipFuncSetAttribute((const void*)mlpq::kmvq_grad_kernel<KD>,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
   (void)attr;
-  hipLaunchKernelGGL((mlpq::kmvq_grad_kernel<KD, OS>), dim3((unsigned)p.n_blocks2), dim3(mlpq::kWaves2 * kWave), p.lds2,
+  hipLaunchKernelGGL((mlpq::kmvq_grad_kernel<KD>), dim3((unsigned)p.n_blocks2), dim3(mlpq::kWaves2 * kWave), p.lds2,
                      st, a);
   return check_launch("kmvq_grad_kernel");
 }
@@ -916,7 +986,7 @@ int q_launch(const mlpq::Args& a, const QPlan& p, hipStream_t st, int pass) {
 bool kmvq_supported(const pdeinv_kmv_mlp_desc* d) {
   if (q_forced_off()) return false;
   if (!(d->dim >= 1 && d->dim <= 8 && d->width >= 1 && d->width <= mlpq::kW && d->n_layers >= 1 &&
-        d->n_layers <= mlpq::kLMax && d->out_features >= 1 && d->out_features <= 48))
+        d->n_layers <= mlpq::kLMax && d->out_features >= 1))
     return false;
   return q_plan(d).lds2 <= 160 * 1024;
 }
@@ -951,7 +1021,6 @@ int kmvq_run(const pdeinv_kmv_mlp_desc* d, const float* z, int64_t set_stride, i
     a.qoff[l] = (int)p.pm.poff[l];
   }
   a.fwd_out = p.fwd[d->n_layers];
-  a.bwd_out = p.bwd[d->n_layers];
   a.bias_out = p.ia.bias_off[d->n_layers];
   a.qoff_out = (int)p.pm.poff[d->n_layers];
   a.P = (int)p.P;
@@ -968,14 +1037,7 @@ int kmvq_run(const pdeinv_kmv_mlp_desc* d, const float* z, int64_t set_stride, i
     rc = check_launch("kmvq_image_kernel");
     if (rc) return rc;
   }
-  const int key = p.KD * 100 + p.OS;
-  switch (key) {
-    case 110: rc = q_launch<1, 10>(a, p, st, pass); break;
-    case 112: rc = q_launch<1, 12>(a, p, st, pass); break;
-    case 210: rc = q_launch<2, 10>(a, p, st, pass); break;
-    case 212: rc = q_launch<2, 12>(a, p, st, pass); break;
-    default: return fail(PDEINV_ERR_UNSUPPORTED, "kmv_mlp mfma pairs: shape");
-  }
+  rc = p.KD == 1 ? q_launch<1>(a, p, st, pass) : q_launch<2>(a, p, st, pass);
   if (rc) return rc;
   if (pass == 0) {
     const int64_t nq = p.items * d->dim;
@@ -983,9 +1045,15 @@ int kmvq_run(const pdeinv_kmv_mlp_desc* d, const float* z, int64_t set_stride, i
                        p.items, p.n_ch, d->dim, a.inv_n, gbar);
     return check_launch("kmvq_gbar_reduce_kernel");
   }
+  const int n_slabs = p.n_blocks2 * mlpq::kWaves2;
   hipLaunchKernelGGL(mlpq::kmvq_reduce_kernel, dim3((unsigned)((p.P + 255) / 256)), dim3(256), 0, st, p.pm, a.gslab,
-                     p.n_blocks2 * mlpq::kWaves2, p.P, a.aslab, (int64_t)p.n_blocks2 * mlpq::kWaves2, grad, acc);
-  return check_launch("kmvq_reduce_kernel");
+                     n_slabs, p.P, a.aslab, (int64_t)n_slabs, grad, acc);
+  rc = check_launch("kmvq_reduce_kernel");
+  if (rc) return rc;
+  const int L = d->n_layers;
+  hipLaunchKernelGGL(mlpq::kmvq_out_post_kernel, dim3(1), dim3(256), 0, st, a.gslab, n_slabs, p.P, a.qoff_out,
+                     d->width, d->out_features, params + p.ia.roff[L], grad + p.ia.roff[L]);
+  return check_launch("kmvq_out_post_kernel");
 }
 
 }  // namespace pdeinv
