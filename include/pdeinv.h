@@ -401,10 +401,13 @@ typedef struct {
   float gamma;            /* friction (weights c = ds2 + ds^2 + gamma ds) */
   const float* tilde_F;   /* HOST [d*d]: Phi* = 0.5 y^T tilde_F y (…_quadratic.py:193-203) */
   int64_t chunk_rows;     /* pair rows per GEMM chunk (library path); 0 => 2^18 */
-  int32_t impl;           /* PDEINV_MLP_IMPL_*: AUTO / FUSED = the hand-written paths — width <= 28: the
-                             pair kernels (pairs built in registers, MFMA weight gradients; dim <= 8,
-                             n_layers <= 16, out <= 64; workspace ~ 2048 waves x (5 W L x 64 + P) floats,
-                             ~0.4 GB for the default 20 x 8 net); width >= 32 (dim in {2, 4, 8},
+  int32_t impl;           /* PDEINV_MLP_IMPL_*: AUTO / FUSED = the hand-written paths — width <= 20 with
+                             n_layers <= 8 and dim <= 8 (the reference default 20 x 8): 16-pair fp32 MFMA
+                             tiles (mlp_pairs_mfma.hip; any out_features; workspace ~ CUs x 4 waves x P
+                             floats + the weight image, ~15 MB for the default net); other widths <= 28:
+                             the register-ring pair kernels (pairs built in registers, MFMA weight
+                             gradients; dim <= 8, n_layers <= 16, out <= 64; workspace ~ 2048 waves x
+                             (5 W L x 64 + P) floats); width >= 32 (dim in {2, 4, 8},
                              2 <= n_layers <= 16, width <= 512 zero-padded to 32/64/128/256/512, out <= 64):
                              chunks of pair rows through the fused fp32-MFMA residual kernels of
                              pdeinv_residual_kfp_mlp; LIBRARY = pair rows through rocBLAS (any shape) */
