@@ -146,6 +146,40 @@ def test_kmv_general_phi_pair_kernels_golden_1400(native):
     assert np.abs(gg - ga).max() < 2e-4 * (1 + np.abs(ga).max()), np.abs(gg - ga).max()
 
 
+def test_kmv_general_phi_mfma_tiles_vs_ring_at_recipe_size(native, monkeypatch):
+    """The reference's KMV recipe size (scripts/parametric/KMV/run_quadratic_online.sh: d = 2, one stamp,
+    n = 5 000 -> 25 M pairs; the default 20 x 8 net, every parameter perturbed so the biases are non-zero):
+    the MFMA pair tiles (mlp_pairs_mfma.hip: 20 reference chunks per particle, every persistent wave over
+    many work units, the folded output layer) against the register-ring kernels (mlp_pairs.hip,
+    PDEINV_PAIRS_IMPL=ring), both checked against the pairwise restatement at smaller sizes above.
+    Loss slots and gradient to 2e-5 relative (fp32 sums over 25 M pairs in different orders)."""
+    from example_problems.kinetic_mckean_vlasov_example_quadratic import KineticMcKeanVlasov
+    from core.model import V_hypothesis
+    from utils import native as nat, prng
+    d, n, n_t = 2, 5000, 1
+    cfg = _cfg(["pde_instance=kinetic_mckean_vlasov", f"pde_instance.domain_dim={d}"])
+    pi = KineticMcKeanVlasov(cfg, prng.PRNGKey(0))
+    rng = np.random.default_rng(11)
+    z = _t(rng.standard_normal((n * n_t, 2 * d)))
+    tau = np.array([0.7])
+    net = V_hypothesis(output_dim=1, hidden_dims=[20] * 8)
+    params = net.init(prng.PRNGKey(11), np.zeros(d), device=DEV)
+    dims = net.dims(d)
+    flat = net.flat(params)
+    flat = flat + torch.as_tensor(0.1 * rng.standard_normal(flat.numel()), dtype=flat.dtype, device=flat.device)
+    coef = pi.coefficients(tau, z.device)
+    _, ds = nat.kmv_weights(d, 1.0, coef, z, n_t, n, 2 * d, n_t * 2 * d, want_ds=True)
+    run = lambda: nat.residual_kmv_mlp(dims, flat, z, n_t, n, 2 * d, n_t * 2 * d, ds,
+                                       pi.initial_configuration["tilde_F"], 1.0, impl=nat.MLP_IMPL_FUSED)
+    acc_q, g_q = run()
+    monkeypatch.setenv("PDEINV_PAIRS_IMPL", "ring")
+    acc_r, g_r = run()
+    a_q, a_r = acc_q.cpu().numpy(), acc_r.cpu().numpy()
+    assert np.abs(a_q - a_r).max() < 2e-5 * (1 + np.abs(a_r).max()), (a_q, a_r)
+    gq, gr = g_q.double().cpu().numpy(), g_r.double().cpu().numpy()
+    assert np.abs(gq - gr).max() < 2e-5 * np.abs(gr).max(), np.abs(gq - gr).max() / np.abs(gr).max()
+
+
 def test_partial_s_log_density_kat(native):
     """test_partial_s_log_density.py:241-311 re-created and ASSERTED: d = 10, s = 0.1,
     central differences delta = 1e-4 (ds) and 1e-3 (ds2), relative RMSE < 1e-3; plus a direct
