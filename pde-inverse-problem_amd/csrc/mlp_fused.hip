@@ -1286,6 +1286,92 @@ __global__ __launch_bounds__(kRT, 1) void wgrad2(WgradArgs a) {
     }
 }
 
+// wgrad_o: the output-layer weight gradient dKo[i][o] = sum_r sum_p A_p[r][i] B_p[r][o] (A = the last
+// hidden layer's [h, s1 z', s1 z'' + s2 z'^2, s1 zetabar], B = [ybar0..2, 2 y], o < out_features <= 64)
+// on v_mfma_f32_16x16x4_f32: 16-wide output tiles pad 40 outputs to 48 (32-wide tiles: 64), and the four
+// sample rows of a k-step sit in the lane's 16-lane group (lane (c, g): row 4 s + g, column c), so every
+// operand is a 64-byte row segment per lane group, loaded straight into registers one step ahead — no
+// LDS, no barrier (the staged fwgrad kernel it replaces ran 2 barriers per 16 rows at 8 waves per CU).
+// One wave per 64 hidden features (4 tiles) x all output tiles; workgroups = row slices.
+template <int OT>
+__global__ __launch_bounds__(kT) void wgrad_o(WgradArgs a) {
+  constexpr int FI = 4;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c16 = lane & 15, rq = lane >> 4;
+  const int slice = xcd_linear(blockIdx.x, gridDim.x);
+  const int64_t rs0 = (int64_t)slice * a.rows_per_slice;
+  const int64_t rs1 = std::min<int64_t>(rs0 + a.rows_per_slice, a.R);
+  const int i0 = wave * 16 * FI;
+  f32x4 acc[FI][OT];
+#pragma unroll
+  for (int fi = 0; fi < FI; ++fi)
+#pragma unroll
+    for (int ot = 0; ot < OT; ++ot) acc[fi][ot] = f32x4{0.f, 0.f, 0.f, 0.f};
+  struct Regs {
+    float a[FI][4], b[OT][4];
+  };
+  auto load = [&](Regs& g, int64_t rb) {  // clamped rows; columns past out_features read column 0 (dropped)
+    const int64_t r = std::min<int64_t>(rb + rq, a.R - 1);
+#pragma unroll
+    for (int fi = 0; fi < FI; ++fi) {
+      const uint32_t o = (uint32_t)(r * a.n_in + i0 + fi * 16 + c16);
+      g.a[fi][0] = ldo(a.pa0, o);
+      g.a[fi][1] = ldo(a.pa1, o);
+      g.a[fi][2] = ldo(a.pa2, o);
+      g.a[fi][3] = ldo(a.pa3, o);
+    }
+#pragma unroll
+    for (int ot = 0; ot < OT; ++ot) {
+      const int oc = ot * 16 + c16;
+      const uint32_t o = (uint32_t)(r * a.n_out + (oc < a.n_out ? oc : 0));
+      g.b[ot][0] = ldo(a.pb0, o);
+      g.b[ot][1] = ldo(a.pb1, o);
+      g.b[ot][2] = ldo(a.pb2, o);
+      g.b[ot][3] = ldo(a.pb3, o);
+    }
+  };
+  auto step = [&](const Regs& g, int64_t rb) {
+    const bool ok = rb + rq < rs1;  // rows past the slice add nothing
+    float av[FI][4];
+#pragma unroll
+    for (int fi = 0; fi < FI; ++fi) {
+      const float h = g.a[fi][0], zd = g.a[fi][1], zdd = g.a[fi][2], zeb = g.a[fi][3];
+      const float s1 = 1.f - h * h, s2 = -2.f * h * s1;
+      av[fi][0] = ok ? h : 0.f;
+      av[fi][1] = ok ? s1 * zd : 0.f;
+      av[fi][2] = ok ? fmaf(s1, zdd, s2 * zd * zd) : 0.f;
+      av[fi][3] = ok ? s1 * zeb : 0.f;
+    }
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+      for (int fi = 0; fi < FI; ++fi)
+#pragma unroll
+        for (int ot = 0; ot < OT; ++ot)
+          acc[fi][ot] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[fi][p], p == 3 ? 2.f * g.b[ot][3] : g.b[ot][p],
+                                                             acc[fi][ot], 0, 0, 0);
+  };
+  Regs g0, g1;
+  load(g0, rs0);
+  for (int64_t rb = rs0; rb < rs1; rb += 8) {  // loads unconditional (clamped), one step ahead
+    load(g1, rb + 4);
+    step(g0, rb);
+    load(g0, rb + 8);
+    step(g1, rb + 4);
+  }
+  float* out = a.part + (int64_t)slice * a.n_in * a.n_out;
+#pragma unroll
+  for (int fi = 0; fi < FI; ++fi)
+#pragma unroll
+    for (int ot = 0; ot < OT; ++ot) {
+      const int oc = ot * 16 + c16;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int i = i0 + fi * 16 + 4 * rq + q;
+        if (oc < a.n_out) out[(int64_t)i * a.n_out + oc] = acc[fi][ot][q];
+      }
+    }
+}
+
 // ---- host side ------------------------------------------------------------------------
 constexpr int kMaxWgradSlices = 256;
 constexpr int kRowGridCap = 1024;  // workgroups per row GEMM launch (persistent over row blocks)
@@ -1391,6 +1477,32 @@ static int launch_wgrad2(WgradArgs a, float* grad_out, float* scratch, hipStream
   int rc = check_launch("kfp_mlp fused weight gradient (wgrad2)");
   if (rc) return rc;
   return sum_slabs(a.part, used, (int64_t)a.n_in * a.n_out, grad_out, scratch, st);
+}
+
+// output-layer weight gradient on wgrad_o (n_in a multiple of 64, <= 256; n_out <= 64)
+template <int OT>
+static int launch_wgrad_o(WgradArgs a, int64_t part_cap, float* grad_out, float* scratch, hipStream_t st) {
+  const int waves = a.n_in / 64;
+  if (a.n_in % 64 || waves < 1 || waves > kT / 64 || a.n_out > 16 * OT || a.n_out <= 16 * (OT - 1))
+    return fail(PDEINV_ERR_INVALID, "kfp_mlp wgrad_o: shape mismatch");
+  // slabs fit in part, and their kFold-group sums in part2 (part / kFold): cap a multiple of kFold
+  int64_t cap = part_cap / ((int64_t)a.n_in * a.n_out);
+  cap = cap >= kFold ? cap / kFold * kFold : std::max<int64_t>(1, cap);
+  const int slices = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)kRowGridCap, cap, (a.R + 63) / 64}));
+  int64_t rps = (a.R + slices - 1) / slices;
+  rps = (rps + 7) & ~(int64_t)7;
+  const int used = (int)((a.R + rps - 1) / rps);
+  a.rows_per_slice = rps;
+  hipLaunchKernelGGL((wgrad_o<OT>), dim3(used), dim3(64 * waves), 0, st, a);
+  int rc = check_launch("kfp_mlp output-layer weight gradient (wgrad_o)");
+  if (rc) return rc;
+  return sum_slabs(a.part, used, (int64_t)a.n_in * a.n_out, grad_out, scratch, st);
+}
+
+// PDEINV_MLP_WGO=0: the output-layer weight gradient on the staged fwgrad kernel (A/B measurements)
+static bool use_wgo() {
+  static const bool on = [] { const char* e = getenv("PDEINV_MLP_WGO"); return !(e && e[0] == '0'); }();
+  return on;
 }
 
 // B-resident row GEMMs / LDS-free weight gradients for W in {128, 256} (PDEINV_MLP_RGEMM=0: the
@@ -1631,7 +1743,17 @@ static int run_chunk_t(const Chunk& c, const LossHook& loss, hipStream_t st) {
     g.R = R; g.n_in = W; g.n_out = O; g.part = part;
     g.pa0 = P(L, P_H); g.pa1 = P(L, P_ZD); g.pa2 = P(L, P_ZDD); g.pa3 = P(L, P_ZETABAR);
     g.pb0 = YB[0]; g.pb1 = YB[1]; g.pb2 = YB[2]; g.pb3 = Ys[0];
-    RC((launch_wgrad<GW, 64, GA_PL, GB_SM>(g, c.grad + c.poff[L], part2, st)));
+    const int64_t cap = (int64_t)part_floats(D, W, O);
+    if (WB >= 64 && WB <= 256 && use_wgo()) {
+      switch ((O + 15) / 16) {
+        case 1: RC((launch_wgrad_o<1>(g, cap, c.grad + c.poff[L], part2, st))); break;
+        case 2: RC((launch_wgrad_o<2>(g, cap, c.grad + c.poff[L], part2, st))); break;
+        case 3: RC((launch_wgrad_o<3>(g, cap, c.grad + c.poff[L], part2, st))); break;
+        default: RC((launch_wgrad_o<4>(g, cap, c.grad + c.poff[L], part2, st))); break;
+      }
+    } else {
+      RC((launch_wgrad<GW, 64, GA_PL, GB_SM>(g, c.grad + c.poff[L], part2, st)));
+    }
   }
   for (int l = L; l >= 3; --l) {
     WgradArgs g{};
