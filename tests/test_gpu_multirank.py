@@ -83,7 +83,7 @@ def test_bench_two_ranks_c4_c5(native, config, port, n):
     --config C4 (closed-form McKean-Vlasov: the mean-path and KMV all-reduces) and C5 (MLP residual +
     its gradient all-reduce) print one line with both ranks' particle-updates."""
     r = _launch(2, [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", config, "--steps", "2", "--warmup", "1",
-                    "--particles", str(n), "--no-cpu-baseline", "--no-recovery"], port, timeout=300)
+                    "--particles", str(n), "--no-cpu-baseline", "--no-recovery"], port, timeout=150)  # ~10 s when healthy: a stuck rendezvous fails fast
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
