@@ -309,20 +309,26 @@ __global__ __launch_bounds__(kT, 2) void fgemm(GemmArgs a) {
         if constexpr (!L1) load_a<BM, AM>(a, ra, r0, k0 + BK);
         load_b<BN, BMD>(a, rb, k0 + BK, n0);
       }
+      // the last tile of a K that is not a BK multiple (the reverse K = out_features product, A_S3)
+      // stops at its last valid k pair: a wave-uniform skip instead of MFMAs on the zero padding (in the
+      // other modes the branch only added spills: not compiled there)
+      const int kv = AM == A_S3 ? a.K - k0 : BK;
 #pragma unroll
       for (int kk = 0; kk < BK; kk += 2) {
-        float bv[NI];
+        if (kk < kv) {
+          float bv[NI];
 #pragma unroll
-        for (int ni = 0; ni < NI; ++ni) bv[ni] = Bs[(kk + hi) * LDB + wn * WN + ni * 32 + l31];
+          for (int ni = 0; ni < NI; ++ni) bv[ni] = Bs[(kk + hi) * LDB + wn * WN + ni * 32 + l31];
 #pragma unroll
-        for (int s = 0; s < S; ++s)
+          for (int s = 0; s < S; ++s)
 #pragma unroll
-          for (int mi = 0; mi < MI; ++mi) {
-            const float av = As[(s * BK + kk + hi) * LDA + wm * WM + mi * 32 + l31];
+            for (int mi = 0; mi < MI; ++mi) {
+              const float av = As[(s * BK + kk + hi) * LDA + wm * WM + mi * 32 + l31];
 #pragma unroll
-            for (int ni = 0; ni < NI; ++ni)
-              acc[s][mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv[ni], acc[s][mi][ni], 0, 0, 0);
-          }
+              for (int ni = 0; ni < NI; ++ni)
+                acc[s][mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv[ni], acc[s][mi][ni], 0, 0, 0);
+            }
+        }
       }
     }
 
