@@ -487,6 +487,68 @@ __global__ __launch_bounds__(kT) void l1_g_kernel(const float* __restrict__ a1, 
   }
 }
 
+// The same g on the matrix pipe (W <= 256): per wave, 16 rows at a time and 16-column groups of
+// layer 1. Z^T[c][row] = [K1; b1]^T[c][:] . [x; 1][row] as (D + 1) / 4 rounded-up v_mfma_f32_16x16x4_f32
+// (A = the K1 columns, lane constants; B = the rows' x) leaves lane (row, h) with columns 4 h + t of the
+// group in register t — exactly the (m = row, k-slot h) A layout of G[row][i] += zeta[row][c] K1[i][c]
+// (4 MFMAs per group, B = K1[i][c] lane constants, i = lane & 15 < D), so zeta = s1(z) a1 never leaves
+// the lane and the d-wide row sums need no cross-lane reduction (the VALU kernel above spends 8 wave
+// reductions per row). a1 is read as one 16-byte run per lane (4 consecutive columns of its row).
+template <int D, int W>
+__global__ __launch_bounds__(kT) void l1_g_mfma_kernel(const float* __restrict__ a1, const float* __restrict__ z,
+                                                       int64_t ldz, const float* __restrict__ K1,
+                                                       const float* __restrict__ b1, int64_t R, float* __restrict__ G) {
+  static_assert(W % 16 == 0 && W <= 256 && D <= 16, "l1_g_mfma: W <= 256, d <= 16");
+  constexpr int NG = W / 16, NS = (D + 1 + 3) / 4;  // column groups; k-steps of [x; 1]
+  const int lane = threadIdx.x & 63, c16 = lane & 15, rq = lane >> 4;
+  float kz[NG][NS], kg[NG][4];
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    const int c = 16 * g + c16;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int i = 4 * s + rq;
+      kz[g][s] = i < D ? K1[i * W + c] : (i == D ? b1[c] : 0.f);
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) kg[g][t] = c16 < D ? K1[c16 * W + 16 * g + 4 * rq + t] : 0.f;
+  }
+  const int64_t nw = (int64_t)gridDim.x * (kT / 64);
+  for (int64_t r0 = ((int64_t)blockIdx.x * (kT / 64) + (threadIdx.x >> 6)) * 16; r0 < R; r0 += nw * 16) {
+    const int64_t row = std::min<int64_t>(r0 + c16, R - 1);
+    float xb[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int i = 4 * s + rq;
+      xb[s] = i < D ? z[row * ldz + i] : (i == D ? 1.f : 0.f);
+    }
+    const f32x4* arow = reinterpret_cast<const f32x4*>(a1 + row * W + 4 * rq);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    f32x4 an = arow[0];
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      const f32x4 av = an;
+      if (g + 1 < NG) an = arow[4 * (g + 1)];  // the next group's a1 run, in flight under this group
+      f32x4 zt = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < NS; ++s) zt = __builtin_amdgcn_mfma_f32_16x16x4f32(kz[g][s], xb[s], zt, 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const float h = ftanh(zt[t]);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32((1.f - h * h) * av[t], kg[g][t], acc, 0, 0, 0);
+      }
+    }
+    // acc: lane (i = c16, h) holds G[r0 + 4 h + q][i] in register q
+    if (c16 < D) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int64_t r = r0 + 4 * rq + q;
+        if (r < R) G[r * D + c16] = acc[q];
+      }
+    }
+  }
+}
+
 // Layer-1 reverse step and its parameter gradient, from hbar1 streams (R2 final GEMM) and a1:
 //   zbar1 = s1 hb + s2 z1' h'b + s3 z1'^2 h''b + s2 a1 zetabar1,  z'bar1 = s1 h'b + 2 s2 z1' h''b,
 //   zeta1 = s1 a1;  K1[i][k] += x_i zbar1 + v_i z'bar1 + abar0_i zeta1,  b1[k] += zbar1
@@ -1505,6 +1567,12 @@ static int launch_wgrad_o(WgradArgs a, int64_t part_cap, float* grad_out, float*
   return sum_slabs(a.part, used, (int64_t)a.n_in * a.n_out, grad_out, scratch, st);
 }
 
+// PDEINV_MLP_L1G=0: g = zeta1 K1^T on the VALU kernel (wave reductions) instead of l1_g_mfma_kernel
+static bool use_l1g_mfma() {
+  static const bool on = [] { const char* e = getenv("PDEINV_MLP_L1G"); return !(e && e[0] == '0'); }();
+  return on;
+}
+
 // PDEINV_MLP_WGO=0: the output-layer weight gradient on the staged fwgrad kernel (A/B measurements)
 static bool use_wgo() {
   static const bool on = [] { const char* e = getenv("PDEINV_MLP_WGO"); return !(e && e[0] == '0'); }();
@@ -1677,7 +1745,14 @@ static int run_chunk_t(const Chunk& c, const LossHook& loss, hipStream_t st) {
     if (RG) RC((launch_rgemm<1, A_S1MUL, B_NT, E_STORE>(a, st)));
     else RC((launch_gemm1<A_S1MUL, B_NT>(a, st)));
   }
-  {
+  if constexpr (WB <= 256) {
+    if (use_l1g_mfma()) {
+      const int blocks = (int)std::min<int64_t>((R + 63) / 64, 2048);
+      hipLaunchKernelGGL((l1_g_mfma_kernel<D, WB>), dim3(blocks), dim3(kT), 0, st, A1, c.z, c.ldz, Kw(1), Bw(1), R, G);
+      RC(check_launch("kfp_mlp fused g (MFMA)"));
+    }
+  }
+  if (WB > 256 || !use_l1g_mfma()) {
     const int blocks = (int)std::min<int64_t>((R + 3) / 4, 2048);
     hipLaunchKernelGGL((l1_g_kernel<D, WB>), dim3(blocks), dim3(kT), 0, st, A1, c.z, c.ldz, Kw(1), Bw(1), R, G);
     RC(check_launch("kfp_mlp fused g"));
