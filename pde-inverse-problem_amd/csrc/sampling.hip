@@ -96,6 +96,24 @@ __global__ void gather_random_step_kernel(const float* __restrict__ traj, int64_
   for (int k = 0; k < m; ++k) dst[k] = src[k];
 }
 
+// m % 4 == 0 and 16-byte aligned rows (the C5 batch: m = 2d = 16): one thread per 16-byte quad of a
+// row, so a row is one contiguous 4-lane run per load / store instead of m scalar accesses strided by
+// the row length across the wave (each thread of a row recomputes the row's Philox draw: cheap).
+__global__ void gather_random_step_vec_kernel(const float* __restrict__ traj, int64_t N, int n_steps, int m,
+                                              uint32_t k0, uint32_t k1, uint32_t ctr, float* __restrict__ out,
+                                              int32_t* __restrict__ t_out) {
+  const int nq = m >> 2;
+  const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (e >= N * nq) return;
+  const int64_t p = e / nq;
+  const int q = (int)(e - p * nq);
+  const uint4 b = philox4x32_10(make_uint4((uint32_t)p, (uint32_t)((uint64_t)p >> 32), ctr, 0x20000000u), k0, k1);
+  const int t = (int)(((uint64_t)b.x * (uint64_t)n_steps) >> 32);  // same draw as the scalar kernel
+  if (t_out && q == 0) t_out[p] = t;
+  const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(traj + ((int64_t)t * N + p) * m) + q);
+  reinterpret_cast<f32x4*>(out + p * m)[q] = v;
+}
+
 }  // namespace pdeinv
 
 using namespace pdeinv;
@@ -105,6 +123,12 @@ extern "C" int pdeinv_gather_random_step(const float* traj, int64_t N, int32_t n
   PDEINV_REQUIRE(N >= 0 && n_steps >= 1 && m >= 1, PDEINV_ERR_INVALID, "gather_random_step: bad sizes");
   if (N == 0) return PDEINV_OK;
   PDEINV_REQUIRE(traj && out, PDEINV_ERR_INVALID, "gather_random_step: null pointer");
+  if (m % 4 == 0 && ((uintptr_t)traj & 15) == 0 && ((uintptr_t)out & 15) == 0) {
+    hipLaunchKernelGGL(gather_random_step_vec_kernel, dim3(grid_for(N * (m / 4))), dim3(kBlock), 0,
+                       (hipStream_t)stream, traj, N, n_steps, m, (uint32_t)seed, (uint32_t)(seed >> 32), ctr, out,
+                       t_out);
+    return check_launch("gather_random_step_vec_kernel");
+  }
   hipLaunchKernelGGL(gather_random_step_kernel, dim3(grid_for(N)), dim3(kBlock), 0, (hipStream_t)stream, traj, N,
                      n_steps, m, (uint32_t)seed, (uint32_t)(seed >> 32), ctr, out, t_out);
   return check_launch("gather_random_step_kernel");

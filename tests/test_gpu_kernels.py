@@ -408,9 +408,10 @@ def test_residual_mlp_library_two_threads_two_streams(native):
             assert torch.allclose(g, ref[t][1], rtol=1e-6, atol=1e-6 * ref[t][1].abs().max().item())
 
 
-def test_gather_random_step(native):
+@pytest.mark.parametrize("m", [8, 16, 6])  # 16-byte quads (m % 4 == 0) and the scalar kernel (m = 6)
+def test_gather_random_step(native, m):
     rng = np.random.default_rng(3)
-    n, N, m = 37, 5000, 8
+    n, N = 37, 5000
     traj = _t(rng.standard_normal((n, N, m)))
     out, t = native.gather_random_step(traj, seed=5, ctr=2, return_t=True)
     t = t.cpu().numpy()
