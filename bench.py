@@ -20,7 +20,10 @@ residual from the moments of all timed steps, with Richardson extrapolation over
 to cancel the O(dt) Euler–Maruyama bias; the CPU baseline — the NumPy
 restatement of sampling_utils.py in oracle/ — is timed on a bounded sample on rank 0.
 
-Launch: python bench.py [--gpus N --steps K --warmup W]; N > 1 under torch.distributed.run.
+Launch: python bench.py [--gpus N --steps K --warmup W]. For N > 1 either under torch.distributed.run
+(WORLD_SIZE must equal N, else the run exits non-zero) or plain, in which case bench.py starts the
+N-rank torch.distributed.run itself as a child process before touching the GPU. The line carries
+`ranks_seen` (the process group's size) and `backend`.
 """
 from __future__ import annotations
 
@@ -111,13 +114,18 @@ def cpu_model():
 RAMP_S = 0.3
 
 
+KERN_STATS = {}  # per-launch spread of the dominant kernel over the timed steps (filled by timed())
+
+
 def timed(step, K, W, dev, ramp=None):
     """Clock ramp, W untimed warmup steps, then K steps between barrier+synchronize; max over ranks.
     step(record) records record[0]/record[1] around the dominant kernel's launch.
     The ramp (untimed setup, like allocating the buffers) repeats the step's work for RAMP_S seconds
     first: an MI355X raises its clocks over the first ~0.1-0.3 s of sustained load (one box measured a
     20-step run 8 % below its 200-step rate without it; on another the ramp changed nothing).
-    ramp() (default: step(None)) must not feed any result of the run."""
+    ramp() (default: step(None)) must not feed any result of the run.
+    Returns (ms per step, mean dominant-launch ms); the launch spread (min over ranks of the per-rank min,
+    max over ranks of the median and of the max) goes to KERN_STATS for roofline.kernel_ms_*."""
     ramp = ramp or (lambda: step(None))
     t_end = time.perf_counter() + RAMP_S
     while time.perf_counter() < t_end:
@@ -135,7 +143,13 @@ def timed(step, K, W, dev, ramp=None):
     torch.cuda.synchronize()
     dist.barrier()
     el = dist.allreduce_max_scalar(time.perf_counter() - t0, device=dev)
-    kern_ms = dist.allreduce_max_scalar(float(np.mean([s.elapsed_time(e) for s, e in evs])), device=dev)
+    per = np.array([s.elapsed_time(e) for s, e in evs])
+    kern_ms = dist.allreduce_max_scalar(float(per.mean()), device=dev)
+    KERN_STATS.clear()
+    KERN_STATS.update(kernel_ms_min=-dist.allreduce_max_scalar(-float(per.min()), device=dev),
+                      kernel_ms_median=dist.allreduce_max_scalar(float(np.median(per)), device=dev),
+                      kernel_ms_max=dist.allreduce_max_scalar(float(per.max()), device=dev),
+                      kernel_launches_timed=int(K))
     return el * 1e3 / K, kern_ms
 
 
@@ -188,7 +202,7 @@ def base_record(a, world, value, ms, config, kern_ms, bytes_launch, kernel, traf
 # ------------------------------------------------------------------------------------------
 def run_c2(a, rank, world, dev):
     from example_problems.kinetic_fokker_planck_example_OU import problem_matrix
-    from methods.consistency_instances.kinetic_fokker_planck import recover_quadratic_drift
+    from methods.consistency_instances.kinetic_fokker_planck import recover_drift_richardson
 
     d, n, T, gamma = 4, a.n_steps, 2.0, 1.0
     N = a.particles or (1 << 21)
@@ -238,35 +252,14 @@ def run_c2(a, rank, world, dev):
         # untimed; a fixed Monte-Carlo budget (independent of --steps) of fresh moments-only passes,
         # on top of the timed steps' moments, at n = 100 and n = 200
         passes = max(a.recovery_passes, a.steps + a.warmup)
-        mom1 = mom_total.clone()
-        for _ in range(passes - (a.steps + a.warmup)):
-            r1 = native.sde_simulate(z0, n, T / n, gamma, pot, seed=seed, counter_offset=counter[0],
-                                     particle_offset=poff, traj=False, tau=False, last=False, moments=True)
-            counter[0] = (counter[0] + n + 1) & 0xFFFFFFFF
-            mom1 += dist.allreduce_sum(r1["moments"])
-        S100, _ = recover_quadratic_drift(mom1, gamma, T, d)
-        mom2 = torch.zeros_like(mom_total)
-        for _ in range(passes):  # n = 200: moments only (no trajectory needed)
-            r2 = native.sde_simulate(z0, 2 * n, T / (2 * n), gamma, pot, seed=seed, counter_offset=counter[0],
-                                     particle_offset=poff, traj=False, tau=False, last=False, moments=True)
-            counter[0] = (counter[0] + 2 * n + 1) & 0xFFFFFFFF
-            mom2 += dist.allreduce_sum(r2["moments"])
-        S200, _ = recover_quadratic_drift(mom2, gamma, T, d)
-        mom4 = torch.zeros_like(mom_total)
-        for _ in range(passes):  # n = 400
-            r4 = native.sde_simulate(z0, 4 * n, T / (4 * n), gamma, pot, seed=seed, counter_offset=counter[0],
-                                     particle_offset=poff, traj=False, tau=False, last=False, moments=True)
-            counter[0] = (counter[0] + 4 * n + 1) & 0xFFFFFFFF
-            mom4 += dist.allreduce_sum(r4["moments"])
-        S400, _ = recover_quadratic_drift(mom4, gamma, T, d)
-        # EM is weak order 1 with a smooth error expansion in dt: two Richardson levels cancel the
-        # dt and dt^2 terms; one level (2 S200 - S100) is reported beside it
-        S_rich = (8 * S400 - 6 * S200 + S100) / 3
-        S_rich1 = 2 * S200 - S100
+        rec = recover_drift_richardson(z0, F, gamma, T, n, seed, passes, counter_offset=counter[0],
+                                       particle_offset=poff, base=mom_total, base_passes=a.steps + a.warmup)
+        counter[0] = rec["counter"]
+        S_rich = rec["S_rich"]
         out["drift_err"] = float(np.abs(S_rich - F).max())
         out["drift_err_l2"] = float(np.linalg.norm(S_rich - F) / np.linalg.norm(F))
-        out["drift_err_richardson1"] = float(np.abs(S_rich1 - F).max())
-        out["drift_err_em_n100"] = float(np.abs(S100 - F).max())
+        out["drift_err_richardson1"] = float(np.abs(rec["S_rich1"] - F).max())
+        out["drift_err_em_n100"] = float(np.abs(rec["S_n"] - F).max())
         out["drift_recovery"] = ("max |S - tilde_F|, S = K + K^T the exact residual minimiser from the EM moments, "
                                  "Richardson (8 S(n=400) - 6 S(n=200) + S(n=100)) / 3, "
                                  f"{passes * world * N} trajectories per level")
@@ -597,15 +590,55 @@ def run_c5(a, rank, world, dev):
     return out
 
 
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(a) -> int:
+    """`--gpus N` (N > 1) without a torch.distributed.run rendezvous: start one as a CHILD process
+    (python -m torch.distributed.run --nproc-per-node N bench.py <same args>), before this process
+    touches the GPU, and hand back its exit code. The ranks inherit stdout, so rank 0's JSON line is
+    this command's line. The reference gets its device count from pmap over all local devices
+    (core/trainer.py:44-53); here one process per GPU is started explicitly."""
+    port = os.environ.get("MASTER_PORT") or str(free_port())
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    print(f"bench.py: launching {a.gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     a = parse()
+    if a.gpus < 1:
+        sys.exit(f"bench.py: --gpus must be >= 1 (got {a.gpus})")
+    env_ws = os.environ.get("WORLD_SIZE")
+    if env_ws is None and a.gpus > 1:
+        sys.exit(launch_ranks(a))
+    if env_ws is not None and int(env_ws) != a.gpus:
+        sys.exit(f"bench.py: launched with WORLD_SIZE={env_ws} but --gpus {a.gpus}; refusing to report a line "
+                 f"whose n_gpus would not match the ranks that ran")
+    backend = os.environ.get("PDEINV_DIST_BACKEND", "nccl")
+    if backend == "nccl" and a.gpus > max(1, torch.cuda.device_count()):
+        sys.exit(f"bench.py: --gpus {a.gpus} but {torch.cuda.device_count()} visible GPUs (RCCL needs one GPU per "
+                 f"rank; PDEINV_DIST_BACKEND=gloo shares a GPU for tests)")
     dist.init_from_env("nccl")
     rank, world = dist.rank(), dist.world_size()
+    ranks_seen = torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1
+    if ranks_seen != a.gpus:
+        sys.exit(f"bench.py: {ranks_seen} ranks joined but --gpus {a.gpus}")
     local = dist.local_device()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     native.lib()
     out = {"C2": run_c2, "C3": run_c3, "C4": run_c4, "C5": run_c5}[a.config](a, rank, world, dev)
+    out["roofline"].update(KERN_STATS)
+    out["ranks_seen"] = ranks_seen
+    out["backend"] = torch.distributed.get_backend() if torch.distributed.is_initialized() else "none (one process)"
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist.is_distributed():

@@ -368,6 +368,8 @@ typedef struct {
 #define PDEINV_MLP_IMPL_AUTO 0
 #define PDEINV_MLP_IMPL_LIBRARY 1
 #define PDEINV_MLP_IMPL_FUSED 2
+#define PDEINV_MLP_IMPL_PAIRS_RING 3 /* pdeinv_residual_kmv_mlp only: force the register-ring pair kernels
+                                        (width <= 28) instead of the MFMA pair tiles — A/B and cross-checks */
 int pdeinv_mlp_fused_supported(int32_t dim, int32_t n_layers, int32_t width, int32_t out_features);
 int64_t pdeinv_mlp_param_count(int32_t dim, int32_t n_layers, int32_t width, int32_t out_features);
 size_t pdeinv_residual_kfp_mlp_workspace_bytes(const pdeinv_kfp_mlp_desc* desc);
@@ -403,8 +405,9 @@ typedef struct {
   int64_t chunk_rows;     /* pair rows per GEMM chunk (library path); 0 => 2^18 */
   int32_t impl;           /* PDEINV_MLP_IMPL_*: AUTO / FUSED = the hand-written paths — width <= 20 with
                              n_layers <= 8 and dim <= 8 (the reference default 20 x 8): 16-pair fp32 MFMA
-                             tiles (mlp_pairs_mfma.hip; any out_features; workspace ~ CUs x 4 waves x P
-                             floats + the weight image, ~15 MB for the default net); other widths <= 28:
+                             tiles (mlp_pairs_mfma.hip; any out_features — routed before the ring limits;
+                             workspace ~ CUs x 4 waves x P floats + the weight image, ~15 MB for the default
+                             net); other widths <= 28 (or every width <= 28 under PAIRS_RING):
                              the register-ring pair kernels (pairs built in registers, MFMA weight
                              gradients; dim <= 8, n_layers <= 16, out <= 64; workspace ~ 2048 waves x
                              (5 W L x 64 + P) floats); width >= 32 (dim in {2, 4, 8},

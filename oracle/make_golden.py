@@ -121,11 +121,28 @@ def main():
                         ds=nr.partial_s_log_density(0.1, xs, cfg), ds2=nr.partial_s2_log_density(0.1, xs, cfg),
                         logp=nr.log_density(0.1, xs, cfg))
 
+    dlogrho_refcfg()
+
     # constants recipe
     np.savez_compressed(os.path.join(OUT, "constants.npz"), **{f"tilde_F_d{d}": nr.problem_constants(d)
                                                                for d in (2, 4, 8, 10)})
     for f in sorted(os.listdir(OUT)):
         print(f, os.path.getsize(os.path.join(OUT, f)))
+
+
+def dlogrho_refcfg():
+    """test_partial_s_log_density.py at its own configuration (:9-62: gamma = 0.1, P_x0 = 1, P_v0 = 0.1,
+    m0 = 0, tilde_L = 2; :243-261: d = 10, T = 1, s = 0.1, x ~ U[0, 1) of shape [3, d]). tilde_F is the
+    build's recipe (the reference's PRNGKey(2217) normals need JAX). Writes
+    tests/golden/dlogrho_d10_refcfg.npz only."""
+    d, gamma, P_x0, P_v0, s = 10, 0.1, 1.0, 0.1, 0.1
+    F = nr.problem_constants(d)
+    cfg = nr.ou_configuration(F, gamma=gamma, P_x0=P_x0, P_v0=P_v0)
+    xs = np.random.default_rng(10).uniform(size=(3, d))
+    np.savez_compressed(os.path.join(OUT, "dlogrho_d10_refcfg.npz"), F=F, x=xs, s=s, gamma=gamma, P_x0=P_x0,
+                        P_v0=P_v0, T=1.0, ds=nr.partial_s_log_density(s, xs, cfg),
+                        ds2=nr.partial_s2_log_density(s, xs, cfg), logp=nr.log_density(s, xs, cfg))
+    print("dlogrho_d10_refcfg.npz", os.path.getsize(os.path.join(OUT, "dlogrho_d10_refcfg.npz")))
 
 
 def kmv_mlp_large():
@@ -182,5 +199,7 @@ def kmv_mlp_large():
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "kmv_mlp_large":
         kmv_mlp_large()
+    elif len(sys.argv) > 1 and sys.argv[1] == "dlogrho_refcfg":
+        dlogrho_refcfg()
     else:
         main()

@@ -657,6 +657,8 @@ extern "C" int pdeinv_residual_kfp_mlp(const pdeinv_kfp_mlp_desc* d, const float
   PDEINV_REQUIRE(D >= 1 && D <= 16, PDEINV_ERR_UNSUPPORTED, "kfp_mlp: dim must be in [1, 16]");
   PDEINV_REQUIRE(d->n_layers >= 1 && d->width >= 1 && d->out_features >= 1, PDEINV_ERR_INVALID,
                  "kfp_mlp: need n_layers, width, out_features >= 1");
+  PDEINV_REQUIRE(d->impl >= PDEINV_MLP_IMPL_AUTO && d->impl <= PDEINV_MLP_IMPL_FUSED, PDEINV_ERR_INVALID,
+                 "kfp_mlp: impl must be AUTO, LIBRARY or FUSED");
   PDEINV_REQUIRE(d->true_kind == PDEINV_POT_QUADRATIC || d->true_kind == PDEINV_POT_GMM, PDEINV_ERR_UNSUPPORTED,
                  "kfp_mlp: true potential must be QUADRATIC or GMM");
   PDEINV_REQUIRE(d->true_params != nullptr, PDEINV_ERR_INVALID, "kfp_mlp: true_params is null");
@@ -1164,6 +1166,10 @@ extern "C" int pdeinv_residual_kmv_mlp(const pdeinv_kmv_mlp_desc* d, const float
   PDEINV_REQUIRE(d->n_sets >= 1 && d->n_rows >= 1, PDEINV_ERR_INVALID, "kmv_mlp: need n_sets, n_rows >= 1");
   PDEINV_REQUIRE(ld >= 2 * d->dim && set_stride >= 0, PDEINV_ERR_INVALID, "kmv_mlp: row stride < 2*dim");
   PDEINV_REQUIRE(z && ds && params && ws && acc && grad && d->tilde_F, PDEINV_ERR_INVALID, "kmv_mlp: null pointer");
+  PDEINV_REQUIRE(d->impl >= PDEINV_MLP_IMPL_AUTO && d->impl <= PDEINV_MLP_IMPL_PAIRS_RING, PDEINV_ERR_INVALID,
+                 "kmv_mlp: impl must be AUTO, LIBRARY, FUSED or PAIRS_RING");
+  PDEINV_REQUIRE(d->impl != PDEINV_MLP_IMPL_PAIRS_RING || kmv_use_pairs(d), PDEINV_ERR_UNSUPPORTED,
+                 "kmv_mlp: PAIRS_RING needs dim <= 8, width <= 28, n_layers <= 16, out_features <= 64");
   hipStream_t st = (hipStream_t)stream;
   if (kmv_use_pairs(d)) {
     switch (d->dim) {

@@ -757,16 +757,19 @@ int dispatch_w(int WP, const mlpp::Args& a, int64_t nw, hipStream_t st, bool pas
 }  // namespace
 
 // the MFMA pair-tile kernels (mlp_pairs_mfma.hip) take the shapes they cover (dim <= 8, width <= 20,
-// n_layers <= 8, out_features <= 48: the reference default); the register-ring kernels here the rest
+// n_layers <= 8, any out_features: the reference default); the register-ring kernels here the rest of
+// width <= 28 (n_layers <= 16, out_features <= 64), or every such shape under PDEINV_MLP_IMPL_PAIRS_RING
 bool kmvq_supported(const pdeinv_kmv_mlp_desc* d);
 size_t kmvq_workspace_bytes(const pdeinv_kmv_mlp_desc* d);
 int kmvq_run(const pdeinv_kmv_mlp_desc* d, const float* z, int64_t set_stride, int64_t ld, const float* ds,
              const float* params, void* ws, double* acc, float* grad, float** gbar_out, int pass, hipStream_t st);
 
-bool kmv_pairs_supported(const pdeinv_kmv_mlp_desc* d) {
+static bool ring_supported(const pdeinv_kmv_mlp_desc* d) {
   return d->dim >= 1 && d->dim <= 8 && d->width >= 1 && d->width <= 28 && d->n_layers >= 1 &&
          d->n_layers <= mlpp::kMaxL && d->out_features >= 1 && d->out_features <= 64;
 }
+
+bool kmv_pairs_supported(const pdeinv_kmv_mlp_desc* d) { return kmvq_supported(d) || ring_supported(d); }
 
 size_t kmv_pairs_workspace_bytes(const pdeinv_kmv_mlp_desc* d) {
   return kmvq_supported(d) ? kmvq_workspace_bytes(d) : pair_plan(d).total;

@@ -958,11 +958,6 @@ QPlan q_plan(const pdeinv_kmv_mlp_desc* d) {
   return p;
 }
 
-bool q_forced_off() {
-  const char* e = getenv("PDEINV_PAIRS_IMPL");  // "ring": the register-ring kernels (A/B experiments)
-  return e && e[0] == 'r';
-}
-
 template <int KD>
 int q_launch(const mlpq::Args& a, const QPlan& p, hipStream_t st, int pass) {
   if (pass == 0) {
@@ -984,7 +979,7 @@ int q_launch(const mlpq::Args& a, const QPlan& p, hipStream_t st, int pass) {
 }  // namespace
 
 bool kmvq_supported(const pdeinv_kmv_mlp_desc* d) {
-  if (q_forced_off()) return false;
+  if (d->impl == PDEINV_MLP_IMPL_PAIRS_RING) return false;  // explicit A/B selection of the register-ring kernels
   if (!(d->dim >= 1 && d->dim <= 8 && d->width >= 1 && d->width <= mlpq::kW && d->n_layers >= 1 &&
         d->n_layers <= mlpq::kLMax && d->out_features >= 1))
     return false;

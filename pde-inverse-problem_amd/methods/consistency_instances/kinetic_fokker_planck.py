@@ -154,6 +154,35 @@ def recover_quadratic_drift(moments3, gamma: float, T: float, d: int):
     return S, -S @ ex + c
 
 
+def recover_drift_richardson(z0, F, gamma: float, T: float, n: int, seed: int, passes: int, counter_offset: int = 0,
+                             particle_offset: int = 0, base=None, base_passes: int = 0):
+    """Recovered drift of the kinetic OU problem (BASELINE metric, third part): S = K + K^T, the exact
+    minimiser of the quadratic-model loss (recover_quadratic_drift — what Adam converges to on this convex
+    loss, main.py:11-29 / kinetic_fokker_planck_example_OU.py:209-220), from the moments of `passes`
+    Philox ensembles simulated at n, 2n and 4n EM steps (moments only, fused into the simulator).
+    Semi-implicit EM is weak order 1 with a smooth expansion in dt, so two Richardson levels
+    (8 S(4n) - 6 S(2n) + S(n)) / 3 cancel the dt and dt^2 bias; one level 2 S(2n) - S(n) is returned too.
+    `base` (+ `base_passes`): moment sums already accumulated at n (bench.py's timed steps). Moments are
+    all-reduced over ranks, so every rank returns the same S. Returns a dict with S_rich, S_rich1, S_n
+    and the next free counter."""
+    d = F.shape[0]
+    pot = dict(kind=native.POT_QUADRATIC, params=F)
+    ctr = int(counter_offset)
+    S = {}
+    for mult in (1, 2, 4):
+        nn = mult * n
+        mom = base.clone() if (mult == 1 and base is not None) else None
+        todo = passes - (base_passes if mult == 1 and base is not None else 0)
+        for _ in range(max(0, todo)):
+            r = native.sde_simulate(z0, nn, T / nn, gamma, pot, seed=seed, counter_offset=ctr,
+                                    particle_offset=particle_offset, traj=False, tau=False, last=False, moments=True)
+            ctr = (ctr + nn + 1) & 0xFFFFFFFF
+            m = dist.allreduce_sum(r["moments"])
+            mom = m.clone() if mom is None else mom.add_(m)
+        S[mult], _ = recover_quadratic_drift(mom, gamma, T, d)
+    return {"S_rich": (8 * S[4] - 6 * S[2] + S[1]) / 3, "S_rich1": 2 * S[2] - S[1], "S_n": S[1], "counter": ctr}
+
+
 def test_fn(forward_fn, pde_instance, rng):
     return {}  # kinetic_fokker_planck.py:72-92 returns {}
 

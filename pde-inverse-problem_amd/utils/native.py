@@ -103,7 +103,7 @@ class KmvMlpDesc(ctypes.Structure):
                 ("impl", ctypes.c_int32)]
 
 
-MLP_IMPL_AUTO, MLP_IMPL_LIBRARY, MLP_IMPL_FUSED = 0, 1, 2
+MLP_IMPL_AUTO, MLP_IMPL_LIBRARY, MLP_IMPL_FUSED, MLP_IMPL_PAIRS_RING = 0, 1, 2, 3  # PAIRS_RING: kmv_mlp only
 
 ACTIVATIONS = {"celu": 0, "relu": 1, "tanh": 2, "elu": 3, "silu": 4, "softplus": 5, "gelu": 6}
 

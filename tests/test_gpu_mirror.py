@@ -151,7 +151,7 @@ def test_kmv_general_phi_mfma_tiles_vs_ring_at_recipe_size(native, monkeypatch):
     n = 5 000 -> 25 M pairs; the default 20 x 8 net, every parameter perturbed so the biases are non-zero):
     the MFMA pair tiles (mlp_pairs_mfma.hip: 20 reference chunks per particle, every persistent wave over
     many work units, the folded output layer) against the register-ring kernels (mlp_pairs.hip,
-    PDEINV_PAIRS_IMPL=ring), both checked against the pairwise restatement at smaller sizes above.
+    impl = MLP_IMPL_PAIRS_RING), both checked against the pairwise restatement at smaller sizes above.
     Loss slots and gradient to 2e-5 relative (fp32 sums over 25 M pairs in different orders)."""
     from example_problems.kinetic_mckean_vlasov_example_quadratic import KineticMcKeanVlasov
     from core.model import V_hypothesis
@@ -169,11 +169,10 @@ def test_kmv_general_phi_mfma_tiles_vs_ring_at_recipe_size(native, monkeypatch):
     flat = flat + torch.as_tensor(0.1 * rng.standard_normal(flat.numel()), dtype=flat.dtype, device=flat.device)
     coef = pi.coefficients(tau, z.device)
     _, ds = nat.kmv_weights(d, 1.0, coef, z, n_t, n, 2 * d, n_t * 2 * d, want_ds=True)
-    run = lambda: nat.residual_kmv_mlp(dims, flat, z, n_t, n, 2 * d, n_t * 2 * d, ds,
-                                       pi.initial_configuration["tilde_F"], 1.0, impl=nat.MLP_IMPL_FUSED)
-    acc_q, g_q = run()
-    monkeypatch.setenv("PDEINV_PAIRS_IMPL", "ring")
-    acc_r, g_r = run()
+    run = lambda impl: nat.residual_kmv_mlp(dims, flat, z, n_t, n, 2 * d, n_t * 2 * d, ds,
+                                            pi.initial_configuration["tilde_F"], 1.0, impl=impl)
+    acc_q, g_q = run(nat.MLP_IMPL_FUSED)
+    acc_r, g_r = run(nat.MLP_IMPL_PAIRS_RING)
     a_q, a_r = acc_q.cpu().numpy(), acc_r.cpu().numpy()
     assert np.abs(a_q - a_r).max() < 2e-5 * (1 + np.abs(a_r).max()), (a_q, a_r)
     gq, gr = g_q.double().cpu().numpy(), g_r.double().cpu().numpy()

@@ -77,6 +77,34 @@ def test_bench_two_ranks(native):
     assert abs(out["value"] * out["ms_per_step"] / 1e3 - 2 * 65536 * 101) < 1e-6 * out["value"]
 
 
+def test_bench_plain_gpus2_launches_two_ranks(native):
+    """A plain `python bench.py --gpus 2` (no torch.distributed.run around it, as the driver may issue it)
+    starts the 2-rank rendezvous itself (a child process, before any GPU call) and the line reports the
+    ranks that really ran (gloo override: both ranks share the test box's one GPU)."""
+    env = dict(os.environ, PDEINV_DIST_BACKEND="gloo")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+                        "--particles", "65536", "--no-cpu-baseline", "--no-recovery"],
+                       env=env, cwd=ROOT, capture_output=True, text=True, timeout=150)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == out["ranks_seen"] == 2 and out["backend"] == "gloo", out
+    assert abs(out["value"] * out["ms_per_step"] / 1e3 - 2 * 65536 * 101) < 1e-6 * out["value"]
+    ks = out["roofline"]
+    assert ks["kernel_ms_min"] <= ks["kernel_ms_median"] <= ks["kernel_ms_max"]
+
+
+def test_bench_mismatched_launch_fails(native):
+    """torch.distributed.run with 2 ranks but --gpus 1: bench.py refuses to print a line (non-zero exit)."""
+    r = _launch(2, [os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "2", "--warmup", "1",
+                    "--particles", "65536", "--no-cpu-baseline", "--no-recovery"], 29619, timeout=120)
+    assert r.returncode != 0
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")], r.stdout[-2000:]
+
+
 @pytest.mark.parametrize("config,port,n", [("C4", 29615, 65536), ("C5", 29617, 65536)])
 def test_bench_two_ranks_c4_c5(native, config, port, n):
     """The driver's 8-GPU scaling launch runs every config through the same code: world-2 bench.py

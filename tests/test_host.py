@@ -230,6 +230,33 @@ def test_abi_argument_validation_without_gpu():
     assert L.pdeinv_realnvp_value_and_grad(None, None, None, 0, None, 0, 0, None, None, None, 0, None) \
         == native.PDEINV_ERR_INVALID
     assert L.pdeinv_mlp_fused_supported(3, 2, 256, 40) == 0 and L.pdeinv_mlp_fused_supported(8, 2, 256, 40) == 1
+    # impl is validated (PDEINV_MLP_IMPL_PAIRS_RING selects the register-ring pair kernels, kmv_mlp only)
+    F = (ctypes.c_float * 4)(1, 0, 0, 1)
+    km = native.KmvMlpDesc()
+    km.dim, km.n_layers, km.width, km.out_features, km.n_sets, km.n_rows, km.gamma = 2, 8, 20, 40, 1, 64, 1.0
+    km.tilde_F = ctypes.cast(F, ctypes.c_void_p)
+    dummy = ctypes.c_void_p(16)
+    call = lambda: L.pdeinv_residual_kmv_mlp(ctypes.byref(km), dummy, 0, 4, dummy, dummy, dummy, dummy, dummy, None)
+    km.impl = 7
+    assert call() == native.PDEINV_ERR_INVALID and b"impl" in L.pdeinv_last_error()
+    km.impl, km.width = native.MLP_IMPL_PAIRS_RING, 64
+    assert call() == native.PDEINV_ERR_UNSUPPORTED and b"PAIRS_RING" in L.pdeinv_last_error()
+    fm = native.KfpMlpDesc()
+    fm.dim, fm.n_layers, fm.width, fm.out_features, fm.impl = 4, 2, 256, 40, native.MLP_IMPL_PAIRS_RING
+    assert L.pdeinv_residual_kfp_mlp(ctypes.byref(fm), None, 0, 0, None, 0, 0, None, 0, 0, None, None, None, None,
+                                     None) == native.PDEINV_ERR_INVALID
+
+
+def test_bench_refuses_mismatched_world_size():
+    """bench.py exits non-zero, printing no line, when torch.distributed.run's WORLD_SIZE disagrees with
+    --gpus (checked before any GPU call, so it runs here), and rejects --gpus 0."""
+    import subprocess
+    import sys
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    for argv in (["--gpus", "1"], ["--gpus", "0"]):
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + argv + ["--steps", "1", "--warmup", "0"],
+                           env=env, capture_output=True, text=True, timeout=120)
+        assert r.returncode != 0 and "{" not in r.stdout, (r.stdout, r.stderr[-2000:])
 
 
 def test_oracle_under_asan():

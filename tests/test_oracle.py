@@ -170,6 +170,33 @@ def test_partial_s_log_density_fd_kat():
     assert np.allclose(nr.partial_s_log_density(s, x, cfg), g["ds"], rtol=1e-12)
 
 
+def test_partial_s_log_density_fd_kat_reference_configuration():
+    """test_partial_s_log_density.py at its own configuration (:9-62: gamma = 0.1, P_v0 = 0.1; d = 10,
+    s = 0.1, x ~ U[0, 1)): the restatement's analytic ds / ds2 vs central differences (delta 1e-4 / 1e-3),
+    relative RMSE < 1e-3, and the build's host coefficient rows (the kernel's inputs) reproduce them."""
+    from example_problems.kinetic_mckean_vlasov_example_quadratic import dlogrho_coefficients
+    from example_problems.kinetic_fokker_planck_example_OU import initialize_configuration
+    g = np.load(os.path.join(GOLD, "dlogrho_d10_refcfg.npz"))
+    assert float(g["gamma"]) == 0.1 and float(g["P_v0"]) == 0.1 and float(g["T"]) == 1.0
+    cfg = nr.ou_configuration(g["F"], gamma=0.1, P_x0=1.0, P_v0=0.1)
+    x, s = g["x"], float(g["s"])
+    fd1 = (nr.log_density(s + 1e-4, x, cfg) - nr.log_density(s - 1e-4, x, cfg)) / 2e-4
+    fd2 = (nr.partial_s_log_density(s + 1e-3, x, cfg) - nr.partial_s_log_density(s - 1e-3, x, cfg)) / 2e-3
+    assert np.sqrt(np.mean(((g["ds"] - fd1) / fd1) ** 2)) < 1e-3
+    assert np.sqrt(np.mean(((g["ds2"] - fd2) / fd2) ** 2)) < 1e-3
+    assert np.allclose(nr.partial_s_log_density(s, x, cfg), g["ds"], rtol=1e-12)
+    # the coefficient rows the GPU kernel consumes: ds = a1 + beta1.r + r^T G1 r, r = m1 - x
+    d = x.shape[1]
+    ic = initialize_configuration(d, gamma_friction=0.1, P_x_0_scale=1.0, P_v_0_scale=0.1)
+    c = dlogrho_coefficients([s], ic, d)[0]
+    m1, a1, b1, G1 = c[:d], c[d], c[d + 1:2 * d + 1], c[2 * d + 1:2 * d + 1 + d * d].reshape(d, d)
+    o = 2 * d + 1 + d * d
+    a2, b2, G2 = c[o], c[o + 1:o + 1 + d], c[o + 1 + d:o + 1 + d + d * d].reshape(d, d)
+    r = m1 - x
+    assert np.allclose(a1 + r @ b1 + np.einsum("ni,ij,nj->n", r, G1, r), g["ds"], rtol=1e-9, atol=1e-9)
+    assert np.allclose(a2 + r @ b2 + np.einsum("ni,ij,nj->n", r, G2, r), g["ds2"], rtol=1e-9, atol=1e-9)
+
+
 @pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLD, "sde_*.npz"))))
 def test_oracle_reproduces_sde_golden(oracle_lib, path):
     g = np.load(path)

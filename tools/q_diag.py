@@ -29,14 +29,10 @@ def run(d, n, n_t, W, L, O=0):
     _, ds = native.kmv_weights(d, 1.0, coef, z, n_t, n, 2 * d, n_t * 2 * d, want_ds=True)
     out = {}
     for impl in ("mfma", "ring"):
-        if impl == "ring":
-            os.environ["PDEINV_PAIRS_IMPL"] = "ring"
-        else:
-            os.environ.pop("PDEINV_PAIRS_IMPL", None)
-        acc, g = native.residual_kmv_mlp(dims, flat, z, n_t, n, 2 * d, n_t * 2 * d, ds, ic["tilde_F"], 1.0, impl=2)
+        acc, g = native.residual_kmv_mlp(dims, flat, z, n_t, n, 2 * d, n_t * 2 * d, ds, ic["tilde_F"], 1.0,
+                                         impl=native.MLP_IMPL_FUSED if impl == "mfma" else native.MLP_IMPL_PAIRS_RING)
         torch.cuda.synchronize()
         out[impl] = (acc.double().cpu().numpy(), g.double().cpu().numpy())
-    os.environ.pop("PDEINV_PAIRS_IMPL", None)
     a0, g0 = out["mfma"]
     a1, g1 = out["ring"]
     print(json.dumps({"d": d, "n": n, "n_t": n_t, "W": W, "L": L, "O": dims[-1],
