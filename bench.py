@@ -614,6 +614,9 @@ def launch_ranks(a) -> int:
 
 def main():
     a = parse()
+    if os.environ.get("PDEINV_BENCH_WATCHDOG"):  # tests: a stuck rank dumps its Python stacks and exits
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["PDEINV_BENCH_WATCHDOG"]), exit=True)
     if a.gpus < 1:
         sys.exit(f"bench.py: --gpus must be >= 1 (got {a.gpus})")
     env_ws = os.environ.get("WORLD_SIZE")

@@ -8,9 +8,9 @@
 // contributes grad Phi(y_ij) (pass 1: gbar_i = mean_j grad Phi), and pass 2 differentiates
 //     l_ij = u_i . grad Phi(y_ij) + c2 v_i^T Hess Phi(y_ij) v_i + c0_i Phi(y_ij)
 // (u_i = 2 s gbar_i, c2 = -2 s, c0_i = 2 s w_it; s = 1 / (n^2 n_sets); loss assembly :74-97) with
-// respect to theta. Covered: dim <= 8, width <= 20 (zero-padded to 20), 1 <= n_layers <= 8,
-// out_features <= 48 — the reference default is 2 -> 20 x 8 -> 40 (configurations/neural_network/
-// MLP.yaml:4-5, model.py:45-47).
+// respect to theta. Covered: dim <= 8, width <= 20 (zero-padded to 20), 1 <= n_layers <= 8, any
+// out_features (the output layer is folded into a 20 x 20 quadratic form) — the reference default is
+// 2 -> 20 x 8 -> 40 (configurations/neural_network/MLP.yaml:4-5, model.py:45-47).
 //
 // Layout. A wave owns 16 pairs (i, j..j+15) of one particle i. Every activation tile is the C/D
 // fragment of a 16x16x4 MFMA: the pair on lane & 15 (the MFMA's N), the feature on (lane >> 4,
@@ -77,6 +77,7 @@ struct Args {
   int fwd[kLMax + 1], bwd[kLMax + 1], bias[kLMax + 1];  // unit offsets (fwd / bwd), float offsets (bias)
   int qoff[kLMax + 1];                                  // gradient-slab offsets (padded layout)
   int fwd_out, bias_out, qoff_out;                      // the output layer's (index L: scalar kernel args)
+  int h0_off;                                           // h0 = the last hidden layer at input 0 (float offset)
   int P;                                                // padded parameter count
   const float* gbar;      // pass 2: [n_items][D]
   float* gpart;           // pass 1: [n_units][D]
@@ -408,13 +409,22 @@ __global__ __launch_bounds__(kWaves2 * kWave, 1) void kmvq_grad_kernel(Args a) {
           streams_of(ckh[l], cku[l], ckv[l], ckw[l], H);
         }
       }
-      // ---- output layer as a quadratic form: Phi = |K_L^T h + b|^2 = h^T M h + 2 c^T h + |b|^2 with
-      // M = K_L K_L^T (20 x 20), c = K_L b (kmvq_image_kernel). The four streams' M-products give every
+      // ---- output layer as a quadratic form: Phi = |K_L^T h + b|^2 = dh^T M dh + 2 c0^T dh + |y0|^2 with
+      // M = K_L K_L^T (20 x 20), dh = h - h0, c0 = K_L y0, y0 = K_L^T h0 + b (kmvq_h0_kernel,
+      // kmvq_image_kernel). The four streams' M-products give every
       // output-side term: T0 = Phi, T2 = v^T Hess Phi v, the adjoints of the four h streams (no backward
       // product through K_L), and dl/dM, dl/dc as two outer products over the pairs (the K_L / b gradient
       // follows once per call, kmvq_out_post_kernel). 40 + 8 + 32 (4x4x1) MFMAs replace 60 + 80 + 96. ----
       float hb[4][kNS];
       {
+        // the primal enters the quadratic form shifted by h0 (Phi = dh^T M dh + 2 c0^T dh + |y0|^2 with
+        // dh = h - h0, y0 = K_L^T h0 + b, c0 = K_L y0): every term is then O(|y|) where the net's output
+        // y is small — pairs near the origin of a trained net, where Phi*(0) = 0 — instead of the
+        // difference of O(|b|^2) terms (the unshifted fold's fp32 cancellation)
+        const float* h0p = img + a.h0_off;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) H[0][k] -= h0p[4 * gq + k];
+        H[0][4] -= h0p[16 + gq];
         float w[12];
         load_units<12>(img, a.fwd_out, lane, w);  // M, unit kk * 2 + mb
         f32x4 Mh[4][2] = {};
@@ -427,11 +437,11 @@ __global__ __launch_bounds__(kWaves2 * kWave, 1) void kmvq_grad_kernel(Args a) {
         float m[4][kNS], cv[kNS];
 #pragma unroll
         for (int s = 0; s < 4; ++s) compact_hidden(Mh[s], m[s]);
-        const float* cb = img + a.bias_out;  // c[20], |b|^2
+        const float* cb = img + a.bias_out;  // c0[20], |y0|^2
 #pragma unroll
         for (int k = 0; k < 4; ++k) cv[k] = cb[4 * gq + k];
         cv[4] = cb[16 + gq];
-        float T0 = gq == 0 ? cb[kW] : 0.f, T2 = 0.f;  // |b|^2 once per pair (lane group 0)
+        float T0 = gq == 0 ? cb[kW] : 0.f, T2 = 0.f;  // |y0|^2 once per pair (lane group 0)
         float q1[kNS], q2[kNS];
 #pragma unroll
         for (int k = 0; k < kNS; ++k) {
@@ -665,7 +675,11 @@ __global__ __launch_bounds__(kWaves * kWave, 2) void kmvq_gbar_kernel(Args a) {
         }
       }
       float hb[kNS];
-      {  // dPhi/dh = 2 (M h + c): the output layer as a quadratic form (see the gradient kernel)
+      {  // dPhi/dh = 2 (M (h - h0) + c0): the output layer as a quadratic form (see the gradient kernel)
+        const float* h0p = img + a.h0_off;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) h[k] -= h0p[4 * gq + k];
+        h[4] -= h0p[16 + gq];
         float w[12];
         load_units<12>(img, a.fwd_out, lane, w);
         f32x4 Mh[2] = {};
@@ -743,35 +757,71 @@ struct ImageArgs {
   int sec_layer[kMaxSec], sec_bwd[kMaxSec], sec_mb[kMaxSec], sec_u0[kMaxSec], sec_units[kMaxSec];
   int64_t roff[kLMax + 1];
   int bias_off[kLMax + 1];
+  int h0_off;  // float offset of h0 (kW + 4 floats)
   int units_total, img_floats;
 };
+
+// h0 = the last tanh layer's output at input 0 and y0 = K_L^T h0 + b (one block): the expansion point of
+// the folded output layer (h0y0 = [h0 (W) | y0 (O)], fp64 slots). h0 goes through the pair kernels' own
+// fp32 arithmetic (ftanh), so that dh = h(y) - h0 vanishes at y = 0 and the tanh approximation's bias
+// cancels in it; any h0 keeps the fold exact (y0 and c0 are formed from the stored h0, in fp64).
+__global__ __launch_bounds__(256) void kmvq_h0_kernel(ImageArgs ia, const float* __restrict__ prm,
+                                                      double* __restrict__ h0y0) {
+  __shared__ float hs[2][kW];
+  const int L = ia.L, W = ia.W, O = ia.O, t = threadIdx.x;
+  for (int l = 0; l < L; ++l) {
+    const int din = l == 0 ? ia.D : W;
+    const float* K = prm + ia.roff[l];
+    if (t < W) {
+      float z = K[(int64_t)din * W + t];  // the bias (layer 0: the input is 0)
+      if (l > 0)
+        for (int k = 0; k < W; ++k) z = fmaf(hs[(l - 1) & 1][k], K[(int64_t)k * W + t], z);
+      hs[l & 1][t] = ftanh(z);
+    }
+    __syncthreads();
+  }
+  const float* h0 = hs[(L - 1) & 1];
+  const float* KL = prm + ia.roff[L];
+  for (int o = t; o < O; o += blockDim.x) {
+    double y = (double)KL[(int64_t)W * O + o];
+    for (int f = 0; f < W; ++f) y += (double)h0[f] * (double)KL[(int64_t)f * O + o];
+    h0y0[W + o] = y;
+  }
+  if (t < W) h0y0[t] = (double)h0[t];
+}
 
 // The image: for each tanh layer l the forward (K_l^T, rows = outputs) and backward (K_l, rows = inputs)
 // A-operand fragments and the raw bias vector; for the output layer the fragments of M = K_L K_L^T
 // (symmetric: one orientation) and [c = K_L b, |b|^2] in its bias slot (the quadratic-form fold).
-__global__ void kmvq_image_kernel(ImageArgs ia, const float* __restrict__ prm, float* __restrict__ img) {
+__global__ void kmvq_image_kernel(ImageArgs ia, const float* __restrict__ prm, const double* __restrict__ h0y0,
+                                  float* __restrict__ img) {
   const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= ia.img_floats) return;
   const int L = ia.L, W = ia.W, O = ia.O;
   const float* KL = prm + ia.roff[L];  // [W][O], then b [O]
-  const float* bL = KL + (int64_t)W * O;
   const int64_t unit_floats = (int64_t)ia.units_total * 64;
   if (q >= unit_floats) {  // biases (padded raw vectors), zero elsewhere
     float v = 0.f;
+    const double* y0 = h0y0 + W;
+    if ((int)q >= ia.h0_off && (int)q < ia.h0_off + kW + 4) {
+      const int o = (int)q - ia.h0_off;
+      img[q] = o < W ? (float)h0y0[o] : 0.f;
+      return;
+    }
     for (int l = 0; l <= L; ++l) {
       const int o = (int)q - ia.bias_off[l];  // bias_off: absolute float offsets
       if (o < 0 || o >= kW + 4) continue;
       if (l < L) {
         const int din = l == 0 ? ia.D : W;
         v = o < W ? prm[ia.roff[l] + (int64_t)din * W + o] : 0.f;
-      } else if (o < W) {  // c = K_L b
-        float c = 0.f;
-        for (int k = 0; k < O; ++k) c = fmaf(KL[(int64_t)o * O + k], bL[k], c);
-        v = c;
-      } else if (o == kW) {  // |b|^2
-        float bb = 0.f;
-        for (int k = 0; k < O; ++k) bb = fmaf(bL[k], bL[k], bb);
-        v = bb;
+      } else if (o < W) {  // c0 = K_L y0
+        double c = 0.0;
+        for (int k = 0; k < O; ++k) c += (double)KL[(int64_t)o * O + k] * y0[k];
+        v = (float)c;
+      } else if (o == kW) {  // |y0|^2
+        double yy = 0.0;
+        for (int k = 0; k < O; ++k) yy += y0[k] * y0[k];
+        v = (float)yy;
       }
       break;
     }
@@ -832,12 +882,15 @@ __global__ void kmvq_reduce_kernel(MlpPadMap pm, const float* __restrict__ gslab
   }
 }
 
-// Output layer from the folded sums (fixed order, fp64): with G_M = dl/dM, G_c = dl/dc, C0 = sum c0,
-//   dl/dK_L = (G_M + G_M^T) K_L + G_c b^T,   dl/db = K_L^T G_c + 2 C0 b.
+// Output layer from the folded sums (fixed order, fp64): with G_M = dl/dM, G_c = dl/dc0, C0 = sum c0 (the
+// weight of |y0|^2), and c0 = K_L y0, y0 = K_L^T h0 + b, M = K_L K_L^T:
+//   dl/dK_L = (G_M + G_M^T) K_L + G_c y0^T + h0 (K_L^T G_c)^T + 2 C0 h0 y0^T,
+//   dl/db   = K_L^T G_c + 2 C0 y0                                  (h0 = 0: the unshifted fold)
 __global__ __launch_bounds__(256) void kmvq_out_post_kernel(const float* __restrict__ gslab, int n_slabs, int64_t P,
                                                             int qoff, int W, int O, const float* __restrict__ KL,
-                                                            float* __restrict__ gL) {
+                                                            const double* __restrict__ h0y0, float* __restrict__ gL) {
   __shared__ double red[kOutRegion];
+  extern __shared__ double ktg[];  // K_L^T G_c [O]
   for (int e = threadIdx.x; e < kOutRegion; e += blockDim.x) {
     double s = 0.0;
     for (int b = 0; b < n_slabs; ++b) s += (double)gslab[(int64_t)b * P + qoff + e];
@@ -848,18 +901,21 @@ __global__ __launch_bounds__(256) void kmvq_out_post_kernel(const float* __restr
   const double* Gc1 = red + kW * kW;           // bias row: sum (2 h'_u + 2 c2 h''_v + c0 h)
   const double* Gc2 = red + (kW + 1) * kW;     // c0 sum h
   const double C0 = red[(kW + 1) * kW + kW];
-  const float* b = KL + (int64_t)W * O;
+  const double* h0 = h0y0;
+  const double* y0 = h0y0 + W;
+  for (int o = threadIdx.x; o < O; o += blockDim.x) {
+    double s = 0.0;
+    for (int f = 0; f < W; ++f) s += (double)KL[(int64_t)f * O + o] * (Gc1[f] + Gc2[f]);
+    ktg[o] = s;
+  }
+  __syncthreads();
   for (int e = threadIdx.x; e < W * O; e += blockDim.x) {
     const int f = e / O, o = e - f * O;
-    double s = (Gc1[f] + Gc2[f]) * (double)b[o];
+    double s = (Gc1[f] + Gc2[f]) * y0[o] + h0[f] * (ktg[o] + 2.0 * C0 * y0[o]);
     for (int f2 = 0; f2 < W; ++f2) s += (GM[f * kW + f2] + GM[f2 * kW + f]) * (double)KL[(int64_t)f2 * O + o];
     gL[e] += (float)s;
   }
-  for (int o = threadIdx.x; o < O; o += blockDim.x) {
-    double s = 2.0 * C0 * (double)b[o];
-    for (int f = 0; f < W; ++f) s += (double)KL[(int64_t)f * O + o] * (Gc1[f] + Gc2[f]);
-    gL[(int64_t)W * O + o] += (float)s;
-  }
+  for (int o = threadIdx.x; o < O; o += blockDim.x) gL[(int64_t)W * O + o] += (float)(ktg[o] + 2.0 * C0 * y0[o]);
 }
 
 }  // namespace mlpq
@@ -882,7 +938,7 @@ struct QPlan {
   int64_t items, n_units, P;
   int fwd[mlpq::kLMax + 1], bwd[mlpq::kLMax + 1];
   size_t lds2, lds1;                                                    // bytes
-  size_t off_img, off_gbar, off_gpart, off_gslab, off_aslab, total;  // bytes
+  size_t off_img, off_gbar, off_gpart, off_gslab, off_aslab, off_h0, total;  // bytes
 };
 
 QPlan q_plan(const pdeinv_kmv_mlp_desc* d) {
@@ -910,8 +966,10 @@ QPlan q_plan(const pdeinv_kmv_mlp_desc* d) {
   int bf = u * 64;
   for (int l = 0; l <= L; ++l) {
     ia.bias_off[l] = bf;
-    bf += mlpq::kW + 4;  // layer L: c [20], |b|^2
+    bf += mlpq::kW + 4;  // layer L: c0 [20], |y0|^2
   }
+  ia.h0_off = bf;
+  bf += mlpq::kW + 4;
   ia.img_floats = (bf + 3) & ~3;
   // padded parameter layout of the gradient slab: K [pin][20] then b [20] for the tanh layers (row
   // pitch 20: 4 pitch = 16 mod 32), then the folded output layer's region (kOutRegion floats). The
@@ -954,6 +1012,7 @@ QPlan q_plan(const pdeinv_kmv_mlp_desc* d) {
   p.off_gpart = take(sizeof(float) * (size_t)p.n_units * d->dim);
   p.off_gslab = take(sizeof(float) * (size_t)cus * mlpq::kWaves2 * p.P);
   p.off_aslab = take(sizeof(float) * (size_t)cus * mlpq::kWaves2 * 8);
+  p.off_h0 = take(sizeof(double) * (size_t)(d->width + d->out_features));
   p.total = o;
   return p;
 }
@@ -1016,6 +1075,7 @@ int kmvq_run(const pdeinv_kmv_mlp_desc* d, const float* z, int64_t set_stride, i
     a.qoff[l] = (int)p.pm.poff[l];
   }
   a.fwd_out = p.fwd[d->n_layers];
+  a.h0_off = p.ia.h0_off;
   a.bias_out = p.ia.bias_off[d->n_layers];
   a.qoff_out = (int)p.pm.poff[d->n_layers];
   a.P = (int)p.P;
@@ -1026,9 +1086,11 @@ int kmvq_run(const pdeinv_kmv_mlp_desc* d, const float* z, int64_t set_stride, i
   a.aslab = (float*)(w + p.off_aslab);
   if (gbar_out) *gbar_out = gbar;
   int rc = PDEINV_OK;
+  double* h0y0 = (double*)(w + p.off_h0);
   if (pass == 0) {
+    hipLaunchKernelGGL(mlpq::kmvq_h0_kernel, dim3(1), dim3(256), 0, st, p.ia, params, h0y0);
     hipLaunchKernelGGL(mlpq::kmvq_image_kernel, dim3((unsigned)((p.ia.img_floats + 255) / 256)), dim3(256), 0, st,
-                       p.ia, params, (float*)(w + p.off_img));
+                       p.ia, params, (const double*)h0y0, (float*)(w + p.off_img));
     rc = check_launch("kmvq_image_kernel");
     if (rc) return rc;
   }
@@ -1046,8 +1108,9 @@ int kmvq_run(const pdeinv_kmv_mlp_desc* d, const float* z, int64_t set_stride, i
   rc = check_launch("kmvq_reduce_kernel");
   if (rc) return rc;
   const int L = d->n_layers;
-  hipLaunchKernelGGL(mlpq::kmvq_out_post_kernel, dim3(1), dim3(256), 0, st, a.gslab, n_slabs, p.P, a.qoff_out,
-                     d->width, d->out_features, params + p.ia.roff[L], grad + p.ia.roff[L]);
+  hipLaunchKernelGGL(mlpq::kmvq_out_post_kernel, dim3(1), dim3(256), sizeof(double) * (size_t)d->out_features, st,
+                     a.gslab, n_slabs, p.P, a.qoff_out, d->width, d->out_features, params + p.ia.roff[L],
+                     (const double*)h0y0, grad + p.ia.roff[L]);
   return check_launch("kmvq_out_post_kernel");
 }
 

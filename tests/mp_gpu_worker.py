@@ -77,6 +77,26 @@ def dp_residual(out_dir, shards="0", B=(3000, 2000, 40000)):
                 res[key + "_loss"] = float(out["loss"])
                 res[key + "_grad_norm"] = float(out["grad_norm"])
                 res[key + "_grad"] = _flat_grad(out["grad"]).double().cpu().numpy()
+    # KMV, quadratic interaction, shared clock (the simulated interacting system): loss and grad from the
+    # all-reduced per-stamp moments (= the residual of the union of the ranks' particles), grad_norm the mean
+    # of the per-rank norms on the rank-local moments. World 1 also evaluates the union ("all").
+    from example_problems.kinetic_mckean_vlasov_example_quadratic import KineticMcKeanVlasov
+    from methods.consistency_instances import kinetic_mckean_vlasov as kmv
+    cfg = config.compose("config", ["pde_instance=kinetic_mckean_vlasov", f"pde_instance.domain_dim={d}"])
+    pi = KineticMcKeanVlasov(cfg, prng.PRNGKey(0))
+    net = QuadraticModel(d)
+    params = net.init(prng.PRNGKey(11), np.zeros(d), device=dev)
+    nk, tau = 4000, np.array([0.3, 0.9, 1.5])
+    zk = (rng.standard_normal((nk, len(tau), 2 * d)) * 1.3).astype(np.float32)
+    kruns = runs + ([("all", 1)] if W > 0 else [])
+    for r, ws in kruns:
+        part = zk if r == "all" else zk[r * (nk // ws):(r + 1) * (nk // ws)]
+        data = {"0T": torch.as_tensor(part.reshape(-1, 2 * d), device=dev), "tau_0T": tau, "shared_time": True}
+        out = kmv.value_and_grad_fn(net.apply, params, data, None, pi)
+        key = f"KMV_quadratic_{r}"
+        res[key + "_loss"] = float(out["loss"])
+        res[key + "_grad_norm"] = float(out["grad_norm"])
+        res[key + "_grad"] = _flat_grad(out["grad"]).double().cpu().numpy()
     np.savez(os.path.join(out_dir, f"rank{rank}.npz"), world=world, **res)
 
 

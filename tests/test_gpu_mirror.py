@@ -146,6 +146,53 @@ def test_kmv_general_phi_pair_kernels_golden_1400(native):
     assert np.abs(gg - ga).max() < 2e-4 * (1 + np.abs(ga).max()), np.abs(gg - ga).max()
 
 
+@pytest.mark.parametrize("scale", [3e-4, 0.005])
+def test_kmv_general_phi_output_near_zero(native, scale):
+    """The regime training drives the interaction net into (Phi*(0) = 0): the output layer's bias is set to
+    b = -K_L^T h(0), so the net's output y vanishes at the origin, and the particles sit close together
+    (x ~ scale N(0, 1)), so every pair's |y| is small against |b|. The MFMA pair tiles fold the output
+    layer into a quadratic form expanded at h(0) (mlp_pairs_mfma.hip): the value term, the Hessian term
+    and the gradient must keep their RELATIVE accuracy against the fp64 pair-tensor restatement (an
+    unshifted fold h^T M h + 2 c^T h + |b|^2 loses it to cancellation, ~eps |b|^2 / |y|^2). Reference
+    default net (20 x 8, out 40), perturbed. Tolerances 2e-4 relative to each term / the gradient norm."""
+    from example_problems.kinetic_mckean_vlasov_example_quadratic import KineticMcKeanVlasov
+    from core.model import V_hypothesis
+    from utils import native as nat, prng
+    d, n, n_t, W, L = 2, 160, 2, 20, 8
+    cfg = _cfg(["pde_instance=kinetic_mckean_vlasov", f"pde_instance.domain_dim={d}"])
+    pi = KineticMcKeanVlasov(cfg, prng.PRNGKey(0))
+    rng = np.random.default_rng(21)
+    x = (scale * rng.standard_normal((n, n_t, d))).astype(np.float32).astype(np.float64)
+    v = rng.standard_normal((n, n_t, d)).astype(np.float32).astype(np.float64)
+    tau = np.array([0.4, 1.2])
+    net = V_hypothesis(output_dim=1, hidden_dims=[W] * L)
+    dims = net.dims(d)
+    flat = net.flat(net.init(prng.PRNGKey(11), np.zeros(d), device=DEV)).double().cpu().numpy()
+    flat = flat + 0.15 * rng.standard_normal(flat.size)
+    P = nr.mlp_unflat(flat.astype(np.float32).astype(np.float64), dims)
+    h0 = np.zeros(d)
+    for K, b in P[:-1]:
+        h0 = np.tanh(h0 @ K + b)
+    Ko, _ = P[-1]
+    P[-1] = (Ko, (-(h0 @ Ko)).astype(np.float32).astype(np.float64))
+    flat = nr.mlp_flat(P)
+    cfg_np = nr.ou_configuration(pi.initial_configuration["tilde_F"], gamma=1.0)
+    loss, loss_gt, parts = nr.kmv_mlp_pairwise_loss(P, x, v, tau, cfg_np)
+    ga = nr.mlp_flat(nr.kmv_mlp_grad_analytic(P, x, v, tau, cfg_np))
+    z = _t(np.concatenate([x, v], -1).reshape(-1, 2 * d))
+    coef = pi.coefficients(tau, z.device)
+    _, ds = nat.kmv_weights(d, 1.0, coef, z, n_t, n, 2 * d, n_t * 2 * d, want_ds=True)
+    acc, g = nat.residual_kmv_mlp(dims, _t(flat), z, n_t, n, 2 * d, n_t * 2 * d, ds,
+                                  pi.initial_configuration["tilde_F"], 1.0, impl=nat.MLP_IMPL_FUSED)
+    out = nat.kfp_terms_finalize(acc, g, 1.0).cpu().numpy()
+    fric = out[nat.KFP_SLOTS.index("loss_friction")]
+    hess = out[nat.KFP_SLOTS.index("loss_Hessian")]
+    assert abs(fric - 2 * parts["value"]) < 2e-4 * abs(2 * parts["value"]), (fric, 2 * parts["value"])
+    assert abs(hess - parts["hessian"]) < 2e-4 * abs(parts["hessian"]), (hess, parts["hessian"])
+    gg = g.double().cpu().numpy()
+    assert np.linalg.norm(gg - ga) < 2e-4 * np.linalg.norm(ga), np.linalg.norm(gg - ga) / np.linalg.norm(ga)
+
+
 def test_kmv_general_phi_mfma_tiles_vs_ring_at_recipe_size(native, monkeypatch):
     """The reference's KMV recipe size (scripts/parametric/KMV/run_quadratic_online.sh: d = 2, one stamp,
     n = 5 000 -> 25 M pairs; the default 20 x 8 net, every parameter perturbed so the biases are non-zero):

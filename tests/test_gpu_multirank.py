@@ -33,6 +33,7 @@ def _launch(nproc, args, port, timeout=180, rccl=False):
         env.update(PDEINV_DIST_FORCE="1", HSA_ENABLE_IPC_MODE_LEGACY="0")
     else:
         env["PDEINV_DIST_BACKEND"] = "gloo"
+    env.setdefault("PDEINV_BENCH_WATCHDOG", str(max(30, timeout - 30)))  # bench.py: stuck ranks dump stacks
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr=127.0.0.1", f"--master-port={port}"] + args
     return subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=timeout)
@@ -123,7 +124,8 @@ def test_bench_two_ranks_c4_c5(native, config, port, n):
 def test_dp_residual_matches_pmap_mean_of_shards(native, tmp_path):
     """2 ranks (gloo) vs the two shards evaluated one at a time: loss and grad = the shard means,
     grad_norm = the mean of the shard gradients' norms (trainer.py:44-53), for the quadratic, GMM and
-    MLP models of the KFP residual. Tolerance 1e-5 relative (fp32 terms, fp64 all-reduce)."""
+    MLP models of the KFP residual; and the shared-clock KMV residual (pooled moments). Tolerance 1e-5
+    relative (fp32 terms, fp64 all-reduce)."""
     worker = [os.path.join(ROOT, "tests", "mp_gpu_worker.py"), "dp_residual"]
     ref_dir, d2 = tmp_path / "shards", tmp_path / "w2"
     ref_dir.mkdir()
@@ -146,6 +148,18 @@ def test_dp_residual_matches_pmap_mean_of_shards(native, tmp_path):
             assert abs(g[f"{kind}_{k}_loss"] - loss) < 1e-5 * (1 + abs(loss)), (kind, g[f"{kind}_{k}_loss"], loss)
             assert abs(g[f"{kind}_{k}_grad_norm"] - gnorm) < 1e-5 * (1 + gnorm), (kind, g[f"{kind}_{k}_grad_norm"], gnorm)
             assert np.abs(g[f"{kind}_{k}_grad"] - grad).max() < 1e-5 * (1 + np.abs(grad).max()), kind
+    # KMV with a shared clock: loss / grad = the residual of the union of both ranks' particles (pooled
+    # per-stamp moments: the moments enter the KMV loss nonlinearly, so this is NOT the mean of the shard
+    # losses), grad_norm = the mean of the per-rank norms on rank-local moments (trainer.py:44-53)
+    kind = "KMV_quadratic"
+    loss, grad = ref[f"{kind}_all_loss"], ref[f"{kind}_all_grad"]
+    gnorm = np.mean([np.linalg.norm(ref[f"{kind}_{r}_grad"]) for r in range(2)])
+    assert abs(loss - np.mean([ref[f"{kind}_{r}_loss"] for r in range(2)])) > 1e-5 * (1 + abs(loss))  # pooled != mean
+    for k in range(2):
+        g = got[k]
+        assert abs(g[f"{kind}_{k}_loss"] - loss) < 1e-5 * (1 + abs(loss)), (g[f"{kind}_{k}_loss"], loss)
+        assert abs(g[f"{kind}_{k}_grad_norm"] - gnorm) < 1e-5 * (1 + gnorm), (g[f"{kind}_{k}_grad_norm"], gnorm)
+        assert np.abs(g[f"{kind}_{k}_grad"] - grad).max() < 1e-5 * (1 + np.abs(grad).max())
 
 
 @pytest.mark.parametrize("exchange,port", [("fused", 29631), ("per_update", 29632)])
