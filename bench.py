@@ -90,6 +90,10 @@ def parse():
     p.add_argument("--c4-separate-sums", action="store_true",
                    help="C4: the next simulate's mean-path sums as their own launch (pdeinv_mf_sums) instead of "
                         "inside the KMV pass (pdeinv_kmv_moments_weights_mf_sums), for A/B")
+    p.add_argument("--c4-schedule", default="fused", choices=["fused", "concurrent"],
+                   help="C4 steady state: 'fused' = the next simulate's mean-path sums inside the KMV pass; "
+                        "'concurrent' = the unfused KMV pass (HBM-bound) on the main stream and pdeinv_mf_sums "
+                        "(VALU-bound) on a side stream at the same time")
     p.add_argument("--cpu-procs", type=int, default=0,
                    help="CPU-baseline shard processes (0 = the per-GPU host share, os.cpu_count() // 8)")
     return p.parse_args()
@@ -392,6 +396,7 @@ def run_c4(a, rank, world, dev):
         return torch.from_numpy(dlogrho_coefficients(tau, ic, d).astype(np.float32)).pin_memory()
 
     coef_next = [host_coef(counter[0])]
+    side = torch.cuda.Stream(device=dev)
     ev = {"sums": [], "res": []}
     sums_next = [None]  # rank-local mean-path sums of the next simulate, from the previous step's KMV pass
 
@@ -413,7 +418,20 @@ def run_c4(a, rank, world, dev):
             record[1].record()
         del keep
         counter[0] = (counter[0] + n + 1) & 0xFFFFFFFF
-        if a.c4_separate_sums:
+        if a.c4_schedule == "concurrent" and not a.c4_separate_sums:
+            # the next simulate's sums depend only on (seed, counter, ids, z0): they run on the side stream
+            # beside the read-bound KMV pass of this step; the next step's all-reduce waits for them
+            desc_n, keep_n = native.mf_desc(N, d, n, T / n, gamma, A, seed=key.seed, counter_offset=counter[0],
+                                            particle_offset=poff)
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                sn = native.mf_sums(desc_n, z0)
+            del keep_n
+            mom, wst = native.kmv_moments_weights(d, gamma, coef, bufs["traj"], n, N, N * 2 * d, 2 * d)
+            torch.cuda.current_stream().wait_stream(side)
+            sn.record_stream(torch.cuda.current_stream())
+            sums_next[0] = sn
+        elif a.c4_separate_sums:
             mom, wst = native.kmv_moments_weights(d, gamma, coef, bufs["traj"], n, N, N * 2 * d, 2 * d)
         else:  # steady state: the KMV pass also sums the next simulate's mean-path noise (same z0 ensemble)
             desc_n, keep_n = native.mf_desc(N, d, n, T / n, gamma, A, seed=key.seed, counter_offset=counter[0],
@@ -502,13 +520,22 @@ def run_c4(a, rank, world, dev):
     res_bytes = N * n * 8 * d
     out["c4_schedule"] = ("two-stream pipeline: simulate k+1 (+ its mean-path sums) on one stream concurrent with "
                           "the KMV pass + residual of step k on another, double-buffered trajectory" if pipeline else
-                          "serial" + (", mean-path sums of the next simulate inside the KMV pass"
-                                      if not a.c4_separate_sums else ", separate mean-path sums"))
+                          "serial" + (", separate mean-path sums" if a.c4_separate_sums else
+                                      (", mean-path sums of the next simulate on a side stream concurrent with the "
+                                       "KMV pass" if a.c4_schedule == "concurrent" else
+                                       ", mean-path sums of the next simulate inside the KMV pass")))
     if a.c4_separate_sums or pipeline:
         out["mean_path"] = {"kernel": "mf_sums_kernel<8> + slab reduce (+ all-reduce) + mf_path_kernel",
                             "ms": sums_ms, "normals_per_s": N * (n + 1) * d / (sums_ms / 1e3)}
         out["residual"] = {"kernel": "kmv_moments_weights_kernel<8> + slab reduce + split", "ms": res_ms,
                            "algorithmic_bytes": res_bytes, "GBps": res_bytes / (res_ms / 1e3) / 1e9}
+    elif a.c4_schedule == "concurrent":
+        out["mean_path"] = {"kernel": "all-reduce of the sums the previous step's side stream produced + mf_path_kernel",
+                            "ms": sums_ms}
+        out["residual"] = {"kernel": "kmv_moments_weights_kernel<8> + slab reduce + split (main stream) concurrent with "
+                                     "the next simulate's mf_sums_kernel<8> (side stream)", "ms": res_ms,
+                           "algorithmic_bytes": res_bytes, "GBps": res_bytes / (res_ms / 1e3) / 1e9,
+                           "next_normals_per_s": N * (n + 1) * d / (res_ms / 1e3)}
     else:
         out["mean_path"] = {"kernel": "all-reduce of the sums the previous KMV pass produced + mf_path_kernel",
                             "ms": sums_ms}
