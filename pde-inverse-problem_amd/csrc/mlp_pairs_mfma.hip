@@ -50,7 +50,7 @@ constexpr int kLMax = 8;     // hidden (tanh) layers
 constexpr int kWaves = 8;    // waves per block of pass 1 (two blocks per CU)
 constexpr int kWaves2 = 4;   // waves per block of pass 2: one per SIMD (512 registers: the checkpoints stay in registers)
 constexpr int kChunk = 256;  // references per work unit (16 tiles)
-constexpr int kPS = 24;      // LDS image row pitch (floats)
+constexpr int kPS = 28;      // LDS image row pitch (floats); odd rows shifted by one 16-byte chunk (img_at)
 constexpr int kRowsA = 48, kRowsB = 32;
 constexpr int kTImg = (kRowsA + kRowsB) * kPS;  // floats per wave: the [A | B] transpose images
 
@@ -114,6 +114,15 @@ __device__ __forceinline__ void load_units(const float* img, int u0, int lane, f
 
 __device__ __forceinline__ int pos_of(int p) { return 4 * (p & 3) + (p >> 2); }
 
+// Transpose-image addressing: element (row, pair position pos) at row * 28 + pos, odd rows one 16-byte
+// chunk further right. Pitch 28 puts the two lane groups of a put_slots ds_write_b32 (rows 4 apart) on
+// opposite bank halves, and the shift keeps get_rows' ds_read_b128 lane groups on 16 distinct chunks;
+// with the edge table below the edge reads are conflict-free as well (bank model: the 24-float pitch had
+// 2-way conflicts on every slot write and on half of the edge reads — SQ_LDS_BANK_CONFLICT was 35 % of
+// the LDS-active cycles of pass 2, profiles/r03_kmv_pairs_mfma_final_pmc.txt).
+__device__ __forceinline__ int img_at(int row, int pos) { return row * kPS + pos + 4 * (row & 1); }
+__device__ __forceinline__ int img_chunk(int row, int c) { return row * kPS + 4 * (c + (row & 1)); }
+
 // Opaque copy: the reverse sweep recomputes s1, s2 and the layer-input streams from the checkpoint;
 // without this the compiler CSEs them with the forward's values and keeps those live across the whole
 // tile (~64 VGPRs per layer instead of the 20 of the checkpoint).
@@ -128,11 +137,11 @@ template <int NS>
 __device__ __forceinline__ void put_slots(float* T, const float (&v)[NS], int p, int g) {
   const int pp = pos_of(p);
 #pragma unroll
-  for (int k = 0; k < NS; ++k) T[slot_feat(NS, k, g) * kPS + pp] = v[k];
+  for (int k = 0; k < NS; ++k) T[img_at(slot_feat(NS, k, g), pp)] = v[k];
 }
 // F layout read: rows 16 blk + (lane & 15), the pairs (lane >> 4) + 4 ks of k-steps ks = 0..3
 __device__ __forceinline__ f32x4 get_rows(const float* T, int blk, int p, int g) {
-  return *reinterpret_cast<const f32x4*>(T + (16 * blk + p) * kPS + 4 * g);
+  return *reinterpret_cast<const f32x4*>(T + img_chunk(16 * blk + p, g));
 }
 
 // Hidden-layer weight gradient dK[in][out] (+ the bias row in = 20) of one 16-pair tile: the 16 x 16
@@ -144,16 +153,20 @@ __device__ __forceinline__ f32x4 get_rows(const float* T, int blk, int p, int g)
 struct EdgeMap;
 __device__ __forceinline__ void fold_ce(float* sl, const f32x4& G0, const f32x4& E, const EdgeMap& em, int pq, int gq,
                                         int lane, float* dump);
+// Edge block of lane group b (in0 / 4, out0 / 4 as nibbles b of these words): the 14 blocks in 16..20 x
+// 0..19 and 0..15 x 16..19, placed so that each ds_read_b128 lane group ({b 0,3,5,6}, {1,2,4,7},
+// {8,11,13,14}, {9,10,12,15}) reads at most 8 distinct image rows, on distinct chunks (a search over the
+// bank model); b = 3 and 7 are unused and read their group's first block (broadcast), never folded.
+constexpr uint64_t kEdgeIn = 0x4404155345542542ull, kEdgeOut = 0x3442423401414004ull;
 struct EdgeMap {
   int ra, rb;  // image rows read by this lane: hprev feature (A), zbar feature (B)
   int in0, out0;
   bool live;
   __device__ __forceinline__ explicit EdgeMap(int lane) {
     const int b = lane >> 2, i = lane & 3;
-    if (b < 8) { in0 = 16 + 4 * (b >> 2); out0 = 4 * (b & 3); }
-    else if (b < 12) { in0 = 4 * (b - 8); out0 = 16; }
-    else { in0 = 16 + 4 * (b - 12); out0 = 16; }
-    live = b < 14;
+    in0 = 4 * (int)((kEdgeIn >> (4 * b)) & 15);
+    out0 = 4 * (int)((kEdgeOut >> (4 * b)) & 15);
+    live = b != 3 && b != 7;
     ra = in0 + i;   // <= 23: rows 21..23 of the input image are never folded
     rb = out0 + i;  // <= 19
   }
@@ -166,18 +179,20 @@ __device__ __forceinline__ void fold_ce(float* sl, const f32x4& G0, const f32x4&
   float* dc[4];
   float* de[4];
   float vc[4], ve[4];
+  bool ok[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     dc[r] = sl + (4 * gq + r) * kW + pq;
     const int in = em.in0 + r, out = em.out0 + (lane & 3);
-    de[r] = (em.live && in <= kW && out < kW) ? sl + in * kW + out : dump;
+    ok[r] = em.live && in <= kW && out < kW;
+    de[r] = ok[r] ? sl + in * kW + out : dc[r];  // padding: read the lane's core word, write nothing
     vc[r] = *dc[r];
     ve[r] = *de[r];
   }
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     *dc[r] = vc[r] + G0[r];
-    *de[r] = ve[r] + E[r];
+    if (ok[r]) *de[r] = ve[r] + E[r];
   }
 }
 
@@ -189,13 +204,13 @@ __device__ __forceinline__ void outer_stream(float* tA, float* tB, const float (
                                              f32x4& G0, f32x4& E) {
   put_slots<kNS>(tA, bv, pq, gq);
   put_slots<kNS>(tB, av, pq, gq);
-  *(gq == 0 ? tB + kW * kPS + ppq : dump) = bias_row;
+  if (gq == 0) tB[img_at(kW, ppq)] = bias_row;
   const f32x4 fa = get_rows(tA, 0, pq, gq), fb = get_rows(tB, 0, pq, gq);
   f32x4 ea[4], eb[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    ea[q] = *reinterpret_cast<const f32x4*>(tB + em.ra * kPS + 4 * q);
-    eb[q] = *reinterpret_cast<const f32x4*>(tA + em.rb * kPS + 4 * q);
+    ea[q] = *reinterpret_cast<const f32x4*>(tB + img_chunk(em.ra, q));
+    eb[q] = *reinterpret_cast<const f32x4*>(tA + img_chunk(em.rb, q));
   }
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) G0 = mfma(fb[ks], fa[ks], G0);
@@ -214,6 +229,7 @@ __device__ __forceinline__ void fold(float* slab, int qoff, int pitch, int nout,
                                      int p, int g, float* dump) {
   float* dst[IBN][OBN][4];
   float v[IBN][OBN][4];
+  bool ok[IBN][OBN][4];
 #pragma unroll
   for (int ib = 0; ib < IBN; ++ib)
 #pragma unroll
@@ -221,7 +237,8 @@ __device__ __forceinline__ void fold(float* slab, int qoff, int pitch, int nout,
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int in = 16 * ib + 4 * g + r, out = 16 * ob + p;
-        dst[ib][ob][r] = (out < nout && in <= pin) ? slab + qoff + in * pitch + out : dump;
+        ok[ib][ob][r] = out < nout && in <= pin;
+        dst[ib][ob][r] = ok[ib][ob][r] ? slab + qoff + in * pitch + out : dump;
         v[ib][ob][r] = *dst[ib][ob][r];
       }
 #pragma unroll
@@ -229,7 +246,8 @@ __device__ __forceinline__ void fold(float* slab, int qoff, int pitch, int nout,
 #pragma unroll
     for (int ob = 0; ob < OBN; ++ob)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) *dst[ib][ob][r] = v[ib][ob][r] + G[ib][ob][r];
+      for (int r = 0; r < 4; ++r)
+        if (ok[ib][ob][r]) *dst[ib][ob][r] = v[ib][ob][r] + G[ib][ob][r];
 }
 
 // the four forward streams entering the next layer from a layer's checkpoint (h, z'_u, z'_v, z''_v)
@@ -507,13 +525,13 @@ __global__ __launch_bounds__(kWaves2 * kWave, 1) void kmvq_grad_kernel(Args a) {
             stream_of<s>(ph, pu, pv, pw, Hp);
             put_slots<kNS>(tA, zb[s], pq, gq);
             put_slots<kNS>(tB, Hp, pq, gq);
-            *(gq == 0 ? tB + kW * kPS + ppq : dump) = s == 0 ? 1.f : 0.f;
+            if (gq == 0) tB[img_at(kW, ppq)] = s == 0 ? 1.f : 0.f;
             const f32x4 fa = get_rows(tA, 0, pq, gq), fb = get_rows(tB, 0, pq, gq);
             f32x4 ea[4], eb[4];  // edge operands: 4 pairs per 16-byte read (pairs q + 4 ks)
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-              ea[q] = *reinterpret_cast<const f32x4*>(tB + em.ra * kPS + 4 * q);
-              eb[q] = *reinterpret_cast<const f32x4*>(tA + em.rb * kPS + 4 * q);
+              ea[q] = *reinterpret_cast<const f32x4*>(tB + img_chunk(em.ra, q));
+              eb[q] = *reinterpret_cast<const f32x4*>(tA + img_chunk(em.rb, q));
             }
             // the backward product of this stream needs no LDS: it covers the images' round trip
 #pragma unroll
@@ -550,9 +568,9 @@ __global__ __launch_bounds__(kWaves2 * kWave, 1) void kmvq_grad_kernel(Args a) {
 #pragma unroll
           for (int kk = 0; kk < KD; ++kk) {
             const int k = 4 * kk + gq;  // rows past D go to row 15 (a column no layer-0 output reads)
-            tB[(k < D ? k : 15) * kPS + ppq] = s == 0 ? yb[kk] : (s == 1 ? ui[kk] : vi[kk]);
+            tB[img_at(k < D ? k : 15, ppq)] = s == 0 ? yb[kk] : (s == 1 ? ui[kk] : vi[kk]);
           }
-          *(gq == 0 ? tB + D * kPS + ppq : dump) = s == 0 ? 1.f : 0.f;
+          if (gq == 0) tB[img_at(D, ppq)] = s == 0 ? 1.f : 0.f;
           f32x4 fa[2], fb;
 #pragma unroll
           for (int b = 0; b < 2; ++b) fa[b] = get_rows(tA, b, pq, gq);
