@@ -337,13 +337,14 @@ int pdeinv_residual_kmv(const pdeinv_kmv_desc* desc, const double* d_mom, const 
  * GMM residual): Taylor-mode forward streams, the grad_x reverse chain, its forward adjoint, the
  * reverse sweep and the weight-gradient outer products, as dense GEMMs (rocBLAS sgemm, fp32) plus
  * fused element-wise kernels, chunked over chunk_rows rows. impl selects the implementation:
- * PDEINV_MLP_IMPL_AUTO picks the fused path when the shape allows it (L >= 2,
- * W in {32, 64, 128, 256, 512}, out <= 64, d in {2, 4, 8, 16}): hand-written fp32 MFMA GEMMs whose prologues and
- * epilogues carry all of the element-wise algebra (layer 1 is recomputed from the rows, never
- * stored). PDEINV_MLP_IMPL_LIBRARY forces the rocBLAS + element-wise-kernel path (any shape);
- * PDEINV_MLP_IMPL_FUSED forces the fused path (PDEINV_ERR_UNSUPPORTED if the shape is not).
- * Narrower widths (e.g. the reference default 20 x 8 layers, MLP.yaml) run the fused kernels
- * zero-padded to the next compiled width (exact; parameters padded / gradient unpadded on the device).
+ * PDEINV_MLP_IMPL_AUTO and PDEINV_MLP_IMPL_FUSED take the hand-written fused path for every d <= 16,
+ * 1 <= L <= 16, W <= 512 and any out_features: fp32 MFMA GEMMs whose prologues and epilogues carry all of
+ * the element-wise algebra (layer 1 is recomputed from the rows, never stored; L = 1 runs the output layer
+ * off the layer-1 prologue). The kernels are compiled for d in {2, 4, 8, 16} and W in {32, 64, 128, 256,
+ * 512}; other d / W (e.g. the reference default 20 x 8 layers, MLP.yaml) run zero-padded to the next
+ * compiled one (exact; rows, parameters and the true potential padded, the gradient unpadded, on the
+ * device). PDEINV_MLP_IMPL_LIBRARY forces the rocBLAS + element-wise-kernel path (explicit opt-in; also
+ * the only path for W > 512); FUSED on a shape outside the above returns PDEINV_ERR_UNSUPPORTED.
  * d_params / d_grad: flat flax order [K_1 (d x W), b_1, K_2 (W x W), b_2, ..., K_o (W x out), b_o]
  * (pdeinv_mlp_param_count floats). d_acc [PDEINV_GMM_NACC] and d_grad are ACCUMULATED (+=): zero
  * them first. pdeinv_kfp_terms_finalize turns (acc, grad) into the PDEINV_KFP_* slots.
@@ -410,10 +411,10 @@ typedef struct {
                              net); other widths <= 28 (or every width <= 28 under PAIRS_RING):
                              the register-ring pair kernels (pairs built in registers, MFMA weight
                              gradients; dim <= 8, n_layers <= 16, out <= 64; workspace ~ 2048 waves x
-                             (5 W L x 64 + P) floats); width >= 32 (dim in {2, 4, 8},
-                             2 <= n_layers <= 16, width <= 512 zero-padded to 32/64/128/256/512, out <= 64):
+                             (5 W L x 64 + P) floats); width >= 32 (dim <= 8 zero-padded to 2/4/8,
+                             1 <= n_layers <= 16, width <= 512 zero-padded to 32/64/128/256/512, any out):
                              chunks of pair rows through the fused fp32-MFMA residual kernels of
-                             pdeinv_residual_kfp_mlp; LIBRARY = pair rows through rocBLAS (any shape) */
+                             pdeinv_residual_kfp_mlp; LIBRARY = pair rows through rocBLAS (explicit opt-in) */
 } pdeinv_kmv_mlp_desc;
 size_t pdeinv_residual_kmv_mlp_workspace_bytes(const pdeinv_kmv_mlp_desc* desc);
 int pdeinv_residual_kmv_mlp(const pdeinv_kmv_mlp_desc* desc, const float* d_z, int64_t set_stride, int64_t ld,

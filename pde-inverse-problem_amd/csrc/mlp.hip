@@ -441,30 +441,39 @@ static MlpPlan make_plan(const pdeinv_kfp_mlp_desc* d) {
 
 using namespace pdeinv;
 
-static bool use_fused(const pdeinv_kfp_mlp_desc* d) {
-  if (d->impl == PDEINV_MLP_IMPL_LIBRARY) return false;
-  return mlpf::supported(d->dim, d->n_layers, d->width, d->out_features);
-}
-
-// Widths the fused MFMA kernels do not compile (the reference's default V_hypothesis is 20 wide,
-// configurations/neural_network/MLP.yaml:4-5) run them zero-padded to the next compiled width: exact
-// (common.h MlpPadMap), at the cost of the padded MACs.
-static int fused_pad_width(const pdeinv_kfp_mlp_desc* d) {
-  if (d->impl == PDEINV_MLP_IMPL_LIBRARY || use_fused(d) || d->n_layers > kMlpPadMaxL) return 0;
+// The shapes the fused fp32-MFMA path takes. The kernels are compiled for dim in {2, 4, 8, 16} and width in
+// {32, 64, 128, 256, 512} (any depth 1..16, any out_features: mlpf::supported); every other dim <= 16 and
+// width <= 512 runs zero-padded to the next compiled one — exact: padded inputs and K1 rows are zero, padded
+// hidden units have zero weights in and out (common.h MlpPadMap) — at the cost of the padded MACs. The
+// reference's default V_hypothesis is 20 wide (configurations/neural_network/MLP.yaml:4-5). Only
+// impl = LIBRARY (or width > 512) reaches the rocBLAS path.
+struct FusedShape {
+  int Dp = 0, Wp = 0;
+  bool pad = false;
+};
+static int pad_dim(int D) { return D <= 2 ? 2 : (D <= 4 ? 4 : (D <= 8 ? 8 : 16)); }
+static bool fused_shape(const pdeinv_kfp_mlp_desc* d, FusedShape* f = nullptr) {
+  if (d->impl == PDEINV_MLP_IMPL_LIBRARY || d->dim < 1 || d->dim > 16 || d->n_layers < 1 ||
+      d->n_layers > kMlpPadMaxL || d->out_features < 1)
+    return false;
+  int Wp = 0;
   for (int w : {32, 64, 128, 256, 512})
-    if (w >= d->width && mlpf::supported(d->dim, d->n_layers, w, d->out_features)) return w;
-  return 0;
+    if (w >= d->width) { Wp = w; break; }
+  const int Dp = pad_dim(d->dim);
+  if (!Wp || !mlpf::supported(Dp, d->n_layers, Wp, d->out_features)) return false;
+  if (f) { f->Dp = Dp; f->Wp = Wp; f->pad = Dp != d->dim || Wp != d->width; }
+  return true;
 }
 
-static MlpPadMap width_pad_map(const pdeinv_kfp_mlp_desc* d, int WP) {
+static MlpPadMap width_pad_map(const pdeinv_kfp_mlp_desc* d, const FusedShape& f) {
   MlpPadMap pm{};
   pm.L = d->n_layers;
   int64_t ro = 0, po = 0;
   for (int l = 0; l <= pm.L; ++l) {
     pm.din[l] = l == 0 ? d->dim : d->width;
     pm.dout[l] = l == pm.L ? d->out_features : d->width;
-    pm.pin[l] = l == 0 ? d->dim : WP;
-    pm.pout[l] = l == pm.L ? d->out_features : WP;
+    pm.pin[l] = l == 0 ? f.Dp : f.Wp;
+    pm.pout[l] = l == pm.L ? d->out_features : f.Wp;
     pm.roff[l] = ro;
     pm.poff[l] = po;
     ro += (int64_t)pm.din[l] * pm.dout[l] + pm.dout[l];
@@ -493,16 +502,41 @@ __global__ void mlp_unpad_grad_kernel(MlpPadMap pm, const float* __restrict__ gp
 
 static int64_t chunk_rows_of(const pdeinv_kfp_mlp_desc* d) { return d->chunk_rows > 0 ? d->chunk_rows : (1 << 18); }
 
+// fused-path workspace (floats): [run_chunk workspace | loss partials | padded params | padded gradient |
+// padded rows (dim padding)]
+struct FusedWs {
+  size_t fl, part, pbuf, gbuf, rows, total;
+  int64_t PP;
+};
+static FusedWs fused_ws(const pdeinv_kfp_mlp_desc* d, const FusedShape& f) {
+  FusedWs w{};
+  const int64_t Bc = chunk_rows_of(d);
+  size_t o = 0;
+  auto take = [&](size_t n) { const size_t at = o; o += (n + 63) & ~(size_t)63; return at; };
+  w.fl = take(mlpf::workspace_floats(f.Dp, d->n_layers, f.Wp, d->out_features, Bc));
+  w.part = take((size_t)PDEINV_GMM_NACC * kLossGrid);
+  w.PP = f.pad ? pad_param_count(width_pad_map(d, f)) : 0;
+  w.pbuf = take((size_t)w.PP);
+  w.gbuf = take((size_t)w.PP);
+  w.rows = take(f.Dp != d->dim ? (size_t)Bc * 2 * f.Dp : 0);
+  w.total = o;
+  return w;
+}
+
+// rows [x | v] of d floats -> [x, 0.. | v, 0..] of Dp (the fused path's dim padding)
+__global__ void mlp_pad_rows_kernel(const float* __restrict__ src, int64_t ld, int64_t R, int D, int Dp,
+                                    float* __restrict__ dst) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= R * 2 * Dp) return;
+  const int64_t r = q / (2 * Dp);
+  const int c = (int)(q - r * 2 * Dp), half = c / Dp, k = c - half * Dp;
+  dst[q] = k < D ? src[r * ld + half * D + k] : 0.f;
+}
+
 extern "C" size_t pdeinv_residual_kfp_mlp_workspace_bytes(const pdeinv_kfp_mlp_desc* d) {
   if (!d || d->dim < 1 || d->n_layers < 1 || d->width < 1 || d->out_features < 1) return 0;
-  if (const int WP = fused_pad_width(d)) {
-    const int64_t P = pad_param_count(width_pad_map(d, WP));
-    return (mlpf::workspace_floats(d->dim, d->n_layers, WP, d->out_features, chunk_rows_of(d)) +
-            (size_t)PDEINV_GMM_NACC * kLossGrid + 2 * (((size_t)P + 63) & ~(size_t)63)) * sizeof(float);
-  }
-  if (use_fused(d))
-    return (mlpf::workspace_floats(d->dim, d->n_layers, d->width, d->out_features, chunk_rows_of(d)) +
-            (size_t)PDEINV_GMM_NACC * kLossGrid) * sizeof(float);
+  FusedShape f;
+  if (fused_shape(d, &f)) return fused_ws(d, f).total * sizeof(float);
   return make_plan(d).total;
 }
 
@@ -695,60 +729,82 @@ extern "C" int pdeinv_residual_kfp_mlp(const pdeinv_kfp_mlp_desc* d, const float
       {z0, n0, ld0 ? ld0 : 2 * D, 0, d->c_nabla, d->c_hess, d->c_fric, 0.f},
       {zi, ni, ldi ? ldi : 2 * D, 1, 0.f, 0.f, bval ? 0.f : d->c_init, bval ? d->c_init : 0.f},
       {zt, nt, ldt ? ldt : 2 * D, 2, 0.f, 0.f, bval ? 0.f : d->c_term, bval ? d->c_term : 0.f}};
-  const int WP = fused_pad_width(d);
-  if (use_fused(d) || WP) {
+  FusedShape fs;
+  if (fused_shape(d, &fs)) {
     const int64_t Bc = chunk_rows_of(d);
-    const int Wf = WP ? WP : p.W;
-    const size_t fl = mlpf::workspace_floats(D, L, Wf, p.O, Bc);
+    const int Wf = fs.Wp, Dp = fs.Dp;
+    const FusedWs fw = fused_ws(d, fs);
+    float* wsf = (float*)ws;
     const float* fparams = params;
     float* fgrad = grad;
     MlpPadMap pm{};
-    int64_t PP = 0;
-    if (WP) {  // zero-padded copy of the parameters and a padded gradient accumulator behind the workspace
-      pm = width_pad_map(d, WP);
-      PP = pad_param_count(pm);
-      float* pbuf = (float*)ws + fl + (size_t)PDEINV_GMM_NACC * kLossGrid;
-      float* gbuf = pbuf + ((PP + 63) & ~(int64_t)63);
-      hipLaunchKernelGGL(mlp_pad_params_kernel, dim3((unsigned)((PP + 255) / 256)), dim3(256), 0, st, pm, params, PP,
-                         pbuf);
-      if (hipMemsetAsync(gbuf, 0, sizeof(float) * PP, st) != hipSuccess) return fail(PDEINV_ERR_HIP, "kfp_mlp: memset");
+    if (fs.pad) {  // zero-padded copy of the parameters and a padded gradient accumulator behind the workspace
+      pm = width_pad_map(d, fs);
+      float* pbuf = wsf + fw.pbuf;
+      float* gbuf = wsf + fw.gbuf;
+      hipLaunchKernelGGL(mlp_pad_params_kernel, dim3((unsigned)((fw.PP + 255) / 256)), dim3(256), 0, st, pm, params,
+                         fw.PP, pbuf);
+      if (hipMemsetAsync(gbuf, 0, sizeof(float) * fw.PP, st) != hipSuccess)
+        return fail(PDEINV_ERR_HIP, "kfp_mlp: memset");
       fparams = pbuf;
       fgrad = gbuf;
-      param_offsets(D, WP, O, L, poff, boff);
+      param_offsets(Dp, Wf, O, L, poff, boff);
     }
     LossCtx lc{};
     lc.la = la;
-    lc.part = (float*)ws + fl;
+    if (Dp != D) {  // the true potential on padded rows: zero rows / columns of tilde_F, zero coordinates of mu_k
+      lc.la.d = Dp;
+      for (int k = 0; k < PDEINV_MAX_PARAMS; ++k) lc.la.tp[k] = 0.f;
+      if (d->true_kind == PDEINV_POT_QUADRATIC) {
+        for (int i = 0; i < D; ++i)
+          for (int j = 0; j < D; ++j) lc.la.tp[i * Dp + j] = d->true_params[i * D + j];
+      } else {
+        PDEINV_REQUIRE(d->n_centers_true * Dp <= PDEINV_MAX_PARAMS, PDEINV_ERR_UNSUPPORTED,
+                       "kfp_mlp: padded true GMM exceeds PDEINV_MAX_PARAMS");
+        for (int k = 0; k < d->n_centers_true; ++k)
+          for (int i = 0; i < D; ++i) lc.la.tp[k * Dp + i] = d->true_params[k * D + i];
+      }
+    }
+    lc.part = wsf + fw.part;
     lc.acc = acc;
-    lc.D = D;
+    lc.D = Dp;
     for (const Set& s : sets) {
       PDEINV_REQUIRE(s.n == 0 || s.ld >= 2 * D, PDEINV_ERR_INVALID, "kfp_mlp: row stride < 2*dim");
       lc.la.set = s.id; lc.la.c1 = s.c1; lc.la.c2 = s.c2; lc.la.c3 = s.c3; lc.la.c0 = s.c0; lc.la.c_true = d->c_true;
       lc.la.inv_n = s.n ? 1.f / (float)s.n : 0.f;
       for (int64_t r0 = 0; r0 < s.n; r0 += Bc) {
         mlpf::Chunk c{};
-        c.d = D; c.L = L; c.W = Wf; c.O = p.O;
+        c.d = Dp; c.L = L; c.W = Wf; c.O = p.O;
         c.R = (s.n - r0) < Bc ? (s.n - r0) : Bc;
         c.z = s.z + r0 * s.ld;
         c.ldz = s.ld;
+        if (Dp != D) {
+          float* rows = wsf + fw.rows;
+          const int64_t nq = c.R * 2 * Dp;
+          hipLaunchKernelGGL(mlp_pad_rows_kernel, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, st, c.z, s.ld, c.R,
+                             D, Dp, rows);
+          c.z = rows;
+          c.ldz = 2 * Dp;
+        }
         c.params = fparams; c.grad = fgrad; c.poff = poff; c.boff = boff;
         c.c2 = s.c2; c.c3 = s.c3; c.c0 = s.c0;
-        c.ws = (float*)ws; c.Bc = Bc;
+        c.ws = wsf; c.Bc = Bc;
         lc.zr = c.z;
-        lc.ld = s.ld;
+        lc.ld = c.ldz;
         const int rc = mlpf::run_chunk(c, mlpf::LossHook{fused_loss_hook, &lc}, st);
         if (rc) return rc;
       }
     }
-    if (WP) {
-      hipLaunchKernelGGL(mlp_unpad_grad_kernel, dim3((unsigned)((PP + 255) / 256)), dim3(256), 0, st, pm, fgrad, PP,
-                         grad);
+    if (fs.pad) {
+      hipLaunchKernelGGL(mlp_unpad_grad_kernel, dim3((unsigned)((fw.PP + 255) / 256)), dim3(256), 0, st, pm, fgrad,
+                         fw.PP, grad);
       return check_launch("mlp_unpad_grad_kernel");
     }
     return PDEINV_OK;
   }
   PDEINV_REQUIRE(d->impl != PDEINV_MLP_IMPL_FUSED, PDEINV_ERR_UNSUPPORTED,
-                 "kfp_mlp: fused path needs L >= 2, W in {32, 64, 128, 256, 512}, out <= 64, d in {2, 4, 8, 16}");
+                 "kfp_mlp: the fused path takes dim <= 16, 1 <= n_layers <= 16, width <= 512 (zero-padded to the "
+                 "compiled dims / widths), any out_features");
   Blas blas{blas_handle(dev), st, w + p.off_kpart};
   if (!blas.h) return fail(PDEINV_ERR_HIP, "kfp_mlp: rocblas_create_handle failed");
   if (rocblas_set_stream(blas.h, st) != rocblas_status_success) return fail(PDEINV_ERR_HIP, "kfp_mlp: rocblas_set_stream");
@@ -777,7 +833,8 @@ extern "C" int pdeinv_residual_kfp_mlp(const pdeinv_kfp_mlp_desc* d, const float
 //           |gbar|^2, |gbar*|^2, |gbar* - gbar|^2 with gbar* = tilde_F (x_i - xbar_t) (Phi* quadratic);
 //   pass 2  the full library path with c2 = -2 s, c0 = 2 s w_it and the input-gradient seed
 //           u_i = 2 s gbar_i, s = 1 / (n^2 n_time)  (oracle/numpy_ref.py kmv_mlp_grad_analytic).
-template <int D>
+// rows of DP >= D floats per block: the particles' D coordinates, zeros past them (the fused path's dim padding)
+template <int D, int DP = D>
 __global__ void kmv_pair_rows_kernel(const float* __restrict__ z, int64_t set_stride, int64_t ld, int64_t t,
                                      int64_t i0, int64_t ni, int64_t j0, int64_t nj, int64_t n_rows,
                                      const float* __restrict__ gbar, const float* __restrict__ ds, float gamma,
@@ -787,24 +844,24 @@ __global__ void kmv_pair_rows_kernel(const float* __restrict__ z, int64_t set_st
   const int64_t il = r / nj, i = i0 + il, j = j0 + (r - il * nj);
   const float* zi = z + t * set_stride + i * ld;
   const float* zj = z + t * set_stride + j * ld;
-  float* o = rows + r * (3 * D + 1);
+  float* o = rows + r * (3 * DP + 1);
   const int64_t p = t * n_rows + i;
 #pragma unroll
-  for (int k = 0; k < D; ++k) {
-    o[k] = zi[k] - zj[k];
-    o[D + k] = zi[D + k];
-    o[2 * D + k] = gbar ? u_scale * gbar[p * D + k] : 0.f;
+  for (int k = 0; k < DP; ++k) {
+    o[k] = k < D ? zi[k] - zj[k] : 0.f;
+    o[DP + k] = k < D ? zi[D + k] : 0.f;
+    o[2 * DP + k] = (k < D && gbar) ? u_scale * gbar[p * D + k] : 0.f;
   }
   float wv = 0.f;
   if (ds) {
     const float a = ds[2 * p], b2 = ds[2 * p + 1];
     wv = b2 + a * a + gamma * a;  // ds2 + ds^2 + gamma ds (kinetic_mckean_vlasov.py:84-89)
   }
-  o[3 * D] = wv;
+  o[3 * DP] = wv;
 }
 
 // gbar[t][i0 + il] += inv_n * sum_jl G[il * nj + jl] (one block per il; fixed-order LDS tree)
-template <int D>
+template <int D, int DP = D>
 __global__ __launch_bounds__(kBlock) void kmv_group_mean_kernel(const float* __restrict__ G, int64_t nj, float inv_n,
                                                                 float* __restrict__ gbar_rows) {
   const int64_t il = blockIdx.x;
@@ -813,7 +870,7 @@ __global__ __launch_bounds__(kBlock) void kmv_group_mean_kernel(const float* __r
   for (int k = 0; k < D; ++k) s[k] = 0.f;
   for (int64_t jl = threadIdx.x; jl < nj; jl += kBlock) {
 #pragma unroll
-    for (int k = 0; k < D; ++k) s[k] += G[(il * nj + jl) * D + k];
+    for (int k = 0; k < D; ++k) s[k] += G[(il * nj + jl) * DP + k];  // G rows of DP (padded dims dropped)
   }
   __shared__ float red[kBlock];
   for (int k = 0; k < D; ++k) {
@@ -1009,14 +1066,15 @@ static pdeinv_kfp_mlp_desc kmv_as_kfp(const pdeinv_kmv_mlp_desc* d) {
 
 static bool kmv_use_fused(const pdeinv_kmv_mlp_desc* d) {
   if (d->impl == PDEINV_MLP_IMPL_LIBRARY || kmv_use_pairs(d)) return false;
-  if (d->dim != 2 && d->dim != 4 && d->dim != 8) return false;
+  if (d->dim < 1 || d->dim > 8) return false;
   const pdeinv_kfp_mlp_desc m = kmv_as_kfp(d);
-  return use_fused(&m) || fused_pad_width(&m) != 0;
+  return fused_shape(&m);
 }
 
 namespace {
 struct KmvFusedPlan {
-  int Wf, WP;
+  int Wf, Dp;
+  bool pad;
   int64_t Bc, ni, nj, PP;
   MlpPadMap pm;
   size_t fl, off_part, off_pbuf, off_gbuf, off_rows, off_gbar, off_spart, total;  // floats
@@ -1025,23 +1083,26 @@ struct KmvFusedPlan {
 KmvFusedPlan kmv_fused_plan(const pdeinv_kmv_mlp_desc* d) {
   const pdeinv_kfp_mlp_desc m = kmv_as_kfp(d);
   KmvFusedPlan k{};
-  k.WP = fused_pad_width(&m);
-  k.Wf = k.WP ? k.WP : d->width;
+  FusedShape fs;
+  fused_shape(&m, &fs);
+  k.Wf = fs.Wp;
+  k.Dp = fs.Dp;
+  k.pad = fs.pad;
   k.Bc = m.chunk_rows;
   const int64_t n = d->n_rows;
   k.nj = n <= k.Bc ? n : k.Bc;
   k.ni = n <= k.Bc ? (k.Bc / n < n ? k.Bc / n : n) : 1;
-  if (k.WP) {
-    k.pm = width_pad_map(&m, k.WP);
+  if (k.pad) {
+    k.pm = width_pad_map(&m, fs);
     k.PP = pad_param_count(k.pm);
   }
   size_t o = 0;
   auto take = [&](size_t floats) { const size_t at = o; o += (floats + 63) & ~(size_t)63; return at; };
-  k.fl = take(mlpf::workspace_floats(d->dim, d->n_layers, k.Wf, d->out_features, k.Bc));
+  k.fl = take(mlpf::workspace_floats(k.Dp, d->n_layers, k.Wf, d->out_features, k.Bc));
   k.off_part = take((size_t)PDEINV_GMM_NACC * kLossGrid);
   k.off_pbuf = take((size_t)k.PP);
   k.off_gbuf = take((size_t)k.PP);
-  k.off_rows = take((size_t)k.Bc * (3 * d->dim + 1));
+  k.off_rows = take((size_t)k.Bc * (3 * k.Dp + 1));
   k.off_gbar = take((size_t)d->n_sets * n * d->dim);
   k.off_spart = take((size_t)d->n_sets * 3 * 2);
   k.total = o * sizeof(float);
@@ -1049,16 +1110,17 @@ KmvFusedPlan kmv_fused_plan(const pdeinv_kmv_mlp_desc* d) {
 }
 }  // namespace
 
-template <int D>
+// D = the particles' dim, DP = the fused kernels' (D zero-padded to 2 / 4 / 8: the pair rows carry the padding)
+template <int D, int DP>
 static int kmv_fused_run(const pdeinv_kmv_mlp_desc* d, const KmvFusedPlan& k, const float* z, int64_t set_stride,
                          int64_t ld, const float* ds, const float* params, float* w, double* acc, float* grad,
                          hipStream_t st) {
   const int L = d->n_layers, O = d->out_features;
   int64_t poff[18], boff[18];
-  param_offsets(D, k.Wf, O, L, poff, boff);
+  param_offsets(DP, k.Wf, O, L, poff, boff);
   const float* fparams = params;
   float* fgrad = grad;
-  if (k.WP) {
+  if (k.pad) {
     float* pbuf = w + k.off_pbuf;
     fgrad = w + k.off_gbuf;
     hipLaunchKernelGGL(mlp_pad_params_kernel, dim3((unsigned)((k.PP + 255) / 256)), dim3(256), 0, st, k.pm, params,
@@ -1066,7 +1128,7 @@ static int kmv_fused_run(const pdeinv_kmv_mlp_desc* d, const KmvFusedPlan& k, co
     if (hipMemsetAsync(fgrad, 0, sizeof(float) * k.PP, st) != hipSuccess) return fail(PDEINV_ERR_HIP, "kmv_mlp: memset");
     fparams = pbuf;
   }
-  const int64_t n = d->n_rows, T = d->n_sets, rld = 3 * D + 1;
+  const int64_t n = d->n_rows, T = d->n_sets, rld = 3 * DP + 1;
   float* rows = w + k.off_rows;
   float* gbar = w + k.off_gbar;
   double* part = (double*)(w + k.off_spart);
@@ -1074,18 +1136,18 @@ static int kmv_fused_run(const pdeinv_kmv_mlp_desc* d, const KmvFusedPlan& k, co
   if (hipMemsetAsync(gbar, 0, sizeof(float) * (size_t)T * n * D, st) != hipSuccess)
     return fail(PDEINV_ERR_HIP, "kmv_mlp: memset");
   LossCtx lc{};
-  lc.la.d = D;
+  lc.la.d = DP;
   lc.la.set = 3;
   lc.la.uw = 1;
   lc.la.c2 = (float)(-2.0 * s);
   lc.la.c0 = (float)(2.0 * s);
   lc.part = w + k.off_part;
   lc.acc = acc;
-  lc.D = D;
+  lc.D = DP;
   lc.zr = rows;
   lc.ld = rld;
   mlpf::Chunk c{};
-  c.d = D; c.L = L; c.W = k.Wf; c.O = O;
+  c.d = DP; c.L = L; c.W = k.Wf; c.O = O;
   c.z = rows; c.ldz = rld;
   c.params = fparams; c.grad = fgrad; c.poff = poff; c.boff = boff;
   c.ws = w; c.Bc = k.Bc;
@@ -1094,7 +1156,7 @@ static int kmv_fused_run(const pdeinv_kmv_mlp_desc* d, const KmvFusedPlan& k, co
     c.c2 = pass ? lc.la.c2 : 0.f;
     c.c3 = 0.f;
     c.c0 = pass ? lc.la.c0 : 0.f;
-    c.wrow = pass ? rows + 3 * D : nullptr;
+    c.wrow = pass ? rows + 3 * DP : nullptr;
     c.ldw = rld;
     for (int64_t t = 0; t < T; ++t) {
       for (int64_t i0 = 0; i0 < n; i0 += k.ni) {
@@ -1102,14 +1164,14 @@ static int kmv_fused_run(const pdeinv_kmv_mlp_desc* d, const KmvFusedPlan& k, co
         for (int64_t j0 = 0; j0 < n; j0 += k.nj) {
           const int64_t nj = (n - j0) < k.nj ? (n - j0) : k.nj;
           c.R = ni * nj;
-          hipLaunchKernelGGL(kmv_pair_rows_kernel<D>, dim3(grid_for(c.R)), dim3(kBlock), 0, st, z, set_stride, ld, t,
-                             i0, ni, j0, nj, n, pass ? gbar : nullptr, pass ? ds : nullptr, d->gamma,
+          hipLaunchKernelGGL((kmv_pair_rows_kernel<D, DP>), dim3(grid_for(c.R)), dim3(kBlock), 0, st, z, set_stride, ld,
+                             t, i0, ni, j0, nj, n, pass ? gbar : nullptr, pass ? ds : nullptr, d->gamma,
                              (float)(2.0 * s), rows);
           const int rc = mlpf::run_chunk(c, mlpf::LossHook{fused_loss_hook, &lc}, st);
           if (rc) return rc;
           if (pass == 0)
-            hipLaunchKernelGGL(kmv_group_mean_kernel<D>, dim3((unsigned)ni), dim3(kBlock), 0, st, mlpf::grad_rows(c),
-                               nj, (float)(1.0 / (double)n), gbar + (t * n + i0) * D);
+            hipLaunchKernelGGL((kmv_group_mean_kernel<D, DP>), dim3((unsigned)ni), dim3(kBlock), 0, st,
+                               mlpf::grad_rows(c), nj, (float)(1.0 / (double)n), gbar + (t * n + i0) * D);
         }
       }
     }
@@ -1122,7 +1184,7 @@ static int kmv_fused_run(const pdeinv_kmv_mlp_desc* d, const KmvFusedPlan& k, co
                          acc);
     }
   }
-  if (k.WP)
+  if (k.pad)
     hipLaunchKernelGGL(mlp_unpad_grad_kernel, dim3((unsigned)((k.PP + 255) / 256)), dim3(256), 0, st, k.pm, fgrad,
                        k.PP, grad);
   return check_launch("kmv_mlp fused kernels");
@@ -1181,14 +1243,15 @@ extern "C" int pdeinv_residual_kmv_mlp(const pdeinv_kmv_mlp_desc* d, const float
   if (kmv_use_fused(d)) {
     const KmvFusedPlan k = kmv_fused_plan(d);
     switch (d->dim) {
-#define CASE(DD) case DD: return kmv_fused_run<DD>(d, k, z, set_stride, ld, ds, params, (float*)ws, acc, grad, st);
-      CASE(2) CASE(4) CASE(8)
+#define CASE(DD, DDP) \
+  case DD: return kmv_fused_run<DD, DDP>(d, k, z, set_stride, ld, ds, params, (float*)ws, acc, grad, st);
+      CASE(1, 2) CASE(2, 2) CASE(3, 4) CASE(4, 4) CASE(5, 8) CASE(6, 8) CASE(7, 8) CASE(8, 8)
 #undef CASE
     }
   }
   PDEINV_REQUIRE(d->impl != PDEINV_MLP_IMPL_FUSED, PDEINV_ERR_UNSUPPORTED,
-                 "kmv_mlp: the hand-written paths need dim <= 8 with width <= 28 (pair kernels), or dim in {2, 4, 8} "
-                 "with 2 <= n_layers <= 16, width <= 512, out_features <= 64 (fused MFMA path)");
+                 "kmv_mlp: the hand-written paths need dim <= 8 with width <= 28 (pair kernels), or dim <= 8 with "
+                 "1 <= n_layers <= 16, width <= 512 (fused MFMA path)");
   const KmvPlan k = kmv_plan(d);
   switch (d->dim) {
 #define CASE(DD) case DD: return kmv_mlp_run<DD>(d, k, z, set_stride, ld, ds, params, (float*)ws, acc, grad, st);

@@ -415,7 +415,8 @@ __global__ __launch_bounds__(kT, 2) void fgemm(GemmArgs a) {
               p2 += __shfl_xor(p2, off, 64);
             }
             const int r = r0 + wm * WM + mi * 32 + (q & 3) + 8 * (q >> 2) + 4 * hi;
-            if (l31 == 0 && r < a.R) a.terms[r] = make_float4(2.f * p1, 2.f * p2, p0, 0.f);
+            // out_features > BN: one partial per column block (by), summed by terms_sum_kernel
+            if (l31 == 0 && r < a.R) a.terms[(int64_t)by * a.R + r] = make_float4(2.f * p1, 2.f * p2, p0, 0.f);
           }
         }
       }
@@ -835,6 +836,18 @@ __global__ __launch_bounds__(kT) void fwgrad(WgradArgs a) {
 // Fixed-order slab sums: out[i] += sum_s part[s][i]. Many slabs are first folded in groups of
 // kFold (more parallelism, same order every run), then the group sums are added.
 constexpr int kFold = 16;
+
+// E_OUT over ncb column blocks (out_features > 64): terms[r] = sum_cb terms[cb * R + r], fixed order
+__global__ void terms_sum_kernel(float4* __restrict__ terms, int ncb, int64_t R) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  float4 t = terms[r];
+  for (int cb = 1; cb < ncb; ++cb) {
+    const float4 u = terms[(int64_t)cb * R + r];
+    t.x += u.x; t.y += u.y; t.z += u.z;
+  }
+  terms[r] = t;
+}
 
 __global__ void fold_slabs_kernel(const float* __restrict__ part, int S, int64_t n, float* __restrict__ out2) {
   const int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x;
@@ -1613,9 +1626,11 @@ static bool use_rgemm(int W) {
   return !off && (W == 128 || W == 256);
 }
 
+// any out_features: the output layer's row reductions (E_OUT) take one partial per 64-column block when
+// out_features > 64; L = 1 runs the output layer straight off the layer-1 prologue modes
 bool supported(int d, int L, int W, int O) {
-  return (d == 2 || d == 4 || d == 8 || d == 16) && L >= 2 && L <= 16 &&
-         (W == 32 || W == 64 || W == 128 || W == 256 || W == 512) && O >= 1 && O <= 64;
+  return (d == 2 || d == 4 || d == 8 || d == 16) && L >= 1 && L <= 16 &&
+         (W == 32 || W == 64 || W == 128 || W == 256 || W == 512) && O >= 1;
 }
 
 // workspace layout (floats), chunk of Bc rows
@@ -1642,7 +1657,7 @@ static Layout layout(int d, int L, int W, int O, int64_t Bc) {
   y.hb1 = take(3 * plane);
   y.ys = take((size_t)3 * Bc * O);
   y.yb = take((size_t)3 * Bc * O);
-  y.terms = take((size_t)4 * Bc);
+  y.terms = take((size_t)4 * Bc * ((O + 63) / 64));  // E_OUT partials per 64-column block
   y.g = take((size_t)Bc * d);
   y.abar0 = take((size_t)Bc * d);
   y.part = take(part_floats(d, W, O));
@@ -1708,6 +1723,71 @@ static int run_chunk_t(const Chunk& c, const LossHook& loss, hipStream_t st) {
 
   const int l1_blocks = (int)std::min<int64_t>((R + kL1Rows - 1) / kL1Rows, kRowGridCap);
   const int64_t l1_rpb = (R + l1_blocks - 1) / l1_blocks;
+  auto sum_terms = [&]() {
+    if (O <= 64) return 0;
+    hipLaunchKernelGGL(terms_sum_kernel, dim3((unsigned)((R + kT - 1) / kT)), dim3(kT), 0, st, terms, (O + 63) / 64, R);
+    return check_launch("kfp_mlp fused terms sum");
+  };
+  if (L == 1) {
+    // one hidden layer: the output layer reads the layer-1 streams straight from the prologue modes (h1,
+    // s1 z1', s2 z1'^2 | s1 (abar0 K1)), the reverse product stops at hbar1 (l1_grad_kernel), and the
+    // output-layer weight gradient rebuilds the layer-1 streams from the rows (GA_L1) — no plane of
+    // layer 1 is stored
+    {
+      GemmArgs a = base;
+      a.K = W; a.N = O; a.Bw = Ko; a.bias = bo;
+      a.po0 = Ys[0]; a.po1 = Ys[1]; a.po2 = Ys[2]; a.terms = terms;
+      RC((launch_gemm<3, 128, 64, 4, A_L1F, B_NN, E_OUT, D>(a, st)));
+      RC(sum_terms());
+    }
+    {
+      GemmArgs a = base;
+      a.K = O; a.N = W; a.Bw = Ko; a.pa0 = Ys[0]; a.po0 = A1;
+      RC((launch_gemm1<A_U, B_NT>(a, st)));
+    }
+    if constexpr (WB <= 256) {
+      if (use_l1g_mfma()) {
+        const int blocks = (int)std::min<int64_t>((R + 63) / 64, 2048);
+        hipLaunchKernelGGL((l1_g_mfma_kernel<D, WB>), dim3(blocks), dim3(kT), 0, st, A1, c.z, c.ldz, Kw(1), Bw(1), R, G);
+        RC(check_launch("kfp_mlp fused g (MFMA)"));
+      }
+    }
+    if (WB > 256 || !use_l1g_mfma()) {
+      const int blocks = (int)std::min<int64_t>((R + 3) / 4, 2048);
+      hipLaunchKernelGGL((l1_g_kernel<D, WB>), dim3(blocks), dim3(kT), 0, st, A1, c.z, c.ldz, Kw(1), Bw(1), R, G);
+      RC(check_launch("kfp_mlp fused g"));
+    }
+    if (c.grad_only) return 0;
+    RC(loss.fn(loss.ctx, G, terms, abar0, R, st));
+    {
+      GemmArgs a = base;
+      a.K = W; a.N = O; a.Bw = Ko;
+      a.pe0 = Ys[0]; a.pe1 = Ys[1]; a.pe2 = Ys[2];
+      a.po0 = YB[0]; a.po1 = YB[1]; a.po2 = YB[2];
+      int gx = 0;
+      RC((launch_gemm<1, 128, 64, 4, A_L1A, B_NN, E_SEEDS, D>(a, st, &gx)));
+      RC(sum_slabs(part, gx, O, c.grad + c.boff[L], part2, st));
+    }
+    {
+      GemmArgs a = base;
+      a.K = O; a.N = W; a.Bw = Ko;
+      a.pa0 = YB[0]; a.pa1 = YB[1]; a.pa2 = YB[2];
+      a.po0 = HB1[0]; a.po1 = HB1[1]; a.po2 = HB1[2];
+      RC((launch_gemm<3, TM, TN, TG, A_S3, B_NT, E_STORE3>(a, st)));
+      hipLaunchKernelGGL((l1_grad_kernel<D, WB>), dim3(l1_blocks), dim3(kT), 0, st, HB1[0], HB1[1], HB1[2], A1, c.z,
+                         c.ldz, abar0, Kw(1), Bw(1), R, l1_rpb, part);
+      RC(check_launch("kfp_mlp fused layer-1 gradient"));
+      RC(sum_slabs(part, l1_blocks, (int64_t)(D + 1) * W, c.grad + c.poff[0], part2, st));  // K1 then b1
+    }
+    {
+      WgradArgs g{};
+      g.R = R; g.n_in = W; g.n_out = O; g.part = part;
+      g.xz = c.z; g.ldxz = c.ldz; g.ab0 = abar0; g.k1 = Kw(1); g.b1 = Bw(1);
+      g.pb0 = YB[0]; g.pb1 = YB[1]; g.pb2 = YB[2]; g.pb3 = Ys[0];
+      RC((launch_wgrad<GW, 64, GA_L1, GB_SM, D>(g, c.grad + c.poff[L], part2, st)));
+    }
+    return 0;
+  }
   // ---- F1 -------------------------------------------------------------------------------
   {  // layer 1 in the prologue (h1 streams never stored), layer 2 on MFMA
     GemmArgs a = base;
@@ -1731,6 +1811,7 @@ static int run_chunk_t(const Chunk& c, const LossHook& loss, hipStream_t st) {
     a.po0 = Ys[0]; a.po1 = Ys[1]; a.po2 = Ys[2]; a.terms = terms;
     if (RG && use_rgemm_out() && O <= 64) RC((launch_rgemm_out<3, A_FWD, E_OUT>(a, st)));
     else RC((launch_gemm<3, 128, 64, 4, A_FWD, B_NN, E_OUT>(a, st)));
+    RC(sum_terms());
   }
   // ---- R1: grad_x chain -------------------------------------------------------------------
   {
@@ -1825,7 +1906,7 @@ static int run_chunk_t(const Chunk& c, const LossHook& loss, hipStream_t st) {
     g.pa0 = P(L, P_H); g.pa1 = P(L, P_ZD); g.pa2 = P(L, P_ZDD); g.pa3 = P(L, P_ZETABAR);
     g.pb0 = YB[0]; g.pb1 = YB[1]; g.pb2 = YB[2]; g.pb3 = Ys[0];
     const int64_t cap = (int64_t)part_floats(D, W, O);
-    if (WB >= 64 && WB <= 256 && use_wgo()) {
+    if (WB >= 64 && WB <= 256 && O <= 64 && use_wgo()) {
       switch ((O + 15) / 16) {
         case 1: RC((launch_wgrad_o<1>(g, cap, c.grad + c.poff[L], part2, st))); break;
         case 2: RC((launch_wgrad_o<2>(g, cap, c.grad + c.poff[L], part2, st))); break;

@@ -317,11 +317,19 @@ LIB, FUSED = 1, 2  # native.MLP_IMPL_LIBRARY / MLP_IMPL_FUSED
     ([8, 64, 64, 64, 40], "quad", 777, FUSED), ([2, 32, 32, 32, 5], "quad", 1 << 18, FUSED),
     # the reference's default net (MLP.yaml: width 20 x 8 layers), zero-padded onto the 32-wide MFMA kernels
     ([2] + [20] * 8 + [40], "gmm", 1000, FUSED), ([4] + [20] * 8 + [40], "quad", 1 << 18, 0),
-    ([8, 100, 100, 40], "gmm", 1500, FUSED)])
+    ([8, 100, 100, 40], "gmm", 1500, FUSED),
+    # one hidden layer (the output layer straight off the layer-1 prologue modes), out_features > 64 (E_OUT
+    # partials per 64-column block), dims other than 2 / 4 / 8 / 16 (rows and the true potential zero-padded)
+    ([4, 64, 40], "quad", 1000, FUSED), ([8, 256, 40], "gmm", 777, FUSED), ([2, 20, 40], "gmm", 1 << 18, FUSED),
+    ([4, 64, 64, 80], "quad", 1000, FUSED), ([8, 128, 128, 200], "gmm", 1500, FUSED),
+    ([3, 32, 32, 40], "gmm", 1000, FUSED), ([10, 64, 64, 40], "quad", 1000, FUSED), ([1, 32, 32, 5], "quad", 777, FUSED),
+    ([5, 20, 40], "gmm", 1000, 0), ([6, 48, 48, 48, 70], "quad", 1 << 18, 0)])
 def test_residual_mlp_vs_restatement(native, dims, true_kind, chunk, impl):
     """V_hypothesis residual (value + d loss/d theta) vs the fp64 restatement whose adjoint is
     FD-checked in tests/test_oracle.py, on both implementations (rocBLAS library path and the
-    fused MFMA path). Multi-chunk paths exercised (chunk < rows); L = 3 covers the middle layers."""
+    fused MFMA path). Multi-chunk paths exercised (chunk < rows); L = 3 covers the middle layers.
+    impl = 0 (AUTO) on out-of-envelope shapes must take the hand-written path: its result equals
+    impl = FUSED bit for bit (the fused path is deterministic), no rocBLAS."""
     rng = np.random.default_rng(len(dims) + dims[1])
     d = dims[0]
     flat = np.concatenate([np.concatenate([rng.standard_normal((dims[i], dims[i + 1])).ravel() * np.sqrt(1.0 / dims[i]),
@@ -336,7 +344,12 @@ def test_residual_mlp_vs_restatement(native, dims, true_kind, chunk, impl):
         kind, tp, gt = native.POT_QUADRATIC, F, nr.grad_quadratic(F)
     acc, grad = native.residual_kfp_mlp(dims, _t(flat), _t(zi), _t(zt), _t(z0), true_kind=kind, true_params=tp,
                                         gamma=0.5, total_time=2.0, chunk_rows=chunk, impl=impl)
-    assert impl != FUSED or native.mlp_fused_supported(dims) or dims[1] not in (32, 64, 128, 256, 512)
+    assert impl != FUSED or native.mlp_fused_supported(dims) or dims[1] not in (32, 64, 128, 256, 512) \
+        or dims[0] not in (2, 4, 8, 16)
+    if impl == 0:
+        acc_f, grad_f = native.residual_kfp_mlp(dims, _t(flat), _t(zi), _t(zt), _t(z0), true_kind=kind, true_params=tp,
+                                                gamma=0.5, total_time=2.0, chunk_rows=chunk, impl=FUSED)
+        assert torch.equal(acc, acc_f) and torch.equal(grad, grad_f)
     out = native.kfp_terms_finalize(acc, grad, 0.5).cpu().numpy()
     loss, loss_gt, parts = nr.kfp_mlp_loss(P, zi, zt, z0, gt, 0.5, 2.0)
     g_ref = nr.mlp_flat(nr.kfp_mlp_grad_analytic(P, zi, zt, z0, 0.5, 2.0))

@@ -57,7 +57,11 @@ def test_kmv_residual_vs_pairwise_restatement(native):
                                                 (2, 70, 300, 28, 12, 2), (2, 60, 300, 64, 2, 2),
                                                 (8, 40, 1 << 18, 256, 2, 0), (4, 45, 500, 100, 3, 2),
                                                 (4, 33, 256, 32, 2, 0), (8, 45, 300, 20, 3, -2), (3, 70, 300, 10, 2, -2),
-                                                (2, 300, 300, 20, 3, -2)])
+                                                (2, 300, 300, 20, 3, -2),
+                                                # dims other than 2 / 4 / 8 and one hidden layer on the fused
+                                                # wide-net path (pair rows zero-padded; no rocBLAS)
+                                                (3, 45, 300, 64, 2, 2), (5, 40, 300, 32, 2, 0),
+                                                (2, 50, 300, 64, 1, 2)])
 def test_kmv_general_phi_mlp_vs_pairwise_restatement(native, d, n, chunk, W, L, impl):
     """General Phi_theta = V_hypothesis (non-parametric KMV, kinetic_mckean_vlasov.py:11-120) == the
     literal pair-tensor restatement (loss, loss ground truth, terms) and its FD-checked analytic gradient

@@ -230,6 +230,7 @@ def test_abi_argument_validation_without_gpu():
     assert L.pdeinv_realnvp_value_and_grad(None, None, None, 0, None, 0, 0, None, None, None, 0, None) \
         == native.PDEINV_ERR_INVALID
     assert L.pdeinv_mlp_fused_supported(3, 2, 256, 40) == 0 and L.pdeinv_mlp_fused_supported(8, 2, 256, 40) == 1
+    assert L.pdeinv_mlp_fused_supported(8, 1, 256, 40) == 1 and L.pdeinv_mlp_fused_supported(8, 2, 256, 80) == 1
     # impl is validated (PDEINV_MLP_IMPL_PAIRS_RING selects the register-ring pair kernels, kmv_mlp only)
     F = (ctypes.c_float * 4)(1, 0, 0, 1)
     km = native.KmvMlpDesc()
