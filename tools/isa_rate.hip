@@ -35,6 +35,21 @@ __global__ void k_fma(float* out, float seed) {
   out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+// v_pk_fma_f32: two fp32 FMAs per lane per instruction (the C3 kernel's centre-pair math)
+__global__ void k_pk_fma(float* out, float seed) {
+  f32x2 x[kChains];
+  for (int c = 0; c < kChains; ++c) x[c] = f32x2{seed + threadIdx.x + c, seed - threadIdx.x - c};
+  const f32x2 m = {0.999f, 0.998f}, a = {0.001f, 0.002f};
+  for (int it = 0; it < kIters; ++it) {
+#pragma unroll
+    for (int c = 0; c < kChains; ++c) x[c] = x[c] * m + a;
+  }
+  float s = 0;
+  for (int c = 0; c < kChains; ++c) s += x[c][0] + x[c][1];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
 __global__ void k_xor(uint32_t* out, uint32_t seed) {
   uint32_t x[kChains];
   for (int c = 0; c < kChains; ++c) x[c] = seed + threadIdx.x * 7 + c;
@@ -72,7 +87,7 @@ int main() {
   hipEventCreate(&a);
   hipEventCreate(&b);
   const double waves = (double)blocks * threads / 64;
-  auto run = [&](const char* name, auto launch, double insts_per_iter) {
+  auto run = [&](const char* name, auto launch, double insts_per_iter, double flop_per_lane_inst = 0) {
     launch();
     hipDeviceSynchronize();
     hipEventRecord(a);
@@ -83,10 +98,14 @@ int main() {
     hipEventElapsedTime(&ms, a, b);
     const double t = ms / 5 * 1e-3;
     const double cyc = t * clk_khz * 1e3 * simds / (waves * kIters * kChains * insts_per_iter);
-    printf("%-40s %.3f ms  %.2f SIMD cycles per wave-instruction (clock %d MHz)\n", name, ms / 5, cyc, clk_khz / 1000);
+    printf("%-40s %.3f ms  %.2f SIMD cycles per wave-instruction (clock %d MHz)", name, ms / 5, cyc, clk_khz / 1000);
+    if (flop_per_lane_inst > 0)  // chip-wide fp32 rate at the measured issue cost
+      printf("  %.1f TFLOP/s", waves * 64 * kIters * kChains * insts_per_iter * flop_per_lane_inst / t / 1e12);
+    printf("\n");
   };
   run("v_mad_u64_u32 (+ v_xor)", [&] { hipLaunchKernelGGL(k_mad_u64, dim3(blocks), dim3(threads), 0, 0, (uint32_t*)buf, 1u); }, 1.0);
-  run("v_fma_f32", [&] { hipLaunchKernelGGL(k_fma, dim3(blocks), dim3(threads), 0, 0, (float*)buf, 1.f); }, 1.0);
+  run("v_fma_f32", [&] { hipLaunchKernelGGL(k_fma, dim3(blocks), dim3(threads), 0, 0, (float*)buf, 1.f); }, 1.0, 2.0);
+  run("v_pk_fma_f32", [&] { hipLaunchKernelGGL(k_pk_fma, dim3(blocks), dim3(threads), 0, 0, (float*)buf, 1.f); }, 1.0, 4.0);
   run("v_bitop3_b32", [&] { hipLaunchKernelGGL(k_xor, dim3(blocks), dim3(threads), 0, 0, (uint32_t*)buf, 1u); }, 1.0);
   run("v_log_f32 (+ v_add)", [&] { hipLaunchKernelGGL(k_log, dim3(blocks), dim3(threads), 0, 0, (float*)buf, 0.f); }, 1.0);
   hipFree(buf);

@@ -63,6 +63,7 @@ def main():
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--only", default=None)
+    ap.add_argument("--out", default=None, help="also append each JSON line to this file")
     a = ap.parse_args()
     import main as entry
     from utils import config as config_lib
@@ -83,9 +84,13 @@ def main():
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
         last = trainer.history[-1]
-        print(json.dumps({"workload": name, "overrides": ov, "iters": iters, "iters_per_s": iters / el,
-                          "ms_per_iter": el * 1e3 / iters, "setup_and_warmup_s": build_s,
-                          "loss": last.get("loss"), "loss ground truth": last.get("loss ground truth")}), flush=True)
+        line = json.dumps({"workload": name, "overrides": ov, "iters": iters, "iters_per_s": iters / el,
+                           "ms_per_iter": el * 1e3 / iters, "setup_and_warmup_s": build_s,
+                           "loss": last.get("loss"), "loss ground truth": last.get("loss ground truth")})
+        print(line, flush=True)
+        if a.out:
+            with open(a.out, "a") as f:
+                f.write(line + "\n")
 
 
 if __name__ == "__main__":
