@@ -185,14 +185,14 @@ __device__ __forceinline__ void fold_ce(float* sl, const f32x4& G0, const f32x4&
     dc[r] = sl + (4 * gq + r) * kW + pq;
     const int in = em.in0 + r, out = em.out0 + (lane & 3);
     ok[r] = em.live && in <= kW && out < kW;
-    de[r] = ok[r] ? sl + in * kW + out : dc[r];  // padding: read the lane's core word, write nothing
+    de[r] = ok[r] ? sl + in * kW + out : dump;  // padding: the lane's own dump word (branch-free)
     vc[r] = *dc[r];
     ve[r] = *de[r];
   }
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     *dc[r] = vc[r] + G0[r];
-    if (ok[r]) *de[r] = ve[r] + E[r];
+    *de[r] = ve[r] + E[r];
   }
 }
 
@@ -204,7 +204,7 @@ __device__ __forceinline__ void outer_stream(float* tA, float* tB, const float (
                                              f32x4& G0, f32x4& E) {
   put_slots<kNS>(tA, bv, pq, gq);
   put_slots<kNS>(tB, av, pq, gq);
-  if (gq == 0) tB[img_at(kW, ppq)] = bias_row;
+  *(gq == 0 ? tB + img_at(kW, ppq) : dump) = bias_row;
   const f32x4 fa = get_rows(tA, 0, pq, gq), fb = get_rows(tB, 0, pq, gq);
   f32x4 ea[4], eb[4];
 #pragma unroll
@@ -246,8 +246,7 @@ __device__ __forceinline__ void fold(float* slab, int qoff, int pitch, int nout,
 #pragma unroll
     for (int ob = 0; ob < OBN; ++ob)
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        if (ok[ib][ob][r]) *dst[ib][ob][r] = v[ib][ob][r] + G[ib][ob][r];
+      for (int r = 0; r < 4; ++r) *dst[ib][ob][r] = v[ib][ob][r] + G[ib][ob][r];
 }
 
 // the four forward streams entering the next layer from a layer's checkpoint (h, z'_u, z'_v, z''_v)
@@ -525,7 +524,7 @@ __global__ __launch_bounds__(kWaves2 * kWave, 1) void kmvq_grad_kernel(Args a) {
             stream_of<s>(ph, pu, pv, pw, Hp);
             put_slots<kNS>(tA, zb[s], pq, gq);
             put_slots<kNS>(tB, Hp, pq, gq);
-            if (gq == 0) tB[img_at(kW, ppq)] = s == 0 ? 1.f : 0.f;
+            *(gq == 0 ? tB + img_at(kW, ppq) : dump) = s == 0 ? 1.f : 0.f;
             const f32x4 fa = get_rows(tA, 0, pq, gq), fb = get_rows(tB, 0, pq, gq);
             f32x4 ea[4], eb[4];  // edge operands: 4 pairs per 16-byte read (pairs q + 4 ks)
 #pragma unroll
@@ -570,7 +569,7 @@ __global__ __launch_bounds__(kWaves2 * kWave, 1) void kmvq_grad_kernel(Args a) {
             const int k = 4 * kk + gq;  // rows past D go to row 15 (a column no layer-0 output reads)
             tB[img_at(k < D ? k : 15, ppq)] = s == 0 ? yb[kk] : (s == 1 ? ui[kk] : vi[kk]);
           }
-          if (gq == 0) tB[img_at(D, ppq)] = s == 0 ? 1.f : 0.f;
+          *(gq == 0 ? tB + img_at(D, ppq) : dump) = s == 0 ? 1.f : 0.f;
           f32x4 fa[2], fb;
 #pragma unroll
           for (int b = 0; b < 2; ++b) fa[b] = get_rows(tA, b, pq, gq);
