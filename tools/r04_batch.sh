@@ -18,7 +18,11 @@ step() {  # step <name> <command...>
   case $rc in 124|134|137|139) echo "fatal rc in step $name: stopping" | tee -a $LOG; exit $rc ;; esac
   return 0
 }
-step tests bash tools/gtest_all.sh $TAG "${GTEST_K:-multirank or accuracy or general_phi or kmv_non or partial_s or residual_mlp}"
+if [ "${GTEST_K:-}" = all ]; then
+  step tests bash tools/gtest_all.sh $TAG
+else
+  step tests bash tools/gtest_all.sh $TAG "${GTEST_K:-multirank or accuracy or general_phi or kmv_non or partial_s or residual_mlp}"
+fi
 step check bash tools/r04_check.sh $TAG skip-tests
 pairs_time() {
   timeout -k 10 300 python3 tools/kmv_mlp_time.py 2,5000,1,20,8,2 2,2000,3,20,8,2 2,5000,1,20,8,3 > gpurun_out/q_time_$TAG.jsonl 2>&1 || return $?
