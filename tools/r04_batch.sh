@@ -40,4 +40,7 @@ isa() {
   timeout -k 10 60 /tmp/isa_rate_$TAG | tee gpurun_out/isa_rate_$TAG.txt
 }
 step isa isa
+step nvp_pmc bash tools/gnvp_pmc.sh $TAG
+nvp_time() { timeout -k 10 200 python3 tools/nvp_bench.py --steps 30 --warmup 5 --dims 2,4 | tee gpurun_out/nvp_$TAG.jsonl; }
+step nvp nvp_time
 cat $LOG
