@@ -127,12 +127,7 @@ constexpr int kMwStride = 20;  // floats per staged row (16 features + pad)
 //    update-t noise over the stamp's particles (row r = particle poff + r), i.e. the mean-path input of
 //    pdeinv_mf_sums for updates t < n_sets: that kernel is pure Philox / Box–Muller VALU work and this
 //    pass is HBM-bound, so the RNG rides in the pass's idle issue slots instead of a separate launch.
-//  * SPLIT (MF only): the block's last wave does all of the block's RNG (three rows per lane) and the other
-//    three stream the rows. With every wave doing both, the RNG's live registers put the kernel at 244
-//    VGPRs (two waves per SIMD) and the row stream starves while the waves sit in Philox; split, the kernel
-//    keeps the streaming pass's register count (three waves per SIMD) and the RNG waves' VALU work runs
-//    beside the streaming waves' loads.
-template <int D, bool PACKED, bool MF = false, bool SPLIT = false>
+template <int D, bool PACKED, bool MF = false>
 __global__ __launch_bounds__(kBlock) void kmv_moments_weights_kernel(float gamma, const float* __restrict__ coef,
                                                                      const float* __restrict__ z, int64_t n_rows,
                                                                      int64_t set_stride, int64_t ld,
@@ -173,9 +168,6 @@ __global__ __launch_bounds__(kBlock) void kmv_moments_weights_kernel(float gamma
 
   f32x4 g4 = {0.f, 0.f, 0.f, 0.f};
   [[maybe_unused]] float xis[MF ? D : 1] = {};
-  // SPLIT: waves 0..2 stream rows (kSw rows per block step), wave 3 draws the normals of those rows
-  constexpr int kSw = SPLIT ? kWavesPerBlock - 1 : kWavesPerBlock;  // streaming waves per block
-  const bool rng_wave = SPLIT && wave == kWavesPerBlock - 1;
   float zs[M] = {};
   float rows = 0.f;
   MomentAcc<D> acc;
@@ -228,26 +220,8 @@ __global__ __launch_bounds__(kBlock) void kmv_moments_weights_kernel(float gamma
     }
   };
   // wave-uniform trip count: every lane joins every MFMA (rows past the end are zeros, weight 0)
-  const int64_t stride = (int64_t)gridDim.x * kSw * kWave;
-  int64_t r0 = (int64_t)blockIdx.x * kSw * kWave + wave * kWave;
-  if constexpr (SPLIT) {
-    if (rng_wave) {  // the normals of every row the block's streaming waves read, three per lane
-      for (int64_t b0 = (int64_t)blockIdx.x * kSw * kWave; b0 < n_rows; b0 += stride) {
-#pragma unroll 1
-        for (int k = 0; k < kSw; ++k) {
-          const int64_t r = b0 + k * kWave + lane;
-          if (r < n_rows) {
-            const uint64_t gid = (uint64_t)(mf.poff + r);
-            float xi[D];
-            stream_normals<D>(mf.k0, mf.k1, mf.ctr_off + (uint32_t)t, (uint32_t)gid, (uint32_t)(gid >> 32), xi);
-#pragma unroll
-            for (int q = 0; q < D; ++q) xis[q] += xi[q];
-          }
-        }
-      }
-      r0 = n_rows;  // no rows to stream: straight to the reductions (zero moment contributions)
-    }
-  }
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  int64_t r0 = (int64_t)blockIdx.x * kBlock + wave * kWave;
   [[maybe_unused]] float vn[PACKED ? 1 : M];
   [[maybe_unused]] f32x4 qn[PACKED ? NQ : 1];
   if constexpr (PACKED) load_packed(r0, qn);
@@ -294,7 +268,7 @@ __global__ __launch_bounds__(kBlock) void kmv_moments_weights_kernel(float gamma
     }
     const float w = active ? q[1] + q[0] * q[0] + gamma * q[0] : 0.f;  // kinetic_mckean_vlasov.py:243-248
     acc.add(v, w);
-    if constexpr (MF && !SPLIT) {  // the next simulate's update-t normals of this lane's particle
+    if constexpr (MF) {  // the next simulate's update-t normals of this lane's particle
       if (active) {
         const uint64_t gid = (uint64_t)(mf.poff + r0 + lane);
         float xi[D];
@@ -589,15 +563,6 @@ extern "C" int pdeinv_residual_kmv(const pdeinv_kmv_desc* d, const double* mom, 
 // fp32 partial slab, rounded up to 256 B so that the fp64 column sums behind it are aligned
 static size_t kmv_mw_slab_bytes(int64_t cols, int bx) { return ((size_t)cols * bx * sizeof(float) + 255) & ~(size_t)255; }
 
-// PDEINV_KMV_MF_SPLIT=0 (A/B): every wave of the fused-sums pass streams rows and draws their normals
-static bool kmv_mf_split() {
-  static const bool v = [] {
-    const char* e = getenv("PDEINV_KMV_MF_SPLIT");
-    return !(e && e[0] == '0');
-  }();
-  return v;
-}
-
 static int kmv_mw_launch(int32_t D, float gamma, const float* coef, const float* z, int64_t n_sets, int64_t n_rows,
                          int64_t set_stride, int64_t ld, void* ws, double* mom, double* wst, hipStream_t st,
                          const MfNoise* mf, float* mf_partials) {
@@ -613,10 +578,7 @@ static int kmv_mw_launch(int32_t D, float gamma, const float* coef, const float*
   switch (D) {
 #define CASE(DD)                                                                                              \
   case DD:                                                                                                    \
-    if (mf && packed && kmv_mf_split())                                                                       \
-      hipLaunchKernelGGL((kmv_moments_weights_kernel<DD, (2 * DD) % 4 == 0, true, true>), g, dim3(kBlock), 0,  \
-                         st, gamma, coef, z, n_rows, set_stride, ld, p, m, mf_partials);                      \
-    else if (mf && packed)                                                                                    \
+    if (mf && packed)                                                                                         \
       hipLaunchKernelGGL((kmv_moments_weights_kernel<DD, (2 * DD) % 4 == 0, true>), g, dim3(kBlock), 0, st,    \
                          gamma, coef, z, n_rows, set_stride, ld, p, m, mf_partials);                          \
     else if (mf)                                                                                              \

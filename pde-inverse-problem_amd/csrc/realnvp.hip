@@ -174,6 +174,11 @@ constexpr int kNvpMaxRows = 8192;  // slab rows (128-sample blocks) per launch +
 constexpr int kNvT = PDEINV_NVT;   // 16-sample tiles per wave (32 samples; 128 per block)
 constexpr int kNvSPB = kWavesPerBlock * 16 * kNvT;  // samples per block = per slab row
 constexpr int kNvWS = 20;          // LDS row stride of a padded 16 x 16 weight matrix
+// Per-wave sample stage: [16 samples][16 components] dense, the 4-float chunk c of sample row r stored at chunk
+// c ^ nv_swz(r). Its 16-byte writes (8-lane groups, rows s = 0..7 of one chunk) and its 4-byte reads (32-lane
+// groups, rows 4t + {0, 1}, 16 components each) then cover the 32 banks of each lane group exactly once.
+constexpr int kNvSS = 16;
+__device__ __forceinline__ int nv_swz(int r) { return (r >> 1) & 3; }
 constexpr int kNvRaw = 8 + 2 * (24 * 8 + 8 + 128 + 16 + 256 + 16 + 16 * 8 + 8);  // one layer's params, d <= 8
 constexpr int kNvPre = (kNvRaw + kBlock - 1) / kBlock;
 
@@ -196,16 +201,31 @@ struct NvM {
   static constexpr int E_W1 = 0, E_B1 = MAT, E_W2 = MAT + 16, E_B2 = 2 * MAT + 16, E_W2T = 2 * MAT + 32,
                        TEMB = 3 * MAT + 32;
 };
-// Per-wave partial-gradient block (flush layout, 16 x 16 matrices dense): one net's W0t, W0x, W1, W2,
-// W3, b0..b3 (the s-net flush adds sf). The time embedding reuses the first 2 x 272 floats.
-struct NvR {
-  static constexpr int W0T = 0, W0X = 256, W1 = 512, W2 = 768, W3 = 1024, B0 = 1280, B1 = 1296, B2 = 1312,
-                       B3 = 1328, NET = 1344;
-  static constexpr int SF = NET, SIZE = NET + 16;
+// Per-wave partial-gradient block of one coupling layer, compact (only the entries a parameter maps to):
+// [t-net | s-net | sf (16, by position)]. Per net, packed layout: W0 [16 input positions][8 hidden units],
+// W1 [8][16], W2 [16][16], W3 [16][4 coordinates], b0..b3 by position (16 each); identity layout: W0T
+// [16 time rows][8], W0X [8 coordinates][8], W1 [8][16], W2, W3 [16][8], b0..b3. The block is also the layer's
+// slab-row segment (the flush sums the four waves' blocks as float4 into it); the reduce maps it to the
+// reference parameter order (nv_slab_col). In LDS the t-net part aliases the wave's sample stage (it is written
+// after the t-net's last weight gradient) and the s-net part + sf sit behind the stage (written as soon as the
+// s-net's backward is done, so its accumulators are dead during the t-net's). The time embedding's flush reuses
+// the first 2 x 272 floats.
+template <bool PK>
+struct NvC {
+  static constexpr int W0T = 0, W0X = 128, W1 = PK ? 128 : 192, W2 = W1 + 128, W3 = W2 + 256,
+                       B0 = W3 + (PK ? 64 : 128), B1 = B0 + 16, B2 = B1 + 16, B3 = B2 + 16, NET = B3 + 16;
+  static constexpr int TNET = 0, SNET = NET, SF = 2 * NET, LAYER = 2 * NET + 16;  // 1296 / 1552 floats
 };
+constexpr int kNvStageF = kNvT * 2 * 16 * kNvSS;  // per-wave sample stage (floats)
+static_assert(NvC<false>::NET <= kNvStageF && NvC<true>::NET <= kNvStageF, "t-net block inside the stage");
+// LDS offset (in the wave's scratch) of compact-block entry o
+template <bool PK>
+__device__ __forceinline__ int nv_flush_lds(int o) { return o < NvC<PK>::NET ? o : o - NvC<PK>::NET + kNvStageF; }
+constexpr int kNvFlush = kNvStageF + NvC<false>::NET + 16;  // per-wave scratch (floats), the larger layout
 
 struct NvLane {
-  int g, s;  // component group, sample within the tile
+  int g, s;    // component group, sample within the tile
+  int sw, sr;  // sample-stage offsets: this lane's 16-byte write (row s, chunk g); its read of row g, component s
 };
 
 // Position of a component in the padded 16-vectors. Packed layout (PK: d <= 4, n_t <= 12): coordinate c
@@ -267,21 +287,23 @@ __device__ __forceinline__ void nv_bcast(NvV& c, const f32x4& b) {
 }
 
 // acc += sum over the wave's samples of a_s d_s^T (rows = a components): per-wave LDS stage
-// [kNvT][2][16 samples][kNvWS], one 16-byte write per lane and tile, one read per operand and k-step.
+// [kNvT][2][16 samples][kNvSS] (swizzled chunks, nv_swz), one 16-byte write per lane and tile, one read per
+// operand and k-step.
 __device__ __forceinline__ f32x4 nv_wgrad(float* stage, const NvLane& ln, const NvV& a, const NvV& d, f32x4 acc) {
   nv_wave_sync();  // the previous reads of the stage are done
 #pragma unroll
   for (int u = 0; u < kNvT; ++u) {
-    *reinterpret_cast<f32x4*>(stage + (2 * u) * 16 * kNvWS + ln.s * kNvWS + 4 * ln.g) = a[u];
-    *reinterpret_cast<f32x4*>(stage + (2 * u + 1) * 16 * kNvWS + ln.s * kNvWS + 4 * ln.g) = d[u];
+    *reinterpret_cast<f32x4*>(stage + (2 * u) * 16 * kNvSS + ln.sw) = a[u];
+    *reinterpret_cast<f32x4*>(stage + (2 * u + 1) * 16 * kNvSS + ln.sw) = d[u];
   }
   nv_wave_sync();
 #pragma unroll
   for (int u = 0; u < kNvT; ++u)
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      const int r = (2 * u) * 16 * kNvWS + (4 * t + ln.g) * kNvWS + ln.s;
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(stage[r], stage[16 * kNvWS + r], acc, 0, 0, 0);
+      // row 4t + g: nv_swz(4t + g) = nv_swz(g) ^ 2 (t & 1), i.e. component s ^ 8 on odd t
+      const int r = (2 * u) * 16 * kNvSS + 4 * t * kNvSS + (ln.sr ^ (t & 1 ? 8 : 0));
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(stage[r], stage[16 * kNvSS + r], acc, 0, 0, 0);
     }
   return acc;
 }
@@ -411,46 +433,93 @@ __device__ __forceinline__ void nv_put_mat(float* r, const NvLane& ln, const f32
 #pragma unroll
   for (int i = 0; i < 4; ++i) r[(4 * ln.g + i) * 16 + ln.s] = m[i];
 }
+// Compact matrix put (NvC): row 4g + i -> row map R (-1: padding), column s -> column map C, width NC.
+template <int NC, typename RM, typename CM>
+__device__ __forceinline__ void nv_put_cmat(float* r, const NvLane& ln, const f32x4& m, RM rm, CM cm) {
+  const int c = cm(ln.s);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int q = rm(4 * ln.g + i);
+    if (q >= 0 && c >= 0) r[q * NC + c] = m[i];
+  }
+}
 __device__ __forceinline__ void nv_put_vec(float* r, const NvLane& ln, const f32x4& v) {
   const f32x4 t = nv_sum16(v);
   if (ln.s == 0) *reinterpret_cast<f32x4*>(r + 4 * ln.g) = t;
 }
 template <bool PK>
 __device__ __forceinline__ void nv_put_net(float* r, const NvLane& ln, const NvNetAcc& a) {
-  nv_put_mat(r + NvR::W0T, ln, a.w0t);
-  if constexpr (!PK) nv_put_mat(r + NvR::W0X, ln, a.w0x);
-  nv_put_mat(r + NvR::W1, ln, a.w1);
-  nv_put_mat(r + NvR::W2, ln, a.w2);
-  nv_put_mat(r + NvR::W3, ln, a.w3);
-  nv_put_vec(r + NvR::B0, ln, a.b0);
-  nv_put_vec(r + NvR::B1, ln, a.b1);
-  nv_put_vec(r + NvR::B2, ln, a.b2);
-  nv_put_vec(r + NvR::B3, ln, a.b3);
+  using C = NvC<PK>;
+  auto all = [](int p) { return p; };
+  auto hid = [](int p) { return PK ? ((p & 3) < 2 ? 2 * (p >> 2) + (p & 1) : -1) : (p < 8 ? p : -1); };  // h0 unit
+  if constexpr (PK) {
+    nv_put_cmat<8>(r + C::W0T, ln, a.w0t, all, hid);
+  } else {
+    nv_put_cmat<8>(r + C::W0T, ln, a.w0t, all, hid);
+    nv_put_cmat<8>(r + C::W0X, ln, a.w0x, [](int p) { return p < 8 ? p : -1; }, hid);
+  }
+  nv_put_cmat<16>(r + C::W1, ln, a.w1, hid, all);
+  nv_put_cmat<16>(r + C::W2, ln, a.w2, all, all);
+  if constexpr (PK)
+    nv_put_cmat<4>(r + C::W3, ln, a.w3, all, [](int p) { return (p & 3) == 0 ? p >> 2 : -1; });
+  else
+    nv_put_cmat<8>(r + C::W3, ln, a.w3, all, [](int p) { return p < 8 ? p : -1; });
+  nv_put_vec(r + C::B0, ln, a.b0);
+  nv_put_vec(r + C::B1, ln, a.b1);
+  nv_put_vec(r + C::B2, ln, a.b2);
+  nv_put_vec(r + C::B3, ln, a.b3);
 }
 
-// Flat (reference-order) parameter f of one BasicMLP -> its index in the flush block, or -1.
+// Flat (reference-order) parameter f of one BasicMLP -> its index in the compact net block (NvC).
 template <bool PK>
-__device__ __forceinline__ int nv_net_src(int f, int d, int n_t) {
+__host__ __device__ __forceinline__ int nv_cb_src(int f, int d, int n_t) {
+  using C = NvC<PK>;
   const int n_in = d + n_t;
   if (f < n_in * 8) {
-    const int r = f / 8, o = nv_hpos<PK>(f - r * 8);
-    if (PK) return NvR::W0T + (r < d ? nv_xpos<PK>(r) : nv_tpos<PK>(r - d)) * 16 + o;
-    return r < d ? NvR::W0X + r * 16 + o : NvR::W0T + (r - d) * 16 + o;
+    const int r = f / 8, o = f - r * 8;
+    if (PK) return C::W0T + (r < d ? 4 * r : 4 * ((r - d) / 3) + 1 + (r - d) % 3) * 8 + o;
+    return r < d ? C::W0X + r * 8 + o : C::W0T + (r - d) * 8 + o;
   }
   f -= n_in * 8;
-  if (f < 8) return NvR::B0 + nv_hpos<PK>(f);
+  if (f < 8) return C::B0 + (PK ? 4 * (f / 2) + f % 2 : f);
   f -= 8;
-  if (f < 128) return NvR::W1 + nv_hpos<PK>(f / 16) * 16 + f % 16;
+  if (f < 128) return C::W1 + f;  // [h0 unit][16]
   f -= 128;
-  if (f < 16) return NvR::B1 + f;
+  if (f < 16) return C::B1 + f;
   f -= 16;
-  if (f < 256) return NvR::W2 + f;
+  if (f < 256) return C::W2 + f;
   f -= 256;
-  if (f < 16) return NvR::B2 + f;
+  if (f < 16) return C::B2 + f;
   f -= 16;
-  if (f < 16 * d) return NvR::W3 + (f / d) * 16 + nv_xpos<PK>(f % d);
+  if (f < 16 * d) return C::W3 + (f / d) * (PK ? 4 : 8) + f % d;
   f -= 16 * d;
-  return f < d ? NvR::B3 + nv_xpos<PK>(f) : -1;
+  return C::B3 + (PK ? 4 * f : f);
+}
+
+// Slab-row layout of the gradient kernel: [L compact layer blocks (NvC::LAYER each) | time embedding (reference
+// order) | loss], row stride rounded up to 4 floats (the layer blocks are stored as float4).
+struct NvSlabMap {
+  int d, n_t, pk, n_layers;
+  int64_t layer_stride, temb_params, n_params, cb;
+};
+__host__ __device__ __forceinline__ int64_t nv_slab_col(const NvSlabMap& m, int64_t c) {
+  const int64_t lcb = (int64_t)m.n_layers * m.cb;
+  if (c >= m.n_params) return lcb + m.temb_params;  // loss
+  if (c < m.temb_params) return lcb + c;
+  c -= m.temb_params;
+  const int64_t l = c / m.layer_stride;
+  int k = (int)(c - l * m.layer_stride);
+  const int64_t base = l * m.cb;
+  if (k < m.d) return base + (m.pk ? NvC<true>::SF + 4 * k : NvC<false>::SF + k);  // sf by position
+  k -= m.d;
+  const int mlp_n = (m.d + m.n_t) * 8 + 8 + 8 * 16 + 16 + 16 * 16 + 16 + 16 * m.d + m.d;
+  const int net = k >= mlp_n ? 1 : 0;
+  k -= net * mlp_n;
+  if (m.pk) return base + (net ? NvC<true>::TNET : NvC<true>::SNET) + nv_cb_src<true>(k, m.d, m.n_t);
+  return base + (net ? NvC<false>::TNET : NvC<false>::SNET) + nv_cb_src<false>(k, m.d, m.n_t);
+}
+__host__ __device__ __forceinline__ int64_t nv_slab_ld(const NvSlabMap& m) {
+  return ((int64_t)m.n_layers * m.cb + m.temb_params + 1 + 3) / 4 * 4;
 }
 
 // Raw coupling-layer parameter k (reference order: sf, s-net, t-net) -> its LDS position(s) in the padded layer
@@ -503,13 +572,13 @@ __global__ __launch_bounds__(kBlock, PDEINV_NVW) void realnvp_grad_kernel(NvpArg
   __shared__ float sM[PDEINV_REALNVP_MAX_LAYERS * 16];  // masks, padded with 1
   __shared__ float sB[16 + 16 * 16];                 // base mean, inverse covariance (0-padded)
   // per-wave wgrad stages during the tile math, per-wave flush blocks after it (a barrier between)
-  constexpr int kScr = NvR::SIZE > kNvT * 2 * 16 * kNvWS ? NvR::SIZE : kNvT * 2 * 16 * kNvWS;
+  constexpr int kScr = kNvFlush;
   __shared__ float sScr[kWavesPerBlock][kScr];
   __shared__ uint32_t sDst[kNvRaw];                  // raw layer parameter -> LDS position(s), nv_layer_dst
-  __shared__ short sMap[2 * (24 * 8 + 8 + 128 + 16 + 256 + 16 + 16 * 8 + 8)];  // flat net param -> NvR index
+  using C = NvC<PK>;
   const int E = a.E;
   const int n_in = a.in_dim, n_t = n_in - d;
-  const int mlp_n = n_in * 8 + 8 + 8 * 16 + 16 + 16 * 16 + 16 + 16 * d + d;
+  const int64_t lcb = (int64_t)a.n_layers * C::LAYER;  // slab-row offset of the time-embedding columns
   const int64_t temb_params = E > 0 ? 2 * ((int64_t)E * E + E) : 0;
   const float* layers = params + temb_params;
   const bool hard = !a.ignore_time && a.soft_init == 0.f;
@@ -520,6 +589,8 @@ __global__ __launch_bounds__(kBlock, PDEINV_NVW) void realnvp_grad_kernel(NvpArg
     asm volatile("" : "+v"(lane));  // opaque: keeps per-use address math out of long-lived registers
     ln.g = lane >> 4;
     ln.s = lane & 15;
+    ln.sw = ln.s * kNvSS + 4 * (ln.g ^ nv_swz(ln.s));
+    ln.sr = ln.g * kNvSS + (ln.s ^ (4 * nv_swz(ln.g)));
   }
   float* stage = sScr[wave];
   float* red = sScr[wave];
@@ -559,7 +630,6 @@ __global__ __launch_bounds__(kBlock, PDEINV_NVW) void realnvp_grad_kernel(NvpArg
     sF[16 + tid] = on && is_sin ? 1.f : 0.f;
     sF[32 + tid] = on && !is_sin ? 1.f : 0.f;
   }
-  for (int f = tid; f < mlp_n; f += kBlock) sMap[f] = (short)nv_net_src<PK>(f, d, n_t);
   for (int k = tid; k < layer_stride; k += kBlock) sDst[k] = nv_layer_dst<PK>(k, d, n_t);
   for (int q = tid; q < NvM::LAYER; q += kBlock) sW[q] = 0.f;  // padding: never written again
   for (int q = tid; q < a.n_layers * 16; q += kBlock) {
@@ -699,14 +769,15 @@ __global__ __launch_bounds__(kBlock, PDEINV_NVW) void realnvp_grad_kernel(NvpArg
   for (int u = 0; u < kNvT; ++u) {
     const f32x4 diff = x[u] - nv_vec(sB, ln);
     nv_wave_sync();
-    *reinterpret_cast<f32x4*>(stage + ln.s * kNvWS + 4 * ln.g) = diff;
+    *reinterpret_cast<f32x4*>(stage + ln.sw) = diff;
     nv_wave_sync();
     float quad = 0.f;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const int r = 4 * ln.g + c;
       float acc = 0.f;
-      for (int q = 0; q < d; ++q) acc = fmaf(sB[16 + r * 16 + q], stage[ln.s * kNvWS + nv_xpos<PK>(q)], acc);
+      for (int q = 0; q < d; ++q)
+        acc = fmaf(sB[16 + r * 16 + q], stage[ln.s * kNvSS + (nv_xpos<PK>(q) ^ (4 * nv_swz(ln.s)))], acc);
       quad = fmaf(diff[c], acc, quad);
       gx[u][c] = -w[u] * acc;
     }
@@ -718,7 +789,6 @@ __global__ __launch_bounds__(kBlock, PDEINV_NVW) void realnvp_grad_kernel(NvpArg
   // ---- backward through layers 0 .. L-1, rebuilding each layer's input ----
   for (int l = 0; l < a.n_layers; ++l) {
     stage_layer(l);
-    const int64_t loff = temb_params + (int64_t)l * layer_stride;
     const f32x4 m = nv_vec(sM + l * 16, ln), sfw = nv_vec(sW + NvM::SF, ln);
     f32x4 sfv, isf;
 #pragma unroll
@@ -754,6 +824,8 @@ __global__ __launch_bounds__(kBlock, PDEINV_NVW) void realnvp_grad_kernel(NvpArg
       }
     }
     nv_mlp_bwd<PK>(sW + NvM::SNET, ln, stage, temb, xm, h, gso, as, gtemb, gacc);
+    nv_put_vec(red + kNvStageF + NvC<PK>::NET, ln, galpha);  // behind the stage (nv_flush_lds)
+    nv_put_net<PK>(red + kNvStageF, ln, as);
     nv_mlp_fwd<PK>(sW + NvM::TNET, ln, temb, xm, h, out);
     nv_mlp_bwd<PK>(sW + NvM::TNET, ln, stage, temb, xm, h, gto, at, gtemb, gacc);
 #pragma unroll
@@ -764,13 +836,21 @@ __global__ __launch_bounds__(kBlock, PDEINV_NVW) void realnvp_grad_kernel(NvpArg
         x[u][c] = x[u][c] * __builtin_amdgcn_rcpf(es[u][c]) - tr;
         gx[u][c] = gx[u][c] * es[u][c] + m[c] * gacc[u][c];
       }
-    __syncthreads();  // every wave is done with its stage (the flush blocks alias it)
-    nv_put_net<PK>(red, ln, as);
-    nv_put_vec(red + NvR::SF, ln, galpha);
-    flush(loff, d + mlp_n, [&](int f) { return f < d ? NvR::SF + nv_xpos<PK>(f) : (int)sMap[f - d]; });  // sf, s-net
-    nv_put_net<PK>(red, ln, at);
-    flush(loff + d + mlp_n, mlp_n, [&](int f) { return (int)sMap[f]; });  // t-net
+    // the t-net partials into the wave's compact block (it aliases only the wave's own stage: no barrier), then
+    // the block's four wave blocks summed as float4 into the layer's slab-row segment. The next stage_layer's
+    // barrier orders these reads before any wave's next stage writes.
+    nv_wave_sync();
+    nv_put_net<PK>(red + C::TNET, ln, at);
+    __syncthreads();
+    for (int q = tid; q < C::LAYER / 4; q += kBlock) {
+      const int o = nv_flush_lds<PK>(4 * q);
+      const f32x4 v = ((*reinterpret_cast<const f32x4*>(&sScr[0][o]) + *reinterpret_cast<const f32x4*>(&sScr[1][o])) +
+                       *reinterpret_cast<const f32x4*>(&sScr[2][o])) +
+                      *reinterpret_cast<const f32x4*>(&sScr[3][o]);
+      *reinterpret_cast<f32x4*>(row + (int64_t)l * C::LAYER + 4 * q) = v;
+    }
   }
+  __syncthreads();  // the last layer's sums are read: the stages are free again
   // ---- time-embedding backward and the loss column ----
   if (E > 0) {
     f32x4 w1 = {0.f, 0.f, 0.f, 0.f}, w2 = w1, b1 = w1, b2 = w1;
@@ -796,7 +876,7 @@ __global__ __launch_bounds__(kBlock, PDEINV_NVW) void realnvp_grad_kernel(NvpArg
     nv_put_mat(red + 272, ln, w2);
     nv_put_vec(red + 528, ln, b2);
     const int EE = E * E + E;
-    flush(0, 2 * EE, [&](int f) {
+    flush(lcb, 2 * EE, [&](int f) {
       const int part = f >= EE, r = f - part * EE;
       const int o = part * 272;  // W2 / b2 columns at the temb positions
       if (r < E * E) return o + (r / E) * 16 + (part ? nv_tpos<PK>(r % E) : r % E);
@@ -808,18 +888,21 @@ __global__ __launch_bounds__(kBlock, PDEINV_NVW) void realnvp_grad_kernel(NvpArg
   lsum += __shfl_xor(lsum, 4, 64);
   lsum += __shfl_xor(lsum, 8, 64);
   if (tid % 64 == 0) red[0] = lsum;
-  flush(n_params, 1, [&](int) { return 0; });
+  flush(lcb + temb_params, 1, [&](int) { return 0; });
 }
 
 // Slab column sums in two fixed-order fp64 stages (bit-reproducible): kNvSplits row splits of the
 // chunk, each summed by 4 row phases of a 64-column block (4 independent loads in flight per
-// lane), then the splits in order. On the last chunk grad[c] = scale * acc[c] (c < n_params) and
+// lane), then the splits in order. Column c of parts is reference parameter c (n_params: the loss),
+// read from slab column nv_slab_col(c). On the last chunk grad[c] = scale * acc[c] (c < n_params) and
 // loss = scale * acc[n_params].
 constexpr int kNvSplits = 16;
-__global__ __launch_bounds__(kBlock) void nvp_slab_split_kernel(const float* __restrict__ slab, int rows, int64_t ld,
-                                                                 int64_t n_cols, double* __restrict__ parts) {
+__global__ __launch_bounds__(kBlock) void nvp_slab_split_kernel(const float* __restrict__ slab_base, int rows,
+                                                                 int64_t ld, NvSlabMap map, int64_t n_cols,
+                                                                 double* __restrict__ parts) {
   __shared__ double part[kBlock];
   const int64_t c = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
+  const float* slab = slab_base + (c < n_cols ? nv_slab_col(map, c) : 0);
   const int g = threadIdx.x >> 6;
   const int rps = (rows + kNvSplits - 1) / kNvSplits;
   const int r0 = blockIdx.y * rps, r1 = r0 + rps < rows ? r0 + rps : rows;
@@ -827,14 +910,14 @@ __global__ __launch_bounds__(kBlock) void nvp_slab_split_kernel(const float* __r
   if (c < n_cols) {
     int r = r0 + g;
     for (; r + 12 < r1; r += 16) {
-      const float v0 = slab[(int64_t)r * ld + c], v1 = slab[(int64_t)(r + 4) * ld + c];
-      const float v2 = slab[(int64_t)(r + 8) * ld + c], v3 = slab[(int64_t)(r + 12) * ld + c];
+      const float v0 = slab[(int64_t)r * ld], v1 = slab[(int64_t)(r + 4) * ld];
+      const float v2 = slab[(int64_t)(r + 8) * ld], v3 = slab[(int64_t)(r + 12) * ld];
       acc += (double)v0;
       acc += (double)v1;
       acc += (double)v2;
       acc += (double)v3;
     }
-    for (; r < r1; r += 4) acc += (double)slab[(int64_t)r * ld + c];
+    for (; r < r1; r += 4) acc += (double)slab[(int64_t)r * ld];
   }
   part[threadIdx.x] = acc;
   __syncthreads();
@@ -920,6 +1003,26 @@ extern "C" int pdeinv_realnvp_logdensity(const pdeinv_realnvp_desc* d, const flo
   return check_launch("realnvp_logdensity_kernel");
 }
 
+// Packed layout where [x | temb] fits one 16-vector with x in register 0 (PDEINV_NVP_PACK=0 forces the
+// identity layout, A/B).
+static bool nvp_packed(const pdeinv_realnvp_desc* d) {
+  static const bool pack_env = [] { const char* e = getenv("PDEINV_NVP_PACK"); return !(e && e[0] == '0'); }();
+  return pack_env && d->dim <= 4 && in_dim_of(d) - d->dim <= 12;
+}
+static NvSlabMap nvp_slab_map(const pdeinv_realnvp_desc* d) {
+  NvSlabMap m{};
+  const int E = d->ignore_time ? 0 : d->embed_time_dim;
+  m.d = d->dim;
+  m.n_t = in_dim_of(d) - d->dim;
+  m.pk = nvp_packed(d) ? 1 : 0;
+  m.n_layers = d->n_layers;
+  m.layer_stride = layer_params(d->dim, in_dim_of(d));
+  m.temb_params = E > 0 ? 2 * ((int64_t)E * E + E) : 0;
+  m.n_params = m.temb_params + (int64_t)d->n_layers * m.layer_stride;
+  m.cb = m.pk ? NvC<true>::LAYER : NvC<false>::LAYER;
+  return m;
+}
+
 static int64_t nvp_grad_rows(int64_t n) {
   const int64_t tiles = (n + kNvSPB - 1) / kNvSPB;
   return tiles < kNvpMaxRows ? tiles : kNvpMaxRows;
@@ -928,7 +1031,7 @@ static int64_t nvp_grad_rows(int64_t n) {
 extern "C" int64_t pdeinv_realnvp_grad_workspace(const pdeinv_realnvp_desc* d, int64_t n) {
   const int64_t P = pdeinv_realnvp_param_count(d);
   if (P < 0 || n < 0) return -1;
-  const int64_t slab = (nvp_grad_rows(n) * (P + 1) * (int64_t)sizeof(float) + 15) / 16 * 16;
+  const int64_t slab = nvp_grad_rows(n) * nv_slab_ld(nvp_slab_map(d)) * (int64_t)sizeof(float);
   return slab + (1 + kNvSplits) * (P + 1) * (int64_t)sizeof(double);
 }
 extern "C" int pdeinv_realnvp_value_and_grad(const pdeinv_realnvp_desc* d, const float* params, const float* t,
@@ -966,28 +1069,28 @@ extern "C" int pdeinv_realnvp_value_and_grad(const pdeinv_realnvp_desc* d, const
   const int64_t ls = layer_params(D, a.in_dim);
   const int64_t P = pdeinv_realnvp_param_count(d);
   const int64_t rows_max = nvp_grad_rows(n);
+  const NvSlabMap map = nvp_slab_map(d);
+  const int64_t sld = nv_slab_ld(map);
   float* slab = (float*)workspace;
-  double* acc64 = (double*)((char*)workspace + (rows_max * (P + 1) * (int64_t)sizeof(float) + 15) / 16 * 16);
+  double* acc64 = (double*)((char*)workspace + rows_max * sld * (int64_t)sizeof(float));
   double* parts = acc64 + (P + 1);
   hipStream_t st = (hipStream_t)stream;
   const int64_t tiles = (n + kNvSPB - 1) / kNvSPB;
-  // any d <= 8 (padded coordinates stay fixed); celu and elu are the same map. Packed layout where
-  // [x | temb] fits one 16-vector with x in register 0 (PDEINV_NVP_PACK=0 forces the identity layout, A/B).
-  static const bool pack_env = [] { const char* e = getenv("PDEINV_NVP_PACK"); return !(e && e[0] == '0'); }();
-  const bool packed = pack_env && D <= 4 && a.in_dim - D <= 12;
+  // any d <= 8 (padded coordinates stay fixed); celu and elu are the same map.
+  const bool packed = map.pk != 0;
   for (int64_t tile0 = 0; tile0 < tiles; tile0 += rows_max) {
     const int64_t rows = tiles - tile0 < rows_max ? tiles - tile0 : rows_max;
     const dim3 g((unsigned)rows);
     if (packed)
       hipLaunchKernelGGL((realnvp_grad_kernel<PDEINV_ACT_CELU, true>), g, dim3(kBlock), 0, st, a, D, params, t,
-                         t_stride, x, n, ld, ls, P, tile0, slab, P + 1);
+                         t_stride, x, n, ld, ls, P, tile0, slab, sld);
     else
       hipLaunchKernelGGL((realnvp_grad_kernel<PDEINV_ACT_CELU, false>), g, dim3(kBlock), 0, st, a, D, params, t,
-                         t_stride, x, n, ld, ls, P, tile0, slab, P + 1);
+                         t_stride, x, n, ld, ls, P, tile0, slab, sld);
     int rc = check_launch("realnvp_grad_kernel");
     if (rc) return rc;
     hipLaunchKernelGGL(nvp_slab_split_kernel, dim3((unsigned)((P + 1 + 63) / 64), kNvSplits), dim3(kBlock), 0, st,
-                       slab, (int)rows, P + 1, P + 1, parts);
+                       slab, (int)rows, sld, map, P + 1, parts);
     rc = check_launch("nvp_slab_split_kernel");
     if (rc) return rc;
     hipLaunchKernelGGL(nvp_grad_reduce_kernel, dim3((unsigned)((P + 1 + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,

@@ -43,4 +43,11 @@ step isa isa
 step nvp_pmc bash tools/gnvp_pmc.sh $TAG
 nvp_time() { timeout -k 10 200 python3 tools/nvp_bench.py --steps 30 --warmup 5 --dims 2,4 | tee gpurun_out/nvp_$TAG.jsonl; }
 step nvp nvp_time
+nvp_trace() {
+  (cd /tmp && export TMPDIR=/tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/nvp_tr_$TAG -o run \
+     --output-format csv -- python3 $R/tools/nvp_bench.py --steps 20 --warmup 5 --dims 4 > $R/gpurun_out/nvp_tr_$TAG.log 2>&1) || return $?
+  cut -d, -f1-4 gpurun_out/nvp_tr_$TAG/run_kernel_stats.csv | cut -c1-150
+}
+step nvp_trace nvp_trace
+step nvp_ab bash tools/ab_nvp.sh $TAG ${NVP_VARS:-}
 cat $LOG
