@@ -340,7 +340,12 @@ __device__ __forceinline__ void nv_mlp_fwd(const float* p, const NvLane& ln, con
     nv_fwdT(p + NvM::W0X, ln, xm, z);
   }
 #pragma unroll
-  for (int u = 0; u < kNvT; ++u) h.h0[u] = nv_celu4(z[u]);
+  for (int u = 0; u < kNvT; ++u) {
+    if constexpr (PK)  // registers 2, 3: padding units (zero weights and bias), celu(0) = 0
+      h.h0[u] = f32x4{nvp_celu(z[u][0]), nvp_celu(z[u][1]), 0.f, 0.f};
+    else
+      h.h0[u] = nv_celu4(z[u]);
+  }
   nv_bcast(z, nv_vec(p + NvM::B1, ln));
   nv_fwdT<PK ? 0x3 : 0xF>(p + NvM::W1, ln, h.h0, z);
 #pragma unroll
@@ -384,7 +389,10 @@ __device__ __forceinline__ void nv_mlp_bwd(const float* p, const NvLane& ln, flo
 #pragma unroll
   for (int u = 0; u < kNvT; ++u) {
     acc.b1 += d[u];
-    d[u] = nv_dact4(e[u], h.h0[u]);
+    if constexpr (PK)  // padding units: their gradient feeds only padding entries (dropped by the flush)
+      d[u] = f32x4{e[u][0] * nvp_celu_grad_h(h.h0[u][0]), e[u][1] * nvp_celu_grad_h(h.h0[u][1]), 0.f, 0.f};
+    else
+      d[u] = nv_dact4(e[u], h.h0[u]);
   }
   if constexpr (PK) {
     NvV in;
@@ -734,13 +742,16 @@ __global__ __launch_bounds__(kBlock, PDEINV_NVW) void realnvp_grad_kernel(NvpArg
 #pragma unroll
       for (int c = 0; c < 4; ++c) temb[u][c] = (!a.ignore_time && 4 * ln.g + c == nv_tpos<PK>(0)) ? tt[u] : 0.f;
   }
+  // Packed layout: the coordinates live in register 0 only (registers 1..3 of x, gx stay exactly 0 through
+  // every coupling layer), so the per-coordinate coupling math runs over NC = 1 register.
+  constexpr int NC = PK ? 1 : 4;
   // ---- likelihood pass (layers L-1 .. 0): x <- (x + tr) e^s ----
   for (int l = a.n_layers - 1; l >= 0; --l) {
     stage_layer(l);
     const f32x4 m = nv_vec(sM + l * 16, ln), sfw = nv_vec(sW + NvM::SF, ln);
     f32x4 sf, isf;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
+    for (int c = 0; c < NC; ++c) {
       sf[c] = nv_exp(sfw[c]);
       isf[c] = __builtin_amdgcn_rcpf(sf[c]);
     }
@@ -755,7 +766,7 @@ __global__ __launch_bounds__(kBlock, PDEINV_NVW) void realnvp_grad_kernel(NvpArg
 #pragma unroll
     for (int u = 0; u < kNvT; ++u) {
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {  // padded / masked k: keep = 0, x unchanged
+      for (int c = 0; c < NC; ++c) {  // padded / masked k: keep = 0, x unchanged
         const float keep = 1.f - m[c];
         const float sk = nv_tanh((hard ? tt[u] * so[u][c] : so[u][c]) * isf[c]) * sf[c] * keep;
         x[u][c] = (x[u][c] + (hard ? tt[u] * to[u][c] : to[u][c]) * keep) * nv_exp(sk);
@@ -792,7 +803,7 @@ __global__ __launch_bounds__(kBlock, PDEINV_NVW) void realnvp_grad_kernel(NvpArg
     const f32x4 m = nv_vec(sM + l * 16, ln), sfw = nv_vec(sW + NvM::SF, ln);
     f32x4 sfv, isf;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
+    for (int c = 0; c < NC; ++c) {
       sfv[c] = nv_exp(sfw[c]);
       isf[c] = __builtin_amdgcn_rcpf(sfv[c]);
     }
@@ -807,8 +818,9 @@ __global__ __launch_bounds__(kBlock, PDEINV_NVW) void realnvp_grad_kernel(NvpArg
     nv_mlp_fwd<PK>(sW + NvM::SNET, ln, temb, xm, h, out);
 #pragma unroll
     for (int u = 0; u < kNvT; ++u) {
+      gso[u] = gto[u] = gacc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
+      for (int c = 0; c < NC; ++c) {
         const float keep = 1.f - m[c];
         const float spre = hard ? tt[u] * out[u][c] : out[u][c];
         const float sf = sfv[c];
@@ -820,7 +832,6 @@ __global__ __launch_bounds__(kBlock, PDEINV_NVW) void realnvp_grad_kernel(NvpArg
         galpha[c] += gs * (th * sf - dth * spre);              // d/d scaling_factor (sf = e^alpha)
         gso[u][c] = (hard ? tt[u] : 1.f) * gs * dth;           // d/d scale_net output
         gto[u][c] = (hard ? tt[u] : 1.f) * gx[u][c] * es[u][c] * keep;  // d/d translate_net output
-        gacc[u][c] = 0.f;
       }
     }
     nv_mlp_bwd<PK>(sW + NvM::SNET, ln, stage, temb, xm, h, gso, as, gtemb, gacc);
@@ -831,7 +842,7 @@ __global__ __launch_bounds__(kBlock, PDEINV_NVW) void realnvp_grad_kernel(NvpArg
 #pragma unroll
     for (int u = 0; u < kNvT; ++u)
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
+      for (int c = 0; c < NC; ++c) {
         const float tr = (hard ? tt[u] * out[u][c] : out[u][c]) * (1.f - m[c]);
         x[u][c] = x[u][c] * __builtin_amdgcn_rcpf(es[u][c]) - tr;
         gx[u][c] = gx[u][c] * es[u][c] + m[c] * gacc[u][c];
