@@ -168,6 +168,9 @@ constexpr int kNvpMaxRows = 8192;  // slab rows (128-sample blocks) per launch +
 #ifndef PDEINV_NVT
 #define PDEINV_NVT 2
 #endif
+#ifndef PDEINV_NVW_PK
+#define PDEINV_NVW_PK 3  // waves per SIMD of the packed-layout gradient kernel (49 KB LDS per block)
+#endif
 #ifndef PDEINV_NVW
 #define PDEINV_NVW 2
 #endif
@@ -193,13 +196,19 @@ __device__ __forceinline__ float nvp_celu(float z) { return z > 0.f ? z : nv_exp
 // and the time embedding.
 // Each matrix is also stored transposed (suffix T): the input-gradient product W d then reads it with
 // the same bank-conflict-free pattern as the forward (a transposed read of W itself is 4-way).
+// Packed layout: no W0X (the joined first layer is W0T). The layer image carries the layer's mask (by
+// position, padded with 1) after sf. The time embedding's matrices use the same LDS array before the first
+// and after the last coupling layer (TEMB floats at its start).
+template <bool PK>
 struct NvM {
   static constexpr int MAT = 16 * kNvWS;
-  static constexpr int W0T = 0, W0X = MAT, W1 = 2 * MAT, W2 = 3 * MAT, W3 = 4 * MAT, TR = 5 * MAT,  // W^T at +TR
-                       B0 = 10 * MAT, B1 = B0 + 16, B2 = B1 + 16, B3 = B2 + 16, NET = B3 + 16;
-  static constexpr int SF = 0, SNET = 16, TNET = 16 + NET, LAYER = 16 + 2 * NET;
+  static constexpr int W0T = 0, W0X = PK ? 0 : MAT, W1 = W0X + MAT, W2 = W1 + MAT, W3 = W2 + MAT,
+                       TR = W3 + MAT,  // W^T at +TR
+                       B0 = 2 * TR, B1 = B0 + 16, B2 = B1 + 16, B3 = B2 + 16, NET = B3 + 16;
+  static constexpr int SF = 0, MASK = 16, SNET = 32, TNET = 32 + NET, LAYER = 32 + 2 * NET;
   static constexpr int E_W1 = 0, E_B1 = MAT, E_W2 = MAT + 16, E_B2 = 2 * MAT + 16, E_W2T = 2 * MAT + 32,
                        TEMB = 3 * MAT + 32;
+  static_assert(TEMB <= LAYER, "time embedding inside the layer image");
 };
 // Per-wave partial-gradient block of one coupling layer, compact (only the entries a parameter maps to):
 // [t-net | s-net | sf (16, by position)]. Per net, packed layout: W0 [16 input positions][8 hidden units],
@@ -216,12 +225,16 @@ struct NvC {
                        B0 = W3 + (PK ? 64 : 128), B1 = B0 + 16, B2 = B1 + 16, B3 = B2 + 16, NET = B3 + 16;
   static constexpr int TNET = 0, SNET = NET, SF = 2 * NET, LAYER = 2 * NET + 16;  // 1296 / 1552 floats
 };
-constexpr int kNvStageF = kNvT * 2 * 16 * kNvSS;  // per-wave sample stage (floats)
-static_assert(NvC<false>::NET <= kNvStageF && NvC<true>::NET <= kNvStageF, "t-net block inside the stage");
+constexpr int kNvStageF = 2 * 16 * kNvSS;  // per-wave sample stage (floats): one tile's two operands
+// Per-wave scratch: [t-net block / sample stage (kNvTR floats) | s-net block | sf]
+template <bool PK>
+struct NvScr {
+  static constexpr int TR = NvC<PK>::NET > kNvStageF ? NvC<PK>::NET : kNvStageF;
+  static constexpr int SIZE = TR + NvC<PK>::NET + 16;
+};
 // LDS offset (in the wave's scratch) of compact-block entry o
 template <bool PK>
-__device__ __forceinline__ int nv_flush_lds(int o) { return o < NvC<PK>::NET ? o : o - NvC<PK>::NET + kNvStageF; }
-constexpr int kNvFlush = kNvStageF + NvC<false>::NET + 16;  // per-wave scratch (floats), the larger layout
+__device__ __forceinline__ int nv_flush_lds(int o) { return o < NvC<PK>::NET ? o : o - NvC<PK>::NET + NvScr<PK>::TR; }
 
 struct NvLane {
   int g, s;    // component group, sample within the tile
@@ -287,24 +300,23 @@ __device__ __forceinline__ void nv_bcast(NvV& c, const f32x4& b) {
 }
 
 // acc += sum over the wave's samples of a_s d_s^T (rows = a components): per-wave LDS stage
-// [kNvT][2][16 samples][kNvSS] (swizzled chunks, nv_swz), one 16-byte write per lane and tile, one read per
-// operand and k-step.
+// [2][16 samples][kNvSS] (swizzled chunks, nv_swz) holding one tile at a time (a wave's LDS instructions run
+// in order, so the next tile's writes follow this tile's reads): one 16-byte write per lane and operand, one
+// read per operand and k-step.
 __device__ __forceinline__ f32x4 nv_wgrad(float* stage, const NvLane& ln, const NvV& a, const NvV& d, f32x4 acc) {
-  nv_wave_sync();  // the previous reads of the stage are done
 #pragma unroll
   for (int u = 0; u < kNvT; ++u) {
-    *reinterpret_cast<f32x4*>(stage + (2 * u) * 16 * kNvSS + ln.sw) = a[u];
-    *reinterpret_cast<f32x4*>(stage + (2 * u + 1) * 16 * kNvSS + ln.sw) = d[u];
-  }
-  nv_wave_sync();
-#pragma unroll
-  for (int u = 0; u < kNvT; ++u)
+    nv_wave_sync();  // the previous reads of the stage are issued
+    *reinterpret_cast<f32x4*>(stage + ln.sw) = a[u];
+    *reinterpret_cast<f32x4*>(stage + 16 * kNvSS + ln.sw) = d[u];
+    nv_wave_sync();
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       // row 4t + g: nv_swz(4t + g) = nv_swz(g) ^ 2 (t & 1), i.e. component s ^ 8 on odd t
-      const int r = (2 * u) * 16 * kNvSS + 4 * t * kNvSS + (ln.sr ^ (t & 1 ? 8 : 0));
+      const int r = 4 * t * kNvSS + (ln.sr ^ (t & 1 ? 8 : 0));
       acc = __builtin_amdgcn_mfma_f32_16x16x4f32(stage[r], stage[16 * kNvSS + r], acc, 0, 0, 0);
     }
+  }
   return acc;
 }
 
@@ -330,14 +342,14 @@ template <bool PK>
 __device__ __forceinline__ void nv_mlp_fwd(const float* p, const NvLane& ln, const NvV& temb, const NvV& xm,
                                            NvAct& h, NvV& out) {
   NvV z;
-  nv_bcast(z, nv_vec(p + NvM::B0, ln));
+  nv_bcast(z, nv_vec(p + NvM<PK>::B0, ln));
   if constexpr (PK) {
     NvV in;
     nv_join(xm, temb, in);
-    nv_fwdT(p + NvM::W0T, ln, in, z);
+    nv_fwdT(p + NvM<PK>::W0T, ln, in, z);
   } else {
-    nv_fwdT(p + NvM::W0T, ln, temb, z);
-    nv_fwdT(p + NvM::W0X, ln, xm, z);
+    nv_fwdT(p + NvM<PK>::W0T, ln, temb, z);
+    nv_fwdT(p + NvM<PK>::W0X, ln, xm, z);
   }
 #pragma unroll
   for (int u = 0; u < kNvT; ++u) {
@@ -346,16 +358,16 @@ __device__ __forceinline__ void nv_mlp_fwd(const float* p, const NvLane& ln, con
     else
       h.h0[u] = nv_celu4(z[u]);
   }
-  nv_bcast(z, nv_vec(p + NvM::B1, ln));
-  nv_fwdT<PK ? 0x3 : 0xF>(p + NvM::W1, ln, h.h0, z);
+  nv_bcast(z, nv_vec(p + NvM<PK>::B1, ln));
+  nv_fwdT<PK ? 0x3 : 0xF>(p + NvM<PK>::W1, ln, h.h0, z);
 #pragma unroll
   for (int u = 0; u < kNvT; ++u) h.h1[u] = nv_celu4(z[u]);
-  nv_bcast(z, nv_vec(p + NvM::B2, ln));
-  nv_fwdT(p + NvM::W2, ln, h.h1, z);
+  nv_bcast(z, nv_vec(p + NvM<PK>::B2, ln));
+  nv_fwdT(p + NvM<PK>::W2, ln, h.h1, z);
 #pragma unroll
   for (int u = 0; u < kNvT; ++u) h.h2[u] = nv_celu4(z[u]);
-  nv_bcast(out, nv_vec(p + NvM::B3, ln));
-  nv_fwdT(p + NvM::W3, ln, h.h2, out);
+  nv_bcast(out, nv_vec(p + NvM<PK>::B3, ln));
+  nv_fwdT(p + NvM<PK>::W3, ln, h.h2, out);
 }
 
 // BasicMLP backward from d(out): parameter gradients into acc, input gradients added to gtemb
@@ -369,7 +381,7 @@ __device__ __forceinline__ void nv_mlp_bwd(const float* p, const NvLane& ln, flo
   NvV d, e;
   acc.w3 = nv_wgrad(stage, ln, h.h2, dout, acc.w3);
   nv_bcast(e, z4);
-  nv_fwdT<PK ? 0x1 : 0xF>(p + NvM::TR + NvM::W3, ln, dout, e);
+  nv_fwdT<PK ? 0x1 : 0xF>(p + NvM<PK>::TR + NvM<PK>::W3, ln, dout, e);
 #pragma unroll
   for (int u = 0; u < kNvT; ++u) {
     acc.b3 += dout[u];
@@ -377,7 +389,7 @@ __device__ __forceinline__ void nv_mlp_bwd(const float* p, const NvLane& ln, flo
   }
   acc.w2 = nv_wgrad(stage, ln, h.h1, d, acc.w2);
   nv_bcast(e, z4);
-  nv_fwdT(p + NvM::TR + NvM::W2, ln, d, e);
+  nv_fwdT(p + NvM<PK>::TR + NvM<PK>::W2, ln, d, e);
 #pragma unroll
   for (int u = 0; u < kNvT; ++u) {
     acc.b2 += d[u];
@@ -385,7 +397,7 @@ __device__ __forceinline__ void nv_mlp_bwd(const float* p, const NvLane& ln, flo
   }
   acc.w1 = nv_wgrad(stage, ln, h.h0, d, acc.w1);
   nv_bcast(e, z4);
-  nv_fwdT(p + NvM::TR + NvM::W1, ln, d, e);
+  nv_fwdT(p + NvM<PK>::TR + NvM<PK>::W1, ln, d, e);
 #pragma unroll
   for (int u = 0; u < kNvT; ++u) {
     acc.b1 += d[u];
@@ -401,7 +413,7 @@ __device__ __forceinline__ void nv_mlp_bwd(const float* p, const NvLane& ln, flo
 #pragma unroll
     for (int u = 0; u < kNvT; ++u) acc.b0 += d[u];
     nv_bcast(e, z4);
-    nv_fwdT<0x3>(p + NvM::TR + NvM::W0T, ln, d, e);
+    nv_fwdT<0x3>(p + NvM<PK>::TR + NvM<PK>::W0T, ln, d, e);
 #pragma unroll
     for (int u = 0; u < kNvT; ++u) {
       gx[u][0] += e[u][0];
@@ -413,8 +425,8 @@ __device__ __forceinline__ void nv_mlp_bwd(const float* p, const NvLane& ln, flo
     acc.w0x = nv_wgrad(stage, ln, xm, d, acc.w0x);
 #pragma unroll
     for (int u = 0; u < kNvT; ++u) acc.b0 += d[u];
-    nv_fwdT(p + NvM::TR + NvM::W0T, ln, d, gtemb);
-    nv_fwdT(p + NvM::TR + NvM::W0X, ln, d, gx);
+    nv_fwdT(p + NvM<PK>::TR + NvM<PK>::W0T, ln, d, gtemb);
+    nv_fwdT(p + NvM<PK>::TR + NvM<PK>::W0X, ln, d, gx);
   }
 }
 
@@ -536,52 +548,50 @@ __host__ __device__ __forceinline__ int64_t nv_slab_ld(const NvSlabMap& m) {
 template <bool PK>
 __device__ __forceinline__ uint32_t nv_layer_dst(int k, int d, int n_t) {
   const int n_in = d + n_t, mlp_n = n_in * 8 + 8 + 8 * 16 + 16 + 16 * 16 + 16 + 16 * d + d;
-  if (k < d) return (uint32_t)(NvM::SF + nv_xpos<PK>(k)) | 0xFFFF0000u;
+  if (k < d) return (uint32_t)(NvM<PK>::SF + nv_xpos<PK>(k)) | 0xFFFF0000u;
   k -= d;
   const int net = k >= mlp_n ? 1 : 0;
   int f = k - net * mlp_n;
-  const int base = net ? NvM::TNET : NvM::SNET;
+  const int base = net ? NvM<PK>::TNET : NvM<PK>::SNET;
   auto mat = [&](int M, int pr, int pc) {
-    return (uint32_t)(base + M + pr * kNvWS + pc) | ((uint32_t)(base + NvM::TR + M + pc * kNvWS + pr) << 16);
+    return (uint32_t)(base + M + pr * kNvWS + pc) | ((uint32_t)(base + NvM<PK>::TR + M + pc * kNvWS + pr) << 16);
   };
   auto vec = [&](int B, int p) { return (uint32_t)(base + B + p) | 0xFFFF0000u; };
   if (f < n_in * 8) {
     const int r = f / 8, o = f - r * 8;
-    if (PK) return mat(NvM::W0T, r < d ? nv_xpos<PK>(r) : nv_tpos<PK>(r - d), nv_hpos<PK>(o));
-    return r < d ? mat(NvM::W0X, r, o) : mat(NvM::W0T, r - d, o);
+    if (PK) return mat(NvM<PK>::W0T, r < d ? nv_xpos<PK>(r) : nv_tpos<PK>(r - d), nv_hpos<PK>(o));
+    return r < d ? mat(NvM<PK>::W0X, r, o) : mat(NvM<PK>::W0T, r - d, o);
   }
   f -= n_in * 8;
-  if (f < 8) return vec(NvM::B0, nv_hpos<PK>(f));
+  if (f < 8) return vec(NvM<PK>::B0, nv_hpos<PK>(f));
   f -= 8;
-  if (f < 128) return mat(NvM::W1, nv_hpos<PK>(f / 16), f % 16);
+  if (f < 128) return mat(NvM<PK>::W1, nv_hpos<PK>(f / 16), f % 16);
   f -= 128;
-  if (f < 16) return vec(NvM::B1, f);
+  if (f < 16) return vec(NvM<PK>::B1, f);
   f -= 16;
-  if (f < 256) return mat(NvM::W2, f / 16, f % 16);
+  if (f < 256) return mat(NvM<PK>::W2, f / 16, f % 16);
   f -= 256;
-  if (f < 16) return vec(NvM::B2, f);
+  if (f < 16) return vec(NvM<PK>::B2, f);
   f -= 16;
-  if (f < 16 * d) return mat(NvM::W3, f / d, nv_xpos<PK>(f % d));
+  if (f < 16 * d) return mat(NvM<PK>::W3, f / d, nv_xpos<PK>(f % d));
   f -= 16 * d;
-  return vec(NvM::B3, nv_xpos<PK>(f));
+  return vec(NvM<PK>::B3, nv_xpos<PK>(f));
 }
 
 template <int ACT, bool PK>
-__global__ __launch_bounds__(kBlock, PDEINV_NVW) void realnvp_grad_kernel(NvpArgs a, int d, const float* __restrict__ params,
+__global__ __launch_bounds__(kBlock, PK ? PDEINV_NVW_PK : PDEINV_NVW) void realnvp_grad_kernel(NvpArgs a, int d, const float* __restrict__ params,
                                                                  const float* __restrict__ tv, int64_t t_stride,
                                                                  const float* __restrict__ xv, int64_t n, int64_t ld,
                                                                  int64_t layer_stride, int64_t n_params,
                                                                  int64_t tile0, float* __restrict__ slab,
                                                                  int64_t slab_ld) {
   static_assert(ACT == PDEINV_ACT_CELU, "celu / elu flow");
-  __shared__ float sW[NvM::LAYER];                   // current coupling layer (padded)
-  __shared__ float sT[NvM::TEMB];                    // time embedding (padded)
-  __shared__ float sF[48];                           // sinusoid table: frequency, sin weight, cos weight
-  __shared__ float sM[PDEINV_REALNVP_MAX_LAYERS * 16];  // masks, padded with 1
-  __shared__ float sB[16 + 16 * 16];                 // base mean, inverse covariance (0-padded)
-  // per-wave wgrad stages during the tile math, per-wave flush blocks after it (a barrier between)
-  constexpr int kScr = kNvFlush;
-  __shared__ float sScr[kWavesPerBlock][kScr];
+  __shared__ float sW[NvM<PK>::LAYER];  // current coupling layer (padded); the time embedding before / after
+  float* const sT = sW;
+  __shared__ float sF[48];              // sinusoid table: frequency, sin weight, cos weight
+  __shared__ float sB[16 + 16 * 16];    // base mean, inverse covariance (0-padded)
+  // per-wave sample stages and flush blocks (NvScr)
+  __shared__ float sScr[kWavesPerBlock][NvScr<PK>::SIZE];
   __shared__ uint32_t sDst[kNvRaw];                  // raw layer parameter -> LDS position(s), nv_layer_dst
   using C = NvC<PK>;
   const int E = a.E;
@@ -622,13 +632,13 @@ __global__ __launch_bounds__(kBlock, PDEINV_NVW) void realnvp_grad_kernel(NvpArg
     }
   };
   auto idn = [](int len) { return [len](int p) { return p < len ? p : -1; }; };
-  if (E > 0) {
+  auto put_temb = [&] {  // the time embedding's matrices into sT (= the start of sW)
     auto tmap = [E](int p) { return nv_tinv<PK>(p, E); };
-    put_mat(sT + NvM::E_W1, nullptr, params, E, idn(E), idn(E));
-    put_vec(sT + NvM::E_B1, params + E * E, idn(E));
-    put_mat(sT + NvM::E_W2, sT + NvM::E_W2T, params + E * E + E, E, idn(E), tmap);  // temb at its positions
-    put_vec(sT + NvM::E_B2, params + 2 * E * E + E, tmap);
-  }
+    put_mat(sT + NvM<PK>::E_W1, nullptr, params, E, idn(E), idn(E));
+    put_vec(sT + NvM<PK>::E_B1, params + E * E, idn(E));
+    put_mat(sT + NvM<PK>::E_W2, sT + NvM<PK>::E_W2T, params + E * E + E, E, idn(E), tmap);  // temb at its positions
+    put_vec(sT + NvM<PK>::E_B2, params + 2 * E * E + E, tmap);
+  };
   if (tid < 16) {
     const int half = E / 2;
     const bool on = E > 0 && tid < E;
@@ -639,11 +649,7 @@ __global__ __launch_bounds__(kBlock, PDEINV_NVW) void realnvp_grad_kernel(NvpArg
     sF[32 + tid] = on && !is_sin ? 1.f : 0.f;
   }
   for (int k = tid; k < layer_stride; k += kBlock) sDst[k] = nv_layer_dst<PK>(k, d, n_t);
-  for (int q = tid; q < NvM::LAYER; q += kBlock) sW[q] = 0.f;  // padding: never written again
-  for (int q = tid; q < a.n_layers * 16; q += kBlock) {
-    const int l = q / 16, k = nv_xinv<PK>(q % 16, d);
-    sM[q] = k >= 0 ? a.masks[l * d + k] : 1.f;
-  }
+  for (int q = tid; q < NvM<PK>::LAYER; q += kBlock) sW[q] = 0.f;  // padding: never written again
   for (int q = tid; q < 16 + 256; q += kBlock) {  // mean at the x positions; inv_cov rows by position, columns by coordinate
     float v = 0.f;
     if (q < 16) {
@@ -668,8 +674,12 @@ __global__ __launch_bounds__(kBlock, PDEINV_NVW) void realnvp_grad_kernel(NvpArg
     }
   };
   int staged = 0;  // layers staged so far
-  auto stage_layer = [&](int) {
+  auto stage_layer = [&](int l) {
     __syncthreads();  // every wave is done with the previous layer
+    if (tid < 16) {  // the layer's mask by position, padded with 1
+      const int k = nv_xinv<PK>(tid, d);
+      sW[NvM<PK>::MASK + tid] = k >= 0 ? a.masks[l * d + k] : 1.f;
+    }
 #pragma unroll
     for (int k = 0; k < kNvPre; ++k) {
       const int q = tid + k * kBlock;
@@ -701,6 +711,8 @@ __global__ __launch_bounds__(kBlock, PDEINV_NVW) void realnvp_grad_kernel(NvpArg
   NvV x, gx, temb, gtemb;
   float tt[kNvT], w[kNvT], ldj[kNvT];
   const int64_t base = (tile0 + blockIdx.x) * kNvSPB + wave * 16 * kNvT;
+  __syncthreads();  // sW zeroed
+  if (E > 0) put_temb();
   __syncthreads();
 #pragma unroll
   for (int u = 0; u < kNvT; ++u) {
@@ -730,12 +742,14 @@ __global__ __launch_bounds__(kBlock, PDEINV_NVW) void realnvp_grad_kernel(NvpArg
   if (E > 0) {
     NvV se, he;
     sinusoid(se);
-    nv_bcast(he, nv_vec(sT + NvM::E_B1, ln));
-    nv_fwdT(sT + NvM::E_W1, ln, se, he);
+    nv_bcast(he, nv_vec(sT + NvM<PK>::E_B1, ln));
+    nv_fwdT(sT + NvM<PK>::E_W1, ln, se, he);
 #pragma unroll
     for (int u = 0; u < kNvT; ++u) he[u] = nv_celu4(he[u]);
-    nv_bcast(temb, nv_vec(sT + NvM::E_B2, ln));
-    nv_fwdT(sT + NvM::E_W2, ln, he, temb);
+    nv_bcast(temb, nv_vec(sT + NvM<PK>::E_B2, ln));
+    nv_fwdT(sT + NvM<PK>::E_W2, ln, he, temb);
+    __syncthreads();  // every wave has read the time embedding: back to the zero-padded layer image
+    for (int q = tid; q < NvM<PK>::TEMB; q += kBlock) sW[q] = 0.f;
   } else {
 #pragma unroll
     for (int u = 0; u < kNvT; ++u)
@@ -748,7 +762,7 @@ __global__ __launch_bounds__(kBlock, PDEINV_NVW) void realnvp_grad_kernel(NvpArg
   // ---- likelihood pass (layers L-1 .. 0): x <- (x + tr) e^s ----
   for (int l = a.n_layers - 1; l >= 0; --l) {
     stage_layer(l);
-    const f32x4 m = nv_vec(sM + l * 16, ln), sfw = nv_vec(sW + NvM::SF, ln);
+    const f32x4 m = nv_vec(sW + NvM<PK>::MASK, ln), sfw = nv_vec(sW + NvM<PK>::SF, ln);
     f32x4 sf, isf;
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
@@ -760,8 +774,8 @@ __global__ __launch_bounds__(kBlock, PDEINV_NVW) void realnvp_grad_kernel(NvpArg
     for (int u = 0; u < kNvT; ++u) xm[u] = x[u] * m;
     {
       NvAct h;
-      nv_mlp_fwd<PK>(sW + NvM::SNET, ln, temb, xm, h, so);
-      nv_mlp_fwd<PK>(sW + NvM::TNET, ln, temb, xm, h, to);
+      nv_mlp_fwd<PK>(sW + NvM<PK>::SNET, ln, temb, xm, h, so);
+      nv_mlp_fwd<PK>(sW + NvM<PK>::TNET, ln, temb, xm, h, to);
     }
 #pragma unroll
     for (int u = 0; u < kNvT; ++u) {
@@ -800,7 +814,7 @@ __global__ __launch_bounds__(kBlock, PDEINV_NVW) void realnvp_grad_kernel(NvpArg
   // ---- backward through layers 0 .. L-1, rebuilding each layer's input ----
   for (int l = 0; l < a.n_layers; ++l) {
     stage_layer(l);
-    const f32x4 m = nv_vec(sM + l * 16, ln), sfw = nv_vec(sW + NvM::SF, ln);
+    const f32x4 m = nv_vec(sW + NvM<PK>::MASK, ln), sfw = nv_vec(sW + NvM<PK>::SF, ln);
     f32x4 sfv, isf;
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
@@ -815,7 +829,7 @@ __global__ __launch_bounds__(kBlock, PDEINV_NVW) void realnvp_grad_kernel(NvpArg
     NvAct h;
 #pragma unroll
     for (int u = 0; u < kNvT; ++u) xm[u] = x[u] * m;
-    nv_mlp_fwd<PK>(sW + NvM::SNET, ln, temb, xm, h, out);
+    nv_mlp_fwd<PK>(sW + NvM<PK>::SNET, ln, temb, xm, h, out);
 #pragma unroll
     for (int u = 0; u < kNvT; ++u) {
       gso[u] = gto[u] = gacc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -834,11 +848,11 @@ __global__ __launch_bounds__(kBlock, PDEINV_NVW) void realnvp_grad_kernel(NvpArg
         gto[u][c] = (hard ? tt[u] : 1.f) * gx[u][c] * es[u][c] * keep;  // d/d translate_net output
       }
     }
-    nv_mlp_bwd<PK>(sW + NvM::SNET, ln, stage, temb, xm, h, gso, as, gtemb, gacc);
-    nv_put_vec(red + kNvStageF + NvC<PK>::NET, ln, galpha);  // behind the stage (nv_flush_lds)
-    nv_put_net<PK>(red + kNvStageF, ln, as);
-    nv_mlp_fwd<PK>(sW + NvM::TNET, ln, temb, xm, h, out);
-    nv_mlp_bwd<PK>(sW + NvM::TNET, ln, stage, temb, xm, h, gto, at, gtemb, gacc);
+    nv_mlp_bwd<PK>(sW + NvM<PK>::SNET, ln, stage, temb, xm, h, gso, as, gtemb, gacc);
+    nv_put_vec(red + NvScr<PK>::TR + NvC<PK>::NET, ln, galpha);  // behind the stage (nv_flush_lds)
+    nv_put_net<PK>(red + NvScr<PK>::TR, ln, as);
+    nv_mlp_fwd<PK>(sW + NvM<PK>::TNET, ln, temb, xm, h, out);
+    nv_mlp_bwd<PK>(sW + NvM<PK>::TNET, ln, stage, temb, xm, h, gto, at, gtemb, gacc);
 #pragma unroll
     for (int u = 0; u < kNvT; ++u)
 #pragma unroll
@@ -861,19 +875,23 @@ __global__ __launch_bounds__(kBlock, PDEINV_NVW) void realnvp_grad_kernel(NvpArg
       *reinterpret_cast<f32x4*>(row + (int64_t)l * C::LAYER + 4 * q) = v;
     }
   }
-  __syncthreads();  // the last layer's sums are read: the stages are free again
+  __syncthreads();  // the last layer's sums are read: the stages and the layer image are free again
+  if (E > 0) {
+    put_temb();
+    __syncthreads();
+  }
   // ---- time-embedding backward and the loss column ----
   if (E > 0) {
     f32x4 w1 = {0.f, 0.f, 0.f, 0.f}, w2 = w1, b1 = w1, b2 = w1;
     NvV se, he, gz;
     sinusoid(se);
-    nv_bcast(he, nv_vec(sT + NvM::E_B1, ln));
-    nv_fwdT(sT + NvM::E_W1, ln, se, he);
+    nv_bcast(he, nv_vec(sT + NvM<PK>::E_B1, ln));
+    nv_fwdT(sT + NvM<PK>::E_W1, ln, se, he);
 #pragma unroll
     for (int u = 0; u < kNvT; ++u) he[u] = nv_celu4(he[u]);
     w2 = nv_wgrad(stage, ln, he, gtemb, w2);
     nv_bcast(gz, f32x4{0.f, 0.f, 0.f, 0.f});
-    nv_fwdT(sT + NvM::E_W2T, ln, gtemb, gz);
+    nv_fwdT(sT + NvM<PK>::E_W2T, ln, gtemb, gz);
 #pragma unroll
     for (int u = 0; u < kNvT; ++u) {
       b2 += gtemb[u];
