@@ -185,12 +185,14 @@ __device__ __forceinline__ int nv_swz(int r) { return (r >> 1) & 3; }
 constexpr int kNvRaw = 8 + 2 * (24 * 8 + 8 + 128 + 16 + 256 + 16 + 16 * 8 + 8);  // one layer's params, d <= 8
 constexpr int kNvPre = (kNvRaw + kBlock - 1) / kBlock;
 
-// Activation derivative from the post-activation value h (celu / elu: e^z = h + 1).
-__device__ __forceinline__ float nvp_celu_grad_h(float h) { return h > 0.f ? 1.f : h + 1.f; }
+// Activation derivative from the post-activation value h (celu / elu: e^z = h + 1): min(h + 1, 1).
+__device__ __forceinline__ float nvp_celu_grad_h(float h) { return fminf(h + 1.f, 1.f); }
 // hardware exp2 / rcp (v_exp_f32, v_rcp_f32: ~1 ulp; the grad kernel's transcendentals)
 __device__ __forceinline__ float nv_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
 __device__ __forceinline__ float nv_tanh(float x) { return 1.f - 2.f * __builtin_amdgcn_rcpf(nv_exp(2.f * x) + 1.f); }
-__device__ __forceinline__ float nvp_celu(float z) { return z > 0.f ? z : nv_exp(z) - 1.f; }
+// celu(z) = median(z, e^z - 1, 0): e^z - 1 >= z everywhere, so the median is z for z > 0 and e^z - 1 for
+// z <= 0 (one v_med3 instead of a compare and a select).
+__device__ __forceinline__ float nvp_celu(float z) { return __builtin_amdgcn_fmed3f(z, nv_exp(z) - 1.f, 0.f); }
 
 // Padded LDS layout of one BasicMLP (weights [in][out] with row stride kNvWS), one coupling layer
 // and the time embedding.
@@ -447,6 +449,34 @@ __device__ __forceinline__ f32x4 nv_sum16(f32x4 v) {
   return v;
 }
 
+// The four bias vectors of a net summed over the 16 samples of each component group at once: a reduce-scatter
+// butterfly over the 16 values (b0..b3, registers 0..3) — row mirror, half-row mirror, quad xor 2, quad xor 1,
+// each stage keeping the half of the values selected by one lane bit — leaves lane s with the total of value s
+// (45 VALU instead of 4 x nv_sum16). Written to r[16 (s / 4) + 4 g + s % 4] (b_{s/4} by position).
+__device__ __forceinline__ void nv_put_bias4(float* r, const NvLane& ln, const f32x4& b0, const f32x4& b1,
+                                             const f32x4& b2, const f32x4& b3) {
+  float v[16];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    v[c] = b0[c];
+    v[4 + c] = b1[c];
+    v[8 + c] = b2[c];
+    v[12 + c] = b3[c];
+  }
+  auto stage = [&](auto dpp, int half, bool hi) {
+#pragma unroll
+    for (int i = 0; i < half; ++i) {
+      const float send = hi ? v[i] : v[i + half], keep = hi ? v[i + half] : v[i];
+      v[i] = keep + dpp(send);
+    }
+  };
+  stage([](float x) { return nv_dpp<0x140>(x); }, 8, (ln.s & 8) != 0);  // partner 15 - s (row mirror)
+  stage([](float x) { return nv_dpp<0x141>(x); }, 4, (ln.s & 4) != 0);  // partner s ^ 7 (half-row mirror)
+  stage([](float x) { return nv_dpp<0x4E>(x); }, 2, (ln.s & 2) != 0);   // s ^ 2
+  stage([](float x) { return nv_dpp<0xB1>(x); }, 1, (ln.s & 1) != 0);   // s ^ 1
+  r[(ln.s >> 2) * 16 + 4 * ln.g + (ln.s & 3)] = v[0];
+}
+
 // A wave's partials into its LDS flush block: matrices in the accumulator layout (row 4g + i,
 // column s), vectors summed over samples.
 __device__ __forceinline__ void nv_put_mat(float* r, const NvLane& ln, const f32x4& m) {
@@ -484,10 +514,8 @@ __device__ __forceinline__ void nv_put_net(float* r, const NvLane& ln, const NvN
     nv_put_cmat<4>(r + C::W3, ln, a.w3, all, [](int p) { return (p & 3) == 0 ? p >> 2 : -1; });
   else
     nv_put_cmat<8>(r + C::W3, ln, a.w3, all, [](int p) { return p < 8 ? p : -1; });
-  nv_put_vec(r + C::B0, ln, a.b0);
-  nv_put_vec(r + C::B1, ln, a.b1);
-  nv_put_vec(r + C::B2, ln, a.b2);
-  nv_put_vec(r + C::B3, ln, a.b3);
+  static_assert(C::B1 == C::B0 + 16 && C::B2 == C::B1 + 16 && C::B3 == C::B2 + 16, "bias vectors contiguous");
+  nv_put_bias4(r + C::B0, ln, a.b0, a.b1, a.b2, a.b3);
 }
 
 // Flat (reference-order) parameter f of one BasicMLP -> its index in the compact net block (NvC).
@@ -723,7 +751,7 @@ __global__ __launch_bounds__(kBlock, PK ? PDEINV_NVW_PK : PDEINV_NVW) void realn
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const int k = nv_xinv<PK>(4 * ln.g + c, d);
-      x[u][c] = (active && k >= 0) ? xv[i * ld + k] : 0.f;
+      x[u][c] = (active && k >= 0 && (!PK || c == 0)) ? xv[i * ld + k] : 0.f;  // packed: registers 1..3 are 0
       gtemb[u][c] = 0.f;
     }
     ldj[u] = 0.f;
@@ -771,7 +799,7 @@ __global__ __launch_bounds__(kBlock, PK ? PDEINV_NVW_PK : PDEINV_NVW) void realn
     }
     NvV xm, so, to;
 #pragma unroll
-    for (int u = 0; u < kNvT; ++u) xm[u] = x[u] * m;
+    for (int u = 0; u < kNvT; ++u) xm[u] = PK ? f32x4{x[u][0] * m[0], 0.f, 0.f, 0.f} : x[u] * m;
     {
       NvAct h;
       nv_mlp_fwd<PK>(sW + NvM<PK>::SNET, ln, temb, xm, h, so);
@@ -804,7 +832,7 @@ __global__ __launch_bounds__(kBlock, PK ? PDEINV_NVW_PK : PDEINV_NVW) void realn
       for (int q = 0; q < d; ++q)
         acc = fmaf(sB[16 + r * 16 + q], stage[ln.s * kNvSS + (nv_xpos<PK>(q) ^ (4 * nv_swz(ln.s)))], acc);
       quad = fmaf(diff[c], acc, quad);
-      gx[u][c] = -w[u] * acc;
+      gx[u][c] = PK && c > 0 ? 0.f : -w[u] * acc;
     }
     float part = ldj[u] - 0.5f * quad;  // the four groups' parts sum to log p + 0.5 log_det
     part += __shfl_xor(part, 16, 64);
@@ -828,7 +856,7 @@ __global__ __launch_bounds__(kBlock, PK ? PDEINV_NVW_PK : PDEINV_NVW) void realn
     NvV xm, out, s, es, gso, gto, gacc;
     NvAct h;
 #pragma unroll
-    for (int u = 0; u < kNvT; ++u) xm[u] = x[u] * m;
+    for (int u = 0; u < kNvT; ++u) xm[u] = PK ? f32x4{x[u][0] * m[0], 0.f, 0.f, 0.f} : x[u] * m;
     nv_mlp_fwd<PK>(sW + NvM<PK>::SNET, ln, temb, xm, h, out);
 #pragma unroll
     for (int u = 0; u < kNvT; ++u) {
