@@ -121,6 +121,24 @@ RAMP_S = 0.3
 KERN_STATS = {}  # per-launch spread of the dominant kernel over the timed steps (filled by timed())
 
 
+def run_ramp(ramp, dev, seconds=RAMP_S, sync=None):
+    """Repeat ramp() in rounds of 8 for about `seconds` of wall clock. Every rank runs the SAME number of
+    rounds: the step a config ramps with may hold collectives (C3 / C4 / C5: the residual's all-reduce), and
+    a rank that stopped one round earlier than its peer on its own clock would leave that peer's collective
+    unmatched (a hang seen in the world-2 GPU tests). So after each round the ranks agree on whether any of
+    them still wants to ramp. Returns the number of rounds."""
+    sync = sync or torch.cuda.synchronize
+    t_end = time.perf_counter() + seconds
+    rounds = 0
+    while True:
+        for _ in range(8):
+            ramp()
+        sync()
+        rounds += 1
+        if dist.allreduce_max_scalar(1.0 if time.perf_counter() < t_end else 0.0, device=dev) == 0.0:
+            return rounds
+
+
 def timed(step, K, W, dev, ramp=None):
     """Clock ramp, W untimed warmup steps, then K steps between barrier+synchronize; max over ranks.
     step(record) records record[0]/record[1] around the dominant kernel's launch.
@@ -130,12 +148,7 @@ def timed(step, K, W, dev, ramp=None):
     ramp() (default: step(None)) must not feed any result of the run.
     Returns (ms per step, mean dominant-launch ms); the launch spread (min over ranks of the per-rank min,
     max over ranks of the median and of the max) goes to KERN_STATS for roofline.kernel_ms_*."""
-    ramp = ramp or (lambda: step(None))
-    t_end = time.perf_counter() + RAMP_S
-    while time.perf_counter() < t_end:
-        for _ in range(8):
-            ramp()
-        torch.cuda.synchronize()
+    run_ramp(ramp or (lambda: step(None)), dev)
     for _ in range(W):
         step(None)
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
