@@ -148,18 +148,22 @@ __global__ __launch_bounds__(kBlock) void realnvp_logdensity_kernel(NvpArgs a, c
 // that same layout — k-slot (j, g) stands for input component 4g + j, and the A operand (the
 // weights, read from LDS) is permuted to match — so layers chain with no data movement at all.
 // The input-gradient product W d uses the transposed read of the same LDS matrix. Weight
-// gradients sum_s a_s d_s^T take the samples as the reduction dimension: the two tiles go
-// through a per-wave LDS stage (one 16-byte write per lane, one read per k-step) into four MFMAs
+// gradients sum_s a_s d_s^T take the samples as the reduction dimension: each tile goes through a
+// per-wave swizzled LDS stage (one 16-byte write per lane, one read per k-step) into four MFMAs
 // whose accumulators (ΔW in the same layout, rows = inputs) stay in registers over the wave's
-// tiles. Bias and scaling-factor gradients are per-lane sums, wave-reduced at the flush.
+// tiles. Bias and scaling-factor gradients are per-lane sums, summed over the samples at the flush
+// (a reduce-scatter butterfly for a net's four bias vectors).
 // All widths are padded to 16 (the net's first layer: 8 outputs; x: d <= 8 coordinates; time:
 // n_t <= 16 features) with zero weights, so padded components stay exactly 0.
 // * The backward pass walks the coupling layers in the opposite order of the likelihood pass and
 //   rebuilds each layer's input by inverting the layer (x_in = x_out e^{-s} - tr; the masked
 //   coordinates, which feed s and tr, pass through unchanged and exact): no per-layer state.
-// * Per coupling layer the block flushes its four waves' partial gradients through LDS into its
-//   slab row (reference parameter order; column P = sum log p); a fixed-order fp64 column reduce
-//   gives grad = -1/n sum. No float atomics: bit-reproducible run to run.
+// * Per coupling layer the block sums its four waves' compact partial blocks (NvC) as float4 into its
+//   slab row; the split reduce reads slab column nv_slab_col(c) for reference parameter c (the loss
+//   after the time embedding's columns), and a fixed-order fp64 column reduce gives grad = -1/n sum.
+//   No float atomics: bit-reproducible run to run.
+// * Packed layout (d <= 4, time features <= 12): 49 KB of LDS per block and 168 VGPRs, three waves per
+//   SIMD.
 // Built for the celu / elu activation (the flow of log_density_estimation.py:103-114).
 // ---------------------------------------------------------------------------------------------
 typedef float f32x4 __attribute__((ext_vector_type(4)));
