@@ -9,7 +9,8 @@ drift recovery. One timed step = one pass of the hot path over one batch:
      accumulated in the same kernel,
   2. [N > 1 GPUs] one RCCL all-reduce of the fp64 moment sums (the pmap mean, trainer.py:52),
   3. the KFP residual value_and_grad for the current parameters (finalize kernel).
-value = particle-updates per second over all ranks = N_total * (n + 1) / step time (weak scaling).
+value = particle-updates per second over all ranks = N_total * (n + 1) / step time (weak scaling; --scaling strong
+fixes N_total instead and splits it over the ranks).
 
 Other workloads (--config): C3 = kinetic FP with a GMM potential (d = 4, K = 8, 2^22 particles,
 simulate + fused GMM residual over init/0T/terminal); C4 = kinetic McKean–Vlasov (d = 8, 2^21
@@ -75,6 +76,11 @@ def parse():
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--config", default="C2", choices=["C2", "C3", "C4", "C5"])
     p.add_argument("--particles", type=int, default=0, help="particles per GPU (0 = the config's)")
+    p.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                   help="weak: a fixed particle count per GPU (the headline); strong: a fixed job total "
+                        "(--particles-total) split over the ranks (SURVEY.md §8(d) asks it for C4)")
+    p.add_argument("--particles-total", type=int, default=0,
+                   help="strong scaling: the job's particles (0 = 8 x the per-GPU count, the 8-GPU configuration)")
     p.add_argument("--n-steps", type=int, default=100)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-recovery", action="store_true")
@@ -192,6 +198,19 @@ def traffic_from_profiles(key):
         return None
 
 
+def particle_share(a, rank, world, per_gpu_default):
+    """(N, first global id, job total) of this rank. Weak scaling: N = --particles or the config's per-GPU count
+    on every rank, ids [rank N, rank N + N). Strong scaling: the job total (--particles-total, default 8 x the
+    per-GPU count — the 8-GPU weak configuration, C4's 2^24 of SURVEY.md §8(d)) in contiguous shares. The
+    Philox streams follow the global ids, so a particle's numbers do not depend on the rank count."""
+    if a.scaling == "strong":
+        total = a.particles_total or 8 * (a.particles or per_gpu_default)
+        poff, N = dist.shard(total, rank, world)
+        return N, poff, total
+    N = a.particles or per_gpu_default
+    return N, rank * N, world * N
+
+
 def base_record(a, world, value, ms, config, kern_ms, bytes_launch, kernel, traffic=None, flops_launch=None):
     """roofline: HBM-bound launches (the simulators) report algorithmic bytes / launch time against the
     HBM peak; a VALU-bound launch (flops_launch given: C3's simulator with the fused GMM residual) reports
@@ -209,7 +228,7 @@ def base_record(a, world, value, ms, config, kern_ms, bytes_launch, kernel, traf
                 "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": bytes_launch}
     return {
         "metric": METRIC, "value": value, "unit": "particle-steps/s", "n_gpus": world, "steps": a.steps,
-        "warmup": a.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
+        "warmup": a.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": a.scaling,
         "vs_baseline": None, "dtype": "f32",
         "data": "synthetic: Philox Gaussian-init ensembles, fresh noise per step",
         "config": config, "hbm_GBps": achieved, "roofline": roof,
@@ -222,11 +241,10 @@ def run_c2(a, rank, world, dev):
     from methods.consistency_instances.kinetic_fokker_planck import recover_drift_richardson
 
     d, n, T, gamma = 4, a.n_steps, 2.0, 1.0
-    N = a.particles or (1 << 21)
+    N, poff, total = particle_share(a, rank, world, 1 << 21)
     F = problem_matrix(d)
     pot = dict(kind=native.POT_QUADRATIC, params=F)
     seed = 0x5EED_0001
-    poff = rank * N  # global particle ids: rank-count invariant streams
     z0 = native.gaussian_sample(N, torch.zeros(2 * d, device=dev), torch.eye(2 * d, device=dev),
                                 seed=seed ^ 0xA5A5, row_offset=poff)
     theta = torch.zeros(d * d + d, device=dev)
@@ -254,9 +272,9 @@ def run_c2(a, rank, world, dev):
                             moments=True, out=bufs)
 
     ms, kern_ms = timed(step, a.steps, a.warmup, dev, ramp=ramp)
-    value = world * N * (n + 1) / (ms / 1e3)
+    value = total * (n + 1) / (ms / 1e3)
     cfg = {"workload": "C2 kinetic OU d=4: EM simulate (traj+tau+last, fused moments) + KFP residual "
-                       "value_and_grad", "dim": d, "n_steps": n, "particles_per_gpu": N, "total_time": T,
+                       "value_and_grad", "dim": d, "n_steps": n, "particles_per_gpu": N, "particles_total": total, "total_time": T,
            "gamma": gamma, "parallelism": f"dp{world}"}
     out = base_record(a, world, value, ms, cfg, kern_ms, sim_bytes(N, n, d),
                       "sde_simulate_kernel<4,QUADRATIC,moments,staged> (+ its slab reduce)",
@@ -279,7 +297,7 @@ def run_c2(a, rank, world, dev):
         out["drift_err_em_n100"] = float(np.abs(rec["S_n"] - F).max())
         out["drift_recovery"] = ("max |S - tilde_F|, S = K + K^T the exact residual minimiser from the EM moments, "
                                  "Richardson (8 S(n=400) - 6 S(n=200) + S(n=100)) / 3, "
-                                 f"{passes * world * N} trajectories per level")
+                                 f"{passes * total} trajectories per level")
     if rank == 0 and world == 1 and not a.no_cpu_baseline:  # the CPU baseline: rank 0 at N = 1 only
         from oracle import cpu_baseline as cb
         from example_problems.kinetic_fokker_planck_example_OU import problem_matrix as pm
@@ -314,17 +332,16 @@ def run_c3(a, rank, world, dev):
     from utils import prng
 
     d, K, n, T, gamma = 4, 8, a.n_steps, 2.0, 0.5
-    N = a.particles or (1 << 22)
+    N, poff, total = particle_share(a, rank, world, 1 << 22)
     mus = gmm_means(d, K, prng.PRNGKey(2))
     pot = dict(kind=native.POT_GMM, params=mus, n_centers=K, sigma=1.0)
     seed = 0x5EED_0003
-    poff = rank * N
     ch = torch.diag(torch.tensor([2.0] * d + [math.sqrt(0.1)] * d, device=dev))  # x0~N(0,4I), v0~N(0,0.1I)
     z0 = native.gaussian_sample(N, torch.zeros(2 * d, device=dev), ch, seed=seed ^ 0xA5A5, row_offset=poff)
     mus_model = torch.as_tensor(np.random.default_rng(0).standard_normal((K, d)), dtype=torch.float32, device=dev)
     bufs = {"traj": torch.empty((n, N, 2 * d), device=dev), "tau": torch.empty((n, N), device=dev),
             "last": torch.empty((N, 2 * d), device=dev)}
-    Ng = world * N
+    Ng = total
     desc = native.kfp_gmm_desc(d, K, mus, gamma, T, Ng, Ng, Ng * n)
     counter = [0]
     last_out = [None]
@@ -341,10 +358,10 @@ def run_c3(a, rank, world, dev):
         last_out[0] = native.residual_kfp_gmm_finalize(desc, acc)
 
     ms, kern_ms = timed(step, a.steps, a.warmup, dev)
-    value = world * N * (n + 1) / (ms / 1e3)
+    value = total * (n + 1) / (ms / 1e3)
     cfg = {"workload": "C3 kinetic FP, GMM potential K=8, d=4: EM simulate (traj+tau+last) with the GMM-model KFP "
                        "residual value_and_grad over init/0T/terminal fused into the same launch",
-           "dim": d, "n_centers": K, "n_steps": n, "particles_per_gpu": N, "total_time": T, "gamma": gamma,
+           "dim": d, "n_centers": K, "n_steps": n, "particles_per_gpu": N, "particles_total": total, "total_time": T, "gamma": gamma,
            "parallelism": f"dp{world}"}
     # VALU-bound: every particle-update runs the GMM simulator step and one residual sample (its 0T row;
     # z0 / last add one sample per particle each)
@@ -389,11 +406,10 @@ def run_c4(a, rank, world, dev):
     from utils import prng
 
     d, n, T = 8, a.n_steps, 2.0
-    N = a.particles or (1 << 21)
+    N, poff, total = particle_share(a, rank, world, 1 << 21)
     ic = initialize_configuration(d)
     gamma = ic["gamma_friction"]
     A = ic["tilde_F"]
-    poff = rank * N
     z0 = native.gaussian_sample(N, torch.zeros(2 * d, device=dev), torch.eye(2 * d, device=dev), seed=7,
                                 row_offset=poff)
     theta = torch.zeros(d * d + d, device=dev)
@@ -519,11 +535,11 @@ def run_c4(a, rank, world, dev):
             coef_next[0] = host_coef(counter[0])
 
     ms, kern_ms = timed(step, a.steps, a.warmup, dev)
-    value = world * N * (n + 1) / (ms / 1e3)
+    value = total * (n + 1) / (ms / 1e3)
     cfg = {"workload": "C4 kinetic McKean-Vlasov quadratic interaction d=8: interacting-particle EM (closed-form "
                        "mean path from one all-reduced noise/z0 sum per simulate, all updates in registers) + KMV "
                        "residual value_and_grad (one fused read of the trajectory)",
-           "dim": d, "n_steps": n, "particles_per_gpu": N, "total_time": T, "gamma": gamma,
+           "dim": d, "n_steps": n, "particles_per_gpu": N, "particles_total": total, "total_time": T, "gamma": gamma,
            "parallelism": f"dp{world}"}
     out = base_record(a, world, value, ms, cfg, kern_ms, sim_bytes(N, n, d),
                       "sde_simulate_kernel<8,MEANFIELD_QUADRATIC,staged> (all 101 updates)",
@@ -567,12 +583,11 @@ def run_c5(a, rank, world, dev):
     from utils import prng
 
     d, K, n, T, gamma, W, L = 8, 8, a.n_steps, 2.0, 0.5, 256, 2
-    N = a.particles or (1 << 22)
+    N, poff, total = particle_share(a, rank, world, 1 << 22)
     nb = N // 16  # boundary batches (initial / terminal)
     mus = gmm_means(d, K, prng.PRNGKey(5))
     pot = dict(kind=native.POT_GMM, params=mus, n_centers=K, sigma=1.0)
     seed = 0x5EED_0005
-    poff = rank * N
     ch = torch.diag(torch.tensor([2.0] * d + [math.sqrt(0.1)] * d, device=dev))
     z0 = native.gaussian_sample(N, torch.zeros(2 * d, device=dev), ch, seed=seed ^ 0xA5A5, row_offset=poff)
     net = V_hypothesis(output_dim=1, hidden_dims=[W] * L)
@@ -607,11 +622,11 @@ def run_c5(a, rank, world, dev):
     ms, kern_ms = timed(step, a.steps, a.warmup, dev)
     rows = N + 2 * nb
     flops = 24.0 * P_mac * rows
-    value = world * N * (n + 1) / (ms / 1e3)
+    value = total * (n + 1) / (ms / 1e3)
     sim_ms = float(np.mean([s.elapsed_time(e) for s, e in sim_ev]))
     cfg = {"workload": "C5 KFP-GMM d=8 K=8: EM simulate (traj+tau+last) + non-parametric MLP residual "
                        "value_and_grad (W=256, L=2, out 40) on one random step per particle + N/16 boundary rows",
-           "dim": d, "n_centers": K, "n_steps": n, "particles_per_gpu": N, "mlp": dims, "residual_rows": rows,
+           "dim": d, "n_centers": K, "n_steps": n, "particles_per_gpu": N, "particles_total": total, "mlp": dims, "residual_rows": rows,
            "parallelism": f"dp{world}"}
     achieved = flops / (kern_ms / 1e3) / 1e12
     out = {

@@ -121,6 +121,22 @@ def test_bench_two_ranks_c4_c5(native, config, port, n):
     assert abs(out["value"] * out["ms_per_step"] / 1e3 - 2 * n * 101) < 1e-6 * out["value"]
 
 
+def test_bench_strong_scaling_c4_two_ranks(native):
+    """bench.py --scaling strong (strong scaling for C4): a fixed job total — odd here, so the
+    two contiguous shares differ by one particle — split over the ranks; value = total x (n + 1) / step time."""
+    total = 100_003
+    r = _launch(2, [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", "C4", "--scaling", "strong",
+                    "--particles-total", str(total), "--steps", "2", "--warmup", "1", "--no-cpu-baseline",
+                    "--no-recovery"], 29625, timeout=150)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["scaling"] == "strong" and out["n_gpus"] == 2 and out["config"]["particles_total"] == total
+    assert out["config"]["particles_per_gpu"] == total // 2 + 1  # rank 0's share
+    assert abs(out["value"] * out["ms_per_step"] / 1e3 - total * 101) < 1e-6 * out["value"]
+
+
 def test_dp_residual_matches_pmap_mean_of_shards(native, tmp_path):
     """2 ranks (gloo) vs the two shards evaluated one at a time: loss and grad = the shard means,
     grad_norm = the mean of the shard gradients' norms (trainer.py:44-53), for the quadratic, GMM and
