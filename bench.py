@@ -96,8 +96,10 @@ def parse():
     p.add_argument("--c4-separate-sums", action="store_true",
                    help="C4: the next simulate's mean-path sums as their own launch (pdeinv_mf_sums) instead of "
                         "inside the KMV pass (pdeinv_kmv_moments_weights_mf_sums), for A/B")
-    p.add_argument("--c4-schedule", default="fused", choices=["fused", "concurrent"],
-                   help="C4 steady state: 'fused' = the next simulate's mean-path sums inside the KMV pass; "
+    p.add_argument("--c4-schedule", default="sim", choices=["fused", "concurrent", "sim"],
+                   help="C4 steady state: 'sim' (default) = the simulator draws the next simulate's noise sums "
+                        "(pdeinv_sde_simulate_mf_next), plain KMV pass; 'fused' = the next simulate's mean-path "
+                        "sums inside the KMV pass; "
                         "'concurrent' = the unfused KMV pass (HBM-bound) on the main stream and pdeinv_mf_sums "
                         "(VALU-bound) on a side stream at the same time")
     p.add_argument("--cpu-procs", type=int, default=0,
@@ -442,12 +444,21 @@ def run_c4(a, rank, world, dev):
         desc.d_meanfield = ctypes.c_void_p(xbar.data_ptr())
         if record is not None:
             record[0].record()
-        native.sde_simulate_desc(desc, z0, bufs["traj"], bufs["tau"], bufs["last"])
+        sim_sums = a.c4_schedule == "sim" and not a.c4_separate_sums
+        if sim_sums:  # the simulator also draws the NEXT simulate's mean-path noise sums (same z0 ensemble)
+            desc_n, keep_n = native.mf_desc(N, d, n, T / n, gamma, A, seed=key.seed,
+                                            counter_offset=(counter[0] + n + 1) & 0xFFFFFFFF, particle_offset=poff)
+            sums_next[0] = native.sde_simulate_mf_next(desc, z0, bufs["traj"], bufs["tau"], bufs["last"], desc_n, z0)
+            del keep_n
+        else:
+            native.sde_simulate_desc(desc, z0, bufs["traj"], bufs["tau"], bufs["last"])
         if record is not None:
             record[1].record()
         del keep
         counter[0] = (counter[0] + n + 1) & 0xFFFFFFFF
-        if a.c4_schedule == "concurrent" and not a.c4_separate_sums:
+        if sim_sums:
+            mom, wst = native.kmv_moments_weights(d, gamma, coef, bufs["traj"], n, N, N * 2 * d, 2 * d)
+        elif a.c4_schedule == "concurrent" and not a.c4_separate_sums:
             # the next simulate's sums depend only on (seed, counter, ids, z0): they run on the side stream
             # beside the read-bound KMV pass of this step; the next step's all-reduce waits for them
             desc_n, keep_n = native.mf_desc(N, d, n, T / n, gamma, A, seed=key.seed, counter_offset=counter[0],
@@ -552,10 +563,18 @@ def run_c4(a, rank, world, dev):
                           "serial" + (", separate mean-path sums" if a.c4_separate_sums else
                                       (", mean-path sums of the next simulate on a side stream concurrent with the "
                                        "KMV pass" if a.c4_schedule == "concurrent" else
-                                       ", mean-path sums of the next simulate inside the KMV pass")))
+                                       (", mean-path noise sums of the next simulate drawn inside the simulator"
+                                        if a.c4_schedule == "sim" else
+                                        ", mean-path sums of the next simulate inside the KMV pass"))))
     if a.c4_separate_sums or pipeline:
         out["mean_path"] = {"kernel": "mf_sums_kernel<8> + slab reduce (+ all-reduce) + mf_path_kernel",
                             "ms": sums_ms, "normals_per_s": N * (n + 1) * d / (sums_ms / 1e3)}
+        out["residual"] = {"kernel": "kmv_moments_weights_kernel<8> + slab reduce + split", "ms": res_ms,
+                           "algorithmic_bytes": res_bytes, "GBps": res_bytes / (res_ms / 1e3) / 1e9}
+    elif a.c4_schedule == "sim":
+        out["mean_path"] = {"kernel": "all-reduce of the sums the previous simulate drew + mf_path_kernel", "ms": sums_ms}
+        out["roofline"]["kernel"] = ("sde_simulate_kernel<8,MEANFIELD_QUADRATIC,staged,next sums> (all 101 updates + the "
+                                     "next simulate's 101 x 8 normals per particle)")
         out["residual"] = {"kernel": "kmv_moments_weights_kernel<8> + slab reduce + split", "ms": res_ms,
                            "algorithmic_bytes": res_bytes, "GBps": res_bytes / (res_ms / 1e3) / 1e9}
     elif a.c4_schedule == "concurrent":

@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define PDEINV_ABI_VERSION 7
+#define PDEINV_ABI_VERSION 8
 #define PDEINV_MAX_DIM 16          /* d (configuration-space dimension) */
 #define PDEINV_MAX_PARAMS 256      /* floats of potential parameters passed by value */
 
@@ -152,6 +152,17 @@ int pdeinv_mf_sums(const pdeinv_sde_desc* desc, const float* d_z0, void* d_works
                    void* stream);
 int pdeinv_mf_mean_path(const pdeinv_sde_desc* desc, const double* d_sums, float* d_xbar, double* d_xsum,
                         void* stream);
+/* ABI 8. pdeinv_sde_simulate (fused McKean–Vlasov path, desc->d_meanfield set) that also returns the NEXT
+ * simulate's pdeinv_mf_sums(next, d_z0_next) in d_sums_next [pdeinv_mf_sums_len] fp64 (rank-local): the noise
+ * sums are drawn inside the store-bound simulator instead of by a separate launch or the KMV pass. `next` may
+ * differ from `desc` in counter_offset only (same seed, particles, particle_offset, dim, n_steps); Philox
+ * noise; even dim <= 8, n_steps + 1 <= 128 (else PDEINV_ERR_UNSUPPORTED: use pdeinv_mf_sums). Equal to
+ * pdeinv_mf_sums up to the fp32 partial-sum order; deterministic. Replaces the sums half of the reference's
+ * per-update mean field (kinetic_mckean_vlasov.py:20-23 through sampling_utils.py:6-22). */
+size_t pdeinv_sde_simulate_mf_next_workspace_bytes(const pdeinv_sde_desc* desc);
+int pdeinv_sde_simulate_mf_next(const pdeinv_sde_desc* desc, const float* d_z0, float* d_traj, float* d_tau,
+                                float* d_last, const pdeinv_sde_desc* next, const float* d_z0_next,
+                                void* d_workspace, double* d_sums_next, void* stream);
 /* tau0 per particle (u*dt from the shift stream, or d_shift_u) -> d_tau0 [N]. */
 int pdeinv_sde_tau0(const pdeinv_sde_desc* desc, float* d_tau0, void* stream);
 

@@ -253,16 +253,34 @@ struct GmmResFused {
   float c_nabla, c_hess, c_fric, c_true, c_init, c_term, inv_ni, inv_nt;
 };
 
+// McKean–Vlasov: the NEXT simulate's mean-path noise sums (the sum_i xi_{i,s} part of pdeinv_mf_sums) drawn
+// inside this simulate (NXT). The sums depend on the particle ids and the next simulate's Philox counter only,
+// so this store-bound kernel can draw them with its idle VALU while it streams the trajectory, and the KMV
+// pass that follows reads at full rate. A wave owns its 64 particles x np1 updates of the next simulate and
+// draws one (particle, update) pair per lane and step: lane l takes pairs q = l np1 + s (s = 0..np1-1, the
+// simulator's own steps), q -> (update q / 64, particle q % 64). A lane's np1 consecutive pairs span at most
+// three updates (np1 <= 128), so it keeps three running sums; after the last step the block combines them in
+// a fixed order (per update: waves, then the 1-3 lanes that drew it) into one slab column per update.
+struct MfNext {
+  float* partials;   // [(np1 * D) columns][gridDim.x]: column s * D + k
+  uint32_t ctr_off;  // the next simulate's Philox counter offset (same key and particle ids)
+  int32_t np1;       // updates per simulate (n_steps + 1), <= 128
+};
+
 // SdeArgs must stay the FIRST parameter: kernarg_params() reads a.params at kernarg offset 0.
-template <int D, int POT, bool MOM, int STORE, int KM = 1, bool NOISE = false, int MINW = 1, bool RES = false>
+template <int D, int POT, bool MOM, int STORE, int KM = 1, bool NOISE = false, int MINW = 1, bool RES = false,
+          bool NXT = false>
 __global__ __launch_bounds__(kBlock, MINW) void sde_simulate_kernel(SdeArgs a, const float* __restrict__ z0,
                                                               float* __restrict__ traj,
                                                               float* __restrict__ tau,
                                                               float* __restrict__ last,
                                                               float* __restrict__ partials,
-                                                              GmmResFused rf = GmmResFused{}) {
+                                                              GmmResFused rf = GmmResFused{},
+                                                              MfNext nx = MfNext{}) {
   constexpr int M = 2 * D;
   static_assert(!RES || (POT == PDEINV_POT_GMM && !MOM), "the fused residual is the GMM simulator's");
+  static_assert(!NXT || (POT == PDEINV_POT_MEANFIELD_QUADRATIC && !NOISE && M % 4 == 0 && D <= 8),
+                "next-simulate sums: McKean–Vlasov, Philox noise, even dim <= 8 (staged stores)");
   const int bid = a.remap ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
   const int64_t i_raw = (int64_t)bid * kBlock + threadIdx.x;
   const bool active = i_raw < a.N;
@@ -360,6 +378,14 @@ __global__ __launch_bounds__(kBlock, MINW) void sde_simulate_kernel(SdeArgs a, c
     if constexpr (kStaged) store_rows_staged<D>(dst, z, slot, lane, n_valid);
     else if (active) store_row<D, STORE>(dst, z);
   };
+  [[maybe_unused]] float nacc[NXT ? 3 : 1][NXT ? D : 1];
+  [[maybe_unused]] const int nbase = NXT ? lane * nx.np1 : 0;  // the lane's first pair
+  if constexpr (NXT) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int k = 0; k < D; ++k) nacc[j][k] = 0.f;
+  }
 
   auto update = [&](float h, float sh, uint32_t s) {
     // RES: re-read the LDS centres every update (hoisted out of the step loop they would take the
@@ -375,6 +401,22 @@ __global__ __launch_bounds__(kBlock, MINW) void sde_simulate_kernel(SdeArgs a, c
       else res_add(z, g, 0);         // traj row s-1 (g = grad V* there): the 0T set
     }
     gen_normals<D, NOISE>(a, plo, phi, s, i, xi);
+    if constexpr (NXT) {  // pair q = nbase + s of the next simulate: update q / 64 of particle wave_row0 + q % 64
+      const int q = nbase + (int)s;
+      const int sp = q >> 6, j = sp - (nbase >> 6);
+      const int64_t ip = wave_row0 + (q & 63);
+      const uint64_t g2 = (uint64_t)(a.poff + ip);
+      float xn[D];
+      stream_normals<D>(a.k0, a.k1, nx.ctr_off + (uint32_t)sp, (uint32_t)g2, (uint32_t)(g2 >> 32), xn);
+      const float wv = ip < a.N ? 1.f : 0.f;
+      const float w0 = j == 0 ? wv : 0.f, w1 = j == 1 ? wv : 0.f, w2 = j == 2 ? wv : 0.f;
+#pragma unroll
+      for (int k = 0; k < D; ++k) {
+        nacc[0][k] = fmaf(w0, xn[k], nacc[0][k]);
+        nacc[1][k] = fmaf(w1, xn[k], nacc[1][k]);
+        nacc[2][k] = fmaf(w2, xn[k], nacc[2][k]);
+      }
+    }
     const float gh = a.gamma * h;
 #pragma unroll
     for (int k = 0; k < D; ++k) {
@@ -403,6 +445,46 @@ __global__ __launch_bounds__(kBlock, MINW) void sde_simulate_kernel(SdeArgs a, c
   // final update: h = dt - tau0, lands exactly at T = n*dt (sampling_utils.py:44-46)
   update(h_last, sqrtf(h_last) * a.ns, (uint32_t)a.n_steps);
   if (active && last) store_row<D, kStoreNT>(last + i * M, z);
+  if constexpr (NXT) {
+    // the block's slab column per update: through the (now free) staging buffer in two passes (running sums
+    // 0-1, then 2; 4 waves x 64 lanes x 2 x D floats = the buffer), fixed order: pass, wave, lane
+    float* red = stage;
+    const int wv = threadIdx.x >> 6;
+    constexpr int NE = (128 * D + kBlock - 1) / kBlock;
+    float v[NE];
+#pragma unroll
+    for (int t = 0; t < NE; ++t) v[t] = 0.f;
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      const int j0 = 2 * pass, nj = pass ? 1 : 2;
+      __syncthreads();  // every wave is done with the buffer (its staged stores / the previous pass)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj)
+        if (jj < nj) {
+#pragma unroll
+          for (int k = 0; k < D; ++k) red[((wv * kWave + lane) * 2 + jj) * D + k] = nacc[j0 + jj][k];
+        }
+      __syncthreads();
+#pragma unroll
+      for (int t = 0; t < NE; ++t) {
+        const int e = threadIdx.x + t * kBlock;
+        if (e < nx.np1 * D) {
+          const int sp = e / D, k = e - sp * D;
+          const int l0 = (64 * sp) / nx.np1, l1 = (64 * sp + 63) / nx.np1;  // the lanes that drew update sp
+          for (int w2 = 0; w2 < kWavesPerBlock; ++w2)
+            for (int l = l0; l <= l1; ++l) {
+              const int jj = sp - ((l * nx.np1) >> 6) - j0;
+              if (jj >= 0 && jj < nj) v[t] += red[((w2 * kWave + l) * 2 + jj) * D + k];
+            }
+        }
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < NE; ++t) {
+      const int e = threadIdx.x + t * kBlock;
+      if (e < nx.np1 * D) nx.partials[(int64_t)e * nb + bid] = v[t];
+    }
+  }
   if constexpr (RES) {
     res_add(z, z, 2);  // last: the terminal set
     constexpr int NR = PDEINV_GMM_NACC + KR * D;
@@ -1052,4 +1134,82 @@ extern "C" int pdeinv_sde_tau0(const pdeinv_sde_desc* d, float* out, void* strea
   PDEINV_REQUIRE(out != nullptr, PDEINV_ERR_INVALID, "sde_tau0: out is null");
   hipLaunchKernelGGL(tau0_kernel, dim3(sim_grid(a.N)), dim3(kBlock), 0, (hipStream_t)stream, a, out);
   return check_launch("tau0_kernel");
+}
+
+// ---- McKean–Vlasov simulate + the next simulate's mean-path sums ------------------------------
+// pdeinv_sde_simulate (fused McKean–Vlasov path) that also returns pdeinv_mf_sums(next, z0_next): the noise
+// sums are drawn inside the simulator (sde_simulate_kernel NXT, the store-bound kernel's idle VALU), the
+// [count, sum x0, sum v0] head by the z0 pass of pdeinv_mf_sums. The next simulate differs from this one in
+// its Philox counter only (same key, particles, dim, n_steps); equal to pdeinv_mf_sums up to the fp32
+// partial-sum order.
+static size_t mf_next_slab_bytes(const pdeinv_sde_desc* d) {
+  return ((size_t)(d->n_steps + 1) * d->dim * sim_grid(d->n_particles) * sizeof(float) + 255) & ~(size_t)255;
+}
+
+extern "C" size_t pdeinv_sde_simulate_mf_next_workspace_bytes(const pdeinv_sde_desc* d) {
+  if (!d || d->dim < 1 || d->dim > 8 || d->n_particles <= 0 || d->n_steps < 1) return 0;
+  return mf_next_slab_bytes(d) + pdeinv_mf_sums_workspace_bytes(d);
+}
+
+#ifndef PDEINV_MF_NEXT_MINW
+#define PDEINV_MF_NEXT_MINW 1
+#endif
+template <int D>
+static void launch_sim_mf_next(const SdeArgs& a, const MfNext& nx, const float* z0, float* traj, float* tau,
+                               float* last, hipStream_t st) {
+  hipLaunchKernelGGL((sde_simulate_kernel<D, PDEINV_POT_MEANFIELD_QUADRATIC, false, kStoreStaged, 1, false,
+                                          PDEINV_MF_NEXT_MINW, false, true>),
+                     dim3(sim_grid(a.N)), dim3(kBlock), 0, st, a, z0, traj, tau, last, nullptr, GmmResFused{}, nx);
+}
+
+extern "C" int pdeinv_sde_simulate_mf_next(const pdeinv_sde_desc* d, const float* z0, float* traj, float* tau,
+                                           float* last, const pdeinv_sde_desc* next, const float* z0_next, void* ws,
+                                           double* sums_next, void* stream) {
+  SdeArgs a;
+  int rc = build_args(d, a);
+  if (rc) return rc;
+  PDEINV_REQUIRE(next != nullptr && sums_next != nullptr, PDEINV_ERR_INVALID, "sde_mf_next: null next / sums");
+  PDEINV_REQUIRE(d->potential.kind == PDEINV_POT_MEANFIELD_QUADRATIC &&
+                     next->potential.kind == PDEINV_POT_MEANFIELD_QUADRATIC,
+                 PDEINV_ERR_INVALID, "sde_mf_next: both simulates must be MEANFIELD_QUADRATIC");
+  PDEINV_REQUIRE(d->d_meanfield != nullptr, PDEINV_ERR_INVALID,
+                 "sde_mf_next: McKean–Vlasov needs d_meanfield (pdeinv_mf_mean_path)");
+  PDEINV_REQUIRE(d->d_shift_u == nullptr, PDEINV_ERR_INVALID,
+                 "sde_mf_next: McKean–Vlasov draws its shared tau0 from the stream (shift_u unsupported)");
+  PDEINV_REQUIRE(d->d_noise == nullptr && next->d_noise == nullptr, PDEINV_ERR_UNSUPPORTED,
+                 "sde_mf_next: Philox noise only (the explicit-noise mode runs pdeinv_mf_sums)");
+  PDEINV_REQUIRE(next->dim == d->dim && next->n_particles == d->n_particles &&
+                     next->particle_offset == d->particle_offset && next->seed == d->seed &&
+                     next->n_steps == d->n_steps,
+                 PDEINV_ERR_INVALID, "sde_mf_next: the next simulate must differ in its counter offset only");
+  const int D = d->dim;
+  PDEINV_REQUIRE(D % 2 == 0 && D <= 8 && d->n_steps + 1 <= 128, PDEINV_ERR_UNSUPPORTED,
+                 "sde_mf_next: even dim <= 8 and n_steps + 1 <= 128");
+  a.xbar = d->d_meanfield;
+  a.tau0_mf = shared_tau0_host(a, d);
+  hipStream_t st = (hipStream_t)stream;
+  if (a.N == 0) {
+    if (hipMemsetAsync(sums_next, 0, sizeof(double) * mf_sums_len(D, d->n_steps), st) != hipSuccess)
+      return fail(PDEINV_ERR_HIP, "sde_mf_next: hipMemsetAsync failed");
+    return PDEINV_OK;
+  }
+  PDEINV_REQUIRE(z0 && z0_next && ws, PDEINV_ERR_INVALID, "sde_mf_next: null pointer");
+  PDEINV_REQUIRE(aligned(traj, 16) && aligned(last, 16) && aligned(tau, 4), PDEINV_ERR_INVALID,
+                 "sde_mf_next: traj/last must be 16-byte aligned");
+  MfNext nx{};
+  nx.partials = (float*)ws;
+  nx.ctr_off = next->counter_offset;
+  nx.np1 = d->n_steps + 1;
+  switch (D) {
+    case 2: launch_sim_mf_next<2>(a, nx, z0, traj, tau, last, st); break;
+    case 4: launch_sim_mf_next<4>(a, nx, z0, traj, tau, last, st); break;
+    case 6: launch_sim_mf_next<6>(a, nx, z0, traj, tau, last, st); break;
+    default: launch_sim_mf_next<8>(a, nx, z0, traj, tau, last, st); break;
+  }
+  rc = check_launch("sde_simulate_kernel<MEANFIELD, next sums>");
+  if (rc) return rc;
+  launch_slab_reduce(nx.partials, sim_grid(a.N), nx.np1 * D, sums_next + 1 + 2 * D, st);
+  rc = check_launch("slab_reduce_kernel");
+  if (rc) return rc;
+  return mf_sums_tail(next, z0_next, d->n_steps + 1, (char*)ws + mf_next_slab_bytes(d), sums_next, st);
 }

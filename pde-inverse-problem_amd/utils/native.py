@@ -36,7 +36,7 @@ GMM_NACC = 8
 GMM_ACC_SLOTS = ("loss", "loss_gt", "nabla", "hessian", "friction", "nabla_true", "initial", "terminal")
 SQRT2 = math.sqrt(2.0)
 
-ABI_VERSION = 7  # PDEINV_ABI_VERSION of include/pdeinv.h this binding was written against
+ABI_VERSION = 8  # PDEINV_ABI_VERSION of include/pdeinv.h this binding was written against
 
 # Every exported symbol of include/pdeinv.h (tests check the library exports all of them).
 EXPORTED_SYMBOLS = (
@@ -59,6 +59,7 @@ EXPORTED_SYMBOLS = (
     "pdeinv_kmv_moments_weights_workspace_bytes", "pdeinv_kmv_moments_weights",
     "pdeinv_kmv_moments_weights_mf_sums_workspace_bytes", "pdeinv_kmv_moments_weights_mf_sums",
     "pdeinv_sde_simulate_kfp_gmm_workspace_bytes", "pdeinv_sde_simulate_kfp_gmm",
+    "pdeinv_sde_simulate_mf_next_workspace_bytes", "pdeinv_sde_simulate_mf_next",
 )
 
 
@@ -158,6 +159,8 @@ def lib():
         "pdeinv_sde_simulate_kfp_gmm": (i32, [P, P, P, P, P, P, P, P, P, P]),
         "pdeinv_mf_sums_len": (i64, [P]),
         "pdeinv_mf_sums_workspace_bytes": (ctypes.c_size_t, [P]),
+        "pdeinv_sde_simulate_mf_next_workspace_bytes": (ctypes.c_size_t, [P]),
+        "pdeinv_sde_simulate_mf_next": (i32, [P, P, P, P, P, P, P, P, P, P]),
         "pdeinv_mf_sums": (i32, [P, P, P, P, P]),
         "pdeinv_mf_mean_path": (i32, [P, P, P, P, P]),
         "pdeinv_kmv_moments_weights_workspace_bytes": (ctypes.c_size_t, [i64, i64, i32]),
@@ -439,6 +442,32 @@ def sde_simulate_desc(desc: SdeDesc, z0: torch.Tensor, traj: Optional[torch.Tens
     _check(lib().pdeinv_sde_simulate(ctypes.byref(desc), _dev(z0, "z0") if N else None, _dev(traj, "traj"),
                                      _dev(tau, "tau"), _dev(last, "last"), None, None, stream_handle()),
            "pdeinv_sde_simulate")
+
+
+def sde_simulate_mf_next(desc: SdeDesc, z0: torch.Tensor, traj: torch.Tensor, tau: Optional[torch.Tensor],
+                         last: torch.Tensor, next_desc: SdeDesc, z0_next: torch.Tensor) -> torch.Tensor:
+    """sde_simulate_desc (fused McKean-Vlasov path) that also returns the NEXT simulate's rank-local mf_sums
+    (pdeinv_sde_simulate_mf_next: the noise sums drawn inside the simulator). next_desc differs from desc in
+    counter_offset only."""
+    _require_gpu()
+    N, m, n = desc.n_particles, 2 * desc.dim, desc.n_steps
+    for t, shape, name in ((traj, (n, N, m), "traj"), (tau, (n, N), "tau"), (last, (N, m), "last")):
+        if t is not None and (tuple(t.shape) != shape or not t.is_contiguous()):
+            raise ValueError(f"{name} must be contiguous {shape}")
+    for t, name in ((z0, "z0"), (z0_next, "z0_next")):
+        if N and (t.dim() != 2 or tuple(t.shape) != (N, m) or t.stride(1) != 1):
+            raise ValueError(f"{name} must be [{N}, {m}] with unit inner stride")
+    desc.ld_z0 = z0.stride(0) if N > 1 else m
+    next_desc.ld_z0 = z0_next.stride(0) if N > 1 else m
+    nbytes = int(lib().pdeinv_sde_simulate_mf_next_workspace_bytes(ctypes.byref(desc)))
+    ws = torch.empty(max((nbytes + 3) // 4, 1), device=z0.device, dtype=torch.float32)
+    sums = torch.empty(int(lib().pdeinv_mf_sums_len(ctypes.byref(next_desc))), device=z0.device, dtype=torch.float64)
+    _check(lib().pdeinv_sde_simulate_mf_next(ctypes.byref(desc), _dev(z0, "z0") if N else None, _dev(traj, "traj"),
+                                             _dev(tau, "tau"), _dev(last, "last"), ctypes.byref(next_desc),
+                                             _dev(z0_next, "z0_next") if N else None, _dev(ws, "ws"),
+                                             _dev(sums, "sums_next", torch.float64), stream_handle()),
+           "pdeinv_sde_simulate_mf_next")
+    return sums
 
 
 def mf_step(desc: SdeDesc, s: int, z: torch.Tensor, z_out: torch.Tensor, tau_row, xbar_sum: torch.Tensor,

@@ -8,6 +8,8 @@ the C oracle (hardware v_log / v_sin / v_cos vs libm in the normals); explicit-n
 of the state scale; the two McKean–Vlasov drivers against each other 2e-5 of the state scale; moment
 sums 1e-5 relative (fp32 per thread / block, fp64 across blocks); residual 1e-4 relative, gradient 1e-3.
 """
+import ctypes
+
 import numpy as np
 import pytest
 import torch
@@ -184,6 +186,59 @@ def test_kmv_pass_fused_with_next_mf_sums(native, d, n_t, n, n_steps, poff):
     noise_scale = np.sqrt(n)  # |sum of n normals| ~ sqrt(n): absolute tolerance on that scale
     assert np.max(np.abs(got[1 + 2 * d:] - ref[1 + 2 * d:])) < 1e-5 * noise_scale
     del keep
+
+
+@pytest.mark.parametrize("d,n,n_steps,poff", [(8, 50_001, 100, 0), (8, 4099, 30, 123_456_789_012), (2, 999, 2, 5),
+                                            (4, 37, 127, 0), (6, 4096, 64, 77)])
+def test_simulate_mf_next_sums(native, d, n, n_steps, poff):
+    """pdeinv_sde_simulate_mf_next (C4: the next simulate's mean-path noise sums drawn inside the simulator):
+    the trajectory, tau and last bit-identical to the plain fused McKean-Vlasov simulate; sums_next ==
+    mf_sums of the next simulate — count and z0 sums exactly (the same z0 pass), the noise sums to fp32
+    partial-sum reassociation — incl. partial waves (n = 37 < 64), n_steps + 1 = 128 (three sums per lane),
+    ids past 2^32."""
+    rng = np.random.default_rng(d + n + n_steps)
+    z0 = _t(rng.standard_normal((n, 2 * d)) + 0.25)
+    A = nr.problem_constants(d)
+    desc, keep = native.mf_desc(n, d, n_steps, 0.02, 1.0, A, seed=0x5EED_0004, counter_offset=777,
+                                particle_offset=poff)
+    xbar, _ = native.mf_mean_path(desc, native.mf_sums(desc, z0), xsum=False)
+    desc.d_meanfield = ctypes.c_void_p(xbar.data_ptr())
+    out = [{k: torch.empty(shape, device="cuda") for k, shape in
+            (("traj", (n_steps, n, 2 * d)), ("tau", (n_steps, n)), ("last", (n, 2 * d)))} for _ in range(2)]
+    native.sde_simulate_desc(desc, z0, out[0]["traj"], out[0]["tau"], out[0]["last"])
+    nxt, keep_n = native.mf_desc(n, d, n_steps, 0.02, 1.0, A, seed=0x5EED_0004, counter_offset=777 + n_steps + 1,
+                                 particle_offset=poff)
+    sums = native.sde_simulate_mf_next(desc, z0, out[1]["traj"], out[1]["tau"], out[1]["last"], nxt, z0)
+    for k in ("traj", "tau", "last"):
+        assert torch.equal(out[0][k], out[1][k]), k
+    ref = native.mf_sums(nxt, z0).cpu().numpy()
+    got = sums.cpu().numpy()
+    assert got.shape == ref.shape and got[0] == ref[0] == n
+    assert np.array_equal(got[1:1 + 2 * d], ref[1:1 + 2 * d])
+    assert np.max(np.abs(got[1 + 2 * d:] - ref[1 + 2 * d:])) < 1e-5 * np.sqrt(n)
+    assert np.abs(got[1 + 2 * d:]).max() > 0.1  # the noise sums are there
+    del keep, keep_n
+
+
+def test_simulate_mf_next_rejects(native):
+    """The next simulate must differ in its counter only; odd dims / long paths are UNSUPPORTED (pdeinv_mf_sums)."""
+    n, d = 1000, 8
+    A = nr.problem_constants(d)
+    z0 = _t(np.zeros((n, 2 * d)))
+    desc, keep = native.mf_desc(n, d, 10, 0.02, 1.0, A, seed=1, counter_offset=0)
+    xbar, _ = native.mf_mean_path(desc, native.mf_sums(desc, z0), xsum=False)
+    desc.d_meanfield = ctypes.c_void_p(xbar.data_ptr())
+    traj, last = torch.empty((10, n, 2 * d), device="cuda"), torch.empty((n, 2 * d), device="cuda")
+    other, keep2 = native.mf_desc(n, d, 10, 0.02, 1.0, A, seed=2, counter_offset=11)
+    with pytest.raises(ValueError):
+        native.sde_simulate_mf_next(desc, z0, traj, None, last, other, z0)
+    long_desc, keep3 = native.mf_desc(n, d, 200, 0.02, 1.0, A, seed=1, counter_offset=0)
+    long_next, keep4 = native.mf_desc(n, d, 200, 0.02, 1.0, A, seed=1, counter_offset=201)
+    long_desc.d_meanfield = ctypes.c_void_p(xbar.data_ptr())
+    with pytest.raises(NotImplementedError):
+        native.sde_simulate_mf_next(long_desc, z0, torch.empty((200, n, 2 * d), device="cuda"), None, last,
+                                    long_next, z0)
+    del keep, keep2, keep3, keep4
 
 
 @pytest.mark.parametrize("name", ["kmv_pairwise_d8.npz", "kmv_pairwise_recipe.npz"])
