@@ -259,12 +259,18 @@ __device__ __forceinline__ float gmm_exp_weights(const f32x2 (*mu)[D], const f32
                                                  f32x2* E) {
   constexpr int KP = KM / 2;
   float amax = -INFINITY;
+  // coordinate-outer: the KP pair chains advance side by side, so no packed FMA waits on the one just issued
+  // (a dependent v_pk_* read costs a wait state on gfx950); each chain keeps its i = 0..D-1 order
+  f32x2 t[KP];
+#pragma unroll
+  for (int p = 0; p < KP; ++p) t[p] = bc2(x[0]) * mu[p][0];
+#pragma unroll
+  for (int i = 1; i < D; ++i)
+#pragma unroll
+    for (int p = 0; p < KP; ++p) t[p] = bc2(x[i]) * mu[p][i] + t[p];
 #pragma unroll
   for (int p = 0; p < KP; ++p) {
-    f32x2 t = bc2(x[0]) * mu[p][0];
-#pragma unroll
-    for (int i = 1; i < D; ++i) t = bc2(x[i]) * mu[p][i] + t;
-    E[p] = t * bc2(l2s) + c[p];
+    E[p] = t[p] * bc2(l2s) + c[p];
     amax = fmaxf(amax, fmaxf(E[p][0], E[p][1]));
   }
   f32x2 S = {0.f, 0.f};
@@ -281,13 +287,15 @@ __device__ __forceinline__ float gmm_exp_weights(const f32x2 (*mu)[D], const f32
 template <int D, int KM>
 __device__ __forceinline__ void gmm_mix(const f32x2 (*mu)[D], const f32x2* E, float* out) {
   constexpr int KP = KM / 2;
+  f32x2 s[D];  // centre-outer: the D coordinate chains side by side (each keeps its p = 0..KP-1 order)
 #pragma unroll
-  for (int i = 0; i < D; ++i) {
-    f32x2 s = E[0] * mu[0][i];
+  for (int i = 0; i < D; ++i) s[i] = E[0] * mu[0][i];
 #pragma unroll
-    for (int p = 1; p < KP; ++p) s = E[p] * mu[p][i] + s;
-    out[i] = s[0] + s[1];
-  }
+  for (int p = 1; p < KP; ++p)
+#pragma unroll
+    for (int i = 0; i < D; ++i) s[i] = E[p] * mu[p][i] + s[i];
+#pragma unroll
+  for (int i = 0; i < D; ++i) out[i] = s[i][0] + s[i][1];
 }
 
 // grad of U = -logsumexp_k(-|q - mu_k|^2 / (2 s^2)) = (q - sum_k w_k mu_k) / s^2 (core/potential.py:32-37;
@@ -355,11 +363,16 @@ __device__ __forceinline__ void gmm_residual_sample(const f32x2 (*mu)[D], const 
   for (int p = 0; p < KP; ++p) {
     PK[p] = bc2(v[0]) * mu[p][0];
     EM[p] = bc2(e[0]) * mu[p][0];
+  }
 #pragma unroll
-    for (int i = 1; i < D; ++i) {
+  for (int i = 1; i < D; ++i)  // coordinate-outer (independent packed FMAs back to back, same per-chain order)
+#pragma unroll
+    for (int p = 0; p < KP; ++p) {
       PK[p] = bc2(v[i]) * mu[p][i] + PK[p];
       EM[p] = bc2(e[i]) * mu[p][i] + EM[p];
     }
+#pragma unroll
+  for (int p = 0; p < KP; ++p) {
     const f32x2 wp = W[p] * PK[p];
     pb += wp;
     wq = wp * PK[p] + wq;
@@ -376,15 +389,28 @@ __device__ __forceinline__ void gmm_residual_sample(const f32x2 (*mu)[D], const 
     fb = W[p] * F[p] + fb;
   }
   const float nsF = -s2 * (fb[0] + fb[1]);
+  f32x2 cw[KP], ce[KP], cv[KP];
 #pragma unroll
   for (int p = 0; p < KP; ++p) {
-    const f32x2 cw = W[p] * (bc2(s2) * F[p] + bc2(nsF));
-    const f32x2 ce = bc2(A1) * W[p];
-    const f32x2 cv = W[p] * (bc2(2.f * A2) * PK[p] + bc2(B));
-    acc.CW[p] += cw;
-#pragma unroll
-    for (int i = 0; i < D; ++i) acc.G[p][i] = cv * bc2(v[i]) + (ce * bc2(e[i]) + (cw * bc2(x[i]) + acc.G[p][i]));
+    cw[p] = W[p] * (bc2(s2) * F[p] + bc2(nsF));
+    ce[p] = bc2(A1) * W[p];
+    cv[p] = W[p] * (bc2(2.f * A2) * PK[p] + bc2(B));
+    acc.CW[p] += cw[p];
   }
+  // G += cw x, then + ce e, then + cv v (the same rounding order per entry as one cv v + (ce e + (cw x + G))),
+  // term-outer so that consecutive packed FMAs are independent
+#pragma unroll
+  for (int p = 0; p < KP; ++p)
+#pragma unroll
+    for (int i = 0; i < D; ++i) acc.G[p][i] = cw[p] * bc2(x[i]) + acc.G[p][i];
+#pragma unroll
+  for (int p = 0; p < KP; ++p)
+#pragma unroll
+    for (int i = 0; i < D; ++i) acc.G[p][i] = ce[p] * bc2(e[i]) + acc.G[p][i];
+#pragma unroll
+  for (int p = 0; p < KP; ++p)
+#pragma unroll
+    for (int i = 0; i < D; ++i) acc.G[p][i] = cv[p] * bc2(v[i]) + acc.G[p][i];
 }
 
 // the lane's mu-gradient in the reference parameter order (k * D + i): G_k - mu_k CW_k
