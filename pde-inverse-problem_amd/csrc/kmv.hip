@@ -177,17 +177,8 @@ __global__ __launch_bounds__(kBlock) void kmv_moments_weights_kernel(float gamma
   // Packed rows (ld == 2d): the wave's 64 rows are one contiguous 256·M-byte block, loaded with M/4
   // fully coalesced 1 KiB dwordx4 instructions and transposed into the row stage through LDS (a
   // lane-private row load spans 64 rows per instruction and touches every line M/4 times).
-  // PACKED (host-checked: 16-byte aligned, ld == 2d)
+  // PACKED (host-checked: 16-byte aligned, ld == 2d, 4 n_rows 2d floats < 2^32 bytes)
   constexpr int NQ = M % 4 == 0 ? M / 4 : 1;
-  auto load_packed = [&](int64_t r0w, f32x4* q) {  // r0w: the wave's first row
-#pragma unroll
-    for (int k = 0; k < NQ; ++k) {
-      const int p = k * 256 + lane * 4;  // float offset inside the wave's block
-      const int64_t r = r0w + p / M;
-      q[k] = r < n_rows ? __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(base + r0w * M + p))
-                        : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-  };
   auto stage_packed = [&](const f32x4* q, float* v) {
 #pragma unroll
     for (int k = 0; k < NQ; ++k) {
@@ -222,27 +213,9 @@ __global__ __launch_bounds__(kBlock) void kmv_moments_weights_kernel(float gamma
   // wave-uniform trip count: every lane joins every MFMA (rows past the end are zeros, weight 0)
   const int64_t stride = (int64_t)gridDim.x * kBlock;
   int64_t r0 = (int64_t)blockIdx.x * kBlock + wave * kWave;
-  [[maybe_unused]] float vn[PACKED ? 1 : M];
-  [[maybe_unused]] f32x4 qn[PACKED ? NQ : 1];
-  if constexpr (PACKED) load_packed(r0, qn);
-  else load(r0 + lane, vn);
-  for (; r0 < n_rows; r0 += stride) {
+  // one row block of the wave: its rows are in stage[wave], v = this lane's row
+  auto consume = [&](const float* v, int64_t r0) {
     const bool active = r0 + lane < n_rows;
-    // keep the coefficient pairs in LDS: hoisted out of the loop they would take 2 d^2 + 2 d VGPRs
-    asm volatile("" ::: "memory");
-    float v[M];
-    if constexpr (PACKED) {
-      __builtin_amdgcn_wave_barrier();  // the previous iteration's stage reads are done
-      stage_packed(qn, v);               // stage the wave's rows (and take this lane's row back)
-      load_packed(r0 + stride, qn);      // software prefetch of the next block
-    } else {
-#pragma unroll
-      for (int k = 0; k < M; ++k) v[k] = vn[k];
-      load(r0 + stride + lane, vn);  // software prefetch of the next row
-      // stage the row, then the Gram of the wave's 64 rows on the matrix pipe
-#pragma unroll
-      for (int k = 0; k < M; k += 2) *reinterpret_cast<f32x2*>(srow + k) = f32x2{v[k], v[k + 1]};
-    }
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
@@ -276,6 +249,43 @@ __global__ __launch_bounds__(kBlock) void kmv_moments_weights_kernel(float gamma
 #pragma unroll
         for (int k = 0; k < D; ++k) xis[k] += xi[k];
       }
+    }
+  };
+  if constexpr (PACKED) {
+    // The set's rows through a buffer descriptor: rows at or past n_rows read as zero (the hardware range
+    // check), so the prefetch loads are unconditional — no per-load compare, zero fill and exec-masked branch
+    // (2.74 -> 2.54 ms at C4, tools/kmv_time.py, profiles/r04_kmv_buffer_ab.txt; prefetching two blocks ahead
+    // instead cost the third wave per SIMD and measured no faster). Host-checked: 4 n_rows 2d floats < 2^32 B.
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, (int)(n_rows * M * 4), 0x00020000);
+    auto load_buf = [&](int64_t r0w, f32x4* q) {
+#pragma unroll
+      for (int k = 0; k < NQ; ++k) {
+        const uint32_t off = (uint32_t)((r0w * M + k * 256 + lane * 4) * 4);
+        q[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 2));  // nt
+      }
+    };
+    f32x4 qa[NQ];
+    load_buf(r0, qa);
+    for (; r0 < n_rows; r0 += stride) {
+      asm volatile("" ::: "memory");  // keep the coefficient pairs in LDS (hoisted: 2 d^2 + 2 d VGPRs)
+      float v[M];
+      __builtin_amdgcn_wave_barrier();  // the previous block's stage reads are done
+      stage_packed(qa, v);
+      load_buf(r0 + stride, qa);  // software prefetch of the wave's next row block
+      consume(v, r0);
+    }
+  } else {
+    float vn[M];
+    load(r0 + lane, vn);
+    for (; r0 < n_rows; r0 += stride) {
+      asm volatile("" ::: "memory");
+      float v[M];
+#pragma unroll
+      for (int k = 0; k < M; ++k) v[k] = vn[k];
+      load(r0 + stride + lane, vn);  // software prefetch of the next row
+#pragma unroll
+      for (int k = 0; k < M; k += 2) *reinterpret_cast<f32x2*>(srow + k) = f32x2{v[k], v[k + 1]};
+      consume(v, r0);
     }
   }
   // the wave's 16 x 16 Gram: lane holds rows 4 (lane / 16) + i, column lane % 16 (symmetric, so the
@@ -573,7 +583,8 @@ static int kmv_mw_launch(int32_t D, float gamma, const float* coef, const float*
   double* both = (double*)((char*)ws + kmv_mw_slab_bytes(cols, bx));
   const dim3 g(bx, (unsigned)n_sets);
   // packed rows (ld == 2d, 16-byte aligned, even d): the coalesced block-load variant
-  const bool packed = (2 * D) % 4 == 0 && ld == 2 * D && set_stride % 4 == 0 && ((uintptr_t)z & 15) == 0;
+  const bool packed = (2 * D) % 4 == 0 && ld == 2 * D && set_stride % 4 == 0 && ((uintptr_t)z & 15) == 0 &&
+                      n_rows * 2 * D * 4 * 4 < ((int64_t)1 << 32);  // 32-bit buffer offsets (row block + prefetch stride)
   const MfNoise m = mf ? *mf : MfNoise{};
   switch (D) {
 #define CASE(DD)                                                                                              \
