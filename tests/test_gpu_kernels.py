@@ -159,6 +159,21 @@ def test_fused_moments_equal_recomputed(native, d):
         assert np.allclose(mom[k], ref[k], rtol=2e-5, atol=1e-3 * max(1.0, ref[k][0] ** 0.5)), k
 
 
+@pytest.mark.parametrize("d,N", [(4, 5003), (4, 64 * 40), (2, 777), (8, 130)])
+def test_fused_moments_without_trajectory(native, d, N):
+    """Moments with no trajectory output equal those of the same simulate with the trajectory written (same
+    seed; the store path and the moment path are independent): full and partial waves."""
+    rng = np.random.default_rng(d + N)
+    F = nr.problem_constants(d)
+    z0 = _t(rng.standard_normal((N, 2 * d)))
+    pot = dict(kind=native.POT_QUADRATIC, params=F)
+    a = native.sde_simulate(z0, 29, 0.02, 1.0, pot, seed=4, moments=True)
+    b = native.sde_simulate(z0, 29, 0.02, 1.0, pot, seed=4, moments=True, traj=False, tau=False, last=False)
+    assert torch.equal(a["moments"], b["moments"])
+    ref = nr.moments(a["traj"].cpu().numpy())
+    assert np.allclose(b["moments"][1].cpu().numpy(), ref, rtol=2e-5, atol=1e-3 * max(1.0, ref[0] ** 0.5))
+
+
 @pytest.mark.parametrize("m", [2, 8, 16, 5])
 def test_moments_kernel_strided(native, m):
     rng = np.random.default_rng(m)
