@@ -13,7 +13,7 @@
 
 namespace pdeinv {
 
-constexpr int kBatchedGridTarget = 3072;  // C4 KMV pass: 2.88 ms at 2048, 2.79 at 2304, 2.785 at 3072 (A/B on one box)
+constexpr int kBatchedGridTarget = 4096;  // C4 KMV pass: r02 2.88 ms at 2048, 2.785 at 3072; r04 (buffer loads) 2.52 at 3072, 2.486 at 4096, 2.51 at 6144 (profiles/r04_kmv_grid_ab.txt)
 
 static int64_t grid_target() {
   static const int64_t t = [] {
