@@ -87,8 +87,10 @@ def parse():
     p.add_argument("--recovery-passes", type=int, default=128,
                    help="ensembles per discretisation for the (untimed) drift recovery")
     p.add_argument("--cpu-particles", type=int, default=1 << 20)
-    p.add_argument("--chunk-rows", type=int, default=1 << 21,
-                   help="C5: MLP-residual rows per chunk (2^19 / 2^20 / 2^21: 114.5 / 113.7 / 113.4 ms; 7 / 14 / 28 GB workspace)")
+    p.add_argument("--chunk-rows", type=int, default=1 << 22,
+                   help="C5: MLP-residual rows per chunk, capped at the call's rows (r02: 2^19 / 2^20 / 2^21: 114.5 / 113.7 / "
+                        "113.4 ms; r04: 2^21 / 2^22 / 5 * 2^20: 99.8 / 98.5-99.0 / 98.5-98.9 ms residual, "
+                        "profiles/r04_c5_chunk_ab.txt; 28 / 56 / 70 GB workspace)")
     p.add_argument("--c4-pipeline", action="store_true",
                    help="C4 at world 1: two streams, simulate k+1 concurrent with the KMV residual of step k on a "
                         "double-buffered trajectory (measured 6.85 vs 6.25 ms/step serial: the step is HBM-bound, "
@@ -632,7 +634,7 @@ def run_c5(a, rank, world, dev):
             sim_ev.append((e0, record[0]))
         acc, grad = native.residual_kfp_mlp(dims, flat, z0[:nb], r["last"][:nb], z0T, true_kind=native.POT_GMM,
                                             true_params=mus, gamma=gamma, total_time=T, world_scale=1.0 / world,
-                                            chunk_rows=a.chunk_rows)
+                                            chunk_rows=min(a.chunk_rows, (N + 2 * nb + 63) // 64 * 64))
         if record is not None:
             record[1].record()
         both = dist.allreduce_sum(torch.cat([acc, grad.double()]))
