@@ -88,9 +88,9 @@ def parse():
                    help="ensembles per discretisation for the (untimed) drift recovery")
     p.add_argument("--cpu-particles", type=int, default=1 << 20)
     p.add_argument("--chunk-rows", type=int, default=1 << 22,
-                   help="C5: MLP-residual rows per chunk, capped at the call's rows (r02: 2^19 / 2^20 / 2^21: 114.5 / 113.7 / "
-                        "113.4 ms; r04: 2^21 / 2^22 / 5 * 2^20: 99.8 / 98.5-99.0 / 98.5-98.9 ms residual, "
-                        "profiles/r04_c5_chunk_ab.txt; 28 / 56 / 70 GB workspace)")
+                   help="C5: MLP-residual rows per chunk, capped at the call's rows; at most 2^30 / width (32-bit byte "
+                        "offsets). r02: 2^19 / 2^20 / 2^21: 114.5 / 113.7 / 113.4 ms; r04: 2^21 / 2^22: 99.8 / 98.5-99.0 ms "
+                        "residual (profiles/r04_c5_chunk_ab.txt); 28 / 56 GB workspace")
     p.add_argument("--c4-pipeline", action="store_true",
                    help="C4 at world 1: two streams, simulate k+1 concurrent with the KMV residual of step k on a "
                         "double-buffered trajectory (measured 6.85 vs 6.25 ms/step serial: the step is HBM-bound, "

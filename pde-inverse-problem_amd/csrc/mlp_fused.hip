@@ -140,7 +140,7 @@ struct ARegs {
   float v[NE][NV > 0 ? NV : 1];
 };
 
-// Loads are unconditional from a clamped 32-bit offset (a chunk's planes stay below 2^31 floats):
+// Loads are unconditional from a clamped 32-bit offset (a chunk's planes stay at or below 2^30 floats):
 // no per-element exec-mask branches. The zeroing select of out-of-range elements happens in the
 // store phase, after the MFMAs, so the loads stay in flight under the current tile's math.
 template <int BM, int AM>
@@ -653,7 +653,7 @@ struct WgradArgs {
   const float* b1;
 };
 
-// Offsets inside one chunk's planes fit in 32 bits (run_chunk checks Bc * W < 2^31), so the
+// Byte offsets inside one chunk's planes fit in 32 bits (run_chunk checks Bc * W <= 2^30), so the
 // loads use a uniform base + 32-bit lane offset.
 template <int D>
 constexpr int xrow_stride() { return (3 * D + 3) & ~3; }  // [x | v | abar0] padded to 16 B
@@ -1959,8 +1959,8 @@ static int run_chunk_d(const Chunk& c, const LossHook& loss, hipStream_t st) {
 
 int run_chunk(const Chunk& c, const LossHook& loss, hipStream_t st) {
   if (!supported(c.d, c.L, c.W, c.O)) return fail(PDEINV_ERR_UNSUPPORTED, "kfp_mlp fused: unsupported shape");
-  if (c.Bc * (int64_t)c.W >= ((int64_t)1 << 31))
-    return fail(PDEINV_ERR_INVALID, "kfp_mlp fused: chunk_rows * width must stay below 2^31");
+  if (c.Bc * (int64_t)c.W > ((int64_t)1 << 30))  // ldo / sto: 32-bit BYTE offsets into a plane (idx << 2)
+    return fail(PDEINV_ERR_INVALID, "kfp_mlp fused: chunk_rows * width must stay at or below 2^30");
   if (c.R <= 0) return 0;
   switch (c.d) {
     case 2: return run_chunk_d<2>(c, loss, st);

@@ -376,6 +376,30 @@ def test_residual_mlp_vs_restatement(native, dims, true_kind, chunk, impl):
     assert abs(out[2] - np.linalg.norm(g_ref)) < 2e-3 * (1 + np.linalg.norm(g_ref))
 
 
+def test_residual_mlp_fused_chunk_at_offset_limit(native):
+    """The C5 default chunk: 2^22 rows x width 256 = 2^30 floats per plane, the largest chunk whose byte offsets
+    (32-bit, from a uniform plane base) do not wrap. One 2^22-row 0T chunk equals two 2^21-row chunks to fp32
+    reassociation; a chunk past 2^30 / W rows is rejected (the old 2^31 bound let byte offsets wrap)."""
+    dims = [8, 256, 256, 40]
+    rng = np.random.default_rng(22)
+    flat = np.concatenate([np.concatenate([rng.standard_normal((dims[i], dims[i + 1])).ravel() * np.sqrt(1.0 / dims[i]),
+                                           0.1 * rng.standard_normal(dims[i + 1])]) for i in range(len(dims) - 1)])
+    n0t = 1 << 22
+    z0 = torch.randn((n0t, 16), device=DEV)
+    zi, zt = torch.randn((1000, 16), device=DEV), torch.randn((1000, 16), device=DEV)
+    mus = nr.gmm_centres(8, 3)
+    kw = dict(true_kind=native.POT_GMM, true_params=mus, gamma=0.5, total_time=2.0, impl=FUSED)
+    acc_a, grad_a = native.residual_kfp_mlp(dims, _t(flat), zi, zt, z0, chunk_rows=1 << 22, **kw)
+    acc_b, grad_b = native.residual_kfp_mlp(dims, _t(flat), zi, zt, z0, chunk_rows=1 << 21, **kw)
+    a, b = acc_a.cpu().numpy(), acc_b.cpu().numpy()
+    assert np.allclose(a, b, rtol=1e-4, atol=1e-4 * np.abs(b).max())
+    ga, gb = grad_a.cpu().numpy(), grad_b.cpu().numpy()
+    assert np.max(np.abs(ga - gb)) < 1e-4 * (1 + np.abs(gb).max())
+    assert np.abs(gb).max() > 0
+    with pytest.raises(ValueError, match="2\\^30"):
+        native.residual_kfp_mlp(dims, _t(flat), zi, zt, z0[:1024], chunk_rows=(1 << 22) + 64, **kw)
+
+
 def test_residual_mlp_fused_matches_library(native):
     """The two implementations agree to fp32 reassociation level on the C5 shape, and the fused
     path is deterministic run to run (fixed-order slab sums, no atomics)."""
