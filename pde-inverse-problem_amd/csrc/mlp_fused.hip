@@ -1959,8 +1959,8 @@ static int run_chunk_d(const Chunk& c, const LossHook& loss, hipStream_t st) {
 
 int run_chunk(const Chunk& c, const LossHook& loss, hipStream_t st) {
   if (!supported(c.d, c.L, c.W, c.O)) return fail(PDEINV_ERR_UNSUPPORTED, "kfp_mlp fused: unsupported shape");
-  if (c.Bc * (int64_t)c.W > ((int64_t)1 << 30))  // ldo / sto: 32-bit BYTE offsets into a plane (idx << 2)
-    return fail(PDEINV_ERR_INVALID, "kfp_mlp fused: chunk_rows * width must stay at or below 2^30");
+  if (c.Bc * (int64_t)std::max(c.W, c.O) > ((int64_t)1 << 30))  // ldo / sto: 32-bit BYTE offsets into a plane
+    return fail(PDEINV_ERR_INVALID, "kfp_mlp fused: chunk_rows * max(width, out_features) must stay at or below 2^30");
   if (c.R <= 0) return 0;
   switch (c.d) {
     case 2: return run_chunk_d<2>(c, loss, st);
