@@ -901,10 +901,11 @@ bool rgemm_shape(int K, int N) { return K % 64 == 0 && K <= 256 && N % kRBN == 0
 // BNC = block columns: 128 for the W x W layers; 64 for the output layer (N = out_features <= 64, one
 // column block, columns past N zero in the staged B and never stored; E_OUT reduces a row's outputs
 // inside one wave, E_SEEDS writes the seeds and the bias-gradient column sums).
-template <int S, int NI, int AM, int BMD, int EM, int D = 0, int V = 0, int BNC = kRBN>
-__global__ __launch_bounds__(kRT, 1) void rgemm(GemmArgs a) {
-  constexpr int WGN = BNC / (32 * NI), WGM = 8 / WGN, BMR = 32 * WGM;  // waves along N / M, block rows
-  static_assert((NI == 2 || NI == 4) && WGN >= 1 && WGN * WGM == 8, "rgemm wave grid");
+template <int S, int NI, int AM, int BMD, int EM, int D = 0, int V = 0, int BNC = kRBN, int NW = 8>
+__global__ __launch_bounds__(NW * 64, 1) void rgemm(GemmArgs a) {
+  constexpr int NT = NW * 64;                                            // threads (NW waves)
+  constexpr int WGN = BNC / (32 * NI), WGM = NW / WGN, BMR = 32 * WGM;  // waves along N / M, block rows
+  static_assert((NI == 2 || NI == 4) && WGN >= 1 && WGN * WGM == NW, "rgemm wave grid");
   static_assert(EM != E_OUT || WGN == 1, "E_OUT reduces each row inside one wave");
   constexpr bool L1 = a_is_l1<AM>();
   constexpr int NV = rg_planes<AM>();
@@ -924,7 +925,7 @@ __global__ __launch_bounds__(kRT, 1) void rgemm(GemmArgs a) {
   const int lid = xcd_linear(blockIdx.x, gridDim.x);  // the column blocks of a row stream adjacent: same XCD
   const int cb = lid % ncb, rs = lid / ncb, nrs = gridDim.x / ncb;
   const int n0 = cb * BNC;
-  for (int e = tid; e < K * BNC; e += kRT) {
+  for (int e = tid; e < K * BNC; e += NT) {
     int k, n;
     float v;
     if constexpr (BMD == B_NN) {
@@ -940,7 +941,7 @@ __global__ __launch_bounds__(kRT, 1) void rgemm(GemmArgs a) {
     else Bt[n * Kp + k] = v;
   }
   if constexpr (L1) {
-    for (int e = tid; e < K * SK; e += kRT) {
+    for (int e = tid; e < K * SK; e += NT) {
       const int k = e / SK, i = e - k * SK;
       k1s[e] = i < D ? a.k1[i * K + k] : (i == D ? a.b1[k] : 0.f);
     }
@@ -1218,7 +1219,7 @@ __global__ __launch_bounds__(kRT, 1) void rgemm(GemmArgs a) {
       if (hi == 0) red[wm * BNC + wn * 32 * NI + ni * 32 + l31] = v;
     }
     __syncthreads();
-    for (int c = tid; c < BNC; c += kRT) {
+    for (int c = tid; c < BNC; c += NT) {
       float t = 0.f;
 #pragma unroll
       for (int w = 0; w < WGM; ++w) t += red[w * BNC + c];
@@ -1526,22 +1527,36 @@ static int sched_variant() {
 
 // S = 1 streams take 32 x 128 wave tiles (4 MFMA tiles per A value: the A prologue is the per-k VALU
 // cost), S = 3 streams 32 x 64 (3 x 2 tiles, 96 accumulator registers).
-template <int S, int AM, int BMD, int EM, int D = 0>
-static int launch_rgemm(GemmArgs a, hipStream_t st, int* grid_x_out = nullptr) {
-  constexpr int NI = S == 1 ? 4 : 2;
-  constexpr int BMR = 32 * (8 / (kRBN / (32 * NI)));
-  if (!rgemm_shape(a.K, a.N)) return fail(PDEINV_ERR_INVALID, "kfp_mlp rgemm: K % 64 == 0, K <= 256, N % 128 == 0");
+// PDEINV_MLP_F1W4=1 (A/B): the layer-1-prologue forward (A_L1F) on 4-wave blocks, one wave per SIMD, NI = 4 — every
+// wave owns all 128 columns of its 32 rows, so each row's layer-1 streams are built twice instead of four times
+static bool use_f1w4() {
+  static const bool on = [] { const char* e = getenv("PDEINV_MLP_F1W4"); return e && e[0] == '1'; }();
+  return on;
+}
+
+template <int S, int AM, int BMD, int EM, int D, int NI, int NW>
+static int launch_rgemm_t(GemmArgs a, hipStream_t st, int* grid_x_out) {
+  constexpr int BMR = 32 * (NW / (kRBN / (32 * NI)));
   const int V = sched_variant();
   const size_t bytes = ((V == 3 ? (size_t)a.K * (kRBN + 1) : (size_t)kRBN * (a.K + 4)) +
                         (a_is_l1<AM>() ? (size_t)a.K * k1_stride<D>() : 0)) * sizeof(float);
-  auto kern = V == 1 ? rgemm<S, NI, AM, BMD, EM, D, 1> : rgemm<S, NI, AM, BMD, EM, D, 0>;
+  auto kern = V == 1 ? rgemm<S, NI, AM, BMD, EM, D, 1, kRBN, NW> : rgemm<S, NI, AM, BMD, EM, D, 0, kRBN, NW>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
   a.n_mblocks = mblocks(a.R, BMR);
   const int ncb = a.N / kRBN;
   const int nrs = std::max(1, std::min(a.n_mblocks, kRGridCap / ncb));
   if (grid_x_out) *grid_x_out = nrs;
-  hipLaunchKernelGGL(kern, dim3(ncb * nrs), dim3(kRT), bytes, st, a);
+  hipLaunchKernelGGL(kern, dim3(ncb * nrs), dim3(NW * 64), bytes, st, a);
   return check_launch("kfp_mlp fused B-resident row GEMM");
+}
+
+template <int S, int AM, int BMD, int EM, int D = 0>
+static int launch_rgemm(GemmArgs a, hipStream_t st, int* grid_x_out = nullptr) {
+  if (!rgemm_shape(a.K, a.N)) return fail(PDEINV_ERR_INVALID, "kfp_mlp rgemm: K % 64 == 0, K <= 256, N % 128 == 0");
+  if constexpr (AM == A_L1F && S == 3) {
+    if (use_f1w4()) return launch_rgemm_t<S, AM, BMD, EM, D, 4, 4>(a, st, grid_x_out);
+  }
+  return launch_rgemm_t<S, AM, BMD, EM, D, (S == 1 ? 4 : 2), 8>(a, st, grid_x_out);
 }
 
 template <int MI, int NI, int GA, int GB, int D = 0>
