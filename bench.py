@@ -642,7 +642,9 @@ def run_c5(a, rank, world, dev):
 
     ms, kern_ms = timed(step, a.steps, a.warmup, dev)
     rows = N + 2 * nb
-    flops = 24.0 * P_mac * rows
+    # 24P per 0T row (value, ∂v, ∂v² Taylor streams, the ∇x reverse and the θ reverse), 12P per
+    # initial / terminal row — the reference evaluates only ∇V·v there (kinetic_fokker_planck.py:34-39)
+    flops = 24.0 * P_mac * N + 12.0 * P_mac * 2 * nb
     value = total * (n + 1) / (ms / 1e3)
     sim_ms = float(np.mean([s.elapsed_time(e) for s, e in sim_ev]))
     cfg = {"workload": "C5 KFP-GMM d=8 K=8: EM simulate (traj+tau+last) + non-parametric MLP residual "

@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define PDEINV_ABI_VERSION 8
+#define PDEINV_ABI_VERSION 9  /* 9: pdeinv_ou_exact_sample, pdeinv_kmv_mlp_path */
 #define PDEINV_MAX_DIM 16          /* d (configuration-space dimension) */
 #define PDEINV_MAX_PARAMS 256      /* floats of potential parameters passed by value */
 
@@ -382,6 +382,8 @@ typedef struct {
 #define PDEINV_MLP_IMPL_FUSED 2
 #define PDEINV_MLP_IMPL_PAIRS_RING 3 /* pdeinv_residual_kmv_mlp only: force the register-ring pair kernels
                                         (width <= 28) instead of the MFMA pair tiles — A/B and cross-checks */
+/* 1 when impl = AUTO runs this V_hypothesis shape on the hand-written fused fp32-MFMA kernels (compiled shapes and
+   the zero-padded envelope: dim <= 16, width <= 512, depth 1..16, any out_features), 0 when it takes rocBLAS */
 int pdeinv_mlp_fused_supported(int32_t dim, int32_t n_layers, int32_t width, int32_t out_features);
 int64_t pdeinv_mlp_param_count(int32_t dim, int32_t n_layers, int32_t width, int32_t out_features);
 size_t pdeinv_residual_kfp_mlp_workspace_bytes(const pdeinv_kfp_mlp_desc* desc);
@@ -427,10 +429,43 @@ typedef struct {
                              chunks of pair rows through the fused fp32-MFMA residual kernels of
                              pdeinv_residual_kfp_mlp; LIBRARY = pair rows through rocBLAS (explicit opt-in) */
 } pdeinv_kmv_mlp_desc;
+/* The path pdeinv_residual_kmv_mlp takes for this descriptor (shape + impl): PDEINV_KMV_PATH_PAIR_TILES (the
+   16-pair MFMA tiles), _PAIR_RING (the register-ring pair kernels), _FUSED_ROWS (pair rows through the fused
+   fp32-MFMA residual kernels), _LIBRARY (pair rows through rocBLAS), or -1 when the shape is unsupported. */
+#define PDEINV_KMV_PATH_PAIR_TILES 0
+#define PDEINV_KMV_PATH_PAIR_RING 1
+#define PDEINV_KMV_PATH_FUSED_ROWS 2
+#define PDEINV_KMV_PATH_LIBRARY 3
+int pdeinv_kmv_mlp_path(const pdeinv_kmv_mlp_desc* desc);
 size_t pdeinv_residual_kmv_mlp_workspace_bytes(const pdeinv_kmv_mlp_desc* desc);
 int pdeinv_residual_kmv_mlp(const pdeinv_kmv_mlp_desc* desc, const float* d_z, int64_t set_stride, int64_t ld,
                             const float* d_ds, const float* d_params, void* d_workspace, double* d_acc,
                             float* d_grad, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Exact kinetic-OU sampler (example_problems/kinetic_fokker_planck_example_OU.py:140-156, the reference's
+ * default KOU data: groups of rows, each from N(m(t_g), P(t_g)) at its own time t_g ~ U(t_min, t_max)),
+ * entirely on the device: per group the Van Loan exponential X = exp(B t_g), B = [[-F, L], [0, F^T]]
+ * (scaled Taylor sum of degree taylor_degree over the host-precomputed powers B^0..B^K, then `squarings`
+ * squarings — the host's ou_moments_batched recipe), m = e^{Ft} m0, P = e^{Ft}(P0 e^{F^T t} + X[:n, n:]),
+ * its lower Cholesky factor R (fp64), and the rows m + R xi with the grouped Gaussian sampler's noise stream
+ * (pdeinv_gaussian_sample_grouped with the same seed / ctr_z / row_off and these means / factors gives the
+ * same rows). t_g = t_min + (t_max - t_min) u_g, u_g = 24 bits of Philox(seed; (g, 0, ctr_t, 0xD0000000)),
+ * unless t_in gives them. Outputs t_out [G], mean_out [G, n], factor_out [G, n, n] are optional (null).
+ * n = 2d in {2..16 even, 20, 24, 32}; d_powers [(taylor_degree + 1), 2n, 2n], d_m0 [n], d_P0 [n, n] fp64.
+ * --------------------------------------------------------------------------------------- */
+typedef struct {
+  int32_t n;              /* 2d */
+  int32_t taylor_degree;  /* K (<= 30) */
+  int32_t squarings;      /* s: |B|_1 t_max / 2^s <= 1 */
+  double t_min, t_max;
+  const double* d_powers; /* B^0 .. B^K */
+  const double* d_m0;
+  const double* d_P0;
+} pdeinv_ou_desc;
+int pdeinv_ou_exact_sample(const pdeinv_ou_desc* desc, int64_t n_groups, int64_t rows_per_group, uint64_t seed,
+                           uint32_t ctr_t, uint32_t ctr_z, int64_t row_off, const float* d_t_in, float* d_t_out,
+                           float* d_mean_out, float* d_factor_out, float* d_out, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Overdamped Fokker–Planck (example_problems/fokker_planck_example.py,

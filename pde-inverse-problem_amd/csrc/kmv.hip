@@ -137,7 +137,7 @@ __global__ __launch_bounds__(kBlock) void kmv_moments_weights_kernel(float gamma
   constexpr int M = 2 * D, NC = 3 * D + 2 + 2 * D * D, LZ = moment_len(M), LW = moment_len(D);
   static_assert(M <= 16, "the 16x16 MFMA Gram holds 2d <= 16 features");
   const int t = blockIdx.y;
-  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  const int lane = threadIdx.x & (kWave - 1), wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const float* c = coef + (int64_t)t * NC;  // [m1 (D), a1, b1 (D), G1 (D*D), a2, b2 (D), G2 (D*D)]
   constexpr int NT = D * (D + 1) / 2;       // upper triangle of the symmetrised (G1, G2)
   __shared__ f32x2 cpair[NT + D];           // (G1_ij + G1_ji, G2_ij + G2_ji) for i < j, (G_ii) on the
@@ -177,7 +177,7 @@ __global__ __launch_bounds__(kBlock) void kmv_moments_weights_kernel(float gamma
   // Packed rows (ld == 2d): the wave's 64 rows are one contiguous 256·M-byte block, loaded with M/4
   // fully coalesced 1 KiB dwordx4 instructions and transposed into the row stage through LDS (a
   // lane-private row load spans 64 rows per instruction and touches every line M/4 times).
-  // PACKED (host-checked: 16-byte aligned, ld == 2d, 4 n_rows 2d floats < 2^32 bytes)
+  // PACKED (host-checked: 16-byte aligned, ld == 2d; any n_rows — the buffer descriptor is rebased per row block)
   constexpr int NQ = M % 4 == 0 ? M / 4 : 1;
   auto stage_packed = [&](const f32x4* q, float* v) {
 #pragma unroll
@@ -255,12 +255,17 @@ __global__ __launch_bounds__(kBlock) void kmv_moments_weights_kernel(float gamma
     // The set's rows through a buffer descriptor: rows at or past n_rows read as zero (the hardware range
     // check), so the prefetch loads are unconditional — no per-load compare, zero fill and exec-masked branch
     // (2.74 -> 2.54 ms at C4, tools/kmv_time.py, profiles/r04_kmv_buffer_ab.txt; prefetching two blocks ahead
-    // instead cost the third wave per SIMD and measured no faster). Host-checked: 4 n_rows 2d floats < 2^32 B.
-    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, (int)(n_rows * M * 4), 0x00020000);
+    // instead cost the third wave per SIMD and measured no faster). The descriptor is rebased on every row block
+    // (64-bit base = the block's first row, records = the block's bytes that exist), so the 32-bit offsets stay
+    // below 64 * 2d * 4 bytes for a set of any size; r0w is wave-uniform (scalar descriptor, no waterfall).
     auto load_buf = [&](int64_t r0w, f32x4* q) {
+      const int64_t left = n_rows - r0w;
+      const int nrec = left <= 0 ? 0 : (int)((left < kWave ? left : (int64_t)kWave) * M * 4);
+      const float* bp = base + (left > 0 ? r0w * M : 0);
+      const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(bp), 0, nrec, 0x00020000);
 #pragma unroll
       for (int k = 0; k < NQ; ++k) {
-        const uint32_t off = (uint32_t)((r0w * M + k * 256 + lane * 4) * 4);
+        const uint32_t off = (uint32_t)((k * 256 + lane * 4) * 4);
         q[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 2));  // nt
       }
     };
@@ -583,8 +588,7 @@ static int kmv_mw_launch(int32_t D, float gamma, const float* coef, const float*
   double* both = (double*)((char*)ws + kmv_mw_slab_bytes(cols, bx));
   const dim3 g(bx, (unsigned)n_sets);
   // packed rows (ld == 2d, 16-byte aligned, even d): the coalesced block-load variant
-  const bool packed = (2 * D) % 4 == 0 && ld == 2 * D && set_stride % 4 == 0 && ((uintptr_t)z & 15) == 0 &&
-                      n_rows * 2 * D * 4 * 4 < ((int64_t)1 << 32);  // 32-bit buffer offsets (row block + prefetch stride)
+  const bool packed = (2 * D) % 4 == 0 && ld == 2 * D && set_stride % 4 == 0 && ((uintptr_t)z & 15) == 0;
   const MfNoise m = mf ? *mf : MfNoise{};
   switch (D) {
 #define CASE(DD)                                                                                              \

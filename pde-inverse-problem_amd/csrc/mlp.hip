@@ -465,6 +465,15 @@ static bool fused_shape(const pdeinv_kfp_mlp_desc* d, FusedShape* f = nullptr) {
   return true;
 }
 
+// The shape runs the hand-written fused fp32-MFMA path under impl = AUTO: the padded envelope of fused_shape (dims
+// and widths zero-padded to the compiled ones), not only the compiled shapes themselves.
+extern "C" int pdeinv_mlp_fused_supported(int32_t dim, int32_t n_layers, int32_t width, int32_t out_features) {
+  pdeinv_kfp_mlp_desc d{};
+  d.dim = dim; d.n_layers = n_layers; d.width = width; d.out_features = out_features;
+  d.impl = PDEINV_MLP_IMPL_AUTO;
+  return fused_shape(&d) ? 1 : 0;
+}
+
 static MlpPadMap width_pad_map(const pdeinv_kfp_mlp_desc* d, const FusedShape& f) {
   MlpPadMap pm{};
   pm.L = d->n_layers;
@@ -1041,6 +1050,7 @@ static int kmv_mlp_run(const pdeinv_kmv_mlp_desc* d, const KmvPlan& k, const flo
 // the narrow-net pair kernels (mlp_pairs.hip): pairs generated in registers, MFMA weight gradients
 namespace pdeinv {
 bool kmv_pairs_supported(const pdeinv_kmv_mlp_desc* d);
+bool kmvq_supported(const pdeinv_kmv_mlp_desc* d);
 size_t kmv_pairs_workspace_bytes(const pdeinv_kmv_mlp_desc* d);
 int kmv_pairs_run(const pdeinv_kmv_mlp_desc* d, const float* z, int64_t set_stride, int64_t ld, const float* ds,
                   const float* params, void* ws, double* acc, float* grad, float** gbar_out, int pass, hipStream_t st);
@@ -1191,6 +1201,13 @@ static int kmv_fused_run(const pdeinv_kmv_mlp_desc* d, const KmvFusedPlan& k, co
 }
 
 static size_t kmv_pairs_part_offset(const pdeinv_kmv_mlp_desc* d) { return (kmv_pairs_workspace_bytes(d) + 255) & ~(size_t)255; }
+
+extern "C" int pdeinv_kmv_mlp_path(const pdeinv_kmv_mlp_desc* d) {
+  if (!d || d->dim < 1 || d->n_layers < 1 || d->n_layers > 16 || d->width < 1 || d->out_features < 1) return -1;
+  if (kmv_use_pairs(d)) return kmvq_supported(d) ? PDEINV_KMV_PATH_PAIR_TILES : PDEINV_KMV_PATH_PAIR_RING;
+  if (d->impl == PDEINV_MLP_IMPL_PAIRS_RING) return -1;
+  return kmv_use_fused(d) ? PDEINV_KMV_PATH_FUSED_ROWS : PDEINV_KMV_PATH_LIBRARY;
+}
 
 extern "C" size_t pdeinv_residual_kmv_mlp_workspace_bytes(const pdeinv_kmv_mlp_desc* d) {
   if (!d || d->dim < 1 || d->n_layers < 1 || d->width < 1 || d->out_features < 1 || d->n_sets < 1 || d->n_rows < 1)

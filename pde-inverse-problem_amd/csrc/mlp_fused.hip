@@ -61,7 +61,8 @@ __device__ __forceinline__ float ftanh(float z) {
   return 1.f - 2.f * __builtin_amdgcn_rcpf(e + 1.f);
 }
 
-// 32-bit byte offsets from a uniform base (saddr addressing): a chunk's planes stay below 2^29 floats
+// 32-bit byte offsets from a uniform base (saddr addressing): a chunk's planes stay at or below 2^30 floats
+// (byte offsets < 2^32, unsigned; run_chunk checks Bc * max(W, out) <= 2^30)
 __device__ __forceinline__ float ldo(const float* base, uint32_t idx) {
   return *reinterpret_cast<const float*>(reinterpret_cast<const char*>(base) + (idx << 2));
 }
@@ -1989,6 +1990,3 @@ int run_chunk(const Chunk& c, const LossHook& loss, hipStream_t st) {
 }  // namespace mlpf
 }  // namespace pdeinv
 
-extern "C" int pdeinv_mlp_fused_supported(int32_t dim, int32_t n_layers, int32_t width, int32_t out_features) {
-  return pdeinv::mlpf::supported(dim, n_layers, width, out_features) ? 1 : 0;
-}

@@ -267,6 +267,102 @@ struct MfNext {
   int32_t np1;       // updates per simulate (n_steps + 1), <= 128
 };
 
+// Step-loop 0T moments at 2d = 8 (the C2 headline kernel), shared by the four lanes of a "quad". PairGram
+// keeps a particle's full sum + Gram (48 accumulators) in its own lane: 96 VGPRs, 5 waves per SIMD, and the
+// store-bound launch runs at 0.77 of the box's write ceiling against 0.95 without moments (42 VGPRs) — the
+// waves in flight, not the FMAs, are what the moments cost. Here the staged rows (already in the wave's LDS
+// slot for the coalesced store) are read back by the four lanes {l, l^8, l^16, l^24} of a quad, and lane
+// class c = (l >> 3) & 3 accumulates, over the quad's four rows, only the Gram entries of the features
+// shifted by 2c: with u_k = z[(k + 2c) mod 8] it sums u0 u0..u5, u1 u1..u3, u1 u5 and (u0, u1) — 12
+// accumulators. The cyclic feature-pair shift maps the 10 Gram representatives onto all 36 entries; the
+// entries (0,4), (2,6), (1,5), (3,7) come out twice (classes c and c + 2 compute the same product on the
+// same rows) and are taken from classes 0 / 1 only. Same FMA count as PairGram (24 packed per update), plus
+// 12 ds_read_b64 per update; the quad choice (lane bits 3 and 4) makes both the Gram reads and the store's
+// chunk reads bank-conflict-free on the unpadded slot (tools/quad_gram_bank_model.py).
+struct QuadGram {
+  f32x2 s, g0, g1, g2, g3;  // (u0,u1); u0*(u0,u1); u0*(u2,u3); u0*(u4,u5); u1*(u2,u3)
+  float h, j;               // u1*u1, u1*u5
+  static constexpr int kSlots = 12;
+  __device__ __forceinline__ void zero() {
+    s = g0 = g1 = g2 = g3 = f32x2{0.f, 0.f};
+    h = j = 0.f;
+  }
+  // the lane's three pair addresses of its quad's row 0 (features 2c .. 2c + 5, cyclic)
+  __device__ __forceinline__ static void addresses(const float* slot_wave, int lane, const f32x2* (&p)[3]) {
+    const int c = (lane >> 3) & 3;
+    const float* row0 = slot_wave + (lane & ~24) * 8;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) p[k] = reinterpret_cast<const f32x2*>(row0 + 2 * ((k + c) & 3));
+  }
+  // rows l, l^8, l^16, l^24 of the quad sit 0 / 8 / 16 / 24 rows (of 4 f32x2) after row 0
+  __device__ __forceinline__ void add(const f32x2* const (&p)[3]) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int o = ((r & 1) * 8 + (r >> 1) * 16) * 4;
+      const f32x2 u01 = p[0][o], u23 = p[1][o], u45 = p[2][o];
+      const f32x2 a0 = f32x2{u01[0], u01[0]}, a1 = f32x2{u01[1], u01[1]};
+      s += u01;
+      g0 = a0 * u01 + g0;
+      g1 = a0 * u23 + g1;
+      g2 = a0 * u45 + g2;
+      g3 = a1 * u23 + g3;
+      h = fmaf(u01[1], u01[1], h);
+      j = fmaf(u01[1], u45[1], j);
+    }
+  }
+  __device__ __forceinline__ float slot(int k) const {
+    switch (k) {
+      case 0: return s[0];
+      case 1: return s[1];
+      case 2: return g0[0];
+      case 3: return g0[1];
+      case 4: return g1[0];
+      case 5: return g1[1];
+      case 6: return g2[0];
+      case 7: return g2[1];
+      case 8: return g3[0];
+      case 9: return g3[1];
+      case 10: return h;
+      default: return j;
+    }
+  }
+};
+
+// moment-vector entry e (1 + e of the MomentAcc layout: 8 sums, then the i <= j triangle) -> source c * 12 + slot
+struct QuadGramMap {
+  int8_t src[8 + 36];
+};
+constexpr int quad_tri(int i, int j) { return i <= j ? i * 8 - i * (i - 1) / 2 + (j - i) : quad_tri(j, i); }
+constexpr QuadGramMap make_quad_gram_map() {
+  QuadGramMap m{};
+  for (int e = 0; e < 44; ++e) m.src[e] = -1;
+  for (int c = 0; c < 4; ++c) {
+    const int f0 = (2 * c) % 8, f1 = (2 * c + 1) % 8, f2 = (2 * c + 2) % 8, f3 = (2 * c + 3) % 8, f4 = (2 * c + 4) % 8,
+              f5 = (2 * c + 5) % 8;
+    const int b = c * QuadGram::kSlots;
+    m.src[f0] = (int8_t)(b + 0);
+    m.src[f1] = (int8_t)(b + 1);
+    m.src[8 + quad_tri(f0, f0)] = (int8_t)(b + 2);
+    m.src[8 + quad_tri(f0, f1)] = (int8_t)(b + 3);
+    m.src[8 + quad_tri(f0, f2)] = (int8_t)(b + 4);
+    m.src[8 + quad_tri(f0, f3)] = (int8_t)(b + 5);
+    if (c < 2) m.src[8 + quad_tri(f0, f4)] = (int8_t)(b + 6);
+    m.src[8 + quad_tri(f0, f5)] = (int8_t)(b + 7);
+    m.src[8 + quad_tri(f1, f2)] = (int8_t)(b + 8);
+    m.src[8 + quad_tri(f1, f3)] = (int8_t)(b + 9);
+    m.src[8 + quad_tri(f1, f1)] = (int8_t)(b + 10);
+    if (c < 2) m.src[8 + quad_tri(f1, f5)] = (int8_t)(b + 11);
+  }
+  return m;
+}
+constexpr QuadGramMap kQuadGramMap = make_quad_gram_map();
+constexpr bool quad_gram_map_complete() {
+  for (int e = 0; e < 44; ++e)
+    if (kQuadGramMap.src[e] < 0) return false;
+  return true;
+}
+static_assert(quad_gram_map_complete(), "QuadGram: the four lane classes must cover every sum and Gram entry");
+
 // SdeArgs must stay the FIRST parameter: kernarg_params() reads a.params at kernarg offset 0.
 template <int D, int POT, bool MOM, int STORE, int KM = 1, bool NOISE = false, int MINW = 1, bool RES = false,
           bool NXT = false>
@@ -361,10 +457,13 @@ __global__ __launch_bounds__(kBlock, MINW) void sde_simulate_kernel(SdeArgs a, c
                                                               : (a.random_shift ? shift_u(a, plo, phi, i) * a.dt : 0.f);
   const float h_last = a.dt - tau0;
 
-  PairGram<(MOM ? M : 2)> acc;
-  acc.zero();
-
   constexpr bool kStaged = (STORE == kStoreStaged) && (M % 4 == 0);
+  constexpr bool kQuad = MOM && M == 8 && kStaged;  // QuadGram: the 0T moments shared by lane quads
+  PairGram<(MOM && !kQuad ? M : 2)> acc;
+  acc.zero();
+  [[maybe_unused]] QuadGram qg;
+  qg.zero();
+
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t wave_row0 = i_raw - lane;
   // wave-uniform by construction; readfirstlane lets the compiler branch on it with SALU
@@ -374,9 +473,46 @@ __global__ __launch_bounds__(kBlock, MINW) void sde_simulate_kernel(SdeArgs a, c
   float* tr = traj ? traj + (kStaged ? wave_row0 : i) * M : nullptr;
   float* ta = tau ? tau + i : nullptr;
   const int64_t tr_stride = a.N * M;
+  [[maybe_unused]] const f32x2* qaddr[3];
+  if constexpr (kQuad) QuadGram::addresses(stage + (threadIdx.x - lane) * M, lane, qaddr);
   auto put = [&](float* dst) {
     if constexpr (kStaged) store_rows_staged<D>(dst, z, slot, lane, n_valid);
     else if (active) store_row<D, STORE>(dst, z);
+  };
+  // kQuad: stage the row (zero for lanes past N, so the quads' sums need no weights), store it if there is a
+  // trajectory, then the quad's Gram reads of the same slot; a wave's LDS traffic only, no block barrier
+  [[maybe_unused]] auto put_mom = [&](float* dst) {
+    if constexpr (kQuad) {
+      if (n_valid == kWave) {
+#pragma unroll
+        for (int k = 0; k < M; k += 4)
+          *reinterpret_cast<f32x4*>(slot + lane * M + k) = f32x4{z[k], z[k + 1], z[k + 2], z[k + 3]};
+      } else {
+#pragma unroll
+        for (int k = 0; k < M; k += 4)
+          *reinterpret_cast<f32x4*>(slot + lane * M + k) =
+              active ? f32x4{z[k], z[k + 1], z[k + 2], z[k + 3]} : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      __builtin_amdgcn_wave_barrier();
+      if (dst) {
+        f32x4 v[M / 4];
+#pragma unroll
+        for (int k = 0; k < M / 4; ++k) v[k] = *reinterpret_cast<const f32x4*>(slot + 4 * (k * 64 + lane));
+        if (n_valid == kWave) {
+#pragma unroll
+          for (int k = 0; k < M / 4; ++k)
+            __builtin_nontemporal_store(v[k], reinterpret_cast<f32x4*>(dst + 4 * (k * 64 + lane)));
+        } else {
+#pragma unroll
+          for (int k = 0; k < M / 4; ++k) {
+            const int c = k * 64 + lane;
+            if (4 * c < n_valid * M) __builtin_nontemporal_store(v[k], reinterpret_cast<f32x4*>(dst + 4 * c));
+          }
+        }
+      }
+      qg.add(qaddr);
+      __builtin_amdgcn_wave_barrier();
+    }
   };
   [[maybe_unused]] float nacc[NXT ? 3 : 1][NXT ? D : 1];
   [[maybe_unused]] const int nbase = NXT ? lane * nx.np1 : 0;  // the lane's first pair
@@ -430,16 +566,18 @@ __global__ __launch_bounds__(kBlock, MINW) void sde_simulate_kernel(SdeArgs a, c
 
   // update 0: h = tau0 (sample at tau0)
   update(tau0, sqrtf(tau0) * a.ns, 0u);
-  if (tr) put(tr);
+  if constexpr (kQuad) put_mom(tr);
+  else if (tr) put(tr);
   if (active && ta) __builtin_nontemporal_store(tau_value(tau0, 0, a.dt), ta);
-  if constexpr (MOM) acc.add(z);
+  if constexpr (MOM && !kQuad) acc.add(z);
 
   const float sh_dt = sqrtf(a.dt) * a.ns;
   for (int s = 1; s < a.n_steps; ++s) {
     update(a.dt, sh_dt, (uint32_t)s);
-    if (tr) put(tr + (int64_t)s * tr_stride);
+    if constexpr (kQuad) put_mom(tr ? tr + (int64_t)s * tr_stride : nullptr);
+    else if (tr) put(tr + (int64_t)s * tr_stride);
     if (active && ta) __builtin_nontemporal_store(tau_value(tau0, s, a.dt), ta + (int64_t)s * a.N);
-    if constexpr (MOM) acc.add(z);
+    if constexpr (MOM && !kQuad) acc.add(z);
   }
 
   // final update: h = dt - tau0, lands exactly at T = n*dt (sampling_utils.py:44-46)
@@ -496,10 +634,45 @@ __global__ __launch_bounds__(kBlock, MINW) void sde_simulate_kernel(SdeArgs a, c
     block_reduce_to_slab(flat, PDEINV_GMM_NACC + rf.K * D, rlds, partials, bid, nb);
   }
 
+  if constexpr (kQuad) {
+    // class totals: the 12 accumulators summed over the 16 lanes of each class (lane bits 0, 1, 2, 5), the
+    // four waves' class totals through LDS, then entry e from its source slot (kQuadGramMap), fixed order
+    float t[QuadGram::kSlots];
+#pragma unroll
+    for (int k = 0; k < QuadGram::kSlots; ++k) {
+      float v = qg.slot(k);
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      v += __shfl_xor(v, 4, 64);
+      v += __shfl_xor(v, 32, 64);
+      t[k] = v;
+    }
+    __shared__ float qlds[kWavesPerBlock * 4 * QuadGram::kSlots];
+    const int wv = threadIdx.x >> 6;
+    __syncthreads();
+    if ((lane & 0x27) == 0) {
+#pragma unroll
+      for (int k = 0; k < QuadGram::kSlots; ++k) qlds[(wv * 4 + (lane >> 3)) * QuadGram::kSlots + k] = t[k];
+    }
+    __syncthreads();
+    float* dst = partials + (int64_t)L * nb;
+    if (threadIdx.x == 0) {
+      const int64_t nact = a.N - (int64_t)bid * kBlock;
+      dst[bid] = (float)a.n_steps * (float)(nact < 0 ? 0 : (nact > kBlock ? kBlock : nact));
+    } else if (threadIdx.x <= 44) {
+      const int src = kQuadGramMap.src[threadIdx.x - 1];
+      float v = 0.f;
+#pragma unroll
+      for (int w2 = 0; w2 < kWavesPerBlock; ++w2) v += qlds[w2 * 4 * QuadGram::kSlots + src];
+      dst[(int64_t)threadIdx.x * nb + bid] = v;
+    }
+  }
   if constexpr (MOM) {
-    float mv[L];
-    acc.finish((float)a.n_steps, w, mv);
-    block_reduce_to_slab(mv, L, lds, partials + (int64_t)L * nb, bid, nb);
+    if constexpr (!kQuad) {
+      float mv[L];
+      acc.finish((float)a.n_steps, w, mv);
+      block_reduce_to_slab(mv, L, lds, partials + (int64_t)L * nb, bid, nb);
+    }
     MomentAcc<M> term;
     term.zero();
     term.add(z, w);
@@ -699,15 +872,23 @@ extern "C" size_t pdeinv_sde_workspace_bytes(const pdeinv_sde_desc* d) {
   return (size_t)3 * moment_len(2 * d->dim) * sim_grid(d->n_particles) * sizeof(float);
 }
 
+// Waves per SIMD asked of the QuadGram (d = 4 moments) instantiation: at 1 the allocator takes 87 VGPRs (5 waves);
+// 6 fits in 80 with no spill; 7 spills a few dwords into the step loop.
+#ifndef PDEINV_QUAD_MINW
+#define PDEINV_QUAD_MINW 6
+#endif
+template <int D, int POT, bool MOM> constexpr int kSimMinWaves = (MOM && D == 4 && POT == PDEINV_POT_QUADRATIC) ? PDEINV_QUAD_MINW : 1;
+
 template <int D, int POT, bool MOM, int KM = 1>
 static void launch_sim(const SdeArgs& a, const float* z0, float* traj, float* tau, float* last,
                        float* ws, hipStream_t st) {
   const dim3 g(sim_grid(a.N)), b(kBlock);
+  constexpr int W = kSimMinWaves<D, POT, MOM>;
   if (a.noise)
-    hipLaunchKernelGGL((sde_simulate_kernel<D, POT, MOM, kStoreStaged, KM, true>), g, b, 0, st, a, z0, traj, tau,
+    hipLaunchKernelGGL((sde_simulate_kernel<D, POT, MOM, kStoreStaged, KM, true, W>), g, b, 0, st, a, z0, traj, tau,
                        last, ws);
   else
-    hipLaunchKernelGGL((sde_simulate_kernel<D, POT, MOM, kStoreStaged, KM, false>), g, b, 0, st, a, z0, traj, tau,
+    hipLaunchKernelGGL((sde_simulate_kernel<D, POT, MOM, kStoreStaged, KM, false, W>), g, b, 0, st, a, z0, traj, tau,
                        last, ws);
 }
 

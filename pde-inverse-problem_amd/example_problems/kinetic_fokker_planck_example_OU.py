@@ -79,6 +79,24 @@ def OU_process(t_space, configuration):  # noqa: N802 - reference name
     return np.stack(ms), np.stack(Ps)
 
 
+def van_loan_powers(configuration, tmax: float, K: int = 18):
+    """B^0..B^K of the Van Loan block B = [[-F, L], [0, F^T]] and the squarings s with |B|_1 tmax / 2^s <= 1 — the
+    per-problem constants of the scaled Taylor exponential (host ou_moments_batched, device pdeinv_ou_exact_sample)."""
+    F, L = configuration["F"], configuration["L"]
+    n = F.shape[0]
+    B = np.zeros((2 * n, 2 * n))
+    B[:n, :n] = -F
+    B[:n, n:] = L
+    B[n:, n:] = F.T
+    nrm = np.abs(B).sum(axis=0).max() * float(tmax)
+    s = max(0, int(np.ceil(np.log2(nrm)))) if nrm > 1.0 else 0
+    pw = np.empty((K + 1, 2 * n, 2 * n))
+    pw[0] = np.eye(2 * n)
+    for k in range(1, K + 1):
+        pw[k] = pw[k - 1] @ B
+    return pw, s
+
+
 def ou_moments_batched(ts, configuration):
     """(m(t_g), P(t_g)) for a batch of times in one vectorised pass — the same Van Loan block
     exponential as OU_process, exp(B t) with B = [[-F, L], [0, F^T]], evaluated for every t_g at
@@ -87,20 +105,11 @@ def ou_moments_batched(ts, configuration):
     (s makes |B| t_max / 2^s <= 1, truncation < 1e-16). Replaces one odeint / expm per random time
     of the reference's exact sampler (…_OU.py:140-156)."""
     ts = np.atleast_1d(np.asarray(ts, dtype=np.float64))
-    F, L, m0, P0 = (configuration[k] for k in ("F", "L", "m_0", "P_0"))
-    n = F.shape[0]
-    B = np.zeros((2 * n, 2 * n))
-    B[:n, :n] = -F
-    B[:n, n:] = L
-    B[n:, n:] = F.T
+    m0, P0 = configuration["m_0"], configuration["P_0"]
+    n = m0.shape[0]
     tmax = float(np.max(np.abs(ts))) if ts.size else 0.0
-    nrm = np.abs(B).sum(axis=0).max() * tmax
-    s = max(0, int(np.ceil(np.log2(nrm)))) if nrm > 1.0 else 0
-    K = 18
-    pw = np.empty((K + 1, 2 * n, 2 * n))
-    pw[0] = np.eye(2 * n)
-    for k in range(1, K + 1):
-        pw[k] = pw[k - 1] @ B
+    pw, s = van_loan_powers(configuration, tmax)
+    K = pw.shape[0] - 1
     tau = ts / (2.0 ** s)
     coef = np.ones((ts.size, K + 1))
     for k in range(1, K + 1):
@@ -161,6 +170,16 @@ class KineticFokkerPlanck(ProblemInstance):
             raise ValueError("x should be either 1D (unbatched) or 2D (batched) array.")
         return self.potential.value(x)
 
+    def exact_sampler(self):
+        """The device exact sampler over distribution_time's range (built once per problem)."""
+        if getattr(self, "_exact_sampler", None) is None:
+            from utils import native
+            ic = self.initial_configuration
+            t_min, t_max = float(self.distribution_time.mins), float(self.distribution_time.maxs)
+            pw, s = van_loan_powers(ic, t_max)
+            self._exact_sampler = native.OuExactSampler(pw, s, ic["m_0"], ic["P_0"], t_min, t_max)
+        return self._exact_sampler
+
     def _next_counter(self, n_steps: int) -> int:
         c = self._counter
         self._counter = (self._counter + n_steps + 1) & 0xFFFFFFFF
@@ -187,14 +206,10 @@ class KineticFokkerPlanck(ProblemInstance):
             sample_per_time = 100
             assert batch_size >= sample_per_time * 2
             n_random_time = batch_size // sample_per_time
-            k_t, k_x = prng.split(rng)
-            # all random times at once; their moments in one batched pass; one grouped launch
-            t = np.asarray(self.distribution_time.sample(n_random_time, k_t), dtype=np.float64).reshape(-1)
-            means, covs = ou_moments_batched(t, self.initial_configuration)
-            f32 = lambda a: torch.as_tensor(a, dtype=torch.float32, device="cuda")
-            from utils import native
-            return native.gaussian_sample_grouped(sample_per_time, f32(means), f32(cov_factor_batched(covs)),
-                                                  seed=k_x.seed)
+            _, k_x = prng.split(rng)
+            # one launch, no host work: the random times, their moments (Van Loan exponential), the Cholesky
+            # factors and the rows, one workgroup per time (pdeinv_ou_exact_sample)
+            return self.exact_sampler().sample(n_random_time, sample_per_time, seed=k_x.seed)
         k_shift, k = prng.split(rng)
         n_time_stamps, sample_per_time = batch_size
         assert n_time_stamps == 1  # …_OU.py:176 (the reference's grid mode is single-stamp)

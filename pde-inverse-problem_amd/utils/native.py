@@ -36,7 +36,7 @@ GMM_NACC = 8
 GMM_ACC_SLOTS = ("loss", "loss_gt", "nabla", "hessian", "friction", "nabla_true", "initial", "terminal")
 SQRT2 = math.sqrt(2.0)
 
-ABI_VERSION = 8  # PDEINV_ABI_VERSION of include/pdeinv.h this binding was written against
+ABI_VERSION = 9  # PDEINV_ABI_VERSION of include/pdeinv.h this binding was written against
 
 # Every exported symbol of include/pdeinv.h (tests check the library exports all of them).
 EXPORTED_SYMBOLS = (
@@ -54,12 +54,12 @@ EXPORTED_SYMBOLS = (
     "pdeinv_kfp_terms_finalize", "pdeinv_gather_random_step", "pdeinv_mlp_fused_supported",
     "pdeinv_adam_update", "pdeinv_realnvp_param_count", "pdeinv_realnvp_logdensity",
     "pdeinv_realnvp_grad_workspace", "pdeinv_realnvp_value_and_grad",
-    "pdeinv_residual_kmv_mlp_workspace_bytes", "pdeinv_residual_kmv_mlp",
+    "pdeinv_residual_kmv_mlp_workspace_bytes", "pdeinv_residual_kmv_mlp", "pdeinv_kmv_mlp_path",
     "pdeinv_mf_sums_len", "pdeinv_mf_sums_workspace_bytes", "pdeinv_mf_sums", "pdeinv_mf_mean_path",
     "pdeinv_kmv_moments_weights_workspace_bytes", "pdeinv_kmv_moments_weights",
     "pdeinv_kmv_moments_weights_mf_sums_workspace_bytes", "pdeinv_kmv_moments_weights_mf_sums",
     "pdeinv_sde_simulate_kfp_gmm_workspace_bytes", "pdeinv_sde_simulate_kfp_gmm",
-    "pdeinv_sde_simulate_mf_next_workspace_bytes", "pdeinv_sde_simulate_mf_next",
+    "pdeinv_sde_simulate_mf_next_workspace_bytes", "pdeinv_sde_simulate_mf_next", "pdeinv_ou_exact_sample",
 )
 
 
@@ -95,6 +95,12 @@ class KfpMlpDesc(ctypes.Structure):
                 ("c_nabla", ctypes.c_float), ("c_hess", ctypes.c_float), ("c_fric", ctypes.c_float),
                 ("c_true", ctypes.c_float), ("c_init", ctypes.c_float), ("c_term", ctypes.c_float),
                 ("chunk_rows", ctypes.c_int64), ("impl", ctypes.c_int32), ("boundary_value", ctypes.c_int32)]
+
+
+class OuDesc(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int32), ("taylor_degree", ctypes.c_int32), ("squarings", ctypes.c_int32),
+                ("t_min", ctypes.c_double), ("t_max", ctypes.c_double), ("d_powers", ctypes.c_void_p),
+                ("d_m0", ctypes.c_void_p), ("d_P0", ctypes.c_void_p)]
 
 
 class KmvMlpDesc(ctypes.Structure):
@@ -176,6 +182,7 @@ def lib():
         "pdeinv_gmm_potential": (i32, [i32, i32, f32, P, P, i64, i64, P, P, P]),
         "pdeinv_gaussian_sample": (i32, [i64, i32, u64, u32, i64, P, P, P, P]),
         "pdeinv_gaussian_sample_grouped": (i32, [i64, i64, i32, u64, u32, i64, P, P, P, P]),
+        "pdeinv_ou_exact_sample": (i32, [P, i64, i64, u64, u32, u32, i64, P, P, P, P, P, P]),
         "pdeinv_philox_fill": (i32, [u64, u32, u32, i64, P, P]),
         "pdeinv_gather_subsample": (i32, [P, i64, i32, i32, P, i64, P, i32, P, P]),
         "pdeinv_abi_version": (i32, []),
@@ -198,6 +205,7 @@ def lib():
         "pdeinv_residual_kfp_mlp": (i32, [P, P, i64, i64, P, i64, i64, P, i64, i64, P, P, P, P, P]),
         "pdeinv_kfp_terms_finalize": (i32, [P, P, i64, f32, P, P]),
         "pdeinv_residual_kmv_mlp_workspace_bytes": (ctypes.c_size_t, [P]),
+        "pdeinv_kmv_mlp_path": (ctypes.c_int, [P]),
         "pdeinv_residual_kmv_mlp": (i32, [P, P, i64, i64, P, P, P, P, P, P]),
         "pdeinv_gather_random_step": (i32, [P, i64, i32, i32, u64, u32, P, P, P]),
         "pdeinv_fp_rows": (i32, [P, i64, i64, i32, i32, P, P]),
@@ -615,6 +623,43 @@ def gaussian_sample_grouped(rows_per_group: int, means: torch.Tensor, cov_halves
     return out
 
 
+class OuExactSampler:
+    """The exact kinetic-OU sampler on the device (pdeinv_ou_exact_sample; …_OU.py:140-156): groups of rows, group g
+    from N(m(t_g), P(t_g)) at t_g ~ U(t_min, t_max) drawn on the device. `powers` = B^0..B^K of the Van Loan block
+    B = [[-F, L], [0, F^T]] (host fp64, once per problem), `squarings` s with |B|_1 t_max / 2^s <= 1."""
+
+    def __init__(self, powers: np.ndarray, squarings: int, m0: np.ndarray, P0: np.ndarray, t_min: float, t_max: float,
+                 device="cuda"):
+        _require_gpu()
+        K1, n2, _ = powers.shape
+        self.n = n2 // 2
+        self._pw = torch.as_tensor(np.ascontiguousarray(powers), dtype=torch.float64, device=device)
+        self._m0 = torch.as_tensor(np.ascontiguousarray(m0, dtype=np.float64), device=device)
+        self._P0 = torch.as_tensor(np.ascontiguousarray(P0, dtype=np.float64), device=device)
+        self.desc = OuDesc(self.n, K1 - 1, int(squarings), float(t_min), float(t_max), self._pw.data_ptr(),
+                           self._m0.data_ptr(), self._P0.data_ptr())
+        self.device = device
+
+    def sample(self, n_groups: int, rows_per_group: int, *, seed: int, ctr_t: int = 0, ctr_z: int = 0,
+               row_offset: int = 0, t: torch.Tensor = None, want_moments: bool = False):
+        """rows [n_groups * rows_per_group, n]; with want_moments also (t [G], means [G, n], factors [G, n, n])."""
+        G, n = int(n_groups), self.n
+        out = torch.empty((G * int(rows_per_group), n), device=self.device, dtype=torch.float32)
+        extra = None
+        if want_moments:
+            extra = (torch.empty(G, device=self.device), torch.empty((G, n), device=self.device),
+                     torch.empty((G, n, n), device=self.device))
+        if t is not None and (t.dtype != torch.float32 or t.numel() != G or not t.is_contiguous()):
+            raise ValueError(f"t must be a contiguous float32 [{G}] tensor")
+        ptr = (lambda x: x.data_ptr() if x is not None else None)
+        _check(lib().pdeinv_ou_exact_sample(ctypes.byref(self.desc), G, int(rows_per_group),
+                                            int(seed) & 0xFFFFFFFFFFFFFFFF, int(ctr_t) & 0xFFFFFFFF,
+                                            int(ctr_z) & 0xFFFFFFFF, int(row_offset), ptr(t),
+                                            *(ptr(x) for x in (extra or (None, None, None))), out.data_ptr(),
+                                            stream_handle()), "pdeinv_ou_exact_sample")
+        return (out, *extra) if want_moments else out
+
+
 def philox_fill(seed: int, ctr_z: int, ctr_w: int, n_blocks: int, device="cuda") -> torch.Tensor:
     _require_gpu()
     out = torch.empty((n_blocks, 4), device=device, dtype=torch.int32)
@@ -990,8 +1035,25 @@ def realnvp_value_and_grad(desc, params: torch.Tensor, t: torch.Tensor, x: torch
     return loss, grad
 
 
+KMV_PATHS = {0: "pair_tiles_mfma", 1: "pair_ring", 2: "fused_rows_mfma", 3: "library_rocblas"}
+
+
+def kmv_mlp_path(dims, impl: int = MLP_IMPL_AUTO) -> str:
+    """Which kernels pdeinv_residual_kmv_mlp runs for this Phi net and impl (pdeinv_kmv_mlp_path): the 16-pair
+    MFMA tiles, the register-ring pair kernels, pair rows through the fused MFMA residual, or rocBLAS."""
+    d, W, O, L = dims[0], dims[1], dims[-1], len(dims) - 2
+    F = np.zeros((d, d), dtype=np.float32)
+    desc = KmvMlpDesc(d, L, W, O, 1, 1, 1.0, F.ctypes.data_as(ctypes.c_void_p), 0, int(impl))
+    p = int(lib().pdeinv_kmv_mlp_path(ctypes.byref(desc)))
+    if p < 0:
+        raise NotImplementedError(f"kmv_mlp: unsupported shape {dims} / impl {impl}")
+    return KMV_PATHS[p]
+
+
 def mlp_fused_supported(dims) -> bool:
-    """True when residual_kfp_mlp runs the fused MFMA path for this V_hypothesis shape."""
+    """True when residual_kfp_mlp (impl = AUTO) runs the hand-written fused MFMA path for this V_hypothesis shape —
+    compiled shapes and the zero-padded envelope (pdeinv_mlp_fused_supported). Not a statement about the KMV pair
+    tiles (kmv_pair_tiles_supported)."""
     return bool(lib().pdeinv_mlp_fused_supported(dims[0], len(dims) - 2, dims[1], dims[-1]))
 
 

@@ -295,6 +295,33 @@ def test_kou_exact_random_time_sampler(native):
     assert np.all(np.abs(emp - Pbar) < 5 * sd + 1e-3)
 
 
+@pytest.mark.parametrize("d", [1, 2, 4, 8, 16])
+def test_ou_exact_sampler_device_moments(native, d):
+    """pdeinv_ou_exact_sample (the device-resident exact KOU sampler): the drawn times lie in [t_min, t_max); the
+    per-group mean and Cholesky factor equal the host closed form (ou_moments_batched, fp64 Van Loan) to fp32
+    rounding — R R^T = P(t_g) to 1e-6 of the covariance scale; the rows equal pdeinv_gaussian_sample_grouped with
+    those means / factors bit for bit; given times reproduce the drawn ones."""
+    from example_problems.kinetic_fokker_planck_example_OU import (initialize_configuration, ou_moments_batched,
+                                                                   van_loan_powers)
+    ic = initialize_configuration(d)
+    T, G, R = 2.0, 37, 100
+    pw, s = van_loan_powers(ic, T)
+    smp = native.OuExactSampler(pw, s, ic["m_0"], ic["P_0"], 1e-4, T)
+    rows, t, means, fac = smp.sample(G, R, seed=123, ctr_t=5, ctr_z=9, want_moments=True)
+    t64 = t.double().cpu().numpy()
+    assert np.all(t64 >= 1e-4) and np.all(t64 < T) and len(np.unique(t64)) == G
+    m_ref, P_ref = ou_moments_batched(t64, ic)
+    scale = np.abs(P_ref).max()
+    assert np.allclose(means.double().cpu().numpy(), m_ref, atol=1e-6 * scale)
+    L = fac.double().cpu().numpy()
+    assert np.all(np.triu(L, 1) == 0)
+    assert np.max(np.abs(L @ np.transpose(L, (0, 2, 1)) - P_ref)) < 1e-6 * scale
+    assert np.max(np.abs(L - np.linalg.cholesky(P_ref))) < 1e-5 * np.sqrt(scale)
+    ref = native.gaussian_sample_grouped(R, means, fac, seed=123, counter_offset=9)
+    assert torch.equal(rows, ref)
+    assert torch.equal(smp.sample(G, R, seed=123, ctr_z=9, t=t), rows)
+
+
 def test_gather_subsample_exact(native):
     rng = np.random.default_rng(1)
     n, N, m = 40, 300, 8

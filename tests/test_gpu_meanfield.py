@@ -160,6 +160,25 @@ def test_kmv_moments_weights_fused_equals_separate(native, d, n_t, n):
         assert np.allclose(a, b, rtol=1e-5, atol=1e-5 * np.abs(b).max())
 
 
+def test_kmv_moments_weights_set_beyond_32bit_offsets(native):
+    """A set of 2^26 + 77 rows at d = 8 (4.3 GB, byte offsets past 2^32): the packed pass rebases its buffer
+    descriptor per row block (the r04 single-descriptor form had to fall back to lane-private loads above
+    2^24 rows) and still equals moments_batched + kmv_weights (lane-private loads) on the same rows."""
+    d, n_t, n = 8, 1, (1 << 26) + 77
+    _, coef = _coef(d, np.array([0.9]))
+    g = torch.Generator(device=DEV)
+    g.manual_seed(26)
+    z = torch.randn((n, 2 * d), device=DEV, generator=g) * 1.3 + 0.1
+    mom, wst = native.kmv_moments_weights(d, 1.0, coef, z, n_t, n, n * 2 * d, 2 * d)
+    mom_s = native.moments_batched(z, n_t, n, 2 * d, n * 2 * d, 2 * d)
+    wst_s, _ = native.kmv_weights(d, 1.0, coef, z, n_t, n, n * 2 * d, 2 * d)
+    assert mom[0, 0].item() == n
+    for a, b in ((mom, mom_s), (wst, wst_s)):
+        a, b = a.cpu().numpy(), b.cpu().numpy()
+        assert np.allclose(a, b, rtol=1e-5, atol=1e-5 * np.abs(b).max())
+    del z
+
+
 @pytest.mark.parametrize("d,n_t,n,n_steps,poff", [(8, 100, 50_001, 100, 0), (8, 7, 4099, 30, 123_456_789_012),
                                                   (2, 3, 999, 2, 5), (5, 4, 4096, 3, 0)])
 def test_kmv_pass_fused_with_next_mf_sums(native, d, n_t, n, n_steps, poff):

@@ -192,7 +192,7 @@ def test_library_exports_every_header_symbol():
     missing = [s for s in _header_functions() if not hasattr(lib, s)]
     assert not missing
     lib.pdeinv_moment_len.restype = ctypes.c_int
-    assert lib.pdeinv_moment_len(8) == 45 and lib.pdeinv_abi_version() == native.ABI_VERSION == 8
+    assert lib.pdeinv_moment_len(8) == 45 and lib.pdeinv_abi_version() == native.ABI_VERSION == 9
 
 
 def test_loader_fails_loudly_without_gpu():
@@ -229,8 +229,16 @@ def test_abi_argument_validation_without_gpu():
     assert sde(ld_z0=5) == native.PDEINV_ERR_INVALID and b"ld_z0" in L.pdeinv_last_error()
     assert L.pdeinv_realnvp_value_and_grad(None, None, None, 0, None, 0, 0, None, None, None, 0, None) \
         == native.PDEINV_ERR_INVALID
-    assert L.pdeinv_mlp_fused_supported(3, 2, 256, 40) == 0 and L.pdeinv_mlp_fused_supported(8, 2, 256, 40) == 1
+    # the query reports the AUTO path: compiled shapes and the zero-padded envelope (d = 3 -> 4, width 20 -> 32);
+    # width > 512 takes rocBLAS
+    assert L.pdeinv_mlp_fused_supported(3, 2, 256, 40) == 1 and L.pdeinv_mlp_fused_supported(8, 2, 256, 40) == 1
     assert L.pdeinv_mlp_fused_supported(8, 1, 256, 40) == 1 and L.pdeinv_mlp_fused_supported(8, 2, 256, 80) == 1
+    assert L.pdeinv_mlp_fused_supported(2, 8, 20, 40) == 1 and L.pdeinv_mlp_fused_supported(8, 2, 1024, 40) == 0
+    assert L.pdeinv_mlp_fused_supported(17, 2, 256, 40) == 0
+    assert native.kmv_mlp_path([2] + [20] * 8 + [40]) == "pair_tiles_mfma"
+    assert native.kmv_mlp_path([2, 24, 24, 40]) == "pair_ring"
+    assert native.kmv_mlp_path([2, 64, 64, 40]) == "fused_rows_mfma"
+    assert native.kmv_mlp_path([2, 64, 64, 40], native.MLP_IMPL_LIBRARY) == "library_rocblas"
     # impl is validated (PDEINV_MLP_IMPL_PAIRS_RING selects the register-ring pair kernels, kmv_mlp only)
     F = (ctypes.c_float * 4)(1, 0, 0, 1)
     km = native.KmvMlpDesc()

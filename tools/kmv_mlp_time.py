@@ -40,7 +40,7 @@ def run(d, n, n_t, W, L, reps=3, impl=0):
     ms = s.elapsed_time(e) / reps
     pairs = n * n * n_t
     print(json.dumps({"case": "kmv_mlp", "impl": impl, "d": d, "n": n, "n_time": n_t, "dims": dims, "pairs": pairs, "ms": ms,
-                      "pairs_per_s": pairs / (ms / 1e3), "fused_mfma": native.mlp_fused_supported(dims),
+                      "pairs_per_s": pairs / (ms / 1e3), "path": native.kmv_mlp_path(dims, impl),
                       "loss_acc0": float(acc[0]), "grad_norm": float(g.norm())}), flush=True)
 
 
