@@ -378,7 +378,7 @@ typedef struct {
                              see pdeinv_fp_rows for the overdamped residual's row layout */
 } pdeinv_kfp_mlp_desc;
 #define PDEINV_MLP_IMPL_AUTO 0
-#define PDEINV_MLP_IMPL_LIBRARY 1
+#define PDEINV_MLP_IMPL_LIBRARY 1 /* rocBLAS sgemm path (cross-check; librocblas.so.5 loaded at run time) */
 #define PDEINV_MLP_IMPL_FUSED 2
 #define PDEINV_MLP_IMPL_PAIRS_RING 3 /* pdeinv_residual_kmv_mlp only: force the register-ring pair kernels
                                         (width <= 28) instead of the MFMA pair tiles — A/B and cross-checks */
@@ -408,7 +408,7 @@ int pdeinv_kfp_terms_finalize(const double* d_acc, const float* d_grad, int64_t 
  * pmap, trainer.py:44-53); average the finalized outputs over ranks.
  * --------------------------------------------------------------------------------------- */
 typedef struct {
-  int32_t dim;            /* d <= 8 */
+  int32_t dim;            /* d <= 16 (the pair kernels and LIBRARY: d <= 8) */
   int32_t n_layers;       /* hidden layers (neural_network.layers) */
   int32_t width;          /* hidden width (neural_network.hidden_dim) */
   int32_t out_features;   /* 40 in the reference */
@@ -424,10 +424,11 @@ typedef struct {
                              net); other widths <= 28 (or every width <= 28 under PAIRS_RING):
                              the register-ring pair kernels (pairs built in registers, MFMA weight
                              gradients; dim <= 8, n_layers <= 16, out <= 64; workspace ~ 2048 waves x
-                             (5 W L x 64 + P) floats); width >= 32 (dim <= 8 zero-padded to 2/4/8,
-                             1 <= n_layers <= 16, width <= 512 zero-padded to 32/64/128/256/512, any out):
+                             (5 W L x 64 + P) floats); width >= 32 (dim <= 16 zero-padded to 2/4/8/16,
+                             1 <= n_layers <= 16, width <= 1024 zero-padded to 32/64/.../1024, any out):
                              chunks of pair rows through the fused fp32-MFMA residual kernels of
-                             pdeinv_residual_kfp_mlp; LIBRARY = pair rows through rocBLAS (explicit opt-in) */
+                             pdeinv_residual_kfp_mlp; LIBRARY = pair rows through rocBLAS (explicit opt-in, loaded
+                             at run time: libpdeinv.so does not link rocBLAS) */
 } pdeinv_kmv_mlp_desc;
 /* The path pdeinv_residual_kmv_mlp takes for this descriptor (shape + impl): PDEINV_KMV_PATH_PAIR_TILES (the
    16-pair MFMA tiles), _PAIR_RING (the register-ring pair kernels), _FUSED_ROWS (pair rows through the fused

@@ -14,9 +14,9 @@
 // on the MFMA f32 path); every element-wise step, the per-row loss terms and the reductions are
 // the kernels below. The derivation is oracle/numpy_ref.py kfp_mlp_grad_analytic, checked against
 // central finite differences.
-#include <rocblas/rocblas.h>
-
+#include <dlfcn.h>
 #include <math.h>
+#include <rocblas/rocblas.h>
 
 #include <mutex>
 
@@ -26,6 +26,39 @@
 namespace pdeinv {
 
 // ---- rocBLAS plumbing ------------------------------------------------------------------------
+// rocBLAS serves only the explicit opt-in impl = LIBRARY (a cross-check of the hand-written kernels): every AUTO /
+// FUSED shape runs on this library's own kernels. So libpdeinv.so does not link it: the first LIBRARY call loads
+// librocblas.so.5 with dlopen and resolves the five entry points it uses; without it that call fails loudly
+// (PDEINV_ERR_UNSUPPORTED), and no other path notices. (rocblas.h supplies the types only.)
+struct BlasApi {
+  decltype(&rocblas_create_handle) create_handle = nullptr;
+  decltype(&rocblas_destroy_handle) destroy_handle = nullptr;
+  decltype(&rocblas_set_stream) set_stream = nullptr;
+  decltype(&rocblas_sgemm) sgemm = nullptr;
+  decltype(&rocblas_sgemm_strided_batched) sgemm_strided_batched = nullptr;
+  bool ok = false;
+};
+
+static const BlasApi& blas_api() {
+  static const BlasApi api = [] {
+    BlasApi a{};
+    void* lib = nullptr;
+    for (const char* name : {"librocblas.so.5", "/opt/rocm/lib/librocblas.so.5", "librocblas.so"}) {
+      lib = dlopen(name, RTLD_NOW | RTLD_LOCAL);
+      if (lib) break;
+    }
+    if (!lib) return a;
+    a.create_handle = (decltype(a.create_handle))dlsym(lib, "rocblas_create_handle");
+    a.destroy_handle = (decltype(a.destroy_handle))dlsym(lib, "rocblas_destroy_handle");
+    a.set_stream = (decltype(a.set_stream))dlsym(lib, "rocblas_set_stream");
+    a.sgemm = (decltype(a.sgemm))dlsym(lib, "rocblas_sgemm");
+    a.sgemm_strided_batched = (decltype(a.sgemm_strided_batched))dlsym(lib, "rocblas_sgemm_strided_batched");
+    a.ok = a.create_handle && a.destroy_handle && a.set_stream && a.sgemm && a.sgemm_strided_batched;
+    return a;
+  }();
+  return api;
+}
+
 // One handle per (host thread, device): a rocBLAS handle carries its stream, so a handle shared
 // between threads lets one thread's rocblas_set_stream retarget another thread's GEMMs (the ABI
 // promises reentrancy across distinct streams, include/pdeinv.h). Thread-local handles need no lock
@@ -34,15 +67,15 @@ struct ThreadBlasHandles {
   rocblas_handle h[64] = {};
   ~ThreadBlasHandles() {
     for (rocblas_handle& x : h)
-      if (x) rocblas_destroy_handle(x);
+      if (x) blas_api().destroy_handle(x);
   }
 };
 
 static rocblas_handle blas_handle(int device) {
   thread_local ThreadBlasHandles handles;
-  if (device < 0 || device >= 64) return nullptr;
+  if (device < 0 || device >= 64 || !blas_api().ok) return nullptr;
   if (!handles.h[device]) {
-    if (rocblas_create_handle(&handles.h[device]) != rocblas_status_success) handles.h[device] = nullptr;
+    if (blas_api().create_handle(&handles.h[device]) != rocblas_status_success) handles.h[device] = nullptr;
   }
   return handles.h[device];
 }
@@ -118,14 +151,14 @@ struct Blas {
   // row-major C[R x n_out] = A[R x n_in] . K[n_in x n_out]
   void fwd(const float* A, const float* K, float* C, int64_t R, int n_in, int n_out) {
     const float one = 1.f, zero = 0.f;
-    if (rocblas_sgemm(h, rocblas_operation_none, rocblas_operation_none, n_out, (rocblas_int)R, n_in, &one, K,
+    if (blas_api().sgemm(h, rocblas_operation_none, rocblas_operation_none, n_out, (rocblas_int)R, n_in, &one, K,
                       n_out, A, n_in, &zero, C, n_out) != rocblas_status_success)
       status = 1;
   }
   // row-major C[R x n_in] = A[R x n_out] . K^T
   void bwd(const float* A, const float* K, float* C, int64_t R, int n_in, int n_out) {
     const float one = 1.f, zero = 0.f;
-    if (rocblas_sgemm(h, rocblas_operation_transpose, rocblas_operation_none, n_in, (rocblas_int)R, n_out, &one, K,
+    if (blas_api().sgemm(h, rocblas_operation_transpose, rocblas_operation_none, n_in, (rocblas_int)R, n_out, &one, K,
                       n_out, A, n_out, &zero, C, n_in) != rocblas_status_success)
       status = 1;
   }
@@ -136,12 +169,12 @@ struct Blas {
     S = S < 1 ? 1 : (S > kMaxKSplit ? kMaxKSplit : S);
     const int64_t Ks = R / S, rem = R - S * Ks;
     const int64_t nout = (int64_t)n_in * n_out;
-    if (rocblas_sgemm_strided_batched(h, rocblas_operation_none, rocblas_operation_transpose, n_out, n_in,
+    if (blas_api().sgemm_strided_batched(h, rocblas_operation_none, rocblas_operation_transpose, n_out, n_in,
                                       (rocblas_int)Ks, &one, B, n_out, Ks * n_out, A, n_in, Ks * n_in, &zero, part,
                                       n_out, nout, (rocblas_int)S) != rocblas_status_success)
       status = 1;
     hipLaunchKernelGGL(sum_slices_kernel, dim3(grid_for(nout, kSumCols)), dim3(kBlock), 0, st, part, (int)S, nout, Kbar);
-    if (rem > 0 && rocblas_sgemm(h, rocblas_operation_none, rocblas_operation_transpose, n_out, n_in,
+    if (rem > 0 && blas_api().sgemm(h, rocblas_operation_none, rocblas_operation_transpose, n_out, n_in,
                                  (rocblas_int)rem, &one, B + S * Ks * n_out, n_out, A + S * Ks * n_in, n_in, &one,
                                  Kbar, n_out) != rocblas_status_success)
       status = 1;
@@ -442,11 +475,11 @@ static MlpPlan make_plan(const pdeinv_kfp_mlp_desc* d) {
 using namespace pdeinv;
 
 // The shapes the fused fp32-MFMA path takes. The kernels are compiled for dim in {2, 4, 8, 16} and width in
-// {32, 64, 128, 256, 512} (any depth 1..16, any out_features: mlpf::supported); every other dim <= 16 and
-// width <= 512 runs zero-padded to the next compiled one — exact: padded inputs and K1 rows are zero, padded
+// {32, 64, 128, 256, 512, 1024} (any depth 1..16, any out_features: mlpf::supported); every other dim <= 16 and
+// width <= 1024 runs zero-padded to the next compiled one — exact: padded inputs and K1 rows are zero, padded
 // hidden units have zero weights in and out (common.h MlpPadMap) — at the cost of the padded MACs. The
 // reference's default V_hypothesis is 20 wide (configurations/neural_network/MLP.yaml:4-5). Only
-// impl = LIBRARY (or width > 512) reaches the rocBLAS path.
+// impl = LIBRARY (or width > 1024) reaches the rocBLAS path.
 struct FusedShape {
   int Dp = 0, Wp = 0;
   bool pad = false;
@@ -457,7 +490,7 @@ static bool fused_shape(const pdeinv_kfp_mlp_desc* d, FusedShape* f = nullptr) {
       d->n_layers > kMlpPadMaxL || d->out_features < 1)
     return false;
   int Wp = 0;
-  for (int w : {32, 64, 128, 256, 512})
+  for (int w : {32, 64, 128, 256, 512, 1024})
     if (w >= d->width) { Wp = w; break; }
   const int Dp = pad_dim(d->dim);
   if (!Wp || !mlpf::supported(Dp, d->n_layers, Wp, d->out_features)) return false;
@@ -472,6 +505,15 @@ extern "C" int pdeinv_mlp_fused_supported(int32_t dim, int32_t n_layers, int32_t
   d.dim = dim; d.n_layers = n_layers; d.width = width; d.out_features = out_features;
   d.impl = PDEINV_MLP_IMPL_AUTO;
   return fused_shape(&d) ? 1 : 0;
+}
+
+// PDEINV_MLP_FIRST_ORDER=0 (A/B): the boundary sets take the full second-order chain as the 0T set does
+static bool first_order_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("PDEINV_MLP_FIRST_ORDER");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
 }
 
 static MlpPadMap width_pad_map(const pdeinv_kfp_mlp_desc* d, const FusedShape& f) {
@@ -798,6 +840,8 @@ extern "C" int pdeinv_residual_kfp_mlp(const pdeinv_kfp_mlp_desc* d, const float
         c.params = fparams; c.grad = fgrad; c.poff = poff; c.boff = boff;
         c.c2 = s.c2; c.c3 = s.c3; c.c0 = s.c0;
         c.ws = wsf; c.Bc = Bc;
+        // the initial / terminal sets weight V' (or V) only: no R1 / F2 (kinetic_fokker_planck.py:34-39)
+        c.first_order = s.id != 0 && s.c1 == 0.f && s.c2 == 0.f && first_order_enabled();
         lc.zr = c.z;
         lc.ld = c.ldz;
         const int rc = mlpf::run_chunk(c, mlpf::LossHook{fused_loss_hook, &lc}, st);
@@ -815,8 +859,10 @@ extern "C" int pdeinv_residual_kfp_mlp(const pdeinv_kfp_mlp_desc* d, const float
                  "kfp_mlp: the fused path takes dim <= 16, 1 <= n_layers <= 16, width <= 512 (zero-padded to the "
                  "compiled dims / widths), any out_features");
   Blas blas{blas_handle(dev), st, w + p.off_kpart};
+  PDEINV_REQUIRE(blas_api().ok, PDEINV_ERR_UNSUPPORTED,
+                 "kfp_mlp: impl = LIBRARY needs rocBLAS (librocblas.so.5 could not be loaded)");
   if (!blas.h) return fail(PDEINV_ERR_HIP, "kfp_mlp: rocblas_create_handle failed");
-  if (rocblas_set_stream(blas.h, st) != rocblas_status_success) return fail(PDEINV_ERR_HIP, "kfp_mlp: rocblas_set_stream");
+  if (blas_api().set_stream(blas.h, st) != rocblas_status_success) return fail(PDEINV_ERR_HIP, "kfp_mlp: rocblas_set_stream");
   LibRun run{p, &blas, w, params, grad, poff, boff, st, acc};
   for (const Set& s : sets) {
     PDEINV_REQUIRE(s.n == 0 || s.ld >= 2 * D, PDEINV_ERR_INVALID, "kfp_mlp: row stride < 2*dim");
@@ -999,8 +1045,10 @@ static int kmv_mlp_run(const pdeinv_kmv_mlp_desc* d, const KmvPlan& k, const flo
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return fail(PDEINV_ERR_HIP, "kmv_mlp: hipGetDevice failed");
   Blas blas{blas_handle(dev), st, w + k.lib.off_kpart};
+  PDEINV_REQUIRE(blas_api().ok, PDEINV_ERR_UNSUPPORTED,
+                 "kmv_mlp: impl = LIBRARY needs rocBLAS (librocblas.so.5 could not be loaded)");
   if (!blas.h) return fail(PDEINV_ERR_HIP, "kmv_mlp: rocblas_create_handle failed");
-  if (rocblas_set_stream(blas.h, st) != rocblas_status_success) return fail(PDEINV_ERR_HIP, "kmv_mlp: rocblas_set_stream");
+  if (blas_api().set_stream(blas.h, st) != rocblas_status_success) return fail(PDEINV_ERR_HIP, "kmv_mlp: rocblas_set_stream");
   int64_t poff[18], boff[18];
   param_offsets(D, d->width, d->out_features, d->n_layers, poff, boff);
   LibRun run{k.lib, &blas, w, params, grad, poff, boff, st, acc};
@@ -1076,7 +1124,7 @@ static pdeinv_kfp_mlp_desc kmv_as_kfp(const pdeinv_kmv_mlp_desc* d) {
 
 static bool kmv_use_fused(const pdeinv_kmv_mlp_desc* d) {
   if (d->impl == PDEINV_MLP_IMPL_LIBRARY || kmv_use_pairs(d)) return false;
-  if (d->dim < 1 || d->dim > 8) return false;
+  if (d->dim < 1 || d->dim > 16) return false;
   const pdeinv_kfp_mlp_desc m = kmv_as_kfp(d);
   return fused_shape(&m);
 }
@@ -1263,12 +1311,13 @@ extern "C" int pdeinv_residual_kmv_mlp(const pdeinv_kmv_mlp_desc* d, const float
 #define CASE(DD, DDP) \
   case DD: return kmv_fused_run<DD, DDP>(d, k, z, set_stride, ld, ds, params, (float*)ws, acc, grad, st);
       CASE(1, 2) CASE(2, 2) CASE(3, 4) CASE(4, 4) CASE(5, 8) CASE(6, 8) CASE(7, 8) CASE(8, 8)
+      CASE(9, 16) CASE(10, 16) CASE(11, 16) CASE(12, 16) CASE(13, 16) CASE(14, 16) CASE(15, 16) CASE(16, 16)
 #undef CASE
     }
   }
   PDEINV_REQUIRE(d->impl != PDEINV_MLP_IMPL_FUSED, PDEINV_ERR_UNSUPPORTED,
-                 "kmv_mlp: the hand-written paths need dim <= 8 with width <= 28 (pair kernels), or dim <= 8 with "
-                 "1 <= n_layers <= 16, width <= 512 (fused MFMA path)");
+                 "kmv_mlp: the hand-written paths need dim <= 8 with width <= 28 (pair kernels), or dim <= 16 with "
+                 "1 <= n_layers <= 16, width <= 1024 (fused MFMA path)");
   const KmvPlan k = kmv_plan(d);
   switch (d->dim) {
 #define CASE(DD) case DD: return kmv_mlp_run<DD>(d, k, z, set_stride, ld, ds, params, (float*)ws, acc, grad, st);

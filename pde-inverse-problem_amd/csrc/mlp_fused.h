@@ -36,6 +36,10 @@ struct Chunk {
   const float* wrow = nullptr;
   int64_t ldw = 0;
   bool grad_only = false;
+  // first_order: the set weights only V' (and V) — no |g|^2, no V'', no input-gradient seed (the KFP initial /
+  // terminal sets, kinetic_fokker_planck.py:34-39): R1 (g = grad_x V) and F2 (the forward adjoint of abar0 = 0)
+  // are skipped, and g, the a planes, a1 and the zetabar planes are zeroed so the later products see exact zeros
+  bool first_order = false;
 };
 
 // g = grad_x V [R x d] of the last run_chunk (workspace view)

@@ -38,6 +38,8 @@
 #include <algorithm>
 #include <type_traits>
 
+#include <vector>
+
 #include "mlp_fused.h"
 
 namespace pdeinv {
@@ -1646,7 +1648,7 @@ static bool use_rgemm(int W) {
 // out_features > 64; L = 1 runs the output layer straight off the layer-1 prologue modes
 bool supported(int d, int L, int W, int O) {
   return (d == 2 || d == 4 || d == 8 || d == 16) && L >= 1 && L <= 16 &&
-         (W == 32 || W == 64 || W == 128 || W == 256 || W == 512) && O >= 1;
+         (W == 32 || W == 64 || W == 128 || W == 256 || W == 512 || W == 1024) && O >= 1;
 }
 
 // workspace layout (floats), chunk of Bc rows
@@ -1685,6 +1687,14 @@ static Layout layout(int d, int L, int W, int O, int64_t Bc) {
 size_t workspace_floats(int d, int L, int W, int O, int64_t Bc) { return layout(d, L, W, O, Bc).total; }
 
 const float* grad_rows(const Chunk& c) { return c.ws + layout(c.d, c.L, c.W, c.O, c.Bc).g; }
+
+// zero the first n floats of every plane and the first ng floats of g (first_order chunks)
+static int zero_planes(const std::vector<float*>& planes, size_t n, float* g, size_t ng, hipStream_t st) {
+  for (float* p : planes)
+    if (hipMemsetAsync(p, 0, n * sizeof(float), st) != hipSuccess) return fail(PDEINV_ERR_HIP, "kfp_mlp fused: memset");
+  if (hipMemsetAsync(g, 0, ng * sizeof(float), st) != hipSuccess) return fail(PDEINV_ERR_HIP, "kfp_mlp fused: memset");
+  return 0;
+}
 
 template <int D, int WB>
 static int run_chunk_t(const Chunk& c, const LossHook& loss, hipStream_t st) {
@@ -1744,6 +1754,18 @@ static int run_chunk_t(const Chunk& c, const LossHook& loss, hipStream_t st) {
     hipLaunchKernelGGL(terms_sum_kernel, dim3((unsigned)((R + kT - 1) / kT)), dim3(kT), 0, st, terms, (O + 63) / 64, R);
     return check_launch("kfp_mlp fused terms sum");
   };
+  auto run_g = [&]() {  // g = zeta1 K1^T (grad_x V) from a1
+    if constexpr (WB <= 256) {
+      if (use_l1g_mfma()) {
+        const int blocks = (int)std::min<int64_t>((R + 63) / 64, 2048);
+        hipLaunchKernelGGL((l1_g_mfma_kernel<D, WB>), dim3(blocks), dim3(kT), 0, st, A1, c.z, c.ldz, Kw(1), Bw(1), R, G);
+        return check_launch("kfp_mlp fused g (MFMA)");
+      }
+    }
+    const int blocks = (int)std::min<int64_t>((R + 3) / 4, 2048);
+    hipLaunchKernelGGL((l1_g_kernel<D, WB>), dim3(blocks), dim3(kT), 0, st, A1, c.z, c.ldz, Kw(1), Bw(1), R, G);
+    return check_launch("kfp_mlp fused g");
+  };
   if (L == 1) {
     // one hidden layer: the output layer reads the layer-1 streams straight from the prologue modes (h1,
     // s1 z1', s2 z1'^2 | s1 (abar0 K1)), the reverse product stops at hbar1 (l1_grad_kernel), and the
@@ -1756,22 +1778,15 @@ static int run_chunk_t(const Chunk& c, const LossHook& loss, hipStream_t st) {
       RC((launch_gemm<3, 128, 64, 4, A_L1F, B_NN, E_OUT, D>(a, st)));
       RC(sum_terms());
     }
-    {
-      GemmArgs a = base;
-      a.K = O; a.N = W; a.Bw = Ko; a.pa0 = Ys[0]; a.po0 = A1;
-      RC((launch_gemm1<A_U, B_NT>(a, st)));
-    }
-    if constexpr (WB <= 256) {
-      if (use_l1g_mfma()) {
-        const int blocks = (int)std::min<int64_t>((R + 63) / 64, 2048);
-        hipLaunchKernelGGL((l1_g_mfma_kernel<D, WB>), dim3(blocks), dim3(kT), 0, st, A1, c.z, c.ldz, Kw(1), Bw(1), R, G);
-        RC(check_launch("kfp_mlp fused g (MFMA)"));
+    if (c.first_order) {
+      RC(zero_planes({A1}, (size_t)R * W, G, (size_t)R * D, st));
+    } else {
+      {
+        GemmArgs a = base;
+        a.K = O; a.N = W; a.Bw = Ko; a.pa0 = Ys[0]; a.po0 = A1;
+        RC((launch_gemm1<A_U, B_NT>(a, st)));
       }
-    }
-    if (WB > 256 || !use_l1g_mfma()) {
-      const int blocks = (int)std::min<int64_t>((R + 3) / 4, 2048);
-      hipLaunchKernelGGL((l1_g_kernel<D, WB>), dim3(blocks), dim3(kT), 0, st, A1, c.z, c.ldz, Kw(1), Bw(1), R, G);
-      RC(check_launch("kfp_mlp fused g"));
+      RC(run_g());
     }
     if (c.grad_only) return 0;
     RC(loss.fn(loss.ctx, G, terms, abar0, R, st));
@@ -1830,45 +1845,45 @@ static int run_chunk_t(const Chunk& c, const LossHook& loss, hipStream_t st) {
     RC(sum_terms());
   }
   // ---- R1: grad_x chain -------------------------------------------------------------------
-  {
-    GemmArgs a = base;
-    a.K = O; a.N = W; a.Bw = Ko; a.pa0 = Ys[0]; a.po0 = P(L, P_A);
-    RC((launch_gemm1<A_U, B_NT>(a, st)));
-  }
-  for (int l = L; l >= 2; --l) {
-    GemmArgs a = base;
-    a.K = W; a.N = W; a.Bw = Kw(l); a.pa0 = P(l, P_H); a.pa1 = P(l, P_A);
-    a.po0 = l > 2 ? P(l - 1, P_A) : A1;
-    if (RG) RC((launch_rgemm<1, A_S1MUL, B_NT, E_STORE>(a, st)));
-    else RC((launch_gemm1<A_S1MUL, B_NT>(a, st)));
-  }
-  if constexpr (WB <= 256) {
-    if (use_l1g_mfma()) {
-      const int blocks = (int)std::min<int64_t>((R + 63) / 64, 2048);
-      hipLaunchKernelGGL((l1_g_mfma_kernel<D, WB>), dim3(blocks), dim3(kT), 0, st, A1, c.z, c.ldz, Kw(1), Bw(1), R, G);
-      RC(check_launch("kfp_mlp fused g (MFMA)"));
+  if (c.first_order) {  // no g, no forward adjoint: zeros where the later products read them
+    std::vector<float*> z0{A1};
+    for (int l = 2; l <= L; ++l) {
+      z0.push_back(P(l, P_A));
+      z0.push_back(P(l, P_ZETABAR));
     }
-  }
-  if (WB > 256 || !use_l1g_mfma()) {
-    const int blocks = (int)std::min<int64_t>((R + 3) / 4, 2048);
-    hipLaunchKernelGGL((l1_g_kernel<D, WB>), dim3(blocks), dim3(kT), 0, st, A1, c.z, c.ldz, Kw(1), Bw(1), R, G);
-    RC(check_launch("kfp_mlp fused g"));
+    RC(zero_planes(z0, (size_t)R * W, G, (size_t)R * D, st));
+  } else {
+    {
+      GemmArgs a = base;
+      a.K = O; a.N = W; a.Bw = Ko; a.pa0 = Ys[0]; a.po0 = P(L, P_A);
+      RC((launch_gemm1<A_U, B_NT>(a, st)));
+    }
+    for (int l = L; l >= 2; --l) {
+      GemmArgs a = base;
+      a.K = W; a.N = W; a.Bw = Kw(l); a.pa0 = P(l, P_H); a.pa1 = P(l, P_A);
+      a.po0 = l > 2 ? P(l - 1, P_A) : A1;
+      if (RG) RC((launch_rgemm<1, A_S1MUL, B_NT, E_STORE>(a, st)));
+      else RC((launch_gemm1<A_S1MUL, B_NT>(a, st)));
+    }
+    RC(run_g());
   }
   if (c.grad_only) return 0;  // KMV pass 1: g of every row is all that is needed
   RC(loss.fn(loss.ctx, G, terms, abar0, R, st));
   // ---- F2: forward adjoint ----------------------------------------------------------------
-  {  // abar1 = s1(z1) (abar0 K1) in the prologue
-    GemmArgs a = base;
-    a.K = W; a.N = W; a.Bw = Kw(2); a.po0 = P(2, P_ZETABAR);
-    if (RG) RC((launch_rgemm<1, A_L1A, B_NN, E_STORE, D>(a, st)));
-    else RC((launch_gemm1<A_L1A, B_NN, D>(a, st)));
-  }
-  for (int l = 3; l <= L; ++l) {
-    GemmArgs a = base;
-    a.K = W; a.N = W; a.Bw = Kw(l); a.pa0 = P(l - 1, P_H); a.pa1 = P(l - 1, P_ZETABAR);
-    a.po0 = P(l, P_ZETABAR);
-    if (RG) RC((launch_rgemm<1, A_S1MUL, B_NN, E_STORE>(a, st)));
-    else RC((launch_gemm1<A_S1MUL, B_NN>(a, st)));
+  if (!c.first_order) {
+    {  // abar1 = s1(z1) (abar0 K1) in the prologue
+      GemmArgs a = base;
+      a.K = W; a.N = W; a.Bw = Kw(2); a.po0 = P(2, P_ZETABAR);
+      if (RG) RC((launch_rgemm<1, A_L1A, B_NN, E_STORE, D>(a, st)));
+      else RC((launch_gemm1<A_L1A, B_NN, D>(a, st)));
+    }
+    for (int l = 3; l <= L; ++l) {
+      GemmArgs a = base;
+      a.K = W; a.N = W; a.Bw = Kw(l); a.pa0 = P(l - 1, P_H); a.pa1 = P(l - 1, P_ZETABAR);
+      a.po0 = P(l, P_ZETABAR);
+      if (RG) RC((launch_rgemm<1, A_S1MUL, B_NN, E_STORE>(a, st)));
+      else RC((launch_gemm1<A_S1MUL, B_NN>(a, st)));
+    }
   }
   {
     GemmArgs a = base;
@@ -1969,7 +1984,8 @@ static int run_chunk_d(const Chunk& c, const LossHook& loss, hipStream_t st) {
     case 128: return run_chunk_t<D, 128>(c, loss, st);
     case 256: return run_chunk_t<D, 256>(c, loss, st);
     case 512: return run_chunk_t<D, 512>(c, loss, st);
-    default: return fail(PDEINV_ERR_UNSUPPORTED, "kfp_mlp fused: width must be 32, 64, 128, 256 or 512");
+    case 1024: return run_chunk_t<D, 1024>(c, loss, st);
+    default: return fail(PDEINV_ERR_UNSUPPORTED, "kfp_mlp fused: width must be 32, 64, 128, 256, 512 or 1024");
   }
 }
 

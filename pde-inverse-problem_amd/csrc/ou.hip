@@ -75,7 +75,7 @@ __global__ __launch_bounds__(kBlock) void ou_exact_sample_kernel(OuArgs a) {
   } else {
     const uint4 r = philox4x32_10(make_uint4((uint32_t)g, (uint32_t)((uint64_t)g >> 32), a.ctr_t, 0xD0000000u), a.k0,
                                   a.k1);
-    t = a.tmin + a.tspan * (double)u32_unit(r.x);
+    t = (double)(float)(a.tmin + a.tspan * (double)u32_unit(r.x));  // the fp32 time t_out reports is the one used
   }
   if (tid == 0) {
     if (a.t_out) a.t_out[g] = (float)t;

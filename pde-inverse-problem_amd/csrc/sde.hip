@@ -267,10 +267,17 @@ struct MfNext {
   int32_t np1;       // updates per simulate (n_steps + 1), <= 128
 };
 
+// PDEINV_SIM_QUAD=1 (build flag, A/B): QuadGram below instead of PairGram for the d = 4 step-loop moments. Measured
+// r05 (profiles/r05_c2_quad_ab.txt, three alternating rounds on one box): PairGram 1.455 ms, QuadGram at 5 waves
+// 1.469, at 6 waves 1.466, at 7 waves (16 dwords spilled) 1.553; the no-moment kernel (42 VGPRs, 10 waves) 1.407 on
+// the same box — the waves in flight were not what the moments cost there, so PairGram stays the default.
+#ifndef PDEINV_SIM_QUAD
+#define PDEINV_SIM_QUAD 0
+#endif
 // Step-loop 0T moments at 2d = 8 (the C2 headline kernel), shared by the four lanes of a "quad". PairGram
-// keeps a particle's full sum + Gram (48 accumulators) in its own lane: 96 VGPRs, 5 waves per SIMD, and the
-// store-bound launch runs at 0.77 of the box's write ceiling against 0.95 without moments (42 VGPRs) — the
-// waves in flight, not the FMAs, are what the moments cost. Here the staged rows (already in the wave's LDS
+// keeps a particle's full sum + Gram (48 accumulators) in its own lane: 96 VGPRs, 5 waves per SIMD; the r01 box ran
+// the launch at 0.77 of its write ceiling against 0.95 without moments (42 VGPRs), which suggested the waves in
+// flight were the cost (the r05 A/B above says otherwise on its box). Here the staged rows (already in the wave's LDS
 // slot for the coalesced store) are read back by the four lanes {l, l^8, l^16, l^24} of a quad, and lane
 // class c = (l >> 3) & 3 accumulates, over the quad's four rows, only the Gram entries of the features
 // shifted by 2c: with u_k = z[(k + 2c) mod 8] it sums u0 u0..u5, u1 u1..u3, u1 u5 and (u0, u1) — 12
@@ -458,7 +465,7 @@ __global__ __launch_bounds__(kBlock, MINW) void sde_simulate_kernel(SdeArgs a, c
   const float h_last = a.dt - tau0;
 
   constexpr bool kStaged = (STORE == kStoreStaged) && (M % 4 == 0);
-  constexpr bool kQuad = MOM && M == 8 && kStaged;  // QuadGram: the 0T moments shared by lane quads
+  constexpr bool kQuad = PDEINV_SIM_QUAD && MOM && M == 8 && kStaged;  // QuadGram: the 0T moments shared by lane quads
   PairGram<(MOM && !kQuad ? M : 2)> acc;
   acc.zero();
   [[maybe_unused]] QuadGram qg;
@@ -877,7 +884,8 @@ extern "C" size_t pdeinv_sde_workspace_bytes(const pdeinv_sde_desc* d) {
 #ifndef PDEINV_QUAD_MINW
 #define PDEINV_QUAD_MINW 6
 #endif
-template <int D, int POT, bool MOM> constexpr int kSimMinWaves = (MOM && D == 4 && POT == PDEINV_POT_QUADRATIC) ? PDEINV_QUAD_MINW : 1;
+template <int D, int POT, bool MOM> constexpr int kSimMinWaves =
+    (PDEINV_SIM_QUAD && MOM && D == 4 && POT == PDEINV_POT_QUADRATIC) ? PDEINV_QUAD_MINW : 1;
 
 template <int D, int POT, bool MOM, int KM = 1>
 static void launch_sim(const SdeArgs& a, const float* z0, float* traj, float* tau, float* last,

@@ -365,7 +365,9 @@ LIB, FUSED = 1, 2  # native.MLP_IMPL_LIBRARY / MLP_IMPL_FUSED
     ([4, 64, 40], "quad", 1000, FUSED), ([8, 256, 40], "gmm", 777, FUSED), ([2, 20, 40], "gmm", 1 << 18, FUSED),
     ([4, 64, 64, 80], "quad", 1000, FUSED), ([8, 128, 128, 200], "gmm", 1500, FUSED),
     ([3, 32, 32, 40], "gmm", 1000, FUSED), ([10, 64, 64, 40], "quad", 1000, FUSED), ([1, 32, 32, 5], "quad", 777, FUSED),
-    ([5, 20, 40], "gmm", 1000, 0), ([6, 48, 48, 48, 70], "quad", 1 << 18, 0)])
+    ([5, 20, 40], "gmm", 1000, 0), ([6, 48, 48, 48, 70], "quad", 1 << 18, 0),
+    # width 1024 (and 1000, zero-padded to it) on the hand-written kernels: AUTO never reaches rocBLAS
+    ([4, 1024, 1024, 40], "quad", 1500, 0), ([3, 1000, 40], "gmm", 1 << 18, 0)])
 def test_residual_mlp_vs_restatement(native, dims, true_kind, chunk, impl):
     """V_hypothesis residual (value + d loss/d theta) vs the fp64 restatement whose adjoint is
     FD-checked in tests/test_oracle.py, on both implementations (rocBLAS library path and the
@@ -425,6 +427,34 @@ def test_residual_mlp_fused_chunk_at_offset_limit(native):
     assert np.abs(gb).max() > 0
     with pytest.raises(ValueError, match="2\\^30"):
         native.residual_kfp_mlp(dims, _t(flat), zi, zt, z0[:1024], chunk_rows=(1 << 22) + 64, **kw)
+
+
+@pytest.mark.parametrize("dims", [[8, 256, 256, 40], [4, 64, 40], [2, 32, 32, 32, 40]])
+def test_residual_mlp_boundary_sets_span_chunks(native, dims):
+    """The initial / terminal sets take the first-order chain (no g, no forward adjoint: c_nabla = c_hess = 0 there,
+    kinetic_fokker_planck.py:34-39) — here with boundary sets larger than the 0T set, split over several chunks
+    (5000 rows at chunk 2048), L = 1 / 2 / 3: loss and gradient equal the fp64 restatement and the rocBLAS library
+    path (which runs the full chain)."""
+    rng = np.random.default_rng(sum(dims))
+    d = dims[0]
+    flat = np.concatenate([np.concatenate([rng.standard_normal((dims[i], dims[i + 1])).ravel() * np.sqrt(1.0 / dims[i]),
+                                           0.1 * rng.standard_normal(dims[i + 1])]) for i in range(len(dims) - 1)])
+    P = nr.mlp_unflat(flat, dims)
+    zi, zt, z0 = (rng.standard_normal((m, 2 * d)).astype(np.float32) for m in (5000, 4500, 1500))
+    F = nr.problem_constants(d)
+    kw = dict(true_kind=native.POT_QUADRATIC, true_params=F, gamma=0.5, total_time=2.0, chunk_rows=2048)
+    acc, grad = native.residual_kfp_mlp(dims, _t(flat), _t(zi), _t(zt), _t(z0), impl=FUSED, **kw)
+    acc_l, grad_l = native.residual_kfp_mlp(dims, _t(flat), _t(zi), _t(zt), _t(z0), impl=LIB, **kw)
+    out = native.kfp_terms_finalize(acc, grad, 0.5).cpu().numpy()
+    loss, loss_gt, _ = nr.kfp_mlp_loss(P, zi, zt, z0, nr.grad_quadratic(F), 0.5, 2.0)
+    g_ref = nr.mlp_flat(nr.kfp_mlp_grad_analytic(P, zi, zt, z0, 0.5, 2.0))
+    assert abs(out[0] - loss) < 1e-3 * (1 + abs(loss)), (out[0], loss)
+    assert abs(out[1] - loss_gt) < 1e-3 * (1 + abs(loss_gt))
+    g = grad.cpu().numpy()
+    assert np.max(np.abs(g - g_ref)) < 2e-3 * (1 + np.abs(g_ref).max()), np.max(np.abs(g - g_ref))
+    a, al = acc.cpu().numpy(), acc_l.cpu().numpy()
+    assert np.allclose(a, al, rtol=2e-4, atol=1e-5 * np.abs(al).max())
+    assert np.max(np.abs(g - grad_l.cpu().numpy())) < 2e-4 * (1 + np.abs(g_ref).max())
 
 
 def test_residual_mlp_fused_matches_library(native):

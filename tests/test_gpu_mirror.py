@@ -61,7 +61,9 @@ def test_kmv_residual_vs_pairwise_restatement(native):
                                                 # dims other than 2 / 4 / 8 and one hidden layer on the fused
                                                 # wide-net path (pair rows zero-padded; no rocBLAS)
                                                 (3, 45, 300, 64, 2, 2), (5, 40, 300, 32, 2, 0),
-                                                (2, 50, 300, 64, 1, 2)])
+                                                (2, 50, 300, 64, 1, 2),
+                                                # dims 9..16 on the fused wide-net path (pair rows padded to 16)
+                                                (12, 40, 300, 64, 2, 0), (16, 30, 300, 32, 1, 2)])
 def test_kmv_general_phi_mlp_vs_pairwise_restatement(native, d, n, chunk, W, L, impl):
     """General Phi_theta = V_hypothesis (non-parametric KMV, kinetic_mckean_vlasov.py:11-120) == the
     literal pair-tensor restatement (loss, loss ground truth, terms) and its FD-checked analytic gradient

@@ -230,10 +230,11 @@ def test_abi_argument_validation_without_gpu():
     assert L.pdeinv_realnvp_value_and_grad(None, None, None, 0, None, 0, 0, None, None, None, 0, None) \
         == native.PDEINV_ERR_INVALID
     # the query reports the AUTO path: compiled shapes and the zero-padded envelope (d = 3 -> 4, width 20 -> 32);
-    # width > 512 takes rocBLAS
+    # width > 1024 takes rocBLAS
     assert L.pdeinv_mlp_fused_supported(3, 2, 256, 40) == 1 and L.pdeinv_mlp_fused_supported(8, 2, 256, 40) == 1
     assert L.pdeinv_mlp_fused_supported(8, 1, 256, 40) == 1 and L.pdeinv_mlp_fused_supported(8, 2, 256, 80) == 1
-    assert L.pdeinv_mlp_fused_supported(2, 8, 20, 40) == 1 and L.pdeinv_mlp_fused_supported(8, 2, 1024, 40) == 0
+    assert L.pdeinv_mlp_fused_supported(2, 8, 20, 40) == 1 and L.pdeinv_mlp_fused_supported(8, 2, 1024, 40) == 1
+    assert L.pdeinv_mlp_fused_supported(8, 2, 1025, 40) == 0 and L.pdeinv_mlp_fused_supported(12, 2, 1000, 40) == 1
     assert L.pdeinv_mlp_fused_supported(17, 2, 256, 40) == 0
     assert native.kmv_mlp_path([2] + [20] * 8 + [40]) == "pair_tiles_mfma"
     assert native.kmv_mlp_path([2, 24, 24, 40]) == "pair_ring"

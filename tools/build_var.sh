@@ -15,6 +15,6 @@ esac
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-result -munsafe-fp-atomics \
   -ffp-contract=fast-honor-pragmas -I$C "$@" -c $src -o $B/var/$name.o
 objs=$(ls $B/*.o | grep -v "/$obj.o$")
-/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 $objs $B/var/$name.o -o $B/var/$name.so -L/opt/rocm/lib -lrocblas
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 $objs $B/var/$name.o -o $B/var/$name.so -ldl
 rm -f $C/.var_$name.hip $B/var/$name.o
 echo built $B/var/$name.so
