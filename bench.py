@@ -328,6 +328,29 @@ def run_c2(a, rank, world, dev):
     return out
 
 
+def c3_valu_issue(kern_ms, N, n):
+    """The C3 launch is VALU-issue-bound, and its FMA-only frac leaves out the transcendentals, Philox's
+    v_mad_u64_u32 and the packed moves. profiles/r05_c3_valu.json (tools/c3_valu_model.py) prices the step loop's
+    VALU opcodes with their measured issue cost (tools/valu_rate.hip, shader cycles) and checks the total against
+    the SQ pass of the same launch (SQ_ACTIVE_INST_VALU). Here: the model's issue cycles over this run's launch
+    time at the nominal 2.4 GHz (the clock the FMA peak is quoted at: a lower bound, the chip runs slower under
+    this load), beside the committed busy shares at the profiled launch's own clock (GRBM_GUI_ACTIVE / 8)."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "r05_c3_valu.json")) as f:
+            m = json.load(f)
+    except Exception:
+        return None
+    wave_updates = N / 64 * (n + 1)
+    cyc = m["model_issue_cycles_per_update_asymptotic"]
+    return {"issue_cycles_per_wave_update_model": cyc,
+            "issue_cycles_per_wave_update_launch_profiled": m["launch_cycles_per_update"],
+            "issue_frac_nominal_clock": cyc * wave_updates / (1024 * 2.4e9 * kern_ms / 1e3),
+            "issue_frac_model_profiled": m["model_valu_busy_asymptotic"],
+            "issue_frac_model_profiled_at_3_waves_per_simd": m["model_valu_busy"],
+            "sq_active_inst_valu_share_profiled": m["sq_active_inst_valu_share"],
+            "profiled_clock_ghz": m.get("profiled_clock_ghz"), "source": "profiles/r05_c3_valu.json"}
+
+
 def run_c3(a, rank, world, dev):
     """KFP-GMM d=4, K=8 (BASELINE configs[2]), the reference's online iteration: simulate (traj, tau, last
     written) with the KFP-GMM residual value_and_grad over init = z0, 0T = every trajectory row,
@@ -375,6 +398,8 @@ def run_c3(a, rank, world, dev):
                       traffic_from_profiles("sde_simulate_C3_bytes_per_launch") if (N, n) == (1 << 22, 100) else None,
                       flops_launch=flops)
     out["loss"] = float(last_out[0][0][0].item())
+    if (N, n) == (1 << 22, 100):
+        out["roofline"]["valu_issue"] = c3_valu_issue(kern_ms, N, n)
 
     # untimed context: the same simulator without the residual, and the standalone residual kernel
     # (the offline-dataset path) over the same trajectory, each timed with events on its stream

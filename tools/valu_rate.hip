@@ -4,7 +4,9 @@
 //   real    = s_memtime ticks (shader clock) of the loop, read by every wave: cycles per instruction per SIMD =
 //             ticks / (instructions per wave x W) — the clock the chip actually ran under this load;
 //   nominal = HIP-event wall time x 2.4 GHz (the clock the 157.3 TFLOP/s fp32 peak is quoted at).
-// Prints one JSON line per opcode (tools/c3_valu_model.py reads them).
+// The loop is unrolled 8 x 8 (64 instructions of the opcode per loop branch). Prints one JSON line per opcode; run
+// under rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE (tools/r05_valu_pmc.sh) for the SIMD cycles
+// per instruction in the SQ's own accounting, which tools/c3_valu_model.py prices the C3 step loop with.
 //   hipcc -O3 --offload-arch=gfx950 tools/valu_rate.hip -o tools/_bin/valu_rate && tools/_bin/valu_rate 3
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -19,7 +21,7 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
   for (int c = 0; c < kChains; ++c) x[c] = 1.1f + 1e-6f * (threadIdx.x + c) + seed; \
   const float k1 = 0.999f, k2 = 0.001f;                                              \
   const uint64_t t0 = __builtin_amdgcn_s_memtime();                                  \
-  for (int it = 0; it < kIters; ++it) {                                              \
+  _Pragma("unroll 8") for (int it = 0; it < kIters; ++it) {                          \
     _Pragma("unroll") for (int c = 0; c < kChains; ++c) asm volatile(ASM : "+v"(x[c]) : "v"(k1), "v"(k2)); \
   }                                                                                  \
   const uint64_t t1 = __builtin_amdgcn_s_memtime();                                  \
@@ -33,7 +35,7 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
   for (int c = 0; c < kChains; ++c) x[c] = f32x2{1.1f + seed + c, 0.9f - 1e-6f * threadIdx.x}; \
   const f32x2 k1 = {0.999f, 0.998f}, k2 = {0.001f, 0.002f};                          \
   const uint64_t t0 = __builtin_amdgcn_s_memtime();                                  \
-  for (int it = 0; it < kIters; ++it) {                                              \
+  _Pragma("unroll 8") for (int it = 0; it < kIters; ++it) {                          \
     _Pragma("unroll") for (int c = 0; c < kChains; ++c) asm volatile(ASM : "+v"(x[c]) : "v"(k1), "v"(k2)); \
   }                                                                                  \
   const uint64_t t1 = __builtin_amdgcn_s_memtime();                                  \
@@ -65,11 +67,32 @@ KP(k_pk_add, "v_pk_add_f32 %0, %0, %1")
 KP(k_mov_b64, "v_mov_b64 %0, %1")
 KP(k_lshl_add_u64, "v_lshl_add_u64 %0, %0, 1, %1")
 
+// a transcendental beside other VALU work: chain 0 v_exp_f32, chains 1..7 v_pk_fma_f32 (the C3 loop issues one
+// transcendental per ~15 other VALU instructions) — prices the exp when it is not the only thing issuing
+__global__ void k_mix_exp_pk(float* out, uint64_t* ticks, float seed) {
+  f32x2 x[kChains];
+  for (int c = 0; c < kChains; ++c) x[c] = f32x2{1.1f + seed + c, 0.9f - 1e-6f * threadIdx.x};
+  const f32x2 k1 = {0.999f, 0.998f}, k2 = {0.001f, 0.002f};
+  const uint64_t t0 = __builtin_amdgcn_s_memtime();
+#pragma unroll 8
+  for (int it = 0; it < kIters; ++it) {
+    asm volatile("v_exp_f32 %0, %0" : "+v"(x[0][0]));
+#pragma unroll
+    for (int c = 1; c < kChains; ++c) asm volatile("v_pk_fma_f32 %0, %0, %1, %2" : "+v"(x[c]) : "v"(k1), "v"(k2));
+  }
+  const uint64_t t1 = __builtin_amdgcn_s_memtime();
+  float s = 0;
+  for (int c = 0; c < kChains; ++c) s += x[c][0] + x[c][1];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+  if ((threadIdx.x & 63) == 0) ticks[blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64] = t1 - t0;
+}
+
 __global__ void k_mad_u64(float* out, uint64_t* ticks, float seed) {
   uint64_t x[kChains];
   for (int c = 0; c < kChains; ++c) x[c] = 0x12345u + threadIdx.x * 7 + c + (uint32_t)seed;
   const uint32_t m = 0xD2511F53u;
   const uint64_t t0 = __builtin_amdgcn_s_memtime();
+#pragma unroll 8
   for (int it = 0; it < kIters; ++it) {
 #pragma unroll
     for (int c = 0; c < kChains; ++c) {
@@ -101,12 +124,16 @@ int main(int argc, char** argv) {
   hipEvent_t a, b;
   hipEventCreate(&a);
   hipEventCreate(&b);
+  // dynamic LDS per block sized so that exactly W blocks fit on a CU (160 KiB / W): the dispatcher cannot stack more
+  // on some CUs than on others, so every SIMD runs W waves for the whole launch
+  const size_t lds = (size_t)(160 * 1024 / W) - 1024;
   auto run = [&](const char* name, void (*k)(float*, uint64_t*, float)) {
-    hipLaunchKernelGGL(k, dim3(blocks), dim3(threads), 0, 0, buf, tk, 1.f);
+    hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(k, dim3(blocks), dim3(threads), lds, 0, buf, tk, 1.f);
     hipDeviceSynchronize();
     hipEventRecord(a);
     const int reps = 5;
-    for (int r = 0; r < reps; ++r) hipLaunchKernelGGL(k, dim3(blocks), dim3(threads), 0, 0, buf, tk, 1.f);
+    for (int r = 0; r < reps; ++r) hipLaunchKernelGGL(k, dim3(blocks), dim3(threads), lds, 0, buf, tk, 1.f);
     hipEventRecord(b);
     hipEventSynchronize(b);
     float ms;
@@ -140,6 +167,7 @@ int main(int argc, char** argv) {
   run("v_mov_b64", k_mov_b64);
   run("v_lshl_add_u64", k_lshl_add_u64);
   run("v_mad_u64_u32", k_mad_u64);
+  run("mix: v_exp_f32 + 7 v_pk_fma_f32", k_mix_exp_pk);
   hipFree(buf);
   hipFree(tk);
   free(h);
