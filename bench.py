@@ -330,13 +330,13 @@ def run_c2(a, rank, world, dev):
 
 def c3_valu_issue(kern_ms, N, n):
     """The C3 launch is VALU-issue-bound, and its FMA-only frac leaves out the transcendentals, Philox's
-    v_mad_u64_u32 and the packed moves. profiles/r05_c3_valu.json (tools/c3_valu_model.py) prices the step loop's
+    v_mad_u64_u32 and the packed moves. profiles/c3_valu_issue.json (tools/c3_valu_model.py) prices the step loop's
     VALU opcodes with their measured issue cost (tools/valu_rate.hip, shader cycles) and checks the total against
     the SQ pass of the same launch (SQ_ACTIVE_INST_VALU). Here: the model's issue cycles over this run's launch
     time at the nominal 2.4 GHz (the clock the FMA peak is quoted at: a lower bound, the chip runs slower under
     this load), beside the committed busy shares at the profiled launch's own clock (GRBM_GUI_ACTIVE / 8)."""
     try:
-        with open(os.path.join(ROOT, "profiles", "r05_c3_valu.json")) as f:
+        with open(os.path.join(ROOT, "profiles", "c3_valu_issue.json")) as f:
             m = json.load(f)
     except Exception:
         return None
@@ -348,7 +348,7 @@ def c3_valu_issue(kern_ms, N, n):
             "issue_frac_model_profiled": m["model_valu_busy_asymptotic"],
             "issue_frac_model_profiled_at_3_waves_per_simd": m["model_valu_busy"],
             "sq_active_inst_valu_share_profiled": m["sq_active_inst_valu_share"],
-            "profiled_clock_ghz": m.get("profiled_clock_ghz"), "source": "profiles/r05_c3_valu.json"}
+            "profiled_clock_ghz": m.get("profiled_clock_ghz"), "source": "profiles/c3_valu_issue.json"}
 
 
 def run_c3(a, rank, world, dev):

@@ -18,7 +18,7 @@ SQ_ACTIVE_INST_VALU is reported beside it but is not an issue-cycle count: it ch
 instruction (two for a transcendental) whatever the opcode's real cost (0.68-1.26 "busy" in the saturated
 microbenchmarks).
 
-    python tools/c3_valu_model.py <sde device .s> <pmc dir: valu_rate/, c3_sq1/, c3_sq2/> > profiles/r05_c3_valu.json
+    python tools/c3_valu_model.py <sde device .s> <pmc dir: valu_rate/, c3_sq1/, c3_sq2/> > profiles/c3_valu_issue.json
 """
 import collections
 import csv
