@@ -193,7 +193,11 @@ __device__ __forceinline__ void store_rows_staged(float* wave_dst, const float* 
   if (n_valid == kWave) {  // wave-uniform: every full wave stores unguarded (one lgkmcnt wait)
 #pragma unroll
     for (int k = 0; k < M / 4; ++k)
+#if PDEINV_SIM_PLAIN_STORES
+      *reinterpret_cast<f32x4*>(wave_dst + 4 * (k * 64 + lane)) = v[k];
+#else
       __builtin_nontemporal_store(v[k], reinterpret_cast<f32x4*>(wave_dst + 4 * (k * 64 + lane)));
+#endif
   } else {
 #pragma unroll
     for (int k = 0; k < M / 4; ++k) {

@@ -115,6 +115,32 @@ def test_ou_moments_batched_match_oracle():
         assert np.allclose(C, np.transpose(C, (0, 2, 1)))
 
 
+def test_ou_exact_sampler_abi_validation_and_van_loan_scaling():
+    """pdeinv_ou_exact_sample rejects a null descriptor, an unsupported dimension, a bad Taylor degree and
+    t_min > t_max before any HIP call; the host's per-problem constants keep |B|_1 t_max / 2^s <= 1 (the scaled
+    Taylor sum's truncation bound) and B^0 = I."""
+    import ctypes
+    from example_problems.kinetic_fokker_planck_example_OU import initialize_configuration, van_loan_powers
+    from utils import native
+    L = native.lib()
+    assert ctypes.sizeof(native.OuDesc) == 56
+    call = lambda d: L.pdeinv_ou_exact_sample(d, 1, 1, 1, 0, 0, 0, None, None, None, None, None, None)
+    assert call(None) == native.PDEINV_ERR_INVALID
+    for kw, err in (({"n": 3}, native.PDEINV_ERR_UNSUPPORTED), ({"n": 34}, native.PDEINV_ERR_UNSUPPORTED),
+                    ({"taylor_degree": 0}, native.PDEINV_ERR_INVALID), ({"t_min": 2.0, "t_max": 1.0}, native.PDEINV_ERR_INVALID),
+                    ({}, native.PDEINV_ERR_INVALID)):  # ({}: valid shape, null device pointers)
+        d = native.OuDesc(8, 18, 3, 1e-4, 2.0, None, None, None)
+        for k, v in kw.items():
+            setattr(d, k, v)
+        assert call(ctypes.byref(d)) == err, (kw, L.pdeinv_last_error())
+    for dim in (1, 4, 16):
+        ic = initialize_configuration(dim)
+        pw, s = van_loan_powers(ic, 2.0)
+        n2 = 4 * dim
+        assert pw.shape == (19, n2, n2) and np.array_equal(pw[0], np.eye(n2))
+        assert np.abs(pw[1]).sum(axis=0).max() * 2.0 / 2.0 ** s <= 1.0
+
+
 def test_adam_matches_optax_semantics():
     import torch
     from core.trainer import Adam, cosine_decay_schedule
