@@ -1,5 +1,5 @@
 """Per-residual HBM traffic of the C5 MLP residual from a tools/profile_r02.sh C5 run: the sum over every
-MLP-residual dispatch (mlpf::*, mlp_loss) of FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE, divided by
+MLP-residual dispatch (mlpf::*, mlp_loss, the runtime fills of the first-order boundary chunks) of FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE, divided by
 the number of residual launches (mlp_loss dispatches / chunks per residual).
     python tools/c5_traffic.py gpurun_out/prof_r02/C5 [chunks_per_residual=10]"""
 import csv
@@ -15,7 +15,8 @@ for counter, sub, scale in (("FETCH_SIZE", "fetch", 2.0), ("WRITE_SIZE", "write"
     for f in glob.glob(os.path.join(root, sub, "**", "*counter_collection.csv"), recursive=True):
         for row in csv.DictReader(open(f)):
             k = row["Kernel_Name"]
-            if row["Counter_Name"] != counter or not ("mlpf::" in k or "mlp_loss" in k):
+            # + the runtime fills of the first-order boundary chunks (g / a / zetabar planes zeroed, r05)
+            if row["Counter_Name"] != counter or not ("mlpf::" in k or "mlp_loss" in k or "fillBuffer" in k):
                 continue
             s += float(row["Counter_Value"]) * 1024 * scale
             n += "mlp_loss" in k
