@@ -31,6 +31,8 @@
 //   L1    layer-1 act_bwd + K1 / b1 gradient   VALU, columns per thread, rows looped
 //   G     Ko += [h2..abar2]^T [ybar..u];  K2 += [h1..abar1]^T [zbar2..zeta2] (layer-1 streams rebuilt
 //         from the rows in the A prologue: the h1 / abar1 planes never exist)
+// First-order chunks (the initial / terminal sets, c1 = c2 = 0; W in {128, 256}) run run_chunk_fo2 instead: the
+// same steps on two streams [h, z'] / [zbar, z'bar], without R1, g, F2 and UB (see there).
 #include <math.h>
 
 #include <stdlib.h>
@@ -82,13 +84,18 @@ __device__ __forceinline__ int xcd_linear(int b, int nb) {
   return x < r ? x * (q + 1) + l : r * (q + 1) + (x - r) * q + l;
 }
 
-enum { A_RAW1 = 0, A_FWD, A_S1MUL, A_U, A_S3, A_L1F, A_L1A };
+enum { A_RAW1 = 0, A_FWD, A_S1MUL, A_U, A_S3, A_L1F, A_L1A, A_FWD2, A_S2 };
 // A_L1F / A_L1A build the layer-1 streams in the prologue from the sample rows (no h1 planes):
 //   A_L1F: [h1, s1 z1', s2 z1'^2] with z1 = x K1 + b1, z1' = v K1      (the FWD operand)
 //   A_L1A: abar1 = s1(z1) (abar0 K1)                                      (the F2 operand)
+// A_FWD2 / A_S2 are the first-order chain's two-stream forms of A_FWD / A_S3 ([h, s1 z'] | two raw planes).
 // One thread owns one row (x and v | abar0 in registers), K1^T and b1 sit in LDS (broadcast reads).
 enum { B_NN = 0, B_NT };
-enum { E_ACT_FWD = 0, E_OUT, E_STORE, E_STORE3, E_SEEDS, E_ACT_BWD };
+enum { E_ACT_FWD = 0, E_OUT, E_STORE, E_STORE3, E_SEEDS, E_ACT_BWD, E_OUT_SEEDS1 };
+// E_OUT_SEEDS1 (first-order chunks, S = 2): the output layer's E_OUT terms and, in the same epilogue, the reverse
+// seeds ybar = 2 c3 y' + 2 c0 y, y'bar = 2 c3 y (c1 = c2 = 0 there, so ubar = 0 and y''bar = 0) with the output bias
+// gradient partials — the UB product and the y planes are not needed. S = 2 epilogues carry only the h and z'
+// streams (E_ACT_FWD / E_STORE3) and, in E_ACT_BWD, drop the z'' and adjoint (a zetabar) terms, which are zero there.
 
 struct GemmArgs {
   int64_t R;
@@ -139,7 +146,7 @@ __device__ __forceinline__ void l1_project(const float* x, const float* y, const
 template <int BM, int AM>
 struct ARegs {
   static constexpr int NE = BM * BK / kT;  // elements per thread
-  static constexpr int NV = (AM == A_FWD || AM == A_S3) ? 3 : (AM == A_S1MUL ? 2 : 1);
+  static constexpr int NV = (AM == A_FWD || AM == A_S3) ? 3 : ((AM == A_S1MUL || AM == A_FWD2 || AM == A_S2) ? 2 : 1);
   float v[NE][NV > 0 ? NV : 1];
 };
 
@@ -184,6 +191,13 @@ __device__ __forceinline__ void store_a(const GemmArgs& a, const ARegs<BM, AM>& 
       v0 = 2.f * ra.v[j][0];
     } else if constexpr (AM == A_RAW1) {
       v0 = ra.v[j][0];
+    } else if constexpr (AM == A_FWD2) {
+      const float h = ra.v[j][0];
+      v0 = h;
+      v1 = (1.f - h * h) * ra.v[j][1];
+    } else if constexpr (AM == A_S2) {
+      v0 = ra.v[j][0];
+      v1 = ra.v[j][1];
     } else {  // A_S3
       v0 = ra.v[j][0];
       v1 = ra.v[j][1];
@@ -315,7 +329,7 @@ __global__ __launch_bounds__(kT, 2) void fgemm(GemmArgs a) {
       // the last tile of a K that is not a BK multiple (the reverse K = out_features product, A_S3)
       // stops at its last valid k pair: a wave-uniform skip instead of MFMAs on the zero padding (in the
       // other modes the branch only added spills: not compiled there)
-      const int kv = AM == A_S3 ? a.K - k0 : BK;
+      const int kv = (AM == A_S3 || AM == A_S2) ? a.K - k0 : BK;
 #pragma unroll
       for (int kk = 0; kk < BK; kk += 2) {
         if (kk < kv) {
@@ -362,7 +376,7 @@ __global__ __launch_bounds__(kT, 2) void fgemm(GemmArgs a) {
               if (ok) {
                 sto(a.po0, o, ftanh(acc[0][mi][ni][q] + bn));
                 sto(a.po1, o, acc[1][mi][ni][q]);
-                sto(a.po2, o, acc[2][mi][ni][q]);
+                if constexpr (S > 2) sto(a.po2, o, acc[S - 1][mi][ni][q]);
               }
             } else if constexpr (EM == E_STORE) {
               if (ok) sto(a.po0, o, acc[0][mi][ni][q]);
@@ -370,7 +384,7 @@ __global__ __launch_bounds__(kT, 2) void fgemm(GemmArgs a) {
               if (ok) {
                 sto(a.po0, o, acc[0][mi][ni][q]);
                 sto(a.po1, o, acc[1][mi][ni][q]);
-                sto(a.po2, o, acc[2][mi][ni][q]);
+                if constexpr (S > 2) sto(a.po2, o, acc[S - 1][mi][ni][q]);
               }
             } else if constexpr (EM == E_OUT) {
               if (ok) {
@@ -395,14 +409,24 @@ __global__ __launch_bounds__(kT, 2) void fgemm(GemmArgs a) {
               }
             } else if constexpr (EM == E_ACT_BWD) {
               if (ok) {
-                const float hb = acc[0][mi][ni][q], hdb = acc[1][mi][ni][q], hddb = acc[2][mi][ni][q];
-                const float h = ldo(a.pe0, o), zd = ldo(a.pe1, o), zdd = ldo(a.pe2, o), aL = ldo(a.pe3, o), zb = ldo(a.pe4, o);
-                const float s1 = 1.f - h * h, s2 = -2.f * h * s1, s3 = -2.f * s1 * s1 - 2.f * h * s2;
-                const float zbar = s1 * hb + s2 * zd * hdb + (s2 * zdd + s3 * zd * zd) * hddb + s2 * aL * zb;
-                sto(a.po0, o, zbar);
-                sto(a.po1, o, s1 * hdb + 2.f * s2 * zd * hddb);
-                sto(a.po2, o, s1 * hddb);
-                pacc[ni] += zbar;
+                const float hb = acc[0][mi][ni][q], hdb = acc[1][mi][ni][q];
+                const float h = ldo(a.pe0, o), zd = ldo(a.pe1, o);
+                const float s1 = 1.f - h * h, s2 = -2.f * h * s1;
+                if constexpr (S > 2) {
+                  const float hddb = acc[S - 1][mi][ni][q];
+                  const float zdd = ldo(a.pe2, o), aL = ldo(a.pe3, o), zb = ldo(a.pe4, o);
+                  const float s3 = -2.f * s1 * s1 - 2.f * h * s2;
+                  const float zbar = s1 * hb + s2 * zd * hdb + (s2 * zdd + s3 * zd * zd) * hddb + s2 * aL * zb;
+                  sto(a.po0, o, zbar);
+                  sto(a.po1, o, s1 * hdb + 2.f * s2 * zd * hddb);
+                  sto(a.po2, o, s1 * hddb);
+                  pacc[ni] += zbar;
+                } else {  // first-order chain: h'' bar = 0, a zetabar = 0
+                  const float zbar = s1 * hb + s2 * zd * hdb;
+                  sto(a.po0, o, zbar);
+                  sto(a.po1, o, s1 * hdb);
+                  pacc[ni] += zbar;
+                }
               }
             }
           }
@@ -557,10 +581,11 @@ __global__ __launch_bounds__(kT) void l1_g_mfma_kernel(const float* __restrict__
 //   zbar1 = s1 hb + s2 z1' h'b + s3 z1'^2 h''b + s2 a1 zetabar1,  z'bar1 = s1 h'b + 2 s2 z1' h''b,
 //   zeta1 = s1 a1;  K1[i][k] += x_i zbar1 + v_i z'bar1 + abar0_i zeta1,  b1[k] += zbar1
 // (the third input stream h0'' = 0 carries nothing). Thread owns columns, loops rows; per-block
-// partial slab [(D + 1) x W] (K1 rows then b1 = the flat parameter order).
+// partial slab [(D + 1) x W] (K1 rows then b1 = the flat parameter order). FO (first-order chunks): h''bar = 0
+// and a1 = abar0 = 0, so zbar1 = s1 hb + s2 z1' h'b, z'bar1 = s1 h'b — hb2, a1 and abar0 are not read.
 constexpr int kL1Rows = 64;  // rows staged in LDS per step
 
-template <int D, int W>
+template <int D, int W, bool FO = false>
 __global__ __launch_bounds__(kT) void l1_grad_kernel(const float* __restrict__ hb0, const float* __restrict__ hb1,
                                                      const float* __restrict__ hb2, const float* __restrict__ a1,
                                                      const float* __restrict__ z, int64_t ldz,
@@ -570,7 +595,8 @@ __global__ __launch_bounds__(kT) void l1_grad_kernel(const float* __restrict__ h
   constexpr int CW = W < kT ? W : kT;       // columns covered per pass
   constexpr int CPT = W / CW;               // columns per thread
   constexpr int RPH = kT / CW;              // row phases
-  __shared__ float xs[kL1Rows * 3 * D];
+  constexpr int XC = FO ? 2 * D : 3 * D;  // staged row: x | v (| abar0)
+  __shared__ float xs[kL1Rows * XC];
   __shared__ float red[(RPH > 1 ? RPH : 1) * W];
   const int tid = threadIdx.x, c0 = tid % CW, ph = tid / CW;
   float k1[CPT][D], bb[CPT], pacc[CPT][D + 1];
@@ -586,36 +612,52 @@ __global__ __launch_bounds__(kT) void l1_grad_kernel(const float* __restrict__ h
   const int64_t re = rs + rpb < R ? rs + rpb : R;
   for (int64_t rb = rs; rb < re; rb += kL1Rows) {
     __syncthreads();
-    for (int e = tid; e < kL1Rows * 3 * D; e += kT) {
-      const int m = e / (3 * D), c = e - m * (3 * D);
+    for (int e = tid; e < kL1Rows * XC; e += kT) {
+      const int m = e / XC, c = e - m * XC;
       const int64_t r = rb + m;
       xs[e] = r < re ? (c < 2 * D ? z[r * ldz + c] : abar0[r * D + c - 2 * D]) : 0.f;
     }
     __syncthreads();
     const int nr = (int)(re - rb < kL1Rows ? re - rb : kL1Rows);
     for (int m = ph; m < nr; m += RPH) {
-      const float* x = xs + m * 3 * D;
+      const float* x = xs + m * XC;
       const int64_t rowo = (rb + m) * W;
 #pragma unroll
       for (int j = 0; j < CPT; ++j) {
         const int64_t o = rowo + c0 + CW * j;
-        const float hb = hb0[o], hdb = hb1[o], hddb = hb2[o], aL = a1[o];
-        float zz = bb[j], zd = 0.f, zb = 0.f;
+        if constexpr (FO) {
+          const float hb = hb0[o], hdb = hb1[o];
+          float zz = bb[j], zd = 0.f;
 #pragma unroll
-        for (int i = 0; i < D; ++i) {
-          zz = fmaf(x[i], k1[j][i], zz);
-          zd = fmaf(x[D + i], k1[j][i], zd);
-          zb = fmaf(x[2 * D + i], k1[j][i], zb);
+          for (int i = 0; i < D; ++i) {
+            zz = fmaf(x[i], k1[j][i], zz);
+            zd = fmaf(x[D + i], k1[j][i], zd);
+          }
+          const float h = ftanh(zz);
+          const float s1 = 1.f - h * h, s2 = -2.f * h * s1;
+          const float zbar = s1 * hb + s2 * zd * hdb, zdbar = s1 * hdb;
+#pragma unroll
+          for (int i = 0; i < D; ++i) pacc[j][i] = fmaf(x[i], zbar, fmaf(x[D + i], zdbar, pacc[j][i]));
+          pacc[j][D] += zbar;
+        } else {
+          const float hb = hb0[o], hdb = hb1[o], hddb = hb2[o], aL = a1[o];
+          float zz = bb[j], zd = 0.f, zb = 0.f;
+#pragma unroll
+          for (int i = 0; i < D; ++i) {
+            zz = fmaf(x[i], k1[j][i], zz);
+            zd = fmaf(x[D + i], k1[j][i], zd);
+            zb = fmaf(x[2 * D + i], k1[j][i], zb);
+          }
+          const float h = ftanh(zz);
+          const float s1 = 1.f - h * h, s2 = -2.f * h * s1, s3 = -2.f * s1 * s1 - 2.f * h * s2;
+          const float zbar = s1 * hb + s2 * zd * hdb + s3 * zd * zd * hddb + s2 * aL * zb;
+          const float zdbar = s1 * hdb + 2.f * s2 * zd * hddb;
+          const float zeta = s1 * aL;
+#pragma unroll
+          for (int i = 0; i < D; ++i)
+            pacc[j][i] = fmaf(x[i], zbar, fmaf(x[D + i], zdbar, fmaf(x[2 * D + i], zeta, pacc[j][i])));
+          pacc[j][D] += zbar;
         }
-        const float h = ftanh(zz);
-        const float s1 = 1.f - h * h, s2 = -2.f * h * s1, s3 = -2.f * s1 * s1 - 2.f * h * s2;
-        const float zbar = s1 * hb + s2 * zd * hdb + s3 * zd * zd * hddb + s2 * aL * zb;
-        const float zdbar = s1 * hdb + 2.f * s2 * zd * hddb;
-        const float zeta = s1 * aL;
-#pragma unroll
-        for (int i = 0; i < D; ++i)
-          pacc[j][i] = fmaf(x[i], zbar, fmaf(x[D + i], zdbar, fmaf(x[2 * D + i], zeta, pacc[j][i])));
-        pacc[j][D] += zbar;
       }
     }
   }
@@ -893,7 +935,8 @@ constexpr int kRGridCap = 256;      // one workgroup per CU (LDS-bound)
 
 template <int AM>
 constexpr int rg_planes() {
-  return (AM == A_FWD || AM == A_S3) ? 3 : (AM == A_S1MUL ? 2 : ((AM == A_U || AM == A_RAW1) ? 1 : 0));
+  return (AM == A_FWD || AM == A_S3) ? 3
+         : ((AM == A_S1MUL || AM == A_FWD2 || AM == A_S2) ? 2 : ((AM == A_U || AM == A_RAW1) ? 1 : 0));
 }
 
 bool rgemm_shape(int K, int N) { return K % 64 == 0 && K <= 256 && N % kRBN == 0; }
@@ -909,14 +952,15 @@ __global__ __launch_bounds__(NW * 64, 1) void rgemm(GemmArgs a) {
   constexpr int NT = NW * 64;                                            // threads (NW waves)
   constexpr int WGN = BNC / (32 * NI), WGM = NW / WGN, BMR = 32 * WGM;  // waves along N / M, block rows
   static_assert((NI == 2 || NI == 4) && WGN >= 1 && WGN * WGM == NW, "rgemm wave grid");
-  static_assert(EM != E_OUT || WGN == 1, "E_OUT reduces each row inside one wave");
+  static_assert((EM != E_OUT && EM != E_OUT_SEEDS1) || WGN == 1, "E_OUT reduces each row inside one wave");
   constexpr bool L1 = a_is_l1<AM>();
   constexpr int NV = rg_planes<AM>();
   constexpr int SK = L1 ? k1_stride<D>() : 1;
-  constexpr int NP = (EM == E_ACT_BWD || EM == E_SEEDS) ? 1 : 0;
+  constexpr int NP = (EM == E_ACT_BWD || EM == E_SEEDS || EM == E_OUT_SEEDS1) ? 1 : 0;
   static_assert(!L1 || D > 0, "layer-1 modes need D");
   static_assert(EM == E_ACT_FWD || EM == E_STORE || EM == E_STORE3 || EM == E_ACT_BWD || EM == E_OUT ||
-                    EM == E_SEEDS, "rgemm epilogues");
+                    EM == E_SEEDS || EM == E_OUT_SEEDS1, "rgemm epilogues");
+  static_assert(EM != E_OUT_SEEDS1 || S == 2, "the first-order output epilogue takes the h and z' streams");
   extern __shared__ float lds[];
   const int Kp = a.K + 4;                          // Bt row pitch: ds_read_b128 of 16 lanes' rows conflict-free
   float* Bt = lds;                                 // [BNC][Kp]: Bt[n][k] = B[k][n0 + n]  (V = 3: [K][BNC + 1])
@@ -1045,7 +1089,7 @@ __global__ __launch_bounds__(NW * 64, 1) void rgemm(GemmArgs a) {
           if constexpr (AM == A_L1F) {
             at[0][q] = h;
             at[1][q] = s1 * zy;
-            at[2][q] = -2.f * h * s1 * zy * zy;
+            if constexpr (S > 2) at[S - 1][q] = -2.f * h * s1 * zy * zy;
           } else {
             at[0][q] = s1 * zy;
           }
@@ -1070,6 +1114,13 @@ __global__ __launch_bounds__(NW * 64, 1) void rgemm(GemmArgs a) {
           av[0] = 2.f * t[0][s];
         } else if constexpr (AM == A_RAW1) {
           av[0] = t[0][s];
+        } else if constexpr (AM == A_FWD2) {
+          const float h = t[0][s];
+          av[0] = h;
+          av[1] = (1.f - h * h) * t[1][s];
+        } else if constexpr (AM == A_S2) {
+          av[0] = t[0][s];
+          av[1] = t[1][s];
         } else {  // A_S3
           av[0] = t[0][s];
           av[1] = t[1][s];
@@ -1123,7 +1174,7 @@ __global__ __launch_bounds__(NW * 64, 1) void rgemm(GemmArgs a) {
     auto epilogue = [&](auto check) {
       constexpr bool CHECK = decltype(check)::value;
       [[maybe_unused]] float t0[16], t1[16], t2[16];  // E_OUT: the row's sum y^2, y y', y'^2 + y y''
-      if constexpr (EM == E_OUT) {
+      if constexpr (EM == E_OUT || EM == E_OUT_SEEDS1) {
 #pragma unroll
         for (int q = 0; q < 16; ++q) t0[q] = t1[q] = t2[q] = 0.f;
       }
@@ -1132,7 +1183,7 @@ __global__ __launch_bounds__(NW * 64, 1) void rgemm(GemmArgs a) {
         const int n = n0 + wn * 32 * NI + ni * 32 + l31;
         const bool nv = BNC == kRBN || n < N;  // output-layer blocks: columns past N are padding
         [[maybe_unused]] float bn = 0.f;
-        if constexpr (EM == E_ACT_FWD || EM == E_OUT) bn = a.bias[nv ? n : 0];
+        if constexpr (EM == E_ACT_FWD || EM == E_OUT || EM == E_OUT_SEEDS1) bn = a.bias[nv ? n : 0];
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
           const int r = r0 + wm * 32 + (q & 3) + 8 * (q >> 2) + 4 * hi;
@@ -1142,7 +1193,7 @@ __global__ __launch_bounds__(NW * 64, 1) void rgemm(GemmArgs a) {
             if (ok) {
               sto(a.po0, o, ftanh(acc[0][ni][q] + bn));
               sto(a.po1, o, acc[1][ni][q]);
-              sto(a.po2, o, acc[2][ni][q]);
+              if constexpr (S > 2) sto(a.po2, o, acc[S - 1][ni][q]);
             }
           } else if constexpr (EM == E_STORE) {
             if (ok) sto(a.po0, o, acc[0][ni][q]);
@@ -1150,7 +1201,19 @@ __global__ __launch_bounds__(NW * 64, 1) void rgemm(GemmArgs a) {
             if (ok) {
               sto(a.po0, o, acc[0][ni][q]);
               sto(a.po1, o, acc[1][ni][q]);
-              sto(a.po2, o, acc[2][ni][q]);
+              if constexpr (S > 2) sto(a.po2, o, acc[S - 1][ni][q]);
+            }
+          } else if constexpr (EM == E_OUT_SEEDS1) {
+            if (ok) {
+              const float y = acc[0][ni][q] + bn, yd = acc[1][ni][q];
+              t0[q] = fmaf(y, y, t0[q]);
+              t1[q] = fmaf(y, yd, t1[q]);
+              t2[q] = fmaf(yd, yd, t2[q]);
+              const float c0r = a.wrow ? a.c0 * a.wrow[(int64_t)r * a.ldw] : a.c0;
+              const float yb = 2.f * a.c3 * yd + 2.f * c0r * y;
+              sto(a.po0, o, yb);
+              sto(a.po1, o, 2.f * a.c3 * y);
+              pacc[ni] += yb;
             }
           } else if constexpr (EM == E_OUT) {
             if (ok) {
@@ -1175,20 +1238,29 @@ __global__ __launch_bounds__(NW * 64, 1) void rgemm(GemmArgs a) {
             }
           } else {  // E_ACT_BWD
             if (ok) {
-              const float hb = acc[0][ni][q], hdb = acc[1][ni][q], hddb = acc[2][ni][q];
-              const float h = ldo(a.pe0, o), zd = ldo(a.pe1, o), zdd = ldo(a.pe2, o), aL = ldo(a.pe3, o),
-                          zb = ldo(a.pe4, o);
-              const float s1 = 1.f - h * h, s2 = -2.f * h * s1, s3 = -2.f * s1 * s1 - 2.f * h * s2;
-              const float zbar = s1 * hb + s2 * zd * hdb + (s2 * zdd + s3 * zd * zd) * hddb + s2 * aL * zb;
-              sto(a.po0, o, zbar);
-              sto(a.po1, o, s1 * hdb + 2.f * s2 * zd * hddb);
-              sto(a.po2, o, s1 * hddb);
-              pacc[ni] += zbar;
+              const float hb = acc[0][ni][q], hdb = acc[1][ni][q];
+              const float h = ldo(a.pe0, o), zd = ldo(a.pe1, o);
+              const float s1 = 1.f - h * h, s2 = -2.f * h * s1;
+              if constexpr (S > 2) {
+                const float hddb = acc[S - 1][ni][q];
+                const float zdd = ldo(a.pe2, o), aL = ldo(a.pe3, o), zb = ldo(a.pe4, o);
+                const float s3 = -2.f * s1 * s1 - 2.f * h * s2;
+                const float zbar = s1 * hb + s2 * zd * hdb + (s2 * zdd + s3 * zd * zd) * hddb + s2 * aL * zb;
+                sto(a.po0, o, zbar);
+                sto(a.po1, o, s1 * hdb + 2.f * s2 * zd * hddb);
+                sto(a.po2, o, s1 * hddb);
+                pacc[ni] += zbar;
+              } else {  // first-order chain: h'' bar = 0, a zetabar = 0
+                const float zbar = s1 * hb + s2 * zd * hdb;
+                sto(a.po0, o, zbar);
+                sto(a.po1, o, s1 * hdb);
+                pacc[ni] += zbar;
+              }
             }
           }
         }
       }
-      if constexpr (EM == E_OUT) {  // per-row reductions over the 32 lanes of each half-wave
+      if constexpr (EM == E_OUT || EM == E_OUT_SEEDS1) {  // per-row reductions over the 32 lanes of each half-wave
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
           float p0 = t0[q], p1 = t1[q], p2 = t2[q];
@@ -1231,13 +1303,16 @@ __global__ __launch_bounds__(NW * 64, 1) void rgemm(GemmArgs a) {
   }
 }
 
-template <int MI, int NI, int GA, int GB, int D = 0, int V = 0>
+// NPR = 2 (first-order chunks, GB_PL): only the pairs (h, zbar) and (s1 z', z'bar); the z'' and adjoint pairs are
+// zero there, so their planes (and, GA_L1, abar0) are not read.
+template <int MI, int NI, int GA, int GB, int D = 0, int V = 0, int NPR = 4>
 __global__ __launch_bounds__(kRT, 1) void wgrad2(WgradArgs a) {
   static_assert(GA != GA_L1 || D > 0, "GA_L1 needs D");
   static_assert(GA != GA_RAW4, "wgrad2: A streams from planes (GA_PL) or rows (GA_L1)");
-  constexpr int NVA = GA == GA_PL ? 4 : 0;     // raw A planes per feature group
-  constexpr int NVB = GB == GB_PL ? 5 : 4;     // raw B planes per column group
-  constexpr int NX = GA == GA_L1 ? 3 * D : 1;  // the row's [x | v | abar0]
+  static_assert(NPR == 4 || (NPR == 2 && GB == GB_PL), "wgrad2: 4 stream pairs, or 2 on the first-order chain");
+  constexpr int NVA = GA == GA_PL ? NPR : 0;                 // raw A planes per feature group
+  constexpr int NVB = NPR == 2 ? 2 : (GB == GB_PL ? 5 : 4);  // raw B planes per column group
+  constexpr int NX = GA == GA_L1 ? (NPR == 2 ? 2 : 3) * D : 1;  // the row's [x | v (| abar0)]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1, l31 = lane & 31, hi = lane >> 5;
   const int slice = xcd_linear(blockIdx.x, gridDim.x);
@@ -1281,8 +1356,10 @@ __global__ __launch_bounds__(kRT, 1) void wgrad2(WgradArgs a) {
     if constexpr (GA == GA_L1) {
 #pragma unroll
       for (int c = 0; c < 2 * D; ++c) g.x[c] = a.xz[r * a.ldxz + c];
+      if constexpr (NPR > 2) {
 #pragma unroll
-      for (int c = 0; c < D; ++c) g.x[2 * D + c] = a.ab0[r * D + c];
+        for (int c = 0; c < D; ++c) g.x[2 * D + c] = a.ab0[r * D + c];
+      }
     }
   };
   auto step = [&](const Regs& g, int64_t rb0) {
@@ -1291,38 +1368,45 @@ __global__ __launch_bounds__(kRT, 1) void wgrad2(WgradArgs a) {
 #pragma unroll
     for (int mi = 0; mi < MI; ++mi) {
       if constexpr (GA == GA_L1) {
-        const float z = kc[mi][D] + dotd<D>(g.x, kc[mi]), zd = dotd<D>(g.x + D, kc[mi]),
-                    zb = dotd<D>(g.x + 2 * D, kc[mi]);
+        const float z = kc[mi][D] + dotd<D>(g.x, kc[mi]), zd = dotd<D>(g.x + D, kc[mi]);
         const float h = ftanh(z), s1 = 1.f - h * h;
         av[mi][0] = h;
         av[mi][1] = s1 * zd;
-        av[mi][2] = -2.f * h * s1 * zd * zd;
-        av[mi][3] = s1 * zb;
+        if constexpr (NPR > 2) {
+          const float zb = dotd<D>(g.x + 2 * D, kc[mi]);
+          av[mi][2] = -2.f * h * s1 * zd * zd;
+          av[mi][3] = s1 * zb;
+        }
       } else {
-        const float h = g.ra[mi][0], zd = g.ra[mi][1], zdd = g.ra[mi][2], zeb = g.ra[mi][3];
+        const float h = g.ra[mi][0], zd = g.ra[mi][1];
         const float s1 = 1.f - h * h, s2 = -2.f * h * s1;
         av[mi][0] = h;
         av[mi][1] = s1 * zd;
-        av[mi][2] = fmaf(s1, zdd, s2 * zd * zd);
-        av[mi][3] = s1 * zeb;
+        if constexpr (NPR > 2) {
+          const float zdd = g.ra[mi][2], zeb = g.ra[mi][3];
+          av[mi][2] = fmaf(s1, zdd, s2 * zd * zd);
+          av[mi][3] = s1 * zeb;
+        }
       }
 #pragma unroll
-      for (int p = 0; p < 4; ++p) av[mi][p] = ok ? av[mi][p] : 0.f;  // rows past the slice add nothing
+      for (int p = 0; p < NPR; ++p) av[mi][p] = ok ? av[mi][p] : 0.f;  // rows past the slice add nothing
     }
 #pragma unroll
     for (int ni = 0; ni < NI; ++ni) {
       bv[ni][0] = g.rb[ni][0];
       bv[ni][1] = g.rb[ni][1];
-      bv[ni][2] = g.rb[ni][2];
-      if constexpr (GB == GB_PL) {
-        const float h = g.rb[ni][3];
-        bv[ni][3] = (1.f - h * h) * g.rb[ni][4];
-      } else {
-        bv[ni][3] = 2.f * g.rb[ni][3];
+      if constexpr (NPR > 2) {
+        bv[ni][2] = g.rb[ni][2];
+        if constexpr (GB == GB_PL) {
+          const float h = g.rb[ni][3];
+          bv[ni][3] = (1.f - h * h) * g.rb[ni][NVB - 1];
+        } else {
+          bv[ni][3] = 2.f * g.rb[ni][3];
+        }
       }
     }
 #pragma unroll
-    for (int p = 0; p < 4; ++p)
+    for (int p = 0; p < NPR; ++p)
 #pragma unroll
       for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
@@ -1334,8 +1418,8 @@ __global__ __launch_bounds__(kRT, 1) void wgrad2(WgradArgs a) {
   // pass merge both paths and wait for the just-issued prefetch (vmcnt(2)) before the MFMAs.
   // One scheduling region per step: the next step's loads spread one per MFMA (sched_group_barrier),
   // the operand transforms between them.
-  constexpr int NLD = (NVA > 0 ? MI * NVA : 0) + NI * NVB + (GA == GA_L1 ? 6 : 0);
-  constexpr int NMF = 4 * MI * NI;
+  constexpr int NLD = (NVA > 0 ? MI * NVA : 0) + NI * NVB + (GA == GA_L1 ? 2 * NPR - 2 : 0);
+  constexpr int NMF = NPR * MI * NI;
   auto region = [&](const Regs& gc, Regs& gn, int64_t rc, int64_t rn) {
     load(gn, rn);
     if constexpr (V == 1) __builtin_amdgcn_sched_barrier(0);
@@ -1378,8 +1462,10 @@ __global__ __launch_bounds__(kRT, 1) void wgrad2(WgradArgs a) {
 // operand is a 64-byte row segment per lane group, loaded straight into registers one step ahead — no
 // LDS, no barrier (the staged fwgrad kernel it replaces ran 2 barriers per 16 rows at 8 waves per CU).
 // One wave per 64 hidden features (4 tiles) x all output tiles; workgroups = row slices.
-template <int OT>
+// NPR = 2 (first-order chunks): only the pairs (h, ybar0) and (s1 z', ybar1) — the others are zero there.
+template <int OT, int NPR = 4>
 __global__ __launch_bounds__(kT) void wgrad_o(WgradArgs a) {
+  static_assert(NPR == 2 || NPR == 4, "wgrad_o: 4 stream pairs, or 2 on the first-order chain");
   constexpr int FI = 4;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c16 = lane & 15, rq = lane >> 4;
   const int slice = xcd_linear(blockIdx.x, gridDim.x);
@@ -1401,8 +1487,10 @@ __global__ __launch_bounds__(kT) void wgrad_o(WgradArgs a) {
       const uint32_t o = (uint32_t)(r * a.n_in + i0 + fi * 16 + c16);
       g.a[fi][0] = ldo(a.pa0, o);
       g.a[fi][1] = ldo(a.pa1, o);
-      g.a[fi][2] = ldo(a.pa2, o);
-      g.a[fi][3] = ldo(a.pa3, o);
+      if constexpr (NPR > 2) {
+        g.a[fi][2] = ldo(a.pa2, o);
+        g.a[fi][3] = ldo(a.pa3, o);
+      }
     }
 #pragma unroll
     for (int ot = 0; ot < OT; ++ot) {
@@ -1410,8 +1498,10 @@ __global__ __launch_bounds__(kT) void wgrad_o(WgradArgs a) {
       const uint32_t o = (uint32_t)(r * a.n_out + (oc < a.n_out ? oc : 0));
       g.b[ot][0] = ldo(a.pb0, o);
       g.b[ot][1] = ldo(a.pb1, o);
-      g.b[ot][2] = ldo(a.pb2, o);
-      g.b[ot][3] = ldo(a.pb3, o);
+      if constexpr (NPR > 2) {
+        g.b[ot][2] = ldo(a.pb2, o);
+        g.b[ot][3] = ldo(a.pb3, o);
+      }
     }
   };
   auto step = [&](const Regs& g, int64_t rb) {
@@ -1419,15 +1509,18 @@ __global__ __launch_bounds__(kT) void wgrad_o(WgradArgs a) {
     float av[FI][4];
 #pragma unroll
     for (int fi = 0; fi < FI; ++fi) {
-      const float h = g.a[fi][0], zd = g.a[fi][1], zdd = g.a[fi][2], zeb = g.a[fi][3];
+      const float h = g.a[fi][0], zd = g.a[fi][1];
       const float s1 = 1.f - h * h, s2 = -2.f * h * s1;
       av[fi][0] = ok ? h : 0.f;
       av[fi][1] = ok ? s1 * zd : 0.f;
-      av[fi][2] = ok ? fmaf(s1, zdd, s2 * zd * zd) : 0.f;
-      av[fi][3] = ok ? s1 * zeb : 0.f;
+      if constexpr (NPR > 2) {
+        const float zdd = g.a[fi][2], zeb = g.a[fi][3];
+        av[fi][2] = ok ? fmaf(s1, zdd, s2 * zd * zd) : 0.f;
+        av[fi][3] = ok ? s1 * zeb : 0.f;
+      }
     }
 #pragma unroll
-    for (int p = 0; p < 4; ++p)
+    for (int p = 0; p < NPR; ++p)
 #pragma unroll
       for (int fi = 0; fi < FI; ++fi)
 #pragma unroll
@@ -1562,7 +1655,7 @@ static int launch_rgemm(GemmArgs a, hipStream_t st, int* grid_x_out = nullptr) {
   return launch_rgemm_t<S, AM, BMD, EM, D, (S == 1 ? 4 : 2), 8>(a, st, grid_x_out);
 }
 
-template <int MI, int NI, int GA, int GB, int D = 0>
+template <int MI, int NI, int GA, int GB, int D = 0, int NPR = 4>
 static int launch_wgrad2(WgradArgs a, float* grad_out, float* scratch, hipStream_t st) {
   if (a.n_in != 128 * MI || a.n_out != 64 * NI) return fail(PDEINV_ERR_INVALID, "kfp_mlp wgrad2: tile / shape mismatch");
   const int slices = (int)std::max<int64_t>(1, std::min<int64_t>(kMaxWgradSlices, (a.R + 63) / 64));
@@ -1571,7 +1664,7 @@ static int launch_wgrad2(WgradArgs a, float* grad_out, float* scratch, hipStream
   const int used = (int)((a.R + rps - 1) / rps);
   a.rows_per_slice = rps;
   const int V = sched_variant();
-  auto kern = V == 1 ? wgrad2<MI, NI, GA, GB, D, 1> : wgrad2<MI, NI, GA, GB, D, 0>;
+  auto kern = V == 1 ? wgrad2<MI, NI, GA, GB, D, 1, NPR> : wgrad2<MI, NI, GA, GB, D, 0, NPR>;
   hipLaunchKernelGGL(kern, dim3(used), dim3(kRT), 0, st, a);
   int rc = check_launch("kfp_mlp fused weight gradient (wgrad2)");
   if (rc) return rc;
@@ -1579,7 +1672,7 @@ static int launch_wgrad2(WgradArgs a, float* grad_out, float* scratch, hipStream
 }
 
 // output-layer weight gradient on wgrad_o (n_in a multiple of 64, <= 256; n_out <= 64)
-template <int OT>
+template <int OT, int NPR = 4>
 static int launch_wgrad_o(WgradArgs a, int64_t part_cap, float* grad_out, float* scratch, hipStream_t st) {
   const int waves = a.n_in / 64;
   if (a.n_in % 64 || waves < 1 || waves > kT / 64 || a.n_out > 16 * OT || a.n_out <= 16 * (OT - 1))
@@ -1592,7 +1685,7 @@ static int launch_wgrad_o(WgradArgs a, int64_t part_cap, float* grad_out, float*
   rps = (rps + 7) & ~(int64_t)7;
   const int used = (int)((a.R + rps - 1) / rps);
   a.rows_per_slice = rps;
-  hipLaunchKernelGGL((wgrad_o<OT>), dim3(used), dim3(64 * waves), 0, st, a);
+  hipLaunchKernelGGL((wgrad_o<OT, NPR>), dim3(used), dim3(64 * waves), 0, st, a);
   int rc = check_launch("kfp_mlp output-layer weight gradient (wgrad_o)");
   if (rc) return rc;
   return sum_slabs(a.part, used, (int64_t)a.n_in * a.n_out, grad_out, scratch, st);
@@ -1693,6 +1786,151 @@ static int zero_planes(const std::vector<float*>& planes, size_t n, float* g, si
   for (float* p : planes)
     if (hipMemsetAsync(p, 0, n * sizeof(float), st) != hipSuccess) return fail(PDEINV_ERR_HIP, "kfp_mlp fused: memset");
   if (hipMemsetAsync(g, 0, ng * sizeof(float), st) != hipSuccess) return fail(PDEINV_ERR_HIP, "kfp_mlp fused: memset");
+  return 0;
+}
+
+// PDEINV_MLP_FO2=0 (A/B): first-order chunks run the full three-stream kernels on zeroed g / a / zetabar planes
+static bool use_fo2() {
+  static const bool on = [] { const char* e = getenv("PDEINV_MLP_FO2"); return !(e && e[0] == '0'); }();
+  return on;
+}
+
+// The first-order chain (initial / terminal sets: c1 = c2 = 0, kinetic_fokker_planck.py:34-39) on two streams, L >= 2,
+// W in {128, 256}, out_features <= 64. Only V' = grad V . v and V enter the loss, so the chain carries [h, z'] forward
+// and [zbar, z'bar] back: no z'' stream, no g / a chain, no forward adjoint (zetabar), no UB product (ubar = 0: the
+// seeds ride in the output layer's epilogue, E_OUT_SEEDS1), and the weight gradients take 2 stream pairs of 4.
+//   FWD   [h2, z2'] = [h1, s1 z1'] K2 (A_L1F, S = 2); middle layers A_FWD2
+//   OUT   y, y' -> terms, seeds ybar = 2 c3 y' + 2 c0 y, y'bar = 2 c3 y, bo gradient     g := 0 (the loss reads it)
+//   R2    [hbar_L, h'bar_L] = [ybar, y'bar] Ko^T, act_bwd (S = 2) ... [hbar1, h'bar1] = [zbar2, z'bar2] K2^T
+//   L1    l1_grad_kernel<FO>;  G: wgrad_o / wgrad2 with 2 pairs
+template <int D, int WB>
+static int run_chunk_fo2(const Chunk& c, const LossHook& loss, hipStream_t st) {
+  constexpr int TN = WB < 128 ? WB : 128;
+  constexpr int TM = TN == 32 ? 128 : 64;
+  constexpr int TG = TN == 32 ? 4 : 2;
+  static_assert(WB == 128 || WB == 256, "first-order chain: the B-resident kernels");
+  const int L = c.L, W = c.W, O = c.O;
+  const int64_t R = c.R;
+  const Layout y = layout(D, L, W, O, c.Bc);
+  float* ws = c.ws;
+  const size_t plane = ((size_t)c.Bc * W + 63) & ~(size_t)63;
+  auto P = [&](int l, int k) { return ws + y.layer0 + y.layer_stride * (size_t)(l - 2) + plane * k; };
+  float* HB1[2] = {ws + y.hb1, ws + y.hb1 + plane};
+  float* YB[2] = {ws + y.yb, ws + y.yb + (size_t)c.Bc * O};
+  float4* terms = (float4*)(ws + y.terms);
+  float* G = ws + y.g;
+  float* abar0 = ws + y.abar0;
+  float* part = ws + y.part;
+  float* part2 = ws + y.part2;
+  const float* prm = c.params;
+  auto Kw = [&](int l) { return prm + c.poff[l - 1]; };
+  auto Bw = [&](int l) { return prm + c.boff[l - 1]; };
+  const float* Ko = prm + c.poff[L];
+  GemmArgs base{};
+  base.R = R;
+  base.c2 = 0.f;
+  base.c3 = c.c3;
+  base.c0 = c.c0;
+  base.part = part;
+  base.xz = c.z;
+  base.ldxz = c.ldz;
+  base.ab0 = abar0;
+  base.k1 = Kw(1);
+  base.b1 = Bw(1);
+  base.wrow = c.wrow;
+  base.ldw = c.ldw;
+  int rc = 0;
+#define RC(x)          \
+  do {                 \
+    rc = (x);          \
+    if (rc) return rc; \
+  } while (0)
+  {
+    GemmArgs a = base;
+    a.K = W; a.N = W; a.Bw = Kw(2); a.bias = Bw(2);
+    a.po0 = P(2, P_H); a.po1 = P(2, P_ZD);
+    RC((launch_rgemm<2, A_L1F, B_NN, E_ACT_FWD, D>(a, st)));
+  }
+  for (int l = 3; l <= L; ++l) {
+    GemmArgs a = base;
+    a.K = W; a.N = W; a.Bw = Kw(l); a.bias = Bw(l);
+    a.pa0 = P(l - 1, P_H); a.pa1 = P(l - 1, P_ZD);
+    a.po0 = P(l, P_H); a.po1 = P(l, P_ZD);
+    RC((launch_rgemm<2, A_FWD2, B_NN, E_ACT_FWD>(a, st)));
+  }
+  {
+    GemmArgs a = base;
+    a.K = W; a.N = O; a.Bw = Ko; a.bias = prm + c.boff[L];
+    a.pa0 = P(L, P_H); a.pa1 = P(L, P_ZD);
+    a.po0 = YB[0]; a.po1 = YB[1]; a.terms = terms;
+    int gx = 0;
+    RC((launch_rgemm_out<2, A_FWD2, E_OUT_SEEDS1>(a, st, &gx)));
+    RC(sum_slabs(part, gx, O, c.grad + c.boff[L], part2, st));
+  }
+  if (hipMemsetAsync(G, 0, (size_t)R * D * sizeof(float), st) != hipSuccess)
+    return fail(PDEINV_ERR_HIP, "kfp_mlp fused: memset");
+  RC(loss.fn(loss.ctx, G, terms, abar0, R, st));
+  {
+    GemmArgs a = base;
+    a.K = O; a.N = W; a.Bw = Ko;
+    a.pa0 = YB[0]; a.pa1 = YB[1];
+    a.pe0 = P(L, P_H); a.pe1 = P(L, P_ZD);
+    a.po0 = P(L, P_ZB0); a.po1 = P(L, P_ZB1);
+    int gx = 0;
+    RC((launch_gemm<2, TM, TN, TG, A_S2, B_NT, E_ACT_BWD>(a, st, &gx)));
+    RC(sum_slabs(part, gx, W, c.grad + c.boff[L - 1], part2, st));
+  }
+  for (int l = L; l >= 3; --l) {
+    GemmArgs a = base;
+    a.K = W; a.N = W; a.Bw = Kw(l);
+    a.pa0 = P(l, P_ZB0); a.pa1 = P(l, P_ZB1);
+    a.pe0 = P(l - 1, P_H); a.pe1 = P(l - 1, P_ZD);
+    a.po0 = P(l - 1, P_ZB0); a.po1 = P(l - 1, P_ZB1);
+    int gx = 0;
+    RC((launch_rgemm<2, A_S2, B_NT, E_ACT_BWD>(a, st, &gx)));
+    RC(sum_slabs(part, gx, W, c.grad + c.boff[l - 2], part2, st));
+  }
+  {
+    GemmArgs a = base;
+    a.K = W; a.N = W; a.Bw = Kw(2);
+    a.pa0 = P(2, P_ZB0); a.pa1 = P(2, P_ZB1);
+    a.po0 = HB1[0]; a.po1 = HB1[1];
+    RC((launch_rgemm<2, A_S2, B_NT, E_STORE3>(a, st)));
+    const int l1_blocks = (int)std::min<int64_t>((R + kL1Rows - 1) / kL1Rows, kRowGridCap);
+    const int64_t l1_rpb = (R + l1_blocks - 1) / l1_blocks;
+    hipLaunchKernelGGL((l1_grad_kernel<D, WB, true>), dim3(l1_blocks), dim3(kT), 0, st, HB1[0], HB1[1], nullptr,
+                       nullptr, c.z, c.ldz, nullptr, Kw(1), Bw(1), R, l1_rpb, part);
+    RC(check_launch("kfp_mlp fused layer-1 gradient (first order)"));
+    RC(sum_slabs(part, l1_blocks, (int64_t)(D + 1) * W, c.grad + c.poff[0], part2, st));
+  }
+  {
+    WgradArgs g{};
+    g.R = R; g.n_in = W; g.n_out = O; g.part = part;
+    g.pa0 = P(L, P_H); g.pa1 = P(L, P_ZD);
+    g.pb0 = YB[0]; g.pb1 = YB[1];
+    const int64_t cap = (int64_t)part_floats(D, W, O);
+    switch ((O + 15) / 16) {
+      case 1: RC((launch_wgrad_o<1, 2>(g, cap, c.grad + c.poff[L], part2, st))); break;
+      case 2: RC((launch_wgrad_o<2, 2>(g, cap, c.grad + c.poff[L], part2, st))); break;
+      case 3: RC((launch_wgrad_o<3, 2>(g, cap, c.grad + c.poff[L], part2, st))); break;
+      default: RC((launch_wgrad_o<4, 2>(g, cap, c.grad + c.poff[L], part2, st))); break;
+    }
+  }
+  for (int l = L; l >= 3; --l) {
+    WgradArgs g{};
+    g.R = R; g.n_in = W; g.n_out = W; g.part = part;
+    g.pa0 = P(l - 1, P_H); g.pa1 = P(l - 1, P_ZD);
+    g.pb0 = P(l, P_ZB0); g.pb1 = P(l, P_ZB1);
+    RC((launch_wgrad2<WB / 128, WB / 64, GA_PL, GB_PL, 0, 2>(g, c.grad + c.poff[l - 1], part2, st)));
+  }
+  {
+    WgradArgs g{};
+    g.R = R; g.n_in = W; g.n_out = W; g.part = part;
+    g.xz = c.z; g.ldxz = c.ldz; g.k1 = Kw(1); g.b1 = Bw(1);
+    g.pb0 = P(2, P_ZB0); g.pb1 = P(2, P_ZB1);
+    RC((launch_wgrad2<WB / 128, WB / 64, GA_L1, GB_PL, D, 2>(g, c.grad + c.poff[1], part2, st)));
+  }
+#undef RC
   return 0;
 }
 
@@ -1818,6 +2056,10 @@ static int run_chunk_t(const Chunk& c, const LossHook& loss, hipStream_t st) {
       RC((launch_wgrad<GW, 64, GA_L1, GB_SM, D>(g, c.grad + c.poff[L], part2, st)));
     }
     return 0;
+  }
+  if constexpr (WB == 128 || WB == 256) {
+    if (c.first_order && !c.grad_only && c.c2 == 0.f && RG && O <= 64 && use_rgemm_out() && use_wgo() && use_fo2())
+      return run_chunk_fo2<D, WB>(c, loss, st);
   }
   // ---- F1 -------------------------------------------------------------------------------
   {  // layer 1 in the prologue (h1 streams never stored), layer 2 on MFMA

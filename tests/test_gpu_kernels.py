@@ -429,12 +429,15 @@ def test_residual_mlp_fused_chunk_at_offset_limit(native):
         native.residual_kfp_mlp(dims, _t(flat), zi, zt, z0[:1024], chunk_rows=(1 << 22) + 64, **kw)
 
 
-@pytest.mark.parametrize("dims", [[8, 256, 256, 40], [4, 64, 40], [2, 32, 32, 32, 40]])
+@pytest.mark.parametrize("dims", [[8, 256, 256, 40], [4, 64, 40], [2, 32, 32, 32, 40], [4, 128, 128, 128, 40],
+                                  [16, 128, 128, 24]])
 def test_residual_mlp_boundary_sets_span_chunks(native, dims):
     """The initial / terminal sets take the first-order chain (no g, no forward adjoint: c_nabla = c_hess = 0 there,
     kinetic_fokker_planck.py:34-39) — here with boundary sets larger than the 0T set, split over several chunks
     (5000 rows at chunk 2048), L = 1 / 2 / 3: loss and gradient equal the fp64 restatement and the rocBLAS library
-    path (which runs the full chain)."""
+    path (which runs the full chain). Widths 128 / 256 run the two-stream kernels (mlp_fused.hip run_chunk_fo2:
+    [h, z'] forward, [zbar, z'bar] back, the seeds in the output epilogue, 2-pair weight gradients), including a
+    middle layer (L = 3) and out_features 24; the narrower nets the zeroed-plane first-order path."""
     rng = np.random.default_rng(sum(dims))
     d = dims[0]
     flat = np.concatenate([np.concatenate([rng.standard_normal((dims[i], dims[i + 1])).ravel() * np.sqrt(1.0 / dims[i]),
