@@ -1313,6 +1313,10 @@ __global__ __launch_bounds__(kRT, 1) void wgrad2(WgradArgs a) {
   constexpr int NVA = GA == GA_PL ? NPR : 0;                 // raw A planes per feature group
   constexpr int NVB = NPR == 2 ? 2 : (GB == GB_PL ? 5 : 4);  // raw B planes per column group
   constexpr int NX = GA == GA_L1 ? (NPR == 2 ? 2 : 3) * D : 1;  // the row's [x | v (| abar0)]
+  // GA_L1: a step's two rows [x | v (| abar0)] come in as NXE floats per lane (element lane + 64 j of the 2 x NXP
+  // slab) and go through a wave-private LDS slab, read back by broadcast: one load per lane instead of NX per lane
+  constexpr int NXP = (NX + 3) & ~3, NXE = GA == GA_L1 ? (2 * NXP + 63) / 64 : 1;
+  __shared__ float xsl[GA == GA_L1 ? 8 * 2 * NXP : 1];  // [wave][2][NXP]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1, l31 = lane & 31, hi = lane >> 5;
   const int slice = xcd_linear(blockIdx.x, gridDim.x);
@@ -1339,8 +1343,9 @@ __global__ __launch_bounds__(kRT, 1) void wgrad2(WgradArgs a) {
   struct Regs {
     float ra[NVA > 0 ? MI : 1][NVA > 0 ? NVA : 1];
     float rb[NI][NVB];
-    float x[NX];
+    float x[NXE];
   };
+  [[maybe_unused]] float* xw = xsl + (GA == GA_L1 ? wave * 2 * NXP : 0);
   const float* pa[4] = {a.pa0, a.pa1, a.pa2, a.pa3};
   const float* pb[5] = {a.pb0, a.pb1, a.pb2, a.pb3, a.pb4};
   auto load = [&](Regs& g, int64_t rb0) {
@@ -1353,27 +1358,41 @@ __global__ __launch_bounds__(kRT, 1) void wgrad2(WgradArgs a) {
     for (int ni = 0; ni < NI; ++ni)
 #pragma unroll
       for (int p = 0; p < NVB; ++p) g.rb[ni][p] = ldo(pb[p], (uint32_t)(r * a.n_out + nb0 + ni * 32 + l31));
-    if constexpr (GA == GA_L1) {
+    if constexpr (GA == GA_L1) {  // element e = lane + 64 j: row rb0 + e / NXP, column e % NXP (clamped, dropped)
 #pragma unroll
-      for (int c = 0; c < 2 * D; ++c) g.x[c] = a.xz[r * a.ldxz + c];
-      if constexpr (NPR > 2) {
-#pragma unroll
-        for (int c = 0; c < D; ++c) g.x[2 * D + c] = a.ab0[r * D + c];
+      for (int j = 0; j < NXE; ++j) {
+        const int e = lane + 64 * j, h = e / NXP < 2 ? e / NXP : 1, c = e - (e / NXP) * NXP;
+        const int cc = c < NX ? c : NX - 1;
+        const int64_t rr = std::min<int64_t>(rb0 + h, a.R - 1);
+        g.x[j] = cc < 2 * D ? a.xz[rr * a.ldxz + cc] : a.ab0[rr * D + (cc - 2 * D)];
       }
     }
   };
   auto step = [&](const Regs& g, int64_t rb0) {
     const bool ok = rb0 + hi < rs1;
     float av[MI][4], bv[NI][4];
+    [[maybe_unused]] float xv[GA == GA_L1 ? NXP : 1];
+    if constexpr (GA == GA_L1) {  // through the wave's slab (LDS ops of one wave complete in order)
+#pragma unroll
+      for (int j = 0; j < NXE; ++j) {
+        const int e = lane + 64 * j;
+        if (e < 2 * NXP) xw[e] = g.x[j];
+      }
+#pragma unroll
+      for (int j = 0; j < NXP / 4; ++j) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(xw + hi * NXP + 4 * j);
+        xv[4 * j] = v[0]; xv[4 * j + 1] = v[1]; xv[4 * j + 2] = v[2]; xv[4 * j + 3] = v[3];
+      }
+    }
 #pragma unroll
     for (int mi = 0; mi < MI; ++mi) {
       if constexpr (GA == GA_L1) {
-        const float z = kc[mi][D] + dotd<D>(g.x, kc[mi]), zd = dotd<D>(g.x + D, kc[mi]);
+        const float z = kc[mi][D] + dotd<D>(xv, kc[mi]), zd = dotd<D>(xv + D, kc[mi]);
         const float h = ftanh(z), s1 = 1.f - h * h;
         av[mi][0] = h;
         av[mi][1] = s1 * zd;
         if constexpr (NPR > 2) {
-          const float zb = dotd<D>(g.x + 2 * D, kc[mi]);
+          const float zb = dotd<D>(xv + 2 * D, kc[mi]);
           av[mi][2] = -2.f * h * s1 * zd * zd;
           av[mi][3] = s1 * zb;
         }
@@ -1418,7 +1437,7 @@ __global__ __launch_bounds__(kRT, 1) void wgrad2(WgradArgs a) {
   // pass merge both paths and wait for the just-issued prefetch (vmcnt(2)) before the MFMAs.
   // One scheduling region per step: the next step's loads spread one per MFMA (sched_group_barrier),
   // the operand transforms between them.
-  constexpr int NLD = (NVA > 0 ? MI * NVA : 0) + NI * NVB + (GA == GA_L1 ? 2 * NPR - 2 : 0);
+  constexpr int NLD = (NVA > 0 ? MI * NVA : 0) + NI * NVB + (GA == GA_L1 ? NXE : 0);
   constexpr int NMF = NPR * MI * NI;
   auto region = [&](const Regs& gc, Regs& gn, int64_t rc, int64_t rn) {
     load(gn, rn);
