@@ -1603,8 +1603,13 @@ static int launch_gemm(GemmArgs a, hipStream_t st, int* grid_x_out = nullptr) {
 }
 
 // single-stream GEMM over N = W: full-width 256-column tiles when W allows (A built once per row)
+// A_U (the R1 head a_L = (2y) Ko^T, K = out_features): 128 x 128 tiles, 4 x 1 waves — the 64 x 256 tile spilled
+// (256 VGPRs + 44 B scratch); C5 1.97 -> 1.68 ms (profiles/r05_c5_g1_tile_ab.txt)
 template <int AM, int BMD, int D = 0>
 static int launch_gemm1(GemmArgs a, hipStream_t st) {
+  if constexpr (AM == A_U) {
+    if (a.N % 128 == 0) return launch_gemm<1, 128, 128, 4, AM, BMD, E_STORE, D>(a, st);
+  }
   if (a.N % 256 == 0) return launch_gemm<1, 64, 256, 2, AM, BMD, E_STORE, D>(a, st);
   if (a.N > 64) return launch_gemm<1, 64, 128, 2, AM, BMD, E_STORE, D>(a, st);
   if (a.N > 32) return launch_gemm<1, 64, 64, 2, AM, BMD, E_STORE, D>(a, st);
