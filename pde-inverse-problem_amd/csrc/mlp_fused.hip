@@ -70,8 +70,30 @@ __device__ __forceinline__ float ftanh(float z) {
 __device__ __forceinline__ float ldo(const float* base, uint32_t idx) {
   return *reinterpret_cast<const float*>(reinterpret_cast<const char*>(base) + (idx << 2));
 }
+// PDEINV_MLP_NT_STORES=1 (build flag, A/B): every plane store of the row-GEMM epilogues non-temporal
+#ifndef PDEINV_MLP_NT_STORES
+#define PDEINV_MLP_NT_STORES 0
+#endif
 __device__ __forceinline__ void sto(float* base, uint32_t idx, float v) {
-  *reinterpret_cast<float*>(reinterpret_cast<char*>(base) + (idx << 2)) = v;
+  float* p = reinterpret_cast<float*>(reinterpret_cast<char*>(base) + (idx << 2));
+  if constexpr (PDEINV_MLP_NT_STORES) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+// The streaming epilogue of the K = out_features reverse product (R2a: five planes in, three out, 1.3 B of plane
+// traffic per FLOP) with non-temporal plane loads / stores: C5 R2a 8.01 -> 7.79 ms, the products that re-read its
+// planes unchanged (profiles/r05_c5_nt_epi_ab.txt). PDEINV_MLP_NT_EPI=0 (build flag): plain accesses.
+#ifndef PDEINV_MLP_NT_EPI
+#define PDEINV_MLP_NT_EPI 1
+#endif
+__device__ __forceinline__ float ldo_s(const float* base, uint32_t idx) {
+  const float* p = reinterpret_cast<const float*>(reinterpret_cast<const char*>(base) + (idx << 2));
+  if constexpr (PDEINV_MLP_NT_EPI) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+__device__ __forceinline__ void sto_s(float* base, uint32_t idx, float v) {
+  float* p = reinterpret_cast<float*>(reinterpret_cast<char*>(base) + (idx << 2));
+  if constexpr (PDEINV_MLP_NT_EPI) __builtin_nontemporal_store(v, p);
+  else *p = v;
 }
 
 // Workgroup placement: the dispatcher hands linear workgroup b to XCD b % 8. xcd_linear(b, nb)
@@ -410,16 +432,16 @@ __global__ __launch_bounds__(kT, 2) void fgemm(GemmArgs a) {
             } else if constexpr (EM == E_ACT_BWD) {
               if (ok) {
                 const float hb = acc[0][mi][ni][q], hdb = acc[1][mi][ni][q];
-                const float h = ldo(a.pe0, o), zd = ldo(a.pe1, o);
+                const float h = ldo_s(a.pe0, o), zd = ldo_s(a.pe1, o);
                 const float s1 = 1.f - h * h, s2 = -2.f * h * s1;
                 if constexpr (S > 2) {
                   const float hddb = acc[S - 1][mi][ni][q];
-                  const float zdd = ldo(a.pe2, o), aL = ldo(a.pe3, o), zb = ldo(a.pe4, o);
+                  const float zdd = ldo_s(a.pe2, o), aL = ldo_s(a.pe3, o), zb = ldo_s(a.pe4, o);
                   const float s3 = -2.f * s1 * s1 - 2.f * h * s2;
                   const float zbar = s1 * hb + s2 * zd * hdb + (s2 * zdd + s3 * zd * zd) * hddb + s2 * aL * zb;
-                  sto(a.po0, o, zbar);
-                  sto(a.po1, o, s1 * hdb + 2.f * s2 * zd * hddb);
-                  sto(a.po2, o, s1 * hddb);
+                  sto_s(a.po0, o, zbar);
+                  sto_s(a.po1, o, s1 * hdb + 2.f * s2 * zd * hddb);
+                  sto_s(a.po2, o, s1 * hddb);
                   pacc[ni] += zbar;
                 } else {  // first-order chain: h'' bar = 0, a zetabar = 0
                   const float zbar = s1 * hb + s2 * zd * hdb;
