@@ -67,8 +67,14 @@ __device__ __forceinline__ float ftanh(float z) {
 
 // 32-bit byte offsets from a uniform base (saddr addressing): a chunk's planes stay at or below 2^30 floats
 // (byte offsets < 2^32, unsigned; run_chunk checks Bc * max(W, out) <= 2^30)
+// PDEINV_MLP_NT_LOADS=1 (build flag, A/B): every plane load non-temporal (scalar and the row GEMMs' 16-byte A loads)
+#ifndef PDEINV_MLP_NT_LOADS
+#define PDEINV_MLP_NT_LOADS 0
+#endif
 __device__ __forceinline__ float ldo(const float* base, uint32_t idx) {
-  return *reinterpret_cast<const float*>(reinterpret_cast<const char*>(base) + (idx << 2));
+  const float* p = reinterpret_cast<const float*>(reinterpret_cast<const char*>(base) + (idx << 2));
+  if constexpr (PDEINV_MLP_NT_LOADS) return __builtin_nontemporal_load(p);
+  else return *p;
 }
 // PDEINV_MLP_NT_STORES=1 (build flag, A/B): every plane store of the row-GEMM epilogues non-temporal
 #ifndef PDEINV_MLP_NT_STORES
@@ -1029,7 +1035,9 @@ __global__ __launch_bounds__(NW * 64, 1) void rgemm(GemmArgs a) {
       const f32x4* src = reinterpret_cast<const f32x4*>(pl[p] + row * K + kt * 32 + 16 * hi);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const f32x4 v = src[j];
+        f32x4 v;
+        if constexpr (PDEINV_MLP_NT_LOADS) v = __builtin_nontemporal_load(src + j);
+        else v = src[j];
         t[p][4 * j] = v[0]; t[p][4 * j + 1] = v[1]; t[p][4 * j + 2] = v[2]; t[p][4 * j + 3] = v[3];
       }
     }
