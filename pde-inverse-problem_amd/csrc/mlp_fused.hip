@@ -67,7 +67,8 @@ __device__ __forceinline__ float ftanh(float z) {
 
 // 32-bit byte offsets from a uniform base (saddr addressing): a chunk's planes stay at or below 2^30 floats
 // (byte offsets < 2^32, unsigned; run_chunk checks Bc * max(W, out) <= 2^30)
-// PDEINV_MLP_NT_LOADS=1 (build flag, A/B): every plane load non-temporal (scalar and the row GEMMs' 16-byte A loads)
+// PDEINV_MLP_NT_LOADS=1 (build flag, A/B): every plane load non-temporal (scalar and the row GEMMs' 16-byte A loads) —
+// measured slower (C5 residual +10 ms: the planes re-read by later products lose their cache hits)
 #ifndef PDEINV_MLP_NT_LOADS
 #define PDEINV_MLP_NT_LOADS 0
 #endif
@@ -76,7 +77,8 @@ __device__ __forceinline__ float ldo(const float* base, uint32_t idx) {
   if constexpr (PDEINV_MLP_NT_LOADS) return __builtin_nontemporal_load(p);
   else return *p;
 }
-// PDEINV_MLP_NT_STORES=1 (build flag, A/B): every plane store of the row-GEMM epilogues non-temporal
+// PDEINV_MLP_NT_STORES=1 (build flag, A/B): every plane store of the row-GEMM epilogues non-temporal — measured
+// mixed (R2b -0.3 ms, the output layer +0.7 ms: its y planes are re-read at once; profiles/r05_c5_out16_nt_ab.txt)
 #ifndef PDEINV_MLP_NT_STORES
 #define PDEINV_MLP_NT_STORES 0
 #endif
@@ -1335,6 +1337,198 @@ __global__ __launch_bounds__(NW * 64, 1) void rgemm(GemmArgs a) {
 
 // NPR = 2 (first-order chunks, GB_PL): only the pairs (h, zbar) and (s1 z', z'bar); the z'' and adjoint pairs are
 // zero there, so their planes (and, GA_L1, abar0) are not read.
+// rgemm16: the output layer (K = W <= 256, N = out_features <= 48) on v_mfma_f32_16x16x4_f32 — 16-column tiles, so
+// 40 outputs take 48 MFMA columns instead of rgemm's 64 (the product was MFMA-bound on that padding). Same B-resident
+// scheme as rgemm (the K x 48 slice of Ko in LDS once per workgroup, Bt[n][k], pitch K + 4), 8 waves of 32 rows x 48
+// columns (2 M-tiles of 16 rows x 3 N-tiles), row blocks of 256. Lane (m = lane & 15, q = lane >> 4) owns rows
+// m and m + 16 of its wave and, within each 32-k tile, the 8 k's [8q, 8q + 8) (the MFMA k-slot bijection is shared
+// with B): two 16-byte loads per row and plane, one tile ahead. The C/D fragment leaves lane (n, q) with rows
+// 4q + i (i < 4, register i) of column n; the per-row reductions of E_OUT / E_OUT_SEEDS1 run over the 16 lanes
+// of a q-group.
+template <int S, int AM, int EM>
+__global__ __launch_bounds__(kRT, 1) void rgemm16(GemmArgs a) {
+  constexpr int NT = 3, BNC = 16 * NT, MI = 2, NW = kRT / 64, BMR = 32 * NW;
+  constexpr int NV = rg_planes<AM>();
+  static_assert(EM == E_OUT || EM == E_SEEDS || EM == E_OUT_SEEDS1, "rgemm16: output-layer epilogues");
+  static_assert(NV >= 1 && !a_is_l1<AM>(), "rgemm16: plane operands");
+  constexpr int NP = (EM == E_SEEDS || EM == E_OUT_SEEDS1) ? 1 : 0;
+  extern __shared__ float lds[];
+  const int K = a.K, N = a.N, Kp = K + 4;
+  float* Bt = lds;  // [BNC][Kp]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l16 = lane & 15, qg = lane >> 4;
+  for (int e = tid; e < K * BNC; e += kRT) {
+    const int k = e / BNC, n = e - k * BNC;
+    Bt[n * Kp + k] = n < N ? a.Bw[(size_t)k * N + n] : 0.f;
+  }
+  __syncthreads();
+  const int rs = xcd_linear(blockIdx.x, gridDim.x), nrs = gridDim.x;
+  [[maybe_unused]] float pacc[NT] = {};
+  const int nk = K / 32;
+  auto row_of = [&](int mb_, int mi) {
+    return std::min<int64_t>((int64_t)mb_ * BMR + wave * 32 + mi * 16 + l16, a.R - 1);
+  };
+  const float* pl[3] = {a.pa0, a.pa1, a.pa2};
+  auto load_tile = [&](float (&t)[NV][MI][8], int kt, int mb_) {
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi) {
+      const int64_t row = row_of(mb_, mi);
+#pragma unroll
+      for (int p = 0; p < NV; ++p) {
+        const f32x4* src = reinterpret_cast<const f32x4*>(pl[p] + row * K + kt * 32 + 8 * qg);
+        const f32x4 v0 = src[0], v1 = src[1];
+        t[p][mi][0] = v0[0]; t[p][mi][1] = v0[1]; t[p][mi][2] = v0[2]; t[p][mi][3] = v0[3];
+        t[p][mi][4] = v1[0]; t[p][mi][5] = v1[1]; t[p][mi][6] = v1[2]; t[p][mi][7] = v1[3];
+      }
+    }
+  };
+  float t0[NV][MI][8], t1[NV][MI][8];
+  if (rs < a.n_mblocks) load_tile(t0, 0, rs);
+  for (int mb = rs; mb < a.n_mblocks; mb += nrs) {
+    const int r0 = mb * BMR;
+    const int mbn = mb + nrs < a.n_mblocks ? mb + nrs : mb;
+    f32x4 acc[S][MI][NT];
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) acc[s][mi][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto steps = [&](const float (&t)[NV][MI][8], int kt) {
+      float bt[NT][8];
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const f32x4 v = *reinterpret_cast<const f32x4*>(Bt + (nt * 16 + l16) * Kp + kt * 32 + 8 * qg + 4 * h);
+          bt[nt][4 * h] = v[0]; bt[nt][4 * h + 1] = v[1]; bt[nt][4 * h + 2] = v[2]; bt[nt][4 * h + 3] = v[3];
+        }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float av[MI][3];
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi) {
+          if constexpr (AM == A_FWD) {
+            const float h = t[0][mi][j], zd = t[1][mi][j], zdd = t[2][mi][j];
+            const float s1 = 1.f - h * h, s2 = -2.f * h * s1;
+            av[mi][0] = h;
+            av[mi][1] = s1 * zd;
+            av[mi][2] = fmaf(s1, zdd, s2 * zd * zd);
+          } else if constexpr (AM == A_FWD2) {
+            const float h = t[0][mi][j];
+            av[mi][0] = h;
+            av[mi][1] = (1.f - h * h) * t[1][mi][j];
+          } else {  // A_S1MUL
+            const float h = t[0][mi][j];
+            av[mi][0] = (1.f - h * h) * t[1][mi][j];
+          }
+        }
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+#pragma unroll
+          for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+              acc[s][mi][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[mi][s], bt[nt][j], acc[s][mi][nt], 0, 0, 0);
+      }
+    };
+    // register double buffer, loads unconditional (the last prefetch reads the next block's tile 0), one fenced
+    // scheduling region per tile (rgemm's V = 1 schedule)
+    __builtin_amdgcn_sched_barrier(0);
+    for (int kt = 0; kt < nk; kt += 2) {
+      load_tile(t1, kt + 1, mb);
+      steps(t0, kt);
+      __builtin_amdgcn_sched_barrier(0);
+      load_tile(t0, kt + 2 < nk ? kt + 2 : 0, kt + 2 < nk ? mb : mbn);
+      steps(t1, kt + 1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // ---- epilogue: acc[s][mi][nt][i] = C[row = 16 mi + 4 q + i][col = 16 nt + n] of the wave's 32 rows
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi) {
+      [[maybe_unused]] float tr0[4] = {}, tr1[4] = {}, tr2[4] = {};
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const int n = nt * 16 + l16;
+        const bool nv = n < N;
+        [[maybe_unused]] float bn = 0.f;
+        if constexpr (EM == E_OUT || EM == E_OUT_SEEDS1) bn = a.bias[nv ? n : 0];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = r0 + wave * 32 + mi * 16 + 4 * qg + i;
+          const bool ok = r < a.R && nv;
+          const uint32_t o = (uint32_t)(r * N + n);
+          if constexpr (EM == E_OUT) {
+            if (ok) {
+              const float y = acc[0][mi][nt][i] + bn, yd = acc[1][mi][nt][i], ydd = acc[2][mi][nt][i];
+              sto(a.po0, o, y);
+              sto(a.po1, o, yd);
+              sto(a.po2, o, ydd);
+              tr0[i] = fmaf(y, y, tr0[i]);
+              tr1[i] = fmaf(y, yd, tr1[i]);
+              tr2[i] = fmaf(yd, yd, fmaf(y, ydd, tr2[i]));
+            }
+          } else if constexpr (EM == E_OUT_SEEDS1) {
+            if (ok) {
+              const float y = acc[0][mi][nt][i] + bn, yd = acc[1][mi][nt][i];
+              tr0[i] = fmaf(y, y, tr0[i]);
+              tr1[i] = fmaf(y, yd, tr1[i]);
+              tr2[i] = fmaf(yd, yd, tr2[i]);
+              const float c0r = a.wrow ? a.c0 * a.wrow[(int64_t)r * a.ldw] : a.c0;
+              const float yb = 2.f * a.c3 * yd + 2.f * c0r * y;
+              sto(a.po0, o, yb);
+              sto(a.po1, o, 2.f * a.c3 * y);
+              pacc[nt] += yb;
+            }
+          } else {  // E_SEEDS
+            if (ok) {
+              const float ub = acc[0][mi][nt][i];
+              const float y = ldo(a.pe0, o), yd = ldo(a.pe1, o), ydd = ldo(a.pe2, o);
+              const float c0r = a.wrow ? a.c0 * a.wrow[(int64_t)r * a.ldw] : a.c0;
+              const float yb = 2.f * a.c3 * yd + 2.f * a.c2 * ydd + 2.f * ub + 2.f * c0r * y;
+              sto(a.po0, o, yb);
+              sto(a.po1, o, 2.f * a.c3 * y + 4.f * a.c2 * yd);
+              sto(a.po2, o, 2.f * a.c2 * y);
+              pacc[nt] += yb;
+            }
+          }
+        }
+      }
+      if constexpr (EM == E_OUT || EM == E_OUT_SEEDS1) {  // per-row sums over the 16 lanes of the q-group
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float p0 = tr0[i], p1 = tr1[i], p2 = tr2[i];
+#pragma unroll
+          for (int off = 8; off > 0; off >>= 1) {
+            p0 += __shfl_xor(p0, off, 64);
+            p1 += __shfl_xor(p1, off, 64);
+            p2 += __shfl_xor(p2, off, 64);
+          }
+          const int r = r0 + wave * 32 + mi * 16 + 4 * qg + i;
+          if (l16 == 0 && r < a.R) a.terms[r] = make_float4(2.f * p1, 2.f * p2, p0, 0.f);
+        }
+      }
+    }
+  }
+  if constexpr (NP > 0) {  // bias-gradient column sums: one slab row per row stream (fixed order)
+    __syncthreads();
+    float* red = lds;  // [NW][BNC] (Bt is dead)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      float v = pacc[nt];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      if (qg == 0) red[wave * BNC + nt * 16 + l16] = v;
+    }
+    __syncthreads();
+    for (int c = tid; c < BNC; c += kRT) {
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) t += red[w * BNC + c];
+      if (c < N) a.part[(int64_t)rs * N + c] = t;
+    }
+  }
+}
+
 template <int MI, int NI, int GA, int GB, int D = 0, int V = 0, int NPR = 4>
 __global__ __launch_bounds__(kRT, 1) void wgrad2(WgradArgs a) {
   static_assert(GA != GA_L1 || D > 0, "GA_L1 needs D");
@@ -1761,8 +1955,35 @@ static bool use_wgo() {
 // staged fgemm / fwgrad kernels, for A/B measurements)
 // The output layer (K = W, N = out_features <= 64) on the B-resident kernel: one 64-column block, 8 waves
 // of 32 rows x 64 columns (NI = 2), row blocks of 256.
+// PDEINV_MLP_OUT16=0 (A/B): the streamed output-layer products (out_features <= 48) on rgemm's 32-wide tiles instead
+// of rgemm16
+static bool use_out16() {
+  static const bool on = [] { const char* e = getenv("PDEINV_MLP_OUT16"); return !(e && e[0] == '0'); }();
+  return on;
+}
+
+template <int S, int AM, int EM>
+static int launch_rgemm16(GemmArgs a, hipStream_t st, int* grid_x_out) {
+  constexpr int BNC = 48, BMR = 256;
+  if (!(a.K % 64 == 0 && a.K <= 256 && a.N >= 1 && a.N <= BNC))
+    return fail(PDEINV_ERR_INVALID, "kfp_mlp rgemm16 (output layer): K % 64 == 0, K <= 256, N <= 48");
+  const size_t bytes = (size_t)BNC * (a.K + 4) * sizeof(float);
+  auto kern = rgemm16<S, AM, EM>;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  a.n_mblocks = mblocks(a.R, BMR);
+  const int nrs = std::max(1, std::min(a.n_mblocks, kRGridCap));
+  if (grid_x_out) *grid_x_out = nrs;
+  hipLaunchKernelGGL(kern, dim3(nrs), dim3(kRT), bytes, st, a);
+  return check_launch("kfp_mlp fused B-resident output-layer GEMM (16-wide)");
+}
+
 template <int S, int AM, int EM>
 static int launch_rgemm_out(GemmArgs a, hipStream_t st, int* grid_x_out = nullptr) {
+  // the streamed output products (S >= 2) on 16-wide tiles: C5 E_OUT 4.20 -> 3.44-3.56 ms; the one-stream UB product
+  // measured no better on them (3.21 -> 3.23-3.45 ms) and stays on rgemm (profiles/r05_c5_out16_nt_ab.txt)
+  if constexpr (S >= 2) {
+    if (a.N <= 48 && use_out16()) return launch_rgemm16<S, AM, EM>(a, st, grid_x_out);
+  }
   constexpr int NI = 2, BNC = 64, BMR = 256;
   if (!(a.K % 64 == 0 && a.K <= 256 && a.N >= 1 && a.N <= BNC))
     return fail(PDEINV_ERR_INVALID, "kfp_mlp rgemm (output layer): K % 64 == 0, K <= 256, N <= 64");
