@@ -93,6 +93,20 @@ __device__ __forceinline__ void sto(float* base, uint32_t idx, float v) {
 #ifndef PDEINV_MLP_NT_EPI
 #define PDEINV_MLP_NT_EPI 1
 #endif
+// The hbar1 planes (written by R2b, read once by l1_grad_kernel) non-temporal: l1_grad 3.79 -> 3.60 ms, R2b
+// 13.61 -> 13.49 ms (profiles/r05_c5_nt_hb1_ab.txt). PDEINV_MLP_NT_HB1=0 (build flag): plain accesses.
+#ifndef PDEINV_MLP_NT_HB1
+#define PDEINV_MLP_NT_HB1 1
+#endif
+__device__ __forceinline__ void sto_h(float* base, uint32_t idx, float v) {
+  float* p = reinterpret_cast<float*>(reinterpret_cast<char*>(base) + (idx << 2));
+  if constexpr (PDEINV_MLP_NT_HB1) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+__device__ __forceinline__ float ld_h(const float* p) {
+  if constexpr (PDEINV_MLP_NT_HB1) return __builtin_nontemporal_load(p);
+  else return *p;
+}
 __device__ __forceinline__ float ldo_s(const float* base, uint32_t idx) {
   const float* p = reinterpret_cast<const float*>(reinterpret_cast<const char*>(base) + (idx << 2));
   if constexpr (PDEINV_MLP_NT_EPI) return __builtin_nontemporal_load(p);
@@ -656,7 +670,7 @@ __global__ __launch_bounds__(kT) void l1_grad_kernel(const float* __restrict__ h
       for (int j = 0; j < CPT; ++j) {
         const int64_t o = rowo + c0 + CW * j;
         if constexpr (FO) {
-          const float hb = hb0[o], hdb = hb1[o];
+          const float hb = ld_h(hb0 + o), hdb = ld_h(hb1 + o);
           float zz = bb[j], zd = 0.f;
 #pragma unroll
           for (int i = 0; i < D; ++i) {
@@ -670,7 +684,7 @@ __global__ __launch_bounds__(kT) void l1_grad_kernel(const float* __restrict__ h
           for (int i = 0; i < D; ++i) pacc[j][i] = fmaf(x[i], zbar, fmaf(x[D + i], zdbar, pacc[j][i]));
           pacc[j][D] += zbar;
         } else {
-          const float hb = hb0[o], hdb = hb1[o], hddb = hb2[o], aL = a1[o];
+          const float hb = ld_h(hb0 + o), hdb = ld_h(hb1 + o), hddb = ld_h(hb2 + o), aL = a1[o];
           float zz = bb[j], zd = 0.f, zb = 0.f;
 #pragma unroll
           for (int i = 0; i < D; ++i) {
@@ -1229,11 +1243,11 @@ __global__ __launch_bounds__(NW * 64, 1) void rgemm(GemmArgs a) {
             }
           } else if constexpr (EM == E_STORE) {
             if (ok) sto(a.po0, o, acc[0][ni][q]);
-          } else if constexpr (EM == E_STORE3) {
+          } else if constexpr (EM == E_STORE3) {  // hbar1 (R2b), read once by l1_grad_kernel
             if (ok) {
-              sto(a.po0, o, acc[0][ni][q]);
-              sto(a.po1, o, acc[1][ni][q]);
-              if constexpr (S > 2) sto(a.po2, o, acc[S - 1][ni][q]);
+              sto_h(a.po0, o, acc[0][ni][q]);
+              sto_h(a.po1, o, acc[1][ni][q]);
+              if constexpr (S > 2) sto_h(a.po2, o, acc[S - 1][ni][q]);
             }
           } else if constexpr (EM == E_OUT_SEEDS1) {
             if (ok) {
@@ -1980,7 +1994,8 @@ static int launch_rgemm16(GemmArgs a, hipStream_t st, int* grid_x_out) {
 template <int S, int AM, int EM>
 static int launch_rgemm_out(GemmArgs a, hipStream_t st, int* grid_x_out = nullptr) {
   // the streamed output products (S >= 2) on 16-wide tiles: C5 E_OUT 4.20 -> 3.44-3.56 ms; the one-stream UB product
-  // measured no better on them (3.21 -> 3.23-3.45 ms) and stays on rgemm (profiles/r05_c5_out16_nt_ab.txt)
+  // measured no better on them (3.21 -> 3.23-3.45 ms at two workgroups per CU, 3.01 -> 3.04 at one) and stays on rgemm
+  // (profiles/r05_c5_out16_nt_ab.txt, r05_c5_nt_hb1_ab.txt)
   if constexpr (S >= 2) {
     if (a.N <= 48 && use_out16()) return launch_rgemm16<S, AM, EM>(a, st, grid_x_out);
   }
