@@ -357,6 +357,8 @@ LIB, FUSED = 1, 2  # native.MLP_IMPL_LIBRARY / MLP_IMPL_FUSED
     ([8, 256, 256, 40], "gmm", 777, FUSED), ([16, 128, 128, 128, 64], "quad", 1500, FUSED),
     ([8, 512, 512, 512, 40], "gmm", 3000, FUSED), ([4, 32, 32, 40], "gmm", 1000, FUSED),
     ([8, 64, 64, 64, 40], "quad", 777, FUSED), ([2, 32, 32, 32, 5], "quad", 1 << 18, FUSED),
+    # out_features filling / partly filling the 16-wide output tiles (rgemm16: 48 = 3 full tiles, 44 a partial third)
+    ([4, 128, 128, 48], "quad", 1500, FUSED), ([8, 256, 256, 44], "gmm", 1000, FUSED),
     # the reference's default net (MLP.yaml: width 20 x 8 layers), zero-padded onto the 32-wide MFMA kernels
     ([2] + [20] * 8 + [40], "gmm", 1000, FUSED), ([4] + [20] * 8 + [40], "quad", 1 << 18, 0),
     ([8, 100, 100, 40], "gmm", 1500, FUSED),
