@@ -1367,12 +1367,16 @@ __global__ __launch_bounds__(kRT, 1) void rgemm16(GemmArgs a) {
   static_assert(NV >= 1 && !a_is_l1<AM>(), "rgemm16: plane operands");
   constexpr int NP = (EM == E_SEEDS || EM == E_OUT_SEEDS1) ? 1 : 0;
   extern __shared__ float lds[];
-  const int K = a.K, N = a.N, Kp = K + 4;
+  // Bt[n][k] at pitch K + 16 with the 16-byte chunks of each 32-k tile XOR-swizzled by n & 7: the 16-lane groups of a
+  // ds_read_b128 (lanes {0-3, 12-15, 20-27} / {4-11, 16-19, 28-31}) then hit 64 distinct banks (the bank model of
+  // tools/quad_gram_bank_model.py's rules: 8 read cycles per two k-halves instead of 16 at pitch K + 4)
+  const int K = a.K, N = a.N, Kp = K + 16;
   float* Bt = lds;  // [BNC][Kp]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l16 = lane & 15, qg = lane >> 4;
   for (int e = tid; e < K * BNC; e += kRT) {
     const int k = e / BNC, n = e - k * BNC;
-    Bt[n * Kp + k] = n < N ? a.Bw[(size_t)k * N + n] : 0.f;
+    const int ks = (k & ~31) | ((((k >> 2) & 7) ^ (n & 7)) << 2) | (k & 3);
+    Bt[n * Kp + ks] = n < N ? a.Bw[(size_t)k * N + n] : 0.f;
   }
   __syncthreads();
   const int rs = xcd_linear(blockIdx.x, gridDim.x), nrs = gridDim.x;
@@ -1413,7 +1417,8 @@ __global__ __launch_bounds__(kRT, 1) void rgemm16(GemmArgs a) {
       for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-          const f32x4 v = *reinterpret_cast<const f32x4*>(Bt + (nt * 16 + l16) * Kp + kt * 32 + 8 * qg + 4 * h);
+          const f32x4 v = *reinterpret_cast<const f32x4*>(Bt + (nt * 16 + l16) * Kp + kt * 32 +
+                                                          4 * ((2 * qg + h) ^ (l16 & 7)));
           bt[nt][4 * h] = v[0]; bt[nt][4 * h + 1] = v[1]; bt[nt][4 * h + 2] = v[2]; bt[nt][4 * h + 3] = v[3];
         }
 #pragma unroll
@@ -1981,7 +1986,7 @@ static int launch_rgemm16(GemmArgs a, hipStream_t st, int* grid_x_out) {
   constexpr int BNC = 48, BMR = 256;
   if (!(a.K % 64 == 0 && a.K <= 256 && a.N >= 1 && a.N <= BNC))
     return fail(PDEINV_ERR_INVALID, "kfp_mlp rgemm16 (output layer): K % 64 == 0, K <= 256, N <= 48");
-  const size_t bytes = (size_t)BNC * (a.K + 4) * sizeof(float);
+  const size_t bytes = (size_t)BNC * (a.K + 16) * sizeof(float);
   auto kern = rgemm16<S, AM, EM>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
   a.n_mblocks = mblocks(a.R, BMR);
