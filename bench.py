@@ -98,8 +98,10 @@ def parse():
     p.add_argument("--c4-separate-sums", action="store_true",
                    help="C4: the next simulate's mean-path sums as their own launch (pdeinv_mf_sums) instead of "
                         "inside the KMV pass (pdeinv_kmv_moments_weights_mf_sums), for A/B")
-    p.add_argument("--c4-schedule", default="sim", choices=["fused", "concurrent", "sim"],
-                   help="C4 steady state: 'sim' (default) = the simulator draws the next simulate's noise sums "
+    p.add_argument("--c4-schedule", default="simkmv", choices=["fused", "concurrent", "sim", "simkmv"],
+                   help="C4 steady state: 'simkmv' (default) = the simulator forms the KMV per-stamp sums from its "
+                        "staged rows and draws the next simulate's noise sums (pdeinv_sde_simulate_mf_kmv: no "
+                        "trajectory re-read); 'sim' = the simulator draws the next simulate's noise sums "
                         "(pdeinv_sde_simulate_mf_next), plain KMV pass; 'fused' = the next simulate's mean-path "
                         "sums inside the KMV pass; "
                         "'concurrent' = the unfused KMV pass (HBM-bound) on the main stream and pdeinv_mf_sums "
@@ -471,8 +473,15 @@ def run_c4(a, rank, world, dev):
         desc.d_meanfield = ctypes.c_void_p(xbar.data_ptr())
         if record is not None:
             record[0].record()
-        sim_sums = a.c4_schedule == "sim" and not a.c4_separate_sums
-        if sim_sums:  # the simulator also draws the NEXT simulate's mean-path noise sums (same z0 ensemble)
+        sim_sums = a.c4_schedule in ("sim", "simkmv") and not a.c4_separate_sums
+        kmv_in_sim = a.c4_schedule == "simkmv" and not a.c4_separate_sums
+        if kmv_in_sim:  # the simulator also forms the KMV per-stamp sums and draws the next simulate's noise sums
+            desc_n, keep_n = native.mf_desc(N, d, n, T / n, gamma, A, seed=key.seed,
+                                            counter_offset=(counter[0] + n + 1) & 0xFFFFFFFF, particle_offset=poff)
+            mom, wst, sums_next[0] = native.sde_simulate_mf_kmv(desc, z0, bufs["traj"], bufs["tau"], bufs["last"],
+                                                                gamma, coef, desc_n, z0)
+            del keep_n
+        elif sim_sums:  # the simulator also draws the NEXT simulate's mean-path noise sums (same z0 ensemble)
             desc_n, keep_n = native.mf_desc(N, d, n, T / n, gamma, A, seed=key.seed,
                                             counter_offset=(counter[0] + n + 1) & 0xFFFFFFFF, particle_offset=poff)
             sums_next[0] = native.sde_simulate_mf_next(desc, z0, bufs["traj"], bufs["tau"], bufs["last"], desc_n, z0)
@@ -483,7 +492,9 @@ def run_c4(a, rank, world, dev):
             record[1].record()
         del keep
         counter[0] = (counter[0] + n + 1) & 0xFFFFFFFF
-        if sim_sums:
+        if kmv_in_sim:
+            pass
+        elif sim_sums:
             mom, wst = native.kmv_moments_weights(d, gamma, coef, bufs["traj"], n, N, N * 2 * d, 2 * d)
         elif a.c4_schedule == "concurrent" and not a.c4_separate_sums:
             # the next simulate's sums depend only on (seed, counter, ids, z0): they run on the side stream

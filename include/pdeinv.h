@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define PDEINV_ABI_VERSION 9  /* 9: pdeinv_ou_exact_sample, pdeinv_kmv_mlp_path */
+#define PDEINV_ABI_VERSION 10  /* 10: pdeinv_sde_simulate_mf_kmv; 9: pdeinv_ou_exact_sample, pdeinv_kmv_mlp_path */
 #define PDEINV_MAX_DIM 16          /* d (configuration-space dimension) */
 #define PDEINV_MAX_PARAMS 256      /* floats of potential parameters passed by value */
 
@@ -163,6 +163,21 @@ size_t pdeinv_sde_simulate_mf_next_workspace_bytes(const pdeinv_sde_desc* desc);
 int pdeinv_sde_simulate_mf_next(const pdeinv_sde_desc* desc, const float* d_z0, float* d_traj, float* d_tau,
                                 float* d_last, const pdeinv_sde_desc* next, const float* d_z0_next,
                                 void* d_workspace, double* d_sums_next, void* stream);
+/* ABI 10. pdeinv_sde_simulate (fused McKean–Vlasov path, desc->d_meanfield set) that also forms the quadratic-Φ
+ * KMV residual's per-time-stamp sums of its own trajectory rows 0..n_steps-1 — exactly what
+ * pdeinv_kmv_moments_weights(dim, gamma, d_coef, d_traj, n_steps, N, N*2d, 2d) returns (d_mom [n_steps,
+ * moment_len(2d)], d_wstats [n_steps, moment_len(d)] fp64, rank-local), up to the fp32 summation order — from the
+ * rows the simulator stages for its stores, so the trajectory is not read back (d_traj may be NULL). d_coef
+ * [n_steps, 3d + 2 + 2d^2] as pdeinv_kmv_weights. With `next` non-NULL it also returns the next simulate's
+ * pdeinv_mf_sums in d_sums_next as pdeinv_sde_simulate_mf_next (same restrictions: counter offset only,
+ * n_steps + 1 <= 128). Even dim <= 8, Philox noise (else PDEINV_ERR_UNSUPPORTED); deterministic. Replaces the
+ * simulate of sampling_utils.py:25-52 followed by the pair sums of kinetic_mckean_vlasov.py:11-120.
+ * Workspace (256-byte aligned): pdeinv_sde_simulate_mf_kmv_workspace_bytes(desc, next != NULL). */
+size_t pdeinv_sde_simulate_mf_kmv_workspace_bytes(const pdeinv_sde_desc* desc, int32_t with_next);
+int pdeinv_sde_simulate_mf_kmv(const pdeinv_sde_desc* desc, const float* d_z0, float* d_traj, float* d_tau,
+                               float* d_last, float gamma, const float* d_coef, double* d_mom, double* d_wstats,
+                               const pdeinv_sde_desc* next, const float* d_z0_next, double* d_sums_next,
+                               void* d_workspace, void* stream);
 /* tau0 per particle (u*dt from the shift stream, or d_shift_u) -> d_tau0 [N]. */
 int pdeinv_sde_tau0(const pdeinv_sde_desc* desc, float* d_tau0, void* stream);
 

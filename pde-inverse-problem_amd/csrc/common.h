@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <string>
 
@@ -15,6 +16,21 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 constexpr int kBlock = 256;          // 4 waves of 64
 constexpr int kWave = 64;
 constexpr int kWavesPerBlock = kBlock / kWave;
+
+// ---- A/B switches of the measurement tools ------------------------------------------------
+// Only a tools/build_var.sh build with -DPDEINV_AB_ENV=1 reads them: the default library reads no environment
+// variable, so a stray variable in a user's shell cannot change which kernels run.
+#ifndef PDEINV_AB_ENV
+#define PDEINV_AB_ENV 0
+#endif
+inline const char* ab_env(const char* name) {
+#if PDEINV_AB_ENV
+  return getenv(name);
+#else
+  (void)name;
+  return nullptr;
+#endif
+}
 
 // ---- error plumbing (host) ------------------------------------------------------------
 void set_error(const std::string& msg);

@@ -17,7 +17,7 @@ constexpr int kBatchedGridTarget = 4096;  // C4 KMV pass: r02 2.88 ms at 2048, 2
 
 static int64_t grid_target() {
   static const int64_t t = [] {
-    const char* e = getenv("PDEINV_KMV_GRID");  // A/B experiments (tools)
+    const char* e = ab_env("PDEINV_KMV_GRID");  // A/B experiments (tools)
     return e ? (int64_t)atol(e) : (int64_t)kBatchedGridTarget;
   }();
   return t;

@@ -510,7 +510,7 @@ extern "C" int pdeinv_mlp_fused_supported(int32_t dim, int32_t n_layers, int32_t
 // PDEINV_MLP_FIRST_ORDER=0 (A/B): the boundary sets take the full second-order chain as the 0T set does
 static bool first_order_enabled() {
   static const bool on = [] {
-    const char* e = getenv("PDEINV_MLP_FIRST_ORDER");
+    const char* e = ab_env("PDEINV_MLP_FIRST_ORDER");
     return !(e && atoi(e) == 0);
   }();
   return on;

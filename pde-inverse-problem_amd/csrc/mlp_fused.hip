@@ -67,55 +67,29 @@ __device__ __forceinline__ float ftanh(float z) {
 
 // 32-bit byte offsets from a uniform base (saddr addressing): a chunk's planes stay at or below 2^30 floats
 // (byte offsets < 2^32, unsigned; run_chunk checks Bc * max(W, out) <= 2^30)
-// PDEINV_MLP_NT_LOADS=1 (build flag, A/B): every plane load non-temporal (scalar and the row GEMMs' 16-byte A loads) —
-// measured slower (C5 residual +10 ms: the planes re-read by later products lose their cache hits)
-#ifndef PDEINV_MLP_NT_LOADS
-#define PDEINV_MLP_NT_LOADS 0
-#endif
+// Plane accesses keep the default cache policy (non-temporal plane loads everywhere measured C5 +10 ms: the planes
+// re-read by later products lose their cache hits; non-temporal epilogue stores everywhere were mixed,
+// profiles/r05_c5_out16_nt_ab.txt), except two streams that are touched once:
 __device__ __forceinline__ float ldo(const float* base, uint32_t idx) {
-  const float* p = reinterpret_cast<const float*>(reinterpret_cast<const char*>(base) + (idx << 2));
-  if constexpr (PDEINV_MLP_NT_LOADS) return __builtin_nontemporal_load(p);
-  else return *p;
+  return *reinterpret_cast<const float*>(reinterpret_cast<const char*>(base) + (idx << 2));
 }
-// PDEINV_MLP_NT_STORES=1 (build flag, A/B): every plane store of the row-GEMM epilogues non-temporal — measured
-// mixed (R2b -0.3 ms, the output layer +0.7 ms: its y planes are re-read at once; profiles/r05_c5_out16_nt_ab.txt)
-#ifndef PDEINV_MLP_NT_STORES
-#define PDEINV_MLP_NT_STORES 0
-#endif
 __device__ __forceinline__ void sto(float* base, uint32_t idx, float v) {
-  float* p = reinterpret_cast<float*>(reinterpret_cast<char*>(base) + (idx << 2));
-  if constexpr (PDEINV_MLP_NT_STORES) __builtin_nontemporal_store(v, p);
-  else *p = v;
+  *reinterpret_cast<float*>(reinterpret_cast<char*>(base) + (idx << 2)) = v;
 }
-// The streaming epilogue of the K = out_features reverse product (R2a: five planes in, three out, 1.3 B of plane
-// traffic per FLOP) with non-temporal plane loads / stores: C5 R2a 8.01 -> 7.79 ms, the products that re-read its
-// planes unchanged (profiles/r05_c5_nt_epi_ab.txt). PDEINV_MLP_NT_EPI=0 (build flag): plain accesses.
-#ifndef PDEINV_MLP_NT_EPI
-#define PDEINV_MLP_NT_EPI 1
-#endif
-// The hbar1 planes (written by R2b, read once by l1_grad_kernel) non-temporal: l1_grad 3.79 -> 3.60 ms, R2b
-// 13.61 -> 13.49 ms (profiles/r05_c5_nt_hb1_ab.txt). PDEINV_MLP_NT_HB1=0 (build flag): plain accesses.
-#ifndef PDEINV_MLP_NT_HB1
-#define PDEINV_MLP_NT_HB1 1
-#endif
+// the hbar1 planes (written by R2b, read once by l1_grad_kernel): l1_grad 3.79 -> 3.60 ms, R2b 13.61 -> 13.49 ms
+// (profiles/r05_c5_nt_hb1_ab.txt)
 __device__ __forceinline__ void sto_h(float* base, uint32_t idx, float v) {
-  float* p = reinterpret_cast<float*>(reinterpret_cast<char*>(base) + (idx << 2));
-  if constexpr (PDEINV_MLP_NT_HB1) __builtin_nontemporal_store(v, p);
-  else *p = v;
+  __builtin_nontemporal_store(v, reinterpret_cast<float*>(reinterpret_cast<char*>(base) + (idx << 2)));
 }
-__device__ __forceinline__ float ld_h(const float* p) {
-  if constexpr (PDEINV_MLP_NT_HB1) return __builtin_nontemporal_load(p);
-  else return *p;
-}
+__device__ __forceinline__ float ld_h(const float* p) { return __builtin_nontemporal_load(p); }
+// the streaming epilogue of the K = out_features reverse product (R2a: five planes in, three out, 1.3 B of plane
+// traffic per FLOP): C5 R2a 8.01 -> 7.79 ms, the products that re-read its planes unchanged
+// (profiles/r05_c5_nt_epi_ab.txt)
 __device__ __forceinline__ float ldo_s(const float* base, uint32_t idx) {
-  const float* p = reinterpret_cast<const float*>(reinterpret_cast<const char*>(base) + (idx << 2));
-  if constexpr (PDEINV_MLP_NT_EPI) return __builtin_nontemporal_load(p);
-  else return *p;
+  return __builtin_nontemporal_load(reinterpret_cast<const float*>(reinterpret_cast<const char*>(base) + (idx << 2)));
 }
 __device__ __forceinline__ void sto_s(float* base, uint32_t idx, float v) {
-  float* p = reinterpret_cast<float*>(reinterpret_cast<char*>(base) + (idx << 2));
-  if constexpr (PDEINV_MLP_NT_EPI) __builtin_nontemporal_store(v, p);
-  else *p = v;
+  __builtin_nontemporal_store(v, reinterpret_cast<float*>(reinterpret_cast<char*>(base) + (idx << 2)));
 }
 
 // Workgroup placement: the dispatcher hands linear workgroup b to XCD b % 8. xcd_linear(b, nb)
@@ -991,7 +965,7 @@ bool rgemm_shape(int K, int N) { return K % 64 == 0 && K <= 256 && N % kRBN == 0
 // BNC = block columns: 128 for the W x W layers; 64 for the output layer (N = out_features <= 64, one
 // column block, columns past N zero in the staged B and never stored; E_OUT reduces a row's outputs
 // inside one wave, E_SEEDS writes the seeds and the bias-gradient column sums).
-template <int S, int NI, int AM, int BMD, int EM, int D = 0, int V = 0, int BNC = kRBN, int NW = 8>
+template <int S, int NI, int AM, int BMD, int EM, int D = 0, int BNC = kRBN, int NW = 8>
 __global__ __launch_bounds__(NW * 64, 1) void rgemm(GemmArgs a) {
   constexpr int NT = NW * 64;                                            // threads (NW waves)
   constexpr int WGN = BNC / (32 * NI), WGM = NW / WGN, BMR = 32 * WGM;  // waves along N / M, block rows
@@ -1007,8 +981,8 @@ __global__ __launch_bounds__(NW * 64, 1) void rgemm(GemmArgs a) {
   static_assert(EM != E_OUT_SEEDS1 || S == 2, "the first-order output epilogue takes the h and z' streams");
   extern __shared__ float lds[];
   const int Kp = a.K + 4;                          // Bt row pitch: ds_read_b128 of 16 lanes' rows conflict-free
-  float* Bt = lds;                                 // [BNC][Kp]: Bt[n][k] = B[k][n0 + n]  (V = 3: [K][BNC + 1])
-  [[maybe_unused]] float* k1s = Bt + (V == 3 ? (size_t)a.K * (BNC + 1) : (size_t)BNC * Kp);  // L1: [K][SK]
+  float* Bt = lds;                                 // [BNC][Kp]: Bt[n][k] = B[k][n0 + n]
+  [[maybe_unused]] float* k1s = Bt + (size_t)BNC * Kp;  // L1: [K][SK]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WGN, wn = wave % WGN, l31 = lane & 31, hi = lane >> 5;
   const int K = a.K, N = a.N;
@@ -1028,8 +1002,7 @@ __global__ __launch_bounds__(NW * 64, 1) void rgemm(GemmArgs a) {
       k = e - n * K;
       v = n0 + n < N ? a.Bw[(size_t)(n0 + n) * K + k] : 0.f;
     }
-    if constexpr (V == 3) Bt[k * (BNC + 1) + n] = v;
-    else Bt[n * Kp + k] = v;
+    Bt[n * Kp + k] = v;
   }
   if constexpr (L1) {
     for (int e = tid; e < K * SK; e += NT) {
@@ -1051,9 +1024,7 @@ __global__ __launch_bounds__(NW * 64, 1) void rgemm(GemmArgs a) {
       const f32x4* src = reinterpret_cast<const f32x4*>(pl[p] + row * K + kt * 32 + 16 * hi);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        f32x4 v;
-        if constexpr (PDEINV_MLP_NT_LOADS) v = __builtin_nontemporal_load(src + j);
-        else v = src[j];
+        const f32x4 v = src[j];
         t[p][4 * j] = v[0]; t[p][4 * j + 1] = v[1]; t[p][4 * j + 2] = v[2]; t[p][4 * j + 3] = v[3];
       }
     }
@@ -1098,12 +1069,11 @@ __global__ __launch_bounds__(NW * 64, 1) void rgemm(GemmArgs a) {
 #pragma unroll
       for (int ni = 0; ni < NI; ++ni)
 #pragma unroll
-        for (int j = 0; j < (V == 3 ? 0 : 4); ++j) {
+        for (int j = 0; j < 4; ++j) {
           // plane modes: the lane's k's are [16 hi, 16 hi + 16); layer-1 modes: the 32x32 MFMA result rows
           // (j & 3) + 8 (j >> 2) + 4 hi, i.e. 16-byte runs at 4 hi + 8 j
           const int ko = L1 ? 4 * hi + 8 * j : 16 * hi + 4 * j;
           const f32x4 v = *reinterpret_cast<const f32x4*>(Bt + (wn * 32 * NI + ni * 32 + l31) * Kp + kt * 32 + ko);
-          static_assert(V != 3 || BNC == kRBN, "V = 3 layout: 128 columns");
           bt[ni][4 * j] = v[0]; bt[ni][4 * j + 1] = v[1]; bt[ni][4 * j + 2] = v[2]; bt[ni][4 * j + 3] = v[3];
         }
       // layer-1 modes: the pre-activations of the lane's row for the tile's 32 k on the matrix pipe,
@@ -1172,11 +1142,6 @@ __global__ __launch_bounds__(NW * 64, 1) void rgemm(GemmArgs a) {
           av[1] = t[1][s];
           av[2] = t[2][s];
         }
-        if constexpr (V == 3) {
-#pragma unroll
-          for (int ni = 0; ni < NI; ++ni)
-            bt[ni][s] = Bt[(kt * 32 + 16 * hi + s) * (BNC + 1) + wn * 32 * NI + ni * 32 + l31];
-        }
 #pragma unroll
         for (int si = 0; si < S; ++si)
 #pragma unroll
@@ -1188,29 +1153,16 @@ __global__ __launch_bounds__(NW * 64, 1) void rgemm(GemmArgs a) {
     // load under a branch makes the waitcnt pass merge the two paths and wait for the just-issued
     // prefetch before the current tile's MFMAs (measured: vmcnt(2) instead of vmcnt(12) in wgrad2).
     // One scheduling region per tile (sched_barrier around it): the B reads, the NEXT tile's A loads and
-    // this tile's MFMAs, with the loads spread one per MFMA (sched_group_barrier) so that no wave parks
-    // on a burst of 4 NV gathers in the memory pipeline, and layer-1 VALU spread between MFMAs. Without
-    // the region fence the machine scheduler sank each prefetch next to its first use (vmcnt(0) before
-    // every k-step) to save registers.
-    constexpr int NMF = 16 * S * NI, NLD = 4 * NV;
-    constexpr int VPM = AM == A_L1F ? 5 : (AM == A_L1A ? 6 : 1);  // layer-1 VALU per MFMA (~28 / 24 per k-step)
+    // this tile's MFMAs. Without the region fence the machine scheduler sank each prefetch next to its first
+    // use (vmcnt(0) before every k-step) to save registers; spreading the loads one per MFMA inside the region
+    // (sched_group_barrier) measured slower (profiles/r03_c5_sched_ab.txt).
     auto tile = [&](const float (&tc)[NV > 0 ? NV : 1][16], float (&tn)[NV > 0 ? NV : 1][16], int kt, int ktn,
                     int64_t rown) {
       if constexpr (NV > 0) load_tile(tn, ktn, rown);
       steps(tc, kt);
-      if constexpr (V == 2) {
-        __builtin_amdgcn_sched_group_barrier(0x100, 4 * NI + (L1 ? 48 : 0), 0);  // DS reads: B (+ K1 columns)
-        if constexpr (L1) __builtin_amdgcn_sched_group_barrier(0x002, 28, 0);      // the first k-step's A
-#pragma unroll
-        for (int i = 0; i < NMF; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          if (i < NLD) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-          if constexpr (L1) __builtin_amdgcn_sched_group_barrier(0x002, VPM, 0);
-        }
-      }
-      if constexpr (V == 1 || V == 2) __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_sched_barrier(0);
     };
-    if constexpr (V == 1 || V == 2) __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_sched_barrier(0);
     for (int kt = 0; kt < nk; kt += 2) {  // t0 holds tile kt on entry (the last pair fetches the next block's tile 0)
       tile(t0, t1, kt, kt + 1, mr);
       tile(t1, t0, kt + 1, kt + 2 < nk ? kt + 2 : 0, kt + 2 < nk ? mr : mrn);
@@ -1548,7 +1500,7 @@ __global__ __launch_bounds__(kRT, 1) void rgemm16(GemmArgs a) {
   }
 }
 
-template <int MI, int NI, int GA, int GB, int D = 0, int V = 0, int NPR = 4>
+template <int MI, int NI, int GA, int GB, int D = 0, int NPR = 4>
 __global__ __launch_bounds__(kRT, 1) void wgrad2(WgradArgs a) {
   static_assert(GA != GA_L1 || D > 0, "GA_L1 needs D");
   static_assert(GA != GA_RAW4, "wgrad2: A streams from planes (GA_PL) or rows (GA_L1)");
@@ -1678,27 +1630,17 @@ __global__ __launch_bounds__(kRT, 1) void wgrad2(WgradArgs a) {
   // Two steps of 2 rows per iteration (register double buffer). Loads and steps are UNCONDITIONAL
   // (clamped rows; the ok mask zeroes rows past the slice): a load under a branch makes the waitcnt
   // pass merge both paths and wait for the just-issued prefetch (vmcnt(2)) before the MFMAs.
-  // One scheduling region per step: the next step's loads spread one per MFMA (sched_group_barrier),
-  // the operand transforms between them.
-  constexpr int NLD = (NVA > 0 ? MI * NVA : 0) + NI * NVB + (GA == GA_L1 ? NXE : 0);
-  constexpr int NMF = NPR * MI * NI;
+  // One scheduling region per step (sched_barrier on both sides of the step): the next step's loads stay ahead of
+  // this step's MFMAs.
   auto region = [&](const Regs& gc, Regs& gn, int64_t rc, int64_t rn) {
     load(gn, rn);
-    if constexpr (V == 1) __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_sched_barrier(0);
     step(gc, rc);
-    if constexpr (V == 2) {
-#pragma unroll
-      for (int i = 0; i < NMF; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        if (i < NLD) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
-      }
-    }
-    if constexpr (V >= 1) __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_sched_barrier(0);
   };
   Regs g0, g1;
   load(g0, rs0);
-  if constexpr (V >= 1) __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_sched_barrier(0);
   for (int64_t rb = rs0; rb < rs1; rb += 4) {
     region(g0, g1, rb, rb + 2);
     region(g1, g0, rb + 2, rb + 4);
@@ -1878,32 +1820,16 @@ static int launch_wgrad(WgradArgs a, float* grad_out, float* scratch, hipStream_
   return sum_slabs(a.part, slices, (int64_t)a.n_in * a.n_out, grad_out, scratch, st);
 }
 
-// PDEINV_MLP_SCHED (A/B of the rgemm / wgrad2 schedules; 1 = fenced regions, the default, measured
-// best: profiles/r03_c5_sched_ab.txt): 0 = compiler schedule.
-static int sched_variant() {
-  static const int v = [] {
-    const char* e = getenv("PDEINV_MLP_SCHED");
-    return e ? (atoi(e) == 0 ? 0 : 1) : 1;
-  }();
-  return v;
-}
 
 // S = 1 streams take 32 x 128 wave tiles (4 MFMA tiles per A value: the A prologue is the per-k VALU
 // cost), S = 3 streams 32 x 64 (3 x 2 tiles, 96 accumulator registers).
-// PDEINV_MLP_F1W4=1 (A/B): the layer-1-prologue forward (A_L1F) on 4-wave blocks, one wave per SIMD, NI = 4 — every
-// wave owns all 128 columns of its 32 rows, so each row's layer-1 streams are built twice instead of four times
-static bool use_f1w4() {
-  static const bool on = [] { const char* e = getenv("PDEINV_MLP_F1W4"); return e && e[0] == '1'; }();
-  return on;
-}
 
 template <int S, int AM, int BMD, int EM, int D, int NI, int NW>
 static int launch_rgemm_t(GemmArgs a, hipStream_t st, int* grid_x_out) {
   constexpr int BMR = 32 * (NW / (kRBN / (32 * NI)));
-  const int V = sched_variant();
-  const size_t bytes = ((V == 3 ? (size_t)a.K * (kRBN + 1) : (size_t)kRBN * (a.K + 4)) +
+  const size_t bytes = ((size_t)kRBN * (a.K + 4) +
                         (a_is_l1<AM>() ? (size_t)a.K * k1_stride<D>() : 0)) * sizeof(float);
-  auto kern = V == 1 ? rgemm<S, NI, AM, BMD, EM, D, 1, kRBN, NW> : rgemm<S, NI, AM, BMD, EM, D, 0, kRBN, NW>;
+  auto kern = rgemm<S, NI, AM, BMD, EM, D, kRBN, NW>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
   a.n_mblocks = mblocks(a.R, BMR);
   const int ncb = a.N / kRBN;
@@ -1916,9 +1842,6 @@ static int launch_rgemm_t(GemmArgs a, hipStream_t st, int* grid_x_out) {
 template <int S, int AM, int BMD, int EM, int D = 0>
 static int launch_rgemm(GemmArgs a, hipStream_t st, int* grid_x_out = nullptr) {
   if (!rgemm_shape(a.K, a.N)) return fail(PDEINV_ERR_INVALID, "kfp_mlp rgemm: K % 64 == 0, K <= 256, N % 128 == 0");
-  if constexpr (AM == A_L1F && S == 3) {
-    if (use_f1w4()) return launch_rgemm_t<S, AM, BMD, EM, D, 4, 4>(a, st, grid_x_out);
-  }
   return launch_rgemm_t<S, AM, BMD, EM, D, (S == 1 ? 4 : 2), 8>(a, st, grid_x_out);
 }
 
@@ -1930,8 +1853,7 @@ static int launch_wgrad2(WgradArgs a, float* grad_out, float* scratch, hipStream
   rps = (rps + 1) & ~(int64_t)1;
   const int used = (int)((a.R + rps - 1) / rps);
   a.rows_per_slice = rps;
-  const int V = sched_variant();
-  auto kern = V == 1 ? wgrad2<MI, NI, GA, GB, D, 1, NPR> : wgrad2<MI, NI, GA, GB, D, 0, NPR>;
+  auto kern = wgrad2<MI, NI, GA, GB, D, NPR>;
   hipLaunchKernelGGL(kern, dim3(used), dim3(kRT), 0, st, a);
   int rc = check_launch("kfp_mlp fused weight gradient (wgrad2)");
   if (rc) return rc;
@@ -1960,13 +1882,13 @@ static int launch_wgrad_o(WgradArgs a, int64_t part_cap, float* grad_out, float*
 
 // PDEINV_MLP_L1G=0: g = zeta1 K1^T on the VALU kernel (wave reductions) instead of l1_g_mfma_kernel
 static bool use_l1g_mfma() {
-  static const bool on = [] { const char* e = getenv("PDEINV_MLP_L1G"); return !(e && e[0] == '0'); }();
+  static const bool on = [] { const char* e = ab_env("PDEINV_MLP_L1G"); return !(e && e[0] == '0'); }();
   return on;
 }
 
 // PDEINV_MLP_WGO=0: the output-layer weight gradient on the staged fwgrad kernel (A/B measurements)
 static bool use_wgo() {
-  static const bool on = [] { const char* e = getenv("PDEINV_MLP_WGO"); return !(e && e[0] == '0'); }();
+  static const bool on = [] { const char* e = ab_env("PDEINV_MLP_WGO"); return !(e && e[0] == '0'); }();
   return on;
 }
 
@@ -1977,7 +1899,7 @@ static bool use_wgo() {
 // PDEINV_MLP_OUT16=0 (A/B): the streamed output-layer products (out_features <= 48) on rgemm's 32-wide tiles instead
 // of rgemm16
 static bool use_out16() {
-  static const bool on = [] { const char* e = getenv("PDEINV_MLP_OUT16"); return !(e && e[0] == '0'); }();
+  static const bool on = [] { const char* e = ab_env("PDEINV_MLP_OUT16"); return !(e && e[0] == '0'); }();
   return on;
 }
 
@@ -2007,9 +1929,8 @@ static int launch_rgemm_out(GemmArgs a, hipStream_t st, int* grid_x_out = nullpt
   constexpr int NI = 2, BNC = 64, BMR = 256;
   if (!(a.K % 64 == 0 && a.K <= 256 && a.N >= 1 && a.N <= BNC))
     return fail(PDEINV_ERR_INVALID, "kfp_mlp rgemm (output layer): K % 64 == 0, K <= 256, N <= 64");
-  const int V = sched_variant();
   const size_t bytes = (size_t)BNC * (a.K + 4) * sizeof(float);
-  auto kern = V == 1 ? rgemm<S, NI, AM, B_NN, EM, 0, 1, BNC> : rgemm<S, NI, AM, B_NN, EM, 0, 0, BNC>;
+  auto kern = rgemm<S, NI, AM, B_NN, EM, 0, BNC>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
   a.n_mblocks = mblocks(a.R, BMR);
   const int nrs = std::max(1, std::min(a.n_mblocks, kRGridCap));
@@ -2020,13 +1941,13 @@ static int launch_rgemm_out(GemmArgs a, hipStream_t st, int* grid_x_out = nullpt
 
 // PDEINV_MLP_RGEMM_OUT=0: the output-layer products on fgemm (A/B)
 static bool use_rgemm_out() {
-  static const bool on = [] { const char* e = getenv("PDEINV_MLP_RGEMM_OUT"); return !(e && e[0] == '0'); }();
+  static const bool on = [] { const char* e = ab_env("PDEINV_MLP_RGEMM_OUT"); return !(e && e[0] == '0'); }();
   return on;
 }
 
 static bool use_rgemm(int W) {
   static const bool off = [] {
-    const char* e = getenv("PDEINV_MLP_RGEMM");
+    const char* e = ab_env("PDEINV_MLP_RGEMM");
     return e && e[0] == '0';
   }();
   return !off && (W == 128 || W == 256);
@@ -2086,7 +2007,7 @@ static int zero_planes(const std::vector<float*>& planes, size_t n, float* g, si
 
 // PDEINV_MLP_FO2=0 (A/B): first-order chunks run the full three-stream kernels on zeroed g / a / zetabar planes
 static bool use_fo2() {
-  static const bool on = [] { const char* e = getenv("PDEINV_MLP_FO2"); return !(e && e[0] == '0'); }();
+  static const bool on = [] { const char* e = ab_env("PDEINV_MLP_FO2"); return !(e && e[0] == '0'); }();
   return on;
 }
 

@@ -672,7 +672,7 @@ constexpr int kPairWaves = 2048;  // persistent grid: 2 waves per SIMD of 256 CU
 
 int pair_waves() {
   static const int w = [] {
-    const char* e = getenv("PDEINV_PAIR_WAVES");  // A/B experiments (tools)
+    const char* e = ab_env("PDEINV_PAIR_WAVES");  // A/B experiments (tools)
     const int v = e ? atoi(e) : kPairWaves;
     return v >= 2 ? v & ~1 : kPairWaves;
   }();

@@ -1067,7 +1067,7 @@ extern "C" int pdeinv_realnvp_logdensity(const pdeinv_realnvp_desc* d, const flo
 // Packed layout where [x | temb] fits one 16-vector with x in register 0 (PDEINV_NVP_PACK=0 forces the
 // identity layout, A/B).
 static bool nvp_packed(const pdeinv_realnvp_desc* d) {
-  static const bool pack_env = [] { const char* e = getenv("PDEINV_NVP_PACK"); return !(e && e[0] == '0'); }();
+  static const bool pack_env = [] { const char* e = ab_env("PDEINV_NVP_PACK"); return !(e && e[0] == '0'); }();
   return pack_env && d->dim <= 4 && in_dim_of(d) - d->dim <= 12;
 }
 static NvSlabMap nvp_slab_map(const pdeinv_realnvp_desc* d) {

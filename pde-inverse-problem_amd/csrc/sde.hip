@@ -16,57 +16,10 @@
 
 #include <type_traits>
 
-#include "common.h"
+#include "sde_common.h"
 
 namespace pdeinv {
 
-struct SdeArgs {
-  int64_t N, poff, ld_z0;
-  int32_t n_steps, random_shift, K, has_center;
-  int32_t remap;  // 1 (default): XCD-contiguous block order (xcd_block); PDEINV_SIM_REMAP=0 disables
-  float dt, gamma, ns, neg_half_inv_s2_log2e, inv_s2, l2s;
-  uint32_t k0, k1, ctr_off;
-  const float* noise;
-  const float* shift_u;
-  // MEANFIELD_QUADRATIC (fused multi-step path): xbar [n_steps+1, d], the ensemble mean of the
-  // positions before each update (pdeinv_mf_mean_path), and the shared clock tau0 of the ensemble
-  const float* xbar;
-  float tau0_mf;
-  // QUADRATIC: A (d*d) then c (d). GMM (packed on the host at compile-time offsets):
-  // GMM: [kMaxGmmK*d raw mu | kMaxGmmK constants c_k = -|mu_k|^2 log2e / (2 s^2)]
-  float params[2 * 16 * PDEINV_MAX_DIM + 16];
-};
-
-constexpr int kMaxGmmK = 16;
-
-// d standard normals for update s of particle (plo, phi) — stream layout of include/pdeinv.h.
-// EXPLICIT (the explicit-noise parity mode) is a compile-time choice: a global load left on the
-// Philox path of the step loop makes the compiler wait vmcnt(0) at the join, and on gfx950 vmcnt
-// also counts the previous steps' trajectory stores — every step would wait for them to retire.
-template <int D, bool EXPLICIT = false>
-__device__ __forceinline__ void gen_normals(const SdeArgs& a, uint32_t plo, uint32_t phi,
-                                            uint32_t s, int64_t i, float* xi) {
-  if constexpr (EXPLICIT) {
-    const float* src = a.noise + ((int64_t)s * a.N + i) * D;
-#pragma unroll
-    for (int k = 0; k < D; ++k) xi[k] = src[k];
-    return;
-  }
-  stream_normals<D>(a.k0, a.k1, a.ctr_off + s, plo, phi, xi);
-}
-
-// grad U(q) = A (q - c) = A q - b, b = A c packed on the host (KOU: A = tilde_F, c = 0,
-// …_OU.py:130-138): the FMA chain starts at -b, so a centre costs no per-step instruction.
-typedef const __attribute__((address_space(4))) float kfloat;
-typedef const __attribute__((address_space(4))) char kchar;
-// SdeArgs::params in the kernel-argument segment (sde_simulate_kernel's first argument, offset 0), made
-// opaque per use: held across the step loop, d^2 + d uniform floats beyond ~32 overflow the scalar
-// register file and the spills come back as v_readlane on every update (d = 8: 46-66 per update).
-__device__ __forceinline__ kfloat* kernarg_params() {
-  kfloat* p = (kfloat*)((kchar*)__builtin_amdgcn_kernarg_segment_ptr() + offsetof(SdeArgs, params));
-  asm volatile("" : "+s"(p));
-  return p;
-}
 
 template <int D>
 __device__ __forceinline__ void grad_quadratic(const SdeArgs& a, const float* q, float* g) {
@@ -114,66 +67,8 @@ struct GmmCentres {
   }
 };
 
-// McKean–Vlasov drift with the mean path precomputed: grad U(q) = A (q - xbar_s), the same
-// operation order as the per-update exchange (mf_step_kernel) and the C oracle (y = q - xbar, then
-// A y). xbar_s is wave-uniform (scalar loads from a small device array, one row per update).
-// A is read from the kernel-argument segment with scalar loads at every update (kernarg_params): held
-// across the step loop, its d^2 SGPRs (64 at d = 8) overflowed the scalar file and the spills came back
-// as 46 v_readlane per update (C4 step loop 208 -> 162 VALU instructions per update).
-template <int D>
-__device__ __forceinline__ void grad_meanfield(const SdeArgs&, const float* q, const float* xb, float* g) {
-  kfloat* A = kernarg_params();
-  float y[D];
-#pragma unroll
-  for (int c = 0; c < D; ++c) y[c] = q[c] - xb[c];
-#pragma unroll
-  for (int r = 0; r < D; ++r) {
-    float acc = 0.f;
-#pragma unroll
-    for (int c = 0; c < D; ++c) acc = fmaf(A[r * D + c], y[c], acc);
-    g[r] = acc;
-  }
-}
 
-// Dispatch order -> particle block: the hardware hands consecutive workgroups to the 8 XCDs in
-// turn (b -> XCD b % 8); this map gives XCD x the contiguous block range [x*nb/8, (x+1)*nb/8), so
-// each XCD's L2 sees one contiguous stretch of every trajectory slab instead of every 8th 8 KiB
-// piece. Measured on the C2 launch, same buffers A/B in one process: 1.53 -> 1.46 ms and
-// 1.26 -> 1.20 ms (4-5 %, every allocation; tools/sim_alloc.py, profiles/r01_sim_remap_ab.log).
-// Results are unchanged: a particle's numbers depend only on its global id, and the moment
-// partial slots are indexed by the mapped block. (Not used by mf_step_kernel: there the C4 bench
-// measured 6.8 ms without vs 7.5 ms with it, across processes.)
-__device__ __forceinline__ int xcd_block(int b, int nb) {
-  const int q = nb / 8, r = nb % 8, x = b % 8, l = b / 8;
-  return x < r ? x * (q + 1) + l : r * (q + 1) + (x - r) * q + l;
-}
 
-// Store modes for the per-step trajectory rows (M = 2d floats per particle):
-//  kStoreNT     — each lane stores its own row (M/4 dwordx4, nontemporal): one store
-//                 instruction covers 64 rows but only 16 of every 4*M bytes;
-//  kStorePlain  — the same with default-policy stores;
-//  kStoreStaged — the wave's 64 rows go through a 64*M*4-byte LDS slot so that every store
-//                 instruction writes 1 KiB contiguous (whole lines), nontemporal.
-enum { kStoreNT = 0, kStorePlain = 1, kStoreStaged = 2 };
-
-template <int D, int STORE>
-__device__ __forceinline__ void store_row(float* dst, const float* z) {
-  constexpr int M = 2 * D;
-  if constexpr (M % 4 == 0) {
-#pragma unroll
-    for (int k = 0; k < M; k += 4) {
-      if constexpr (STORE == kStorePlain)
-        *reinterpret_cast<f32x4*>(dst + k) = f32x4{z[k], z[k + 1], z[k + 2], z[k + 3]};
-      else
-        __builtin_nontemporal_store(f32x4{z[k], z[k + 1], z[k + 2], z[k + 3]},
-                                    reinterpret_cast<f32x4*>(dst + k));
-    }
-  } else {
-#pragma unroll
-    for (int k = 0; k < M; k += 2)
-      __builtin_nontemporal_store(f32x2{z[k], z[k + 1]}, reinterpret_cast<f32x2*>(dst + k));
-  }
-}
 
 // Wave-cooperative store of 64 consecutive rows [wave_row0, wave_row0 + 64) of M floats:
 // row -> LDS (lane-private 4M bytes), then 16-byte chunk c = k*64 + lane -> global. Rows at or
@@ -193,11 +88,7 @@ __device__ __forceinline__ void store_rows_staged(float* wave_dst, const float* 
   if (n_valid == kWave) {  // wave-uniform: every full wave stores unguarded (one lgkmcnt wait)
 #pragma unroll
     for (int k = 0; k < M / 4; ++k)
-#if PDEINV_SIM_PLAIN_STORES
-      *reinterpret_cast<f32x4*>(wave_dst + 4 * (k * 64 + lane)) = v[k];
-#else
       __builtin_nontemporal_store(v[k], reinterpret_cast<f32x4*>(wave_dst + 4 * (k * 64 + lane)));
-#endif
   } else {
 #pragma unroll
     for (int k = 0; k < M / 4; ++k) {
@@ -233,10 +124,6 @@ __device__ __forceinline__ void load_rows_staged(const float* wave_src, float* z
   __builtin_amdgcn_wave_barrier();
 }
 
-__device__ __forceinline__ float tau_value(float tau0, int s, float dt) {
-#pragma clang fp contract(off)
-  return tau0 + (float)s * dt;  // tau_0 + arange(n)*dt, two roundings (sampling_utils.py:48)
-}
 
 __device__ __forceinline__ float shift_u(const SdeArgs& a, uint32_t plo, uint32_t phi, int64_t i) {
   if (a.shift_u) return a.shift_u[i];
@@ -257,122 +144,6 @@ struct GmmResFused {
   float c_nabla, c_hess, c_fric, c_true, c_init, c_term, inv_ni, inv_nt;
 };
 
-// McKean–Vlasov: the NEXT simulate's mean-path noise sums (the sum_i xi_{i,s} part of pdeinv_mf_sums) drawn
-// inside this simulate (NXT). The sums depend on the particle ids and the next simulate's Philox counter only,
-// so this store-bound kernel can draw them with its idle VALU while it streams the trajectory, and the KMV
-// pass that follows reads at full rate. A wave owns its 64 particles x np1 updates of the next simulate and
-// draws one (particle, update) pair per lane and step: lane l takes pairs q = l np1 + s (s = 0..np1-1, the
-// simulator's own steps), q -> (update q / 64, particle q % 64). A lane's np1 consecutive pairs span at most
-// three updates (np1 <= 128), so it keeps three running sums; after the last step the block combines them in
-// a fixed order (per update: waves, then the 1-3 lanes that drew it) into one slab column per update.
-struct MfNext {
-  float* partials;   // [(np1 * D) columns][gridDim.x]: column s * D + k
-  uint32_t ctr_off;  // the next simulate's Philox counter offset (same key and particle ids)
-  int32_t np1;       // updates per simulate (n_steps + 1), <= 128
-};
-
-// PDEINV_SIM_QUAD=1 (build flag, A/B): QuadGram below instead of PairGram for the d = 4 step-loop moments. Measured
-// r05 (profiles/r05_c2_quad_ab.txt, three alternating rounds on one box): PairGram 1.455 ms, QuadGram at 5 waves
-// 1.469, at 6 waves 1.466, at 7 waves (16 dwords spilled) 1.553; the no-moment kernel (42 VGPRs, 10 waves) 1.407 on
-// the same box — the waves in flight were not what the moments cost there, so PairGram stays the default.
-#ifndef PDEINV_SIM_QUAD
-#define PDEINV_SIM_QUAD 0
-#endif
-// Step-loop 0T moments at 2d = 8 (the C2 headline kernel), shared by the four lanes of a "quad". PairGram
-// keeps a particle's full sum + Gram (48 accumulators) in its own lane: 96 VGPRs, 5 waves per SIMD; the r01 box ran
-// the launch at 0.77 of its write ceiling against 0.95 without moments (42 VGPRs), which suggested the waves in
-// flight were the cost (the r05 A/B above says otherwise on its box). Here the staged rows (already in the wave's LDS
-// slot for the coalesced store) are read back by the four lanes {l, l^8, l^16, l^24} of a quad, and lane
-// class c = (l >> 3) & 3 accumulates, over the quad's four rows, only the Gram entries of the features
-// shifted by 2c: with u_k = z[(k + 2c) mod 8] it sums u0 u0..u5, u1 u1..u3, u1 u5 and (u0, u1) — 12
-// accumulators. The cyclic feature-pair shift maps the 10 Gram representatives onto all 36 entries; the
-// entries (0,4), (2,6), (1,5), (3,7) come out twice (classes c and c + 2 compute the same product on the
-// same rows) and are taken from classes 0 / 1 only. Same FMA count as PairGram (24 packed per update), plus
-// 12 ds_read_b64 per update; the quad choice (lane bits 3 and 4) makes both the Gram reads and the store's
-// chunk reads bank-conflict-free on the unpadded slot (tools/quad_gram_bank_model.py).
-struct QuadGram {
-  f32x2 s, g0, g1, g2, g3;  // (u0,u1); u0*(u0,u1); u0*(u2,u3); u0*(u4,u5); u1*(u2,u3)
-  float h, j;               // u1*u1, u1*u5
-  static constexpr int kSlots = 12;
-  __device__ __forceinline__ void zero() {
-    s = g0 = g1 = g2 = g3 = f32x2{0.f, 0.f};
-    h = j = 0.f;
-  }
-  // the lane's three pair addresses of its quad's row 0 (features 2c .. 2c + 5, cyclic)
-  __device__ __forceinline__ static void addresses(const float* slot_wave, int lane, const f32x2* (&p)[3]) {
-    const int c = (lane >> 3) & 3;
-    const float* row0 = slot_wave + (lane & ~24) * 8;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) p[k] = reinterpret_cast<const f32x2*>(row0 + 2 * ((k + c) & 3));
-  }
-  // rows l, l^8, l^16, l^24 of the quad sit 0 / 8 / 16 / 24 rows (of 4 f32x2) after row 0
-  __device__ __forceinline__ void add(const f32x2* const (&p)[3]) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int o = ((r & 1) * 8 + (r >> 1) * 16) * 4;
-      const f32x2 u01 = p[0][o], u23 = p[1][o], u45 = p[2][o];
-      const f32x2 a0 = f32x2{u01[0], u01[0]}, a1 = f32x2{u01[1], u01[1]};
-      s += u01;
-      g0 = a0 * u01 + g0;
-      g1 = a0 * u23 + g1;
-      g2 = a0 * u45 + g2;
-      g3 = a1 * u23 + g3;
-      h = fmaf(u01[1], u01[1], h);
-      j = fmaf(u01[1], u45[1], j);
-    }
-  }
-  __device__ __forceinline__ float slot(int k) const {
-    switch (k) {
-      case 0: return s[0];
-      case 1: return s[1];
-      case 2: return g0[0];
-      case 3: return g0[1];
-      case 4: return g1[0];
-      case 5: return g1[1];
-      case 6: return g2[0];
-      case 7: return g2[1];
-      case 8: return g3[0];
-      case 9: return g3[1];
-      case 10: return h;
-      default: return j;
-    }
-  }
-};
-
-// moment-vector entry e (1 + e of the MomentAcc layout: 8 sums, then the i <= j triangle) -> source c * 12 + slot
-struct QuadGramMap {
-  int8_t src[8 + 36];
-};
-constexpr int quad_tri(int i, int j) { return i <= j ? i * 8 - i * (i - 1) / 2 + (j - i) : quad_tri(j, i); }
-constexpr QuadGramMap make_quad_gram_map() {
-  QuadGramMap m{};
-  for (int e = 0; e < 44; ++e) m.src[e] = -1;
-  for (int c = 0; c < 4; ++c) {
-    const int f0 = (2 * c) % 8, f1 = (2 * c + 1) % 8, f2 = (2 * c + 2) % 8, f3 = (2 * c + 3) % 8, f4 = (2 * c + 4) % 8,
-              f5 = (2 * c + 5) % 8;
-    const int b = c * QuadGram::kSlots;
-    m.src[f0] = (int8_t)(b + 0);
-    m.src[f1] = (int8_t)(b + 1);
-    m.src[8 + quad_tri(f0, f0)] = (int8_t)(b + 2);
-    m.src[8 + quad_tri(f0, f1)] = (int8_t)(b + 3);
-    m.src[8 + quad_tri(f0, f2)] = (int8_t)(b + 4);
-    m.src[8 + quad_tri(f0, f3)] = (int8_t)(b + 5);
-    if (c < 2) m.src[8 + quad_tri(f0, f4)] = (int8_t)(b + 6);
-    m.src[8 + quad_tri(f0, f5)] = (int8_t)(b + 7);
-    m.src[8 + quad_tri(f1, f2)] = (int8_t)(b + 8);
-    m.src[8 + quad_tri(f1, f3)] = (int8_t)(b + 9);
-    m.src[8 + quad_tri(f1, f1)] = (int8_t)(b + 10);
-    if (c < 2) m.src[8 + quad_tri(f1, f5)] = (int8_t)(b + 11);
-  }
-  return m;
-}
-constexpr QuadGramMap kQuadGramMap = make_quad_gram_map();
-constexpr bool quad_gram_map_complete() {
-  for (int e = 0; e < 44; ++e)
-    if (kQuadGramMap.src[e] < 0) return false;
-  return true;
-}
-static_assert(quad_gram_map_complete(), "QuadGram: the four lane classes must cover every sum and Gram entry");
 
 // SdeArgs must stay the FIRST parameter: kernarg_params() reads a.params at kernarg offset 0.
 template <int D, int POT, bool MOM, int STORE, int KM = 1, bool NOISE = false, int MINW = 1, bool RES = false,
@@ -469,11 +240,8 @@ __global__ __launch_bounds__(kBlock, MINW) void sde_simulate_kernel(SdeArgs a, c
   const float h_last = a.dt - tau0;
 
   constexpr bool kStaged = (STORE == kStoreStaged) && (M % 4 == 0);
-  constexpr bool kQuad = PDEINV_SIM_QUAD && MOM && M == 8 && kStaged;  // QuadGram: the 0T moments shared by lane quads
-  PairGram<(MOM && !kQuad ? M : 2)> acc;
+  PairGram<(MOM ? M : 2)> acc;  // the 0T moments, lane-private (sharing them over lane quads measured slower, §4.6)
   acc.zero();
-  [[maybe_unused]] QuadGram qg;
-  qg.zero();
 
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t wave_row0 = i_raw - lane;
@@ -484,46 +252,9 @@ __global__ __launch_bounds__(kBlock, MINW) void sde_simulate_kernel(SdeArgs a, c
   float* tr = traj ? traj + (kStaged ? wave_row0 : i) * M : nullptr;
   float* ta = tau ? tau + i : nullptr;
   const int64_t tr_stride = a.N * M;
-  [[maybe_unused]] const f32x2* qaddr[3];
-  if constexpr (kQuad) QuadGram::addresses(stage + (threadIdx.x - lane) * M, lane, qaddr);
   auto put = [&](float* dst) {
     if constexpr (kStaged) store_rows_staged<D>(dst, z, slot, lane, n_valid);
     else if (active) store_row<D, STORE>(dst, z);
-  };
-  // kQuad: stage the row (zero for lanes past N, so the quads' sums need no weights), store it if there is a
-  // trajectory, then the quad's Gram reads of the same slot; a wave's LDS traffic only, no block barrier
-  [[maybe_unused]] auto put_mom = [&](float* dst) {
-    if constexpr (kQuad) {
-      if (n_valid == kWave) {
-#pragma unroll
-        for (int k = 0; k < M; k += 4)
-          *reinterpret_cast<f32x4*>(slot + lane * M + k) = f32x4{z[k], z[k + 1], z[k + 2], z[k + 3]};
-      } else {
-#pragma unroll
-        for (int k = 0; k < M; k += 4)
-          *reinterpret_cast<f32x4*>(slot + lane * M + k) =
-              active ? f32x4{z[k], z[k + 1], z[k + 2], z[k + 3]} : f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-      __builtin_amdgcn_wave_barrier();
-      if (dst) {
-        f32x4 v[M / 4];
-#pragma unroll
-        for (int k = 0; k < M / 4; ++k) v[k] = *reinterpret_cast<const f32x4*>(slot + 4 * (k * 64 + lane));
-        if (n_valid == kWave) {
-#pragma unroll
-          for (int k = 0; k < M / 4; ++k)
-            __builtin_nontemporal_store(v[k], reinterpret_cast<f32x4*>(dst + 4 * (k * 64 + lane)));
-        } else {
-#pragma unroll
-          for (int k = 0; k < M / 4; ++k) {
-            const int c = k * 64 + lane;
-            if (4 * c < n_valid * M) __builtin_nontemporal_store(v[k], reinterpret_cast<f32x4*>(dst + 4 * c));
-          }
-        }
-      }
-      qg.add(qaddr);
-      __builtin_amdgcn_wave_barrier();
-    }
   };
   [[maybe_unused]] float nacc[NXT ? 3 : 1][NXT ? D : 1];
   [[maybe_unused]] const int nbase = NXT ? lane * nx.np1 : 0;  // the lane's first pair
@@ -577,18 +308,16 @@ __global__ __launch_bounds__(kBlock, MINW) void sde_simulate_kernel(SdeArgs a, c
 
   // update 0: h = tau0 (sample at tau0)
   update(tau0, sqrtf(tau0) * a.ns, 0u);
-  if constexpr (kQuad) put_mom(tr);
-  else if (tr) put(tr);
+  if (tr) put(tr);
   if (active && ta) __builtin_nontemporal_store(tau_value(tau0, 0, a.dt), ta);
-  if constexpr (MOM && !kQuad) acc.add(z);
+  if constexpr (MOM) acc.add(z);
 
   const float sh_dt = sqrtf(a.dt) * a.ns;
   for (int s = 1; s < a.n_steps; ++s) {
     update(a.dt, sh_dt, (uint32_t)s);
-    if constexpr (kQuad) put_mom(tr ? tr + (int64_t)s * tr_stride : nullptr);
-    else if (tr) put(tr + (int64_t)s * tr_stride);
+    if (tr) put(tr + (int64_t)s * tr_stride);
     if (active && ta) __builtin_nontemporal_store(tau_value(tau0, s, a.dt), ta + (int64_t)s * a.N);
-    if constexpr (MOM && !kQuad) acc.add(z);
+    if constexpr (MOM) acc.add(z);
   }
 
   // final update: h = dt - tau0, lands exactly at T = n*dt (sampling_utils.py:44-46)
@@ -645,45 +374,10 @@ __global__ __launch_bounds__(kBlock, MINW) void sde_simulate_kernel(SdeArgs a, c
     block_reduce_to_slab(flat, PDEINV_GMM_NACC + rf.K * D, rlds, partials, bid, nb);
   }
 
-  if constexpr (kQuad) {
-    // class totals: the 12 accumulators summed over the 16 lanes of each class (lane bits 0, 1, 2, 5), the
-    // four waves' class totals through LDS, then entry e from its source slot (kQuadGramMap), fixed order
-    float t[QuadGram::kSlots];
-#pragma unroll
-    for (int k = 0; k < QuadGram::kSlots; ++k) {
-      float v = qg.slot(k);
-      v += __shfl_xor(v, 1, 64);
-      v += __shfl_xor(v, 2, 64);
-      v += __shfl_xor(v, 4, 64);
-      v += __shfl_xor(v, 32, 64);
-      t[k] = v;
-    }
-    __shared__ float qlds[kWavesPerBlock * 4 * QuadGram::kSlots];
-    const int wv = threadIdx.x >> 6;
-    __syncthreads();
-    if ((lane & 0x27) == 0) {
-#pragma unroll
-      for (int k = 0; k < QuadGram::kSlots; ++k) qlds[(wv * 4 + (lane >> 3)) * QuadGram::kSlots + k] = t[k];
-    }
-    __syncthreads();
-    float* dst = partials + (int64_t)L * nb;
-    if (threadIdx.x == 0) {
-      const int64_t nact = a.N - (int64_t)bid * kBlock;
-      dst[bid] = (float)a.n_steps * (float)(nact < 0 ? 0 : (nact > kBlock ? kBlock : nact));
-    } else if (threadIdx.x <= 44) {
-      const int src = kQuadGramMap.src[threadIdx.x - 1];
-      float v = 0.f;
-#pragma unroll
-      for (int w2 = 0; w2 < kWavesPerBlock; ++w2) v += qlds[w2 * 4 * QuadGram::kSlots + src];
-      dst[(int64_t)threadIdx.x * nb + bid] = v;
-    }
-  }
   if constexpr (MOM) {
-    if constexpr (!kQuad) {
-      float mv[L];
-      acc.finish((float)a.n_steps, w, mv);
-      block_reduce_to_slab(mv, L, lds, partials + (int64_t)L * nb, bid, nb);
-    }
+    float mv[L];
+    acc.finish((float)a.n_steps, w, mv);
+    block_reduce_to_slab(mv, L, lds, partials + (int64_t)L * nb, bid, nb);
     MomentAcc<M> term;
     term.zero();
     term.add(z, w);
@@ -786,89 +480,6 @@ __global__ void tau0_kernel(SdeArgs a, float* __restrict__ out) {
 }
 
 // ---- host side ----------------------------------------------------------------------------
-static int build_args(const pdeinv_sde_desc* d, SdeArgs& a) {
-  PDEINV_REQUIRE(d != nullptr, PDEINV_ERR_INVALID, "sde: null descriptor");
-  PDEINV_REQUIRE(d->dim >= 1 && d->dim <= PDEINV_MAX_DIM, PDEINV_ERR_UNSUPPORTED,
-                 "sde: dim must be in [1, 16]");
-  PDEINV_REQUIRE(d->n_steps >= 1, PDEINV_ERR_INVALID, "sde: n_steps must be >= 1");
-  PDEINV_REQUIRE(d->n_particles >= 0, PDEINV_ERR_INVALID, "sde: n_particles must be >= 0");
-  PDEINV_REQUIRE(d->particle_offset >= 0, PDEINV_ERR_INVALID, "sde: particle_offset must be >= 0");
-  PDEINV_REQUIRE(std::isfinite(d->dt) && d->dt > 0.f, PDEINV_ERR_INVALID, "sde: dt must be > 0");
-  PDEINV_REQUIRE(std::isfinite(d->gamma) && std::isfinite(d->noise_scale), PDEINV_ERR_INVALID,
-                 "sde: gamma / noise_scale must be finite");
-  const int D = d->dim;
-  a = SdeArgs{};
-  a.N = d->n_particles;
-  a.poff = d->particle_offset;
-  a.ld_z0 = d->ld_z0 ? d->ld_z0 : 2 * D;
-  PDEINV_REQUIRE(a.ld_z0 >= 2 * D, PDEINV_ERR_INVALID, "sde: ld_z0 < 2*dim");
-  a.n_steps = d->n_steps;
-  a.random_shift = d->random_shift ? 1 : 0;
-  a.dt = d->dt;
-  a.gamma = d->gamma;
-  a.ns = d->noise_scale;
-  a.k0 = (uint32_t)d->seed;
-  a.k1 = (uint32_t)(d->seed >> 32);
-  a.ctr_off = d->counter_offset;
-  a.noise = d->d_noise;
-  a.shift_u = d->d_shift_u;
-  {
-    const char* r = getenv("PDEINV_SIM_REMAP");  // A/B switch for tools/sim_alloc.py
-    a.remap = r ? atoi(r) : 1;
-  }
-  const pdeinv_potential& p = d->potential;
-  int n_params = 0;
-  switch (p.kind) {
-    case PDEINV_POT_QUADRATIC:
-    case PDEINV_POT_MEANFIELD_QUADRATIC:
-      a.has_center = (p.kind == PDEINV_POT_QUADRATIC && p.has_center) ? 1 : 0;
-      n_params = D * D + (a.has_center ? D : 0);
-      break;
-    case PDEINV_POT_GMM:
-      PDEINV_REQUIRE(p.n_centers >= 1 && p.n_centers <= kMaxGmmK &&
-                         p.n_centers * D <= PDEINV_MAX_PARAMS,
-                     PDEINV_ERR_UNSUPPORTED, "sde: GMM needs 1 <= n_centers <= 16");
-      PDEINV_REQUIRE(std::isfinite(p.sigma) && p.sigma > 0.f, PDEINV_ERR_INVALID,
-                     "sde: GMM sigma must be > 0");
-      PDEINV_REQUIRE(p.params != nullptr, PDEINV_ERR_INVALID, "sde: potential params are null");
-      a.K = p.n_centers;
-      a.inv_s2 = 1.0f / (p.sigma * p.sigma);
-      a.neg_half_inv_s2_log2e = -0.5f * a.inv_s2 * 1.4426950408889634f;
-      a.l2s = (float)(1.4426950408889634 / ((double)p.sigma * (double)p.sigma));
-      {
-        const double sc = 1.4426950408889634 / ((double)p.sigma * (double)p.sigma);
-        const int K = p.n_centers;
-        for (int k = 0; k < K; ++k) {
-          double n2 = 0;
-          for (int i = 0; i < D; ++i) {
-            const double m = p.params[k * D + i];
-            a.params[k * D + i] = (float)m;
-            n2 += m * m;
-          }
-          a.params[kMaxGmmK * D + k] = (float)(-0.5 * n2 * sc);
-        }
-      }
-      n_params = 0;  // packed above
-      break;
-    case PDEINV_POT_NONE:
-      n_params = 0;  // quadratic with A = 0
-      break;
-    default:
-      return fail(PDEINV_ERR_UNSUPPORTED, "sde: unknown potential kind");
-  }
-  if (n_params) {
-    PDEINV_REQUIRE(p.params != nullptr, PDEINV_ERR_INVALID, "sde: potential params are null");
-    for (int k = 0; k < D * D; ++k) a.params[k] = p.params[k];
-    if (a.has_center) {  // b = A c in fp64, rounded once (grad_quadratic)
-      for (int r = 0; r < D; ++r) {
-        double b = 0;
-        for (int c = 0; c < D; ++c) b += (double)p.params[r * D + c] * (double)p.params[D * D + c];
-        a.params[D * D + r] = (float)b;
-      }
-    }
-  }
-  return PDEINV_OK;
-}
 
 static int sim_grid(int64_t N) { return grid_for(N); }
 
@@ -883,24 +494,15 @@ extern "C" size_t pdeinv_sde_workspace_bytes(const pdeinv_sde_desc* d) {
   return (size_t)3 * moment_len(2 * d->dim) * sim_grid(d->n_particles) * sizeof(float);
 }
 
-// Waves per SIMD asked of the QuadGram (d = 4 moments) instantiation: at 1 the allocator takes 87 VGPRs (5 waves);
-// 6 fits in 80 with no spill; 7 spills a few dwords into the step loop.
-#ifndef PDEINV_QUAD_MINW
-#define PDEINV_QUAD_MINW 6
-#endif
-template <int D, int POT, bool MOM> constexpr int kSimMinWaves =
-    (PDEINV_SIM_QUAD && MOM && D == 4 && POT == PDEINV_POT_QUADRATIC) ? PDEINV_QUAD_MINW : 1;
-
 template <int D, int POT, bool MOM, int KM = 1>
 static void launch_sim(const SdeArgs& a, const float* z0, float* traj, float* tau, float* last,
                        float* ws, hipStream_t st) {
   const dim3 g(sim_grid(a.N)), b(kBlock);
-  constexpr int W = kSimMinWaves<D, POT, MOM>;
   if (a.noise)
-    hipLaunchKernelGGL((sde_simulate_kernel<D, POT, MOM, kStoreStaged, KM, true, W>), g, b, 0, st, a, z0, traj, tau,
+    hipLaunchKernelGGL((sde_simulate_kernel<D, POT, MOM, kStoreStaged, KM, true>), g, b, 0, st, a, z0, traj, tau,
                        last, ws);
   else
-    hipLaunchKernelGGL((sde_simulate_kernel<D, POT, MOM, kStoreStaged, KM, false, W>), g, b, 0, st, a, z0, traj, tau,
+    hipLaunchKernelGGL((sde_simulate_kernel<D, POT, MOM, kStoreStaged, KM, false>), g, b, 0, st, a, z0, traj, tau,
                        last, ws);
 }
 
@@ -950,9 +552,7 @@ static int dispatch_sim(const SdeArgs& a, int pot, bool mom, const float* z0, fl
   return 0;
 }
 
-static float shared_tau0_host(const SdeArgs& a, const pdeinv_sde_desc* d);
 
-static bool aligned(const void* p, size_t a) { return p == nullptr || ((uintptr_t)p % a) == 0; }
 
 extern "C" int pdeinv_sde_simulate(const pdeinv_sde_desc* d, const float* z0, float* traj,
                                    float* tau, float* last, void* ws, double* moments,
@@ -1113,26 +713,6 @@ extern "C" int pdeinv_mf_step(const pdeinv_sde_desc* d, int32_t s, const float* 
   return check_launch("slab_reduce_kernel");
 }
 
-// The interacting ensemble shares one clock: tau0 from global id UINT64_MAX (include/pdeinv.h).
-// Computed on the host with the same Philox so that every rank and every step agrees.
-static float shared_tau0_host(const SdeArgs& a, const pdeinv_sde_desc* d) {
-  if (!a.random_shift) return 0.f;
-  uint32_t c0 = 0xFFFFFFFFu, c1 = 0xFFFFFFFFu, c2 = a.ctr_off, c3 = 0x80000000u;
-  uint32_t k0 = a.k0, k1 = a.k1;
-  for (int r = 0; r < 10; ++r) {
-    const uint64_t p0 = (uint64_t)kM0 * c0, p1 = (uint64_t)kM1 * c2;
-    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0, n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
-    c1 = (uint32_t)p1;
-    c3 = (uint32_t)p0;
-    c0 = n0;
-    c2 = n2;
-    k0 += kW0;
-    k1 += kW1;
-  }
-  const float u = (float)(c0 >> 8) * 0x1p-24f;
-  (void)d;
-  return u * a.dt;
-}
 
 // ---- McKean–Vlasov, fused multi-step path ----------------------------------------------------
 // The quadratic interaction makes the ensemble mean exactly solvable: averaged over the particles
@@ -1148,7 +728,6 @@ static float shared_tau0_host(const SdeArgs& a, const pdeinv_sde_desc* d) {
 // agree to fp32 rounding (tests/test_gpu_meanfield.py).
 constexpr int kMfSumsPerThread = 16;  // particles per thread in pdeinv_mf_sums
 
-__host__ __device__ inline int64_t mf_sums_len(int D, int n_steps) { return 1 + 2 * D + (int64_t)(n_steps + 1) * D; }
 
 // grid.x: particle tiles of kBlock*kMfSumsPerThread; grid.y = n_steps + 2: y <= n_steps sums the update-y
 // noise, y = n_steps + 1 sums [count, x0, v0]. Slab columns: [count, x0 (D), v0 (D), xi_0 (D), ..., xi_n (D)].
@@ -1344,14 +923,11 @@ extern "C" size_t pdeinv_sde_simulate_mf_next_workspace_bytes(const pdeinv_sde_d
   return mf_next_slab_bytes(d) + pdeinv_mf_sums_workspace_bytes(d);
 }
 
-#ifndef PDEINV_MF_NEXT_MINW
-#define PDEINV_MF_NEXT_MINW 1
-#endif
 template <int D>
 static void launch_sim_mf_next(const SdeArgs& a, const MfNext& nx, const float* z0, float* traj, float* tau,
                                float* last, hipStream_t st) {
   hipLaunchKernelGGL((sde_simulate_kernel<D, PDEINV_POT_MEANFIELD_QUADRATIC, false, kStoreStaged, 1, false,
-                                          PDEINV_MF_NEXT_MINW, false, true>),
+                                          1, false, true>),
                      dim3(sim_grid(a.N)), dim3(kBlock), 0, st, a, z0, traj, tau, last, nullptr, GmmResFused{}, nx);
 }
 
@@ -1406,3 +982,4 @@ extern "C" int pdeinv_sde_simulate_mf_next(const pdeinv_sde_desc* d, const float
   if (rc) return rc;
   return mf_sums_tail(next, z0_next, d->n_steps + 1, (char*)ws + mf_next_slab_bytes(d), sums_next, st);
 }
+

@@ -36,11 +36,12 @@ GMM_NACC = 8
 GMM_ACC_SLOTS = ("loss", "loss_gt", "nabla", "hessian", "friction", "nabla_true", "initial", "terminal")
 SQRT2 = math.sqrt(2.0)
 
-ABI_VERSION = 9  # PDEINV_ABI_VERSION of include/pdeinv.h this binding was written against
+ABI_VERSION = 10  # PDEINV_ABI_VERSION of include/pdeinv.h this binding was written against
 
 # Every exported symbol of include/pdeinv.h (tests check the library exports all of them).
 EXPORTED_SYMBOLS = (
     "pdeinv_moment_len", "pdeinv_sde_workspace_bytes", "pdeinv_sde_simulate",
+    "pdeinv_sde_simulate_mf_kmv_workspace_bytes", "pdeinv_sde_simulate_mf_kmv",
     "pdeinv_mf_workspace_bytes", "pdeinv_mf_step", "pdeinv_sde_tau0",
     "pdeinv_moments_workspace_bytes", "pdeinv_moments", "pdeinv_residual_kfp_quadratic",
     "pdeinv_residual_kfp_gmm_workspace_bytes", "pdeinv_residual_kfp_gmm",
@@ -167,6 +168,8 @@ def lib():
         "pdeinv_mf_sums_workspace_bytes": (ctypes.c_size_t, [P]),
         "pdeinv_sde_simulate_mf_next_workspace_bytes": (ctypes.c_size_t, [P]),
         "pdeinv_sde_simulate_mf_next": (i32, [P, P, P, P, P, P, P, P, P, P]),
+        "pdeinv_sde_simulate_mf_kmv_workspace_bytes": (ctypes.c_size_t, [P, i32]),
+        "pdeinv_sde_simulate_mf_kmv": (i32, [P, P, P, P, P, f32, P, P, P, P, P, P, P, P]),
         "pdeinv_mf_sums": (i32, [P, P, P, P, P]),
         "pdeinv_mf_mean_path": (i32, [P, P, P, P, P]),
         "pdeinv_kmv_moments_weights_workspace_bytes": (ctypes.c_size_t, [i64, i64, i32]),
@@ -476,6 +479,44 @@ def sde_simulate_mf_next(desc: SdeDesc, z0: torch.Tensor, traj: torch.Tensor, ta
                                              _dev(sums, "sums_next", torch.float64), stream_handle()),
            "pdeinv_sde_simulate_mf_next")
     return sums
+
+
+def sde_simulate_mf_kmv(desc: SdeDesc, z0: torch.Tensor, traj: Optional[torch.Tensor], tau: Optional[torch.Tensor],
+                        last: torch.Tensor, gamma: float, coef: torch.Tensor, next_desc: Optional[SdeDesc] = None,
+                        z0_next: Optional[torch.Tensor] = None):
+    """sde_simulate_desc (fused McKean-Vlasov path) that also forms the quadratic-Phi KMV residual's per-stamp
+    sums of its own trajectory rows — (mom [n, moment_len(2d)], wst [n, moment_len(d)]) fp64, rank-local, what
+    kmv_moments_weights(d, gamma, coef, traj, n, N, N * 2d, 2d) returns up to the fp32 summation order — without
+    reading the trajectory back (traj may be None). With next_desc (counter offset differs only) also the next
+    simulate's rank-local mf_sums: (mom, wst, sums_next). pdeinv_sde_simulate_mf_kmv."""
+    _require_gpu()
+    N, m, n, d = desc.n_particles, 2 * desc.dim, desc.n_steps, desc.dim
+    for t, shape, name in ((traj, (n, N, m), "traj"), (tau, (n, N), "tau"), (last, (N, m), "last")):
+        if t is not None and (tuple(t.shape) != shape or not t.is_contiguous()):
+            raise ValueError(f"{name} must be contiguous {shape}")
+    if tuple(coef.shape) != (n, kmv_ncoef(d)) or not coef.is_contiguous():
+        raise ValueError(f"coef must be contiguous [{n}, {kmv_ncoef(d)}]")
+    if N and (z0.dim() != 2 or tuple(z0.shape) != (N, m) or z0.stride(1) != 1):
+        raise ValueError(f"z0 must be [{N}, {m}] with unit inner stride")
+    desc.ld_z0 = z0.stride(0) if N > 1 else m
+    if next_desc is not None:
+        if z0_next is None or (N and (z0_next.dim() != 2 or tuple(z0_next.shape) != (N, m) or z0_next.stride(1) != 1)):
+            raise ValueError(f"z0_next must be [{N}, {m}] with unit inner stride")
+        next_desc.ld_z0 = z0_next.stride(0) if N > 1 else m
+    nbytes = int(lib().pdeinv_sde_simulate_mf_kmv_workspace_bytes(ctypes.byref(desc), int(next_desc is not None)))
+    ws = torch.empty(max((nbytes + 3) // 4, 1), device=z0.device, dtype=torch.float32)
+    mom = torch.empty((n, moment_len(m)), device=z0.device, dtype=torch.float64)
+    wst = torch.empty((n, moment_len(d)), device=z0.device, dtype=torch.float64)
+    sums = (torch.empty(int(lib().pdeinv_mf_sums_len(ctypes.byref(next_desc))), device=z0.device, dtype=torch.float64)
+            if next_desc is not None else None)
+    _check(lib().pdeinv_sde_simulate_mf_kmv(ctypes.byref(desc), _dev(z0, "z0") if N else None, _dev(traj, "traj"),
+                                            _dev(tau, "tau"), _dev(last, "last"), float(gamma), _dev(coef, "coef"),
+                                            _dev(mom, "mom", torch.float64), _dev(wst, "wst", torch.float64),
+                                            ctypes.byref(next_desc) if next_desc is not None else None,
+                                            _dev(z0_next, "z0_next") if (next_desc is not None and N) else None,
+                                            _dev(sums, "sums_next", torch.float64), _dev(ws, "ws"), stream_handle()),
+           "pdeinv_sde_simulate_mf_kmv")
+    return (mom, wst) if next_desc is None else (mom, wst, sums)
 
 
 def mf_step(desc: SdeDesc, s: int, z: torch.Tensor, z_out: torch.Tensor, tau_row, xbar_sum: torch.Tensor,

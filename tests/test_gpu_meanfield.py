@@ -239,6 +239,86 @@ def test_simulate_mf_next_sums(native, d, n, n_steps, poff):
     del keep, keep_n
 
 
+@pytest.mark.parametrize("d,n,n_steps,poff", [(8, 50_001, 100, 0), (8, 4099, 30, 123_456_789_012), (2, 999, 2, 5),
+                                            (4, 37, 127, 0), (6, 4096, 64, 77), (8, 70_000, 1, 3)])
+def test_simulate_mf_kmv_equals_separate(native, d, n, n_steps, poff):
+    """pdeinv_sde_simulate_mf_kmv (C4: the KMV residual's per-stamp sums formed inside the simulator from its
+    LDS-staged rows, on the matrix pipe): trajectory / tau / last bit-identical to the plain fused simulate;
+    mom / wst == kmv_moments_weights over the written trajectory to fp32 reassociation (1e-5 relative, as
+    test_kmv_moments_weights_fused_equals_separate); with the next simulate, sums_next as
+    test_simulate_mf_next_sums. Partial waves (n = 37), rows past N inside a block (4099, 999), ids past 2^32,
+    one stamp (n_steps = 1), three running noise sums per lane (n_steps + 1 = 128)."""
+    rng = np.random.default_rng(d + n + n_steps + 1)
+    z0 = _t(rng.standard_normal((n, 2 * d)) * 0.8 + 0.25)
+    A = nr.problem_constants(d)
+    desc, keep = native.mf_desc(n, d, n_steps, 0.02, 1.0, A, seed=0x5EED_0004, counter_offset=777,
+                                particle_offset=poff)
+    xbar, _ = native.mf_mean_path(desc, native.mf_sums(desc, z0), xsum=False)
+    desc.d_meanfield = ctypes.c_void_p(xbar.data_ptr())
+    out = [{k: torch.empty(shape, device="cuda") for k, shape in
+            (("traj", (n_steps, n, 2 * d)), ("tau", (n_steps, n)), ("last", (n, 2 * d)))} for _ in range(3)]
+    native.sde_simulate_desc(desc, z0, out[0]["traj"], out[0]["tau"], out[0]["last"])
+    from utils.mean_field import stamp_times
+    _, coef = _coef(d, stamp_times(0x5EED_0004, 777, n_steps, 0.02).astype(np.float64) + 0.05)
+    mom_s, wst_s = native.kmv_moments_weights(d, 1.0, coef, out[0]["traj"], n_steps, n, n * 2 * d, 2 * d)
+    nxt, keep_n = native.mf_desc(n, d, n_steps, 0.02, 1.0, A, seed=0x5EED_0004, counter_offset=777 + n_steps + 1,
+                                 particle_offset=poff)
+    mom, wst = native.sde_simulate_mf_kmv(desc, z0, out[1]["traj"], out[1]["tau"], out[1]["last"], 1.0, coef)
+    mom2, wst2, sums = native.sde_simulate_mf_kmv(desc, z0, out[2]["traj"], out[2]["tau"], out[2]["last"], 1.0, coef,
+                                                  nxt, z0)
+    for k in ("traj", "tau", "last"):
+        assert torch.equal(out[0][k], out[1][k]) and torch.equal(out[0][k], out[2][k]), k
+    assert torch.equal(mom, mom2) and torch.equal(wst, wst2)  # the same stamp sums with and without the next sums
+    assert np.array_equal(mom[:, 0].cpu().numpy(), np.full(n_steps, float(n)))
+    for a, b in ((mom, mom_s), (wst, wst_s)):
+        a, b = a.cpu().numpy(), b.cpu().numpy()
+        assert np.allclose(a, b, rtol=1e-5, atol=1e-5 * np.abs(b).max())
+    ref = native.mf_sums(nxt, z0).cpu().numpy()
+    got = sums.cpu().numpy()
+    assert got.shape == ref.shape and got[0] == ref[0] == n
+    assert np.array_equal(got[1:1 + 2 * d], ref[1:1 + 2 * d])
+    assert np.max(np.abs(got[1 + 2 * d:] - ref[1 + 2 * d:])) < 1e-5 * np.sqrt(n)
+    # no trajectory at all: the stamp sums still come out (nothing is read back)
+    last = torch.empty((n, 2 * d), device="cuda")
+    mom3, wst3 = native.sde_simulate_mf_kmv(desc, z0, None, None, last, 1.0, coef)
+    assert torch.equal(mom3, mom) and torch.equal(wst3, wst) and torch.equal(last, out[0]["last"])
+    del keep, keep_n
+
+
+def test_simulate_mf_kmv_rejects(native):
+    """Odd dims and long paths with next sums are UNSUPPORTED; a next simulate that differs in more than its
+    counter, a coefficient table of the wrong shape and a non-McKean-Vlasov descriptor are INVALID."""
+    n, d = 1000, 8
+    A = nr.problem_constants(d)
+    z0 = _t(np.zeros((n, 2 * d)))
+    desc, keep = native.mf_desc(n, d, 10, 0.02, 1.0, A, seed=1, counter_offset=0)
+    xbar, _ = native.mf_mean_path(desc, native.mf_sums(desc, z0), xsum=False)
+    desc.d_meanfield = ctypes.c_void_p(xbar.data_ptr())
+    last = torch.empty((n, 2 * d), device="cuda")
+    _, coef = _coef(d, np.linspace(0.1, 1.0, 10))
+    other, keep2 = native.mf_desc(n, d, 10, 0.02, 1.0, A, seed=2, counter_offset=11)
+    with pytest.raises(ValueError):
+        native.sde_simulate_mf_kmv(desc, z0, None, None, last, 1.0, coef, other, z0)
+    with pytest.raises(ValueError):
+        native.sde_simulate_mf_kmv(desc, z0, None, None, last, 1.0, coef[:5].contiguous())
+    long_desc, keep3 = native.mf_desc(n, d, 200, 0.02, 1.0, A, seed=1, counter_offset=0)
+    long_next, keep4 = native.mf_desc(n, d, 200, 0.02, 1.0, A, seed=1, counter_offset=201)
+    long_desc.d_meanfield = ctypes.c_void_p(xbar.data_ptr())
+    _, coef200 = _coef(d, np.linspace(0.01, 2.0, 200))
+    with pytest.raises(NotImplementedError):
+        native.sde_simulate_mf_kmv(long_desc, z0, None, None, last, 1.0, coef200, long_next, z0)
+    d3 = 3
+    A3 = nr.problem_constants(d3)
+    z03 = _t(np.zeros((n, 2 * d3)))
+    desc3, keep5 = native.mf_desc(n, d3, 10, 0.02, 1.0, A3, seed=1, counter_offset=0)
+    xbar3, _ = native.mf_mean_path(desc3, native.mf_sums(desc3, z03), xsum=False)
+    desc3.d_meanfield = ctypes.c_void_p(xbar3.data_ptr())
+    _, coef3 = _coef(d3, np.linspace(0.1, 1.0, 10))
+    with pytest.raises(NotImplementedError):
+        native.sde_simulate_mf_kmv(desc3, z03, None, None, torch.empty((n, 2 * d3), device="cuda"), 1.0, coef3)
+    del keep, keep2, keep3, keep4, keep5
+
+
 def test_simulate_mf_next_rejects(native):
     """The next simulate must differ in its counter only; odd dims / long paths are UNSUPPORTED (pdeinv_mf_sums)."""
     n, d = 1000, 8

@@ -218,7 +218,7 @@ def test_library_exports_every_header_symbol():
     missing = [s for s in _header_functions() if not hasattr(lib, s)]
     assert not missing
     lib.pdeinv_moment_len.restype = ctypes.c_int
-    assert lib.pdeinv_moment_len(8) == 45 and lib.pdeinv_abi_version() == native.ABI_VERSION == 9
+    assert lib.pdeinv_moment_len(8) == 45 and lib.pdeinv_abi_version() == native.ABI_VERSION == 10
 
 
 def test_loader_fails_loudly_without_gpu():
