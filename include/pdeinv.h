@@ -398,8 +398,12 @@ typedef struct {
 #define PDEINV_MLP_IMPL_PAIRS_RING 3 /* pdeinv_residual_kmv_mlp only: force the register-ring pair kernels
                                         (width <= 28) instead of the MFMA pair tiles — A/B and cross-checks */
 /* 1 when impl = AUTO runs this V_hypothesis shape on the hand-written fused fp32-MFMA kernels (compiled shapes and
-   the zero-padded envelope: dim <= 16, width <= 512, depth 1..16, any out_features), 0 when it takes rocBLAS */
+   the zero-padded envelope: dim <= 16, width <= 1024, depth 1..16, any out_features), 0 when AUTO rejects it
+   (PDEINV_ERR_UNSUPPORTED: only the explicit impl = LIBRARY cross-check runs such shapes, on rocBLAS) */
 int pdeinv_mlp_fused_supported(int32_t dim, int32_t n_layers, int32_t width, int32_t out_features);
+/* Residual calls (pdeinv_residual_kfp_mlp / pdeinv_residual_kmv_mlp) served by rocBLAS in this process so far: only
+   impl = LIBRARY ever adds to it (ABI 10). */
+int64_t pdeinv_rocblas_calls(void);
 int64_t pdeinv_mlp_param_count(int32_t dim, int32_t n_layers, int32_t width, int32_t out_features);
 size_t pdeinv_residual_kfp_mlp_workspace_bytes(const pdeinv_kfp_mlp_desc* desc);
 int pdeinv_residual_kfp_mlp(const pdeinv_kfp_mlp_desc* desc, const float* d_init, int64_t n_init,
@@ -468,7 +472,7 @@ int pdeinv_residual_kmv_mlp(const pdeinv_kmv_mlp_desc* desc, const float* d_z, i
  * (pdeinv_gaussian_sample_grouped with the same seed / ctr_z / row_off and these means / factors gives the
  * same rows). t_g = t_min + (t_max - t_min) u_g, u_g = 24 bits of Philox(seed; (g, 0, ctr_t, 0xD0000000)),
  * unless t_in gives them. Outputs t_out [G], mean_out [G, n], factor_out [G, n, n] are optional (null).
- * n = 2d in {2..16 even, 20, 24, 32}; d_powers [(taylor_degree + 1), 2n, 2n], d_m0 [n], d_P0 [n, n] fp64.
+ * n = 2d, any even n <= 32 (d = 1..16); d_powers [(taylor_degree + 1), 2n, 2n], d_m0 [n], d_P0 [n, n] fp64.
  * --------------------------------------------------------------------------------------- */
 typedef struct {
   int32_t n;              /* 2d */

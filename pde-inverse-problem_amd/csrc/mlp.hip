@@ -15,6 +15,8 @@
 // the kernels below. The derivation is oracle/numpy_ref.py kfp_mlp_grad_analytic, checked against
 // central finite differences.
 #include <dlfcn.h>
+
+#include <atomic>
 #include <math.h>
 #include <rocblas/rocblas.h>
 
@@ -38,6 +40,9 @@ struct BlasApi {
   decltype(&rocblas_sgemm_strided_batched) sgemm_strided_batched = nullptr;
   bool ok = false;
 };
+
+// residual calls served by rocBLAS in this process (pdeinv_rocblas_calls: AUTO / FUSED never add to it)
+static std::atomic<int64_t> g_rocblas_calls{0};
 
 static const BlasApi& blas_api() {
   static const BlasApi api = [] {
@@ -478,8 +483,8 @@ using namespace pdeinv;
 // {32, 64, 128, 256, 512, 1024} (any depth 1..16, any out_features: mlpf::supported); every other dim <= 16 and
 // width <= 1024 runs zero-padded to the next compiled one — exact: padded inputs and K1 rows are zero, padded
 // hidden units have zero weights in and out (common.h MlpPadMap) — at the cost of the padded MACs. The
-// reference's default V_hypothesis is 20 wide (configurations/neural_network/MLP.yaml:4-5). Only
-// impl = LIBRARY (or width > 1024) reaches the rocBLAS path.
+// reference's default V_hypothesis is 20 wide (configurations/neural_network/MLP.yaml:4-5). Only the explicit
+// impl = LIBRARY reaches the rocBLAS path; an AUTO / FUSED shape outside the envelope is UNSUPPORTED.
 struct FusedShape {
   int Dp = 0, Wp = 0;
   bool pad = false;
@@ -500,6 +505,8 @@ static bool fused_shape(const pdeinv_kfp_mlp_desc* d, FusedShape* f = nullptr) {
 
 // The shape runs the hand-written fused fp32-MFMA path under impl = AUTO: the padded envelope of fused_shape (dims
 // and widths zero-padded to the compiled ones), not only the compiled shapes themselves.
+extern "C" int64_t pdeinv_rocblas_calls(void) { return g_rocblas_calls.load(std::memory_order_relaxed); }
+
 extern "C" int pdeinv_mlp_fused_supported(int32_t dim, int32_t n_layers, int32_t width, int32_t out_features) {
   pdeinv_kfp_mlp_desc d{};
   d.dim = dim; d.n_layers = n_layers; d.width = width; d.out_features = out_features;
@@ -753,6 +760,10 @@ extern "C" int pdeinv_residual_kfp_mlp(const pdeinv_kfp_mlp_desc* d, const float
   PDEINV_REQUIRE(n0 >= 1 && ni >= 0 && nt >= 0, PDEINV_ERR_INVALID, "kfp_mlp: 0T set must be non-empty");
   PDEINV_REQUIRE(params && ws && acc && grad && z0 && (ni == 0 || zi) && (nt == 0 || zt), PDEINV_ERR_INVALID,
                  "kfp_mlp: null pointer");
+  // rocBLAS serves the explicit impl = LIBRARY only: AUTO / FUSED outside the hand-written envelope are rejected
+  PDEINV_REQUIRE(d->impl == PDEINV_MLP_IMPL_LIBRARY || fused_shape(d), PDEINV_ERR_UNSUPPORTED,
+                 "kfp_mlp: the hand-written path takes dim <= 16, 1 <= n_layers <= 16, width <= 1024 (zero-padded to "
+                 "the compiled dims / widths), any out_features; impl = LIBRARY (rocBLAS) is the opt-in cross-check");
   const MlpPlan p = make_plan(d);
   PDEINV_REQUIRE(p.Bc <= (1 << 26), PDEINV_ERR_INVALID, "kfp_mlp: chunk_rows too large");
   hipStream_t st = (hipStream_t)stream;
@@ -855,14 +866,12 @@ extern "C" int pdeinv_residual_kfp_mlp(const pdeinv_kfp_mlp_desc* d, const float
     }
     return PDEINV_OK;
   }
-  PDEINV_REQUIRE(d->impl != PDEINV_MLP_IMPL_FUSED, PDEINV_ERR_UNSUPPORTED,
-                 "kfp_mlp: the fused path takes dim <= 16, 1 <= n_layers <= 16, width <= 512 (zero-padded to the "
-                 "compiled dims / widths), any out_features");
   Blas blas{blas_handle(dev), st, w + p.off_kpart};
   PDEINV_REQUIRE(blas_api().ok, PDEINV_ERR_UNSUPPORTED,
                  "kfp_mlp: impl = LIBRARY needs rocBLAS (librocblas.so.5 could not be loaded)");
   if (!blas.h) return fail(PDEINV_ERR_HIP, "kfp_mlp: rocblas_create_handle failed");
   if (blas_api().set_stream(blas.h, st) != rocblas_status_success) return fail(PDEINV_ERR_HIP, "kfp_mlp: rocblas_set_stream");
+  g_rocblas_calls.fetch_add(1, std::memory_order_relaxed);
   LibRun run{p, &blas, w, params, grad, poff, boff, st, acc};
   for (const Set& s : sets) {
     PDEINV_REQUIRE(s.n == 0 || s.ld >= 2 * D, PDEINV_ERR_INVALID, "kfp_mlp: row stride < 2*dim");
@@ -1049,6 +1058,7 @@ static int kmv_mlp_run(const pdeinv_kmv_mlp_desc* d, const KmvPlan& k, const flo
                  "kmv_mlp: impl = LIBRARY needs rocBLAS (librocblas.so.5 could not be loaded)");
   if (!blas.h) return fail(PDEINV_ERR_HIP, "kmv_mlp: rocblas_create_handle failed");
   if (blas_api().set_stream(blas.h, st) != rocblas_status_success) return fail(PDEINV_ERR_HIP, "kmv_mlp: rocblas_set_stream");
+  g_rocblas_calls.fetch_add(1, std::memory_order_relaxed);
   int64_t poff[18], boff[18];
   param_offsets(D, d->width, d->out_features, d->n_layers, poff, boff);
   LibRun run{k.lib, &blas, w, params, grad, poff, boff, st, acc};
@@ -1254,7 +1264,9 @@ extern "C" int pdeinv_kmv_mlp_path(const pdeinv_kmv_mlp_desc* d) {
   if (!d || d->dim < 1 || d->n_layers < 1 || d->n_layers > 16 || d->width < 1 || d->out_features < 1) return -1;
   if (kmv_use_pairs(d)) return kmvq_supported(d) ? PDEINV_KMV_PATH_PAIR_TILES : PDEINV_KMV_PATH_PAIR_RING;
   if (d->impl == PDEINV_MLP_IMPL_PAIRS_RING) return -1;
-  return kmv_use_fused(d) ? PDEINV_KMV_PATH_FUSED_ROWS : PDEINV_KMV_PATH_LIBRARY;
+  if (kmv_use_fused(d)) return PDEINV_KMV_PATH_FUSED_ROWS;
+  // rocBLAS only on the explicit opt-in, and only for the shapes its kernels take (dim 1..8)
+  return d->impl == PDEINV_MLP_IMPL_LIBRARY && d->dim <= 8 ? PDEINV_KMV_PATH_LIBRARY : -1;
 }
 
 extern "C" size_t pdeinv_residual_kmv_mlp_workspace_bytes(const pdeinv_kmv_mlp_desc* d) {
@@ -1297,6 +1309,10 @@ extern "C" int pdeinv_residual_kmv_mlp(const pdeinv_kmv_mlp_desc* d, const float
                  "kmv_mlp: impl must be AUTO, LIBRARY, FUSED or PAIRS_RING");
   PDEINV_REQUIRE(d->impl != PDEINV_MLP_IMPL_PAIRS_RING || kmv_use_pairs(d), PDEINV_ERR_UNSUPPORTED,
                  "kmv_mlp: PAIRS_RING needs dim <= 8, width <= 28, n_layers <= 16, out_features <= 64");
+  PDEINV_REQUIRE(pdeinv_kmv_mlp_path(d) >= 0, PDEINV_ERR_UNSUPPORTED,
+                 "kmv_mlp: the hand-written paths need dim <= 8 with width <= 28 (pair kernels), or dim <= 16 with "
+                 "1 <= n_layers <= 16, width <= 1024 (fused MFMA path); impl = LIBRARY (rocBLAS, dim <= 8) is the "
+                 "opt-in cross-check");
   hipStream_t st = (hipStream_t)stream;
   if (kmv_use_pairs(d)) {
     switch (d->dim) {
@@ -1315,9 +1331,6 @@ extern "C" int pdeinv_residual_kmv_mlp(const pdeinv_kmv_mlp_desc* d, const float
 #undef CASE
     }
   }
-  PDEINV_REQUIRE(d->impl != PDEINV_MLP_IMPL_FUSED, PDEINV_ERR_UNSUPPORTED,
-                 "kmv_mlp: the hand-written paths need dim <= 8 with width <= 28 (pair kernels), or dim <= 16 with "
-                 "1 <= n_layers <= 16, width <= 1024 (fused MFMA path)");
   const KmvPlan k = kmv_plan(d);
   switch (d->dim) {
 #define CASE(DD) case DD: return kmv_mlp_run<DD>(d, k, z, set_stride, ld, ds, params, (float*)ws, acc, grad, st);

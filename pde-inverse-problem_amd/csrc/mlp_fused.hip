@@ -1568,11 +1568,13 @@ __global__ __launch_bounds__(kRT, 1) void wgrad2(WgradArgs a) {
     float av[MI][4], bv[NI][4];
     [[maybe_unused]] float xv[GA == GA_L1 ? NXP : 1];
     if constexpr (GA == GA_L1) {  // through the wave's slab (LDS ops of one wave complete in order)
+      __builtin_amdgcn_wave_barrier();  // the previous step's cross-lane reads of the slab stay before these stores
 #pragma unroll
       for (int j = 0; j < NXE; ++j) {
         const int e = lane + 64 * j;
         if (e < 2 * NXP) xw[e] = g.x[j];
       }
+      __builtin_amdgcn_wave_barrier();  // and these stores before the cross-lane reads below
 #pragma unroll
       for (int j = 0; j < NXP / 4; ++j) {
         const f32x4 v = *reinterpret_cast<const f32x4*>(xw + hi * NXP + 4 * j);

@@ -179,8 +179,8 @@ extern "C" int pdeinv_ou_exact_sample(const pdeinv_ou_desc* d, int64_t n_groups,
                                       const float* t_in, float* t_out, float* mean_out, float* factor_out, float* out,
                                       void* stream) {
   PDEINV_REQUIRE(d != nullptr, PDEINV_ERR_INVALID, "ou_exact_sample: null descriptor");
-  PDEINV_REQUIRE(d->n >= 2 && d->n <= 32 && d->n % 2 == 0 && (d->n <= 16 || d->n == 20 || d->n == 24 || d->n == 32),
-                 PDEINV_ERR_UNSUPPORTED, "ou_exact_sample: dim must be 1-8, 10, 12 or 16");
+  PDEINV_REQUIRE(d->n >= 2 && d->n <= 2 * PDEINV_MAX_DIM && d->n % 2 == 0, PDEINV_ERR_UNSUPPORTED,
+                 "ou_exact_sample: dim must be in [1, 16]");
   PDEINV_REQUIRE(d->taylor_degree >= 1 && d->taylor_degree <= 30 && d->squarings >= 0 && d->squarings <= 30,
                  PDEINV_ERR_INVALID, "ou_exact_sample: need 1 <= taylor_degree <= 30, 0 <= squarings <= 30");
   PDEINV_REQUIRE(n_groups >= 0 && rows_per_group >= 0 && row_off >= 0 && n_groups <= 0x7FFFFFFF, PDEINV_ERR_INVALID,
@@ -214,7 +214,8 @@ extern "C" int pdeinv_ou_exact_sample(const pdeinv_ou_desc* d, int64_t n_groups,
   hipStream_t st = (hipStream_t)stream;
   switch (d->n) {
 #define CASE(MM) case MM: hipLaunchKernelGGL(ou_exact_sample_kernel<MM>, dim3((unsigned)n_groups), dim3(kBlock), 0, st, a); break;
-    CASE(2) CASE(4) CASE(6) CASE(8) CASE(10) CASE(12) CASE(14) CASE(16) CASE(20) CASE(24) CASE(32)
+    CASE(2) CASE(4) CASE(6) CASE(8) CASE(10) CASE(12) CASE(14) CASE(16) CASE(18) CASE(20) CASE(22) CASE(24)
+    CASE(26) CASE(28) CASE(30) CASE(32)
 #undef CASE
   }
   return check_launch("ou_exact_sample_kernel");

@@ -152,10 +152,11 @@ extern "C" int pdeinv_gaussian_sample_grouped(int64_t n_groups, int64_t rows_per
   switch (m) {
 #define CASE(MM) case MM: hipLaunchKernelGGL(gaussian_sample_kernel<MM>, g, dim3(kBlock), 0, st, n, k0, k1, ctr, row_off, mean, ch, out, rows_per_group); break;
     CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) CASE(9) CASE(10) CASE(11)
-    CASE(12) CASE(13) CASE(14) CASE(15) CASE(16) CASE(18) CASE(20) CASE(24) CASE(32)
+    CASE(12) CASE(13) CASE(14) CASE(15) CASE(16) CASE(18) CASE(20) CASE(22) CASE(24) CASE(26) CASE(28) CASE(30)
+    CASE(32)
 #undef CASE
     default:
-      return fail(PDEINV_ERR_UNSUPPORTED, "gaussian_sample: dim must be 1-16, 18, 20, 24 or 32");
+      return fail(PDEINV_ERR_UNSUPPORTED, "gaussian_sample: dim must be 1-16 or an even number up to 32");
   }
   return check_launch("gaussian_sample_kernel");
 }

@@ -51,7 +51,7 @@ EXPORTED_SYMBOLS = (
     "pdeinv_runtime_version", "pdeinv_moments_batched_workspace_bytes", "pdeinv_moments_batched",
     "pdeinv_kmv_weights_workspace_bytes", "pdeinv_kmv_weights", "pdeinv_residual_kmv",
     "pdeinv_residual_kmv_workspace_bytes",
-    "pdeinv_mlp_param_count", "pdeinv_residual_kfp_mlp_workspace_bytes", "pdeinv_residual_kfp_mlp",
+    "pdeinv_mlp_param_count", "pdeinv_rocblas_calls", "pdeinv_residual_kfp_mlp_workspace_bytes", "pdeinv_residual_kfp_mlp",
     "pdeinv_kfp_terms_finalize", "pdeinv_gather_random_step", "pdeinv_mlp_fused_supported",
     "pdeinv_adam_update", "pdeinv_realnvp_param_count", "pdeinv_realnvp_logdensity",
     "pdeinv_realnvp_grad_workspace", "pdeinv_realnvp_value_and_grad",
@@ -198,6 +198,7 @@ def lib():
         "pdeinv_residual_kmv_workspace_bytes": (ctypes.c_size_t, [P]),
         "pdeinv_residual_kmv": (i32, [P, P, P, P, P, P, P, P]),
         "pdeinv_mlp_param_count": (i64, [i32, i32, i32, i32]),
+        "pdeinv_rocblas_calls": (i64, []),
         "pdeinv_mlp_fused_supported": (i32, [i32, i32, i32, i32]),
         "pdeinv_adam_update": (i32, [P, P, P, P, i64, f32, f32, f32, f32, f32, i32, P]),
         "pdeinv_realnvp_param_count": (i64, [P]),
@@ -1089,6 +1090,11 @@ def kmv_mlp_path(dims, impl: int = MLP_IMPL_AUTO) -> str:
     if p < 0:
         raise NotImplementedError(f"kmv_mlp: unsupported shape {dims} / impl {impl}")
     return KMV_PATHS[p]
+
+
+def rocblas_calls() -> int:
+    """Residual calls served by rocBLAS in this process (pdeinv_rocblas_calls): only impl = LIBRARY adds to it."""
+    return int(lib().pdeinv_rocblas_calls())
 
 
 def mlp_fused_supported(dims) -> bool:

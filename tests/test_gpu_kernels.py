@@ -295,7 +295,7 @@ def test_kou_exact_random_time_sampler(native):
     assert np.all(np.abs(emp - Pbar) < 5 * sd + 1e-3)
 
 
-@pytest.mark.parametrize("d", [1, 2, 4, 8, 16])
+@pytest.mark.parametrize("d", [1, 2, 4, 8, 9, 10, 12, 15, 16])
 def test_ou_exact_sampler_device_moments(native, d):
     """pdeinv_ou_exact_sample (the device-resident exact KOU sampler): the drawn times lie in [t_min, t_max); the
     per-group mean and Cholesky factor equal the host closed form (ou_moments_batched, fp64 Van Loan) to fp32
@@ -407,6 +407,34 @@ def test_residual_mlp_vs_restatement(native, dims, true_kind, chunk, impl):
     assert abs(out[2] - np.linalg.norm(g_ref)) < 2e-3 * (1 + np.linalg.norm(g_ref))
 
 
+def test_auto_never_reaches_rocblas(native):
+    """impl = AUTO never resolves to rocBLAS: AUTO KFP MLP residuals across the hand-written envelope (padded dims /
+    widths, width 1024, depth 3, out 56) leave pdeinv_rocblas_calls unchanged, one shape past the envelope
+    ([4, 2048, 2048, 40]) raises NotImplementedError, and the explicit impl = LIBRARY call does count."""
+    pc = lambda dims: int(native.lib().pdeinv_mlp_param_count(dims[0], len(dims) - 2, dims[1], dims[-1]))
+    rng = np.random.default_rng(5)
+    before = native.rocblas_calls()
+    for dims in ([4, 256, 256, 40], [3, 20, 20, 40], [4, 1024, 1024, 40], [12, 100, 60], [4, 64, 64, 64, 56]):
+        d = dims[0]
+        flat = _t(rng.standard_normal(pc(dims)) * 0.05)
+        z = [_t(rng.standard_normal((m, 2 * d))) for m in (300, 200, 700)]
+        native.residual_kfp_mlp(dims, flat, z[0], z[1], z[2], true_kind=native.POT_QUADRATIC,
+                                true_params=np.eye(d, dtype=np.float32), gamma=0.5, total_time=2.0, chunk_rows=256)
+    wide = [4, 2048, 2048, 40]
+    with pytest.raises(NotImplementedError):
+        native.residual_kfp_mlp(wide, torch.zeros(pc(wide), device=DEV), *[torch.zeros((64, 8), device=DEV)] * 3,
+                                true_kind=native.POT_QUADRATIC, true_params=np.eye(4, dtype=np.float32), gamma=0.5,
+                                total_time=2.0, chunk_rows=64)
+    torch.cuda.synchronize()
+    assert native.rocblas_calls() == before
+    dims = [4, 64, 64, 40]
+    z = [_t(rng.standard_normal((m, 8))) for m in (300, 200, 700)]
+    native.residual_kfp_mlp(dims, _t(rng.standard_normal(pc(dims)) * 0.05), z[0], z[1], z[2],
+                            true_kind=native.POT_QUADRATIC, true_params=np.eye(4, dtype=np.float32), gamma=0.5,
+                            total_time=2.0, impl=native.MLP_IMPL_LIBRARY)
+    assert native.rocblas_calls() == before + 1
+
+
 def test_residual_mlp_fused_chunk_at_offset_limit(native):
     """The C5 default chunk: 2^22 rows x width 256 = 2^30 floats per plane, the largest chunk whose byte offsets
     (32-bit, from a uniform plane base) do not wrap. One 2^22-row 0T chunk equals two 2^21-row chunks to fp32
@@ -432,14 +460,15 @@ def test_residual_mlp_fused_chunk_at_offset_limit(native):
 
 
 @pytest.mark.parametrize("dims", [[8, 256, 256, 40], [4, 64, 40], [2, 32, 32, 32, 40], [4, 128, 128, 128, 40],
-                                  [16, 128, 128, 24]])
+                                  [16, 128, 128, 24], [8, 128, 128, 64], [4, 256, 256, 56]])
 def test_residual_mlp_boundary_sets_span_chunks(native, dims):
     """The initial / terminal sets take the first-order chain (no g, no forward adjoint: c_nabla = c_hess = 0 there,
     kinetic_fokker_planck.py:34-39) — here with boundary sets larger than the 0T set, split over several chunks
     (5000 rows at chunk 2048), L = 1 / 2 / 3: loss and gradient equal the fp64 restatement and the rocBLAS library
     path (which runs the full chain). Widths 128 / 256 run the two-stream kernels (mlp_fused.hip run_chunk_fo2:
     [h, z'] forward, [zbar, z'bar] back, the seeds in the output epilogue, 2-pair weight gradients), including a
-    middle layer (L = 3) and out_features 24; the narrower nets the zeroed-plane first-order path."""
+    middle layer (L = 3) and out_features 24 / 40 (the 16-wide output tiles of rgemm16) and 56 / 64 (past 48 columns:
+    the 64-column rgemm E_OUT_SEEDS1 epilogue); the narrower nets the zeroed-plane first-order path."""
     rng = np.random.default_rng(sum(dims))
     d = dims[0]
     flat = np.concatenate([np.concatenate([rng.standard_normal((dims[i], dims[i + 1])).ravel() * np.sqrt(1.0 / dims[i]),

@@ -256,7 +256,7 @@ def test_abi_argument_validation_without_gpu():
     assert L.pdeinv_realnvp_value_and_grad(None, None, None, 0, None, 0, 0, None, None, None, 0, None) \
         == native.PDEINV_ERR_INVALID
     # the query reports the AUTO path: compiled shapes and the zero-padded envelope (d = 3 -> 4, width 20 -> 32);
-    # width > 1024 takes rocBLAS
+    # width > 1024 is rejected under AUTO (only the explicit LIBRARY cross-check reaches rocBLAS)
     assert L.pdeinv_mlp_fused_supported(3, 2, 256, 40) == 1 and L.pdeinv_mlp_fused_supported(8, 2, 256, 40) == 1
     assert L.pdeinv_mlp_fused_supported(8, 1, 256, 40) == 1 and L.pdeinv_mlp_fused_supported(8, 2, 256, 80) == 1
     assert L.pdeinv_mlp_fused_supported(2, 8, 20, 40) == 1 and L.pdeinv_mlp_fused_supported(8, 2, 1024, 40) == 1
@@ -266,6 +266,15 @@ def test_abi_argument_validation_without_gpu():
     assert native.kmv_mlp_path([2, 24, 24, 40]) == "pair_ring"
     assert native.kmv_mlp_path([2, 64, 64, 40]) == "fused_rows_mfma"
     assert native.kmv_mlp_path([2, 64, 64, 40], native.MLP_IMPL_LIBRARY) == "library_rocblas"
+    # LIBRARY only where the rocBLAS path runs (dim <= 8); AUTO never resolves to it
+    with pytest.raises(NotImplementedError):
+        native.kmv_mlp_path([12, 64, 64, 40], native.MLP_IMPL_LIBRARY)
+    with pytest.raises(NotImplementedError):
+        native.kmv_mlp_path([4, 2048, 2048, 40])
+    with pytest.raises(NotImplementedError):
+        native.kmv_mlp_path([17, 64, 64, 40])
+    for dims in ([2] + [20] * 8 + [40], [2, 24, 24, 40], [2, 64, 64, 40], [12, 1000, 1000, 40], [16, 1024, 40]):
+        assert native.kmv_mlp_path(dims) != "library_rocblas"
     # impl is validated (PDEINV_MLP_IMPL_PAIRS_RING selects the register-ring pair kernels, kmv_mlp only)
     F = (ctypes.c_float * 4)(1, 0, 0, 1)
     km = native.KmvMlpDesc()
@@ -281,6 +290,15 @@ def test_abi_argument_validation_without_gpu():
     fm.dim, fm.n_layers, fm.width, fm.out_features, fm.impl = 4, 2, 256, 40, native.MLP_IMPL_PAIRS_RING
     assert L.pdeinv_residual_kfp_mlp(ctypes.byref(fm), None, 0, 0, None, 0, 0, None, 0, 0, None, None, None, None,
                                      None) == native.PDEINV_ERR_INVALID
+    # AUTO past the hand-written envelope is UNSUPPORTED before any HIP call (no rocBLAS fallback)
+    Fq = (ctypes.c_float * 16)(*np.eye(4, dtype=np.float32).ravel())
+    fm.width, fm.impl, fm.true_kind, fm.true_params = 2048, native.MLP_IMPL_AUTO, native.POT_QUADRATIC, \
+        ctypes.cast(Fq, ctypes.c_void_p)
+    assert L.pdeinv_residual_kfp_mlp(ctypes.byref(fm), dummy, 64, 8, dummy, 64, 8, dummy, 64, 8, dummy, dummy, dummy,
+                                     dummy, None) == native.PDEINV_ERR_UNSUPPORTED
+    assert b"LIBRARY" in L.pdeinv_last_error()
+    km.impl, km.width, km.n_layers = native.MLP_IMPL_AUTO, 2048, 2
+    assert call() == native.PDEINV_ERR_UNSUPPORTED and b"LIBRARY" in L.pdeinv_last_error()
 
 
 def test_bench_refuses_mismatched_world_size():
