@@ -98,11 +98,12 @@ def parse():
     p.add_argument("--c4-separate-sums", action="store_true",
                    help="C4: the next simulate's mean-path sums as their own launch (pdeinv_mf_sums) instead of "
                         "inside the KMV pass (pdeinv_kmv_moments_weights_mf_sums), for A/B")
-    p.add_argument("--c4-schedule", default="simkmv", choices=["fused", "concurrent", "sim", "simkmv"],
-                   help="C4 steady state: 'simkmv' (default) = the simulator forms the KMV per-stamp sums from its "
-                        "staged rows and draws the next simulate's noise sums (pdeinv_sde_simulate_mf_kmv: no "
-                        "trajectory re-read); 'sim' = the simulator draws the next simulate's noise sums "
-                        "(pdeinv_sde_simulate_mf_next), plain KMV pass; 'fused' = the next simulate's mean-path "
+    p.add_argument("--c4-schedule", default="sim", choices=["fused", "concurrent", "sim", "simkmv"],
+                   help="C4 steady state: 'sim' (default) = the simulator draws the next simulate's noise sums "
+                        "(pdeinv_sde_simulate_mf_next), plain KMV pass; 'simkmv' = the simulator also forms the KMV "
+                        "per-stamp sums from its staged rows (pdeinv_sde_simulate_mf_kmv: no trajectory re-read, "
+                        "measured slower with the trajectory written, DESIGN.md §4.3 r06); 'fused' = the next "
+                        "simulate's mean-path "
                         "sums inside the KMV pass; "
                         "'concurrent' = the unfused KMV pass (HBM-bound) on the main stream and pdeinv_mf_sums "
                         "(VALU-bound) on a side stream at the same time")

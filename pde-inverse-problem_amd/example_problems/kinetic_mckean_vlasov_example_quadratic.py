@@ -105,15 +105,28 @@ class KineticMcKeanVlasov(KineticFokkerPlanck):
         F = torch.as_tensor(self.initial_configuration["tilde_F"], dtype=x.dtype, device=x.device)
         return 0.5 * torch.sum(x * (x @ F.T), -1)
 
-    def simulate_interacting(self, rng: Key, batch_size: int, n_steps: int = None, particle_offset: int = 0):
-        """The McKean–Vlasov particle system (sample_scheme SDE): traj [n, N, 2d], shared tau [n]."""
-        from utils.mean_field import simulate_mean_field
+    def simulate_interacting(self, rng: Key, batch_size: int, n_steps: int = None, particle_offset: int = 0,
+                             stamp_sums: bool = False):
+        """The McKean–Vlasov particle system (sample_scheme SDE): traj [n, N, 2d], shared tau [n].
+        stamp_sums=True: no trajectory; instead the quadratic-Phi KMV residual's per-stamp sums formed inside the
+        simulator ("kmv_mom" / "kmv_wst", pdeinv_sde_simulate_mf_kmv) and the shared stamps "tau_0T" [n] (fp64 of
+        the simulator's fp32 stamps, computed on the host from the same Philox draw)."""
+        from utils.mean_field import simulate_mean_field, stamp_times
         n_steps = n_steps or self.n_steps
         k_init, k_sde = prng.split(rng)
         z0 = self.distribution_initial.sample(batch_size, k_init, row_offset=particle_offset)
         dt = self.total_evolving_time / n_steps
-        r = simulate_mean_field(z0, n_steps, dt, k_sde, self.interaction, self.initial_configuration["gamma_friction"],
-                                particle_offset=particle_offset, counter_offset=self._next_counter(n_steps))
+        gamma = self.initial_configuration["gamma_friction"]
+        ctr = self._next_counter(n_steps)
+        if not stamp_sums:
+            r = simulate_mean_field(z0, n_steps, dt, k_sde, self.interaction, gamma, particle_offset=particle_offset,
+                                    counter_offset=ctr)
+            return z0, r
+        tau = stamp_times(k_sde.seed, ctr, n_steps, dt).astype(np.float64)
+        r = simulate_mean_field(z0, n_steps, dt, k_sde, self.interaction, gamma, particle_offset=particle_offset,
+                                counter_offset=ctr, traj=False, tau=False,
+                                kmv_coef=self.coefficients(tau, z0.device), kmv_gamma=gamma)
+        r["tau_0T"] = tau
         return z0, r
 
     def create_parametric_model(self):

@@ -10,7 +10,8 @@ Deviations (documented in DESIGN.md):
     calls get_time_sample_ground_truth, which raises NotImplementedError for KOU in its default
     random_time mode (SURVEY.md §0.1);
   * for a quadratic model on an SDE-sampled problem the simulator accumulates the residual's
-    moment sets in the same kernel (data["moments"]), so the trajectory is never re-read.
+    moment sets in the same kernel (data["moments"]; McKean–Vlasov: the per-stamp sums, data["kmv_sums"]),
+    so the trajectory is never re-read.
 """
 from __future__ import annotations
 
@@ -80,11 +81,18 @@ class ConsistencyBased(Method):
                 if needs_tau:
                     data["tau_0T"] = pi.get_time_sample_ground_truth(rng_0T, spec)
             elif pi.sample_scheme == "SDE" and hasattr(pi, "simulate_interacting"):
-                # McKean–Vlasov: the interacting system on a shared clock (one tau per time stamp)
+                # McKean–Vlasov: the interacting system on a shared clock (one tau per time stamp). For a quadratic
+                # model the residual needs only per-stamp sums, which the simulator forms from its own rows
+                # (data["kmv_sums"], even dim <= 8): no trajectory is written or re-read
                 B = int(tr.sample_per_time)
-                _, r = pi.simulate_interacting(rng_0T, B, particle_offset=rank * B)
-                data = {"0T_tm": r["traj"], "tau_0T": r["tau"][:, 0].double().cpu().numpy(),
-                        "shared_time": True}
+                model = getattr(forward_fn, "__self__", forward_fn)
+                if getattr(model, "residual_kind", None) == "quadratic" and pi.dim % 2 == 0 and pi.dim <= 8:
+                    _, r = pi.simulate_interacting(rng_0T, B, particle_offset=rank * B, stamp_sums=True)
+                    data = {"kmv_sums": (r["kmv_mom"], r["kmv_wst"]), "tau_0T": r["tau_0T"], "shared_time": True}
+                else:
+                    _, r = pi.simulate_interacting(rng_0T, B, particle_offset=rank * B)
+                    data = {"0T_tm": r["traj"], "tau_0T": r["tau"][:, 0].double().cpu().numpy(),
+                            "shared_time": True}
             elif pi.sample_scheme == "SDE":
                 model = getattr(forward_fn, "__self__", forward_fn)
                 fused = getattr(model, "residual_kind", None) == "quadratic" and hasattr(pi, "simulate")

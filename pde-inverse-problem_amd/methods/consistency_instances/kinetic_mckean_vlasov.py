@@ -7,10 +7,10 @@ For a general Phi_theta (the non-parametric V_hypothesis of get_model) the pairs
 as they are in the reference — every (i, j) of each time stamp's particles — in two passes over
 pair rows on the MLP path (pdeinv_residual_kmv_mlp: gbar_i = mean_j grad Phi, then the per-pair
 adjoint). For the quadratic Phi_theta every pairwise mean is a function of the time stamp's moments, so
-the [m, n, n_time, d] pair tensor of :20-23 is replaced by:
-  pass 1  pdeinv_moments_batched — per time stamp [count, sum z, sum z z^T];
-  pass 2  pdeinv_kmv_weights     — per particle ds/ds2 log rho (the score/log-density
-          evaluation) and per time stamp the c-weighted [sum c, sum c x, sum c x x^T];
+the [m, n, n_time, d] pair tensor of :20-23 is replaced by per-time-stamp sums — [count, sum z, sum z z^T] and,
+with the per-particle ds/ds2 log rho (the score/log-density evaluation) as weight c, [sum c, sum c x, sum c x x^T] —
+  formed inside the McKean-Vlasov simulator from its own rows (pdeinv_sde_simulate_mf_kmv, data["kmv_sums"]), or
+  by one read of given rows (pdeinv_kmv_moments_weights; d > 8: pdeinv_moments_batched + pdeinv_kmv_weights);
   final   pdeinv_residual_kmv    — loss, loss ground truth, d loss / d(K, b).
 Multi-GPU: with a shared clock (the simulated interacting system, sample_scheme SDE) the
 per-time-stamp sums are all-reduced before the finalize (the exact global loss); with
@@ -50,10 +50,16 @@ def value_and_grad_fn(forward_fn, params, data, rng, pde_instance):
         raise NotImplementedError(f"no native KMV residual for model kind '{model.residual_kind}'")
     d = pde_instance.dim
     gamma = float(pde_instance.initial_configuration["gamma_friction"])
-    z, n_sets, n_rows, set_stride, ld, tau = layout(data, d)
-    mom = native.moments_batched(z, n_sets, n_rows, 2 * d, set_stride, ld)
-    coef = pde_instance.coefficients(tau, z.device)
-    wst, _ = native.kmv_weights(d, gamma, coef, z, n_sets, n_rows, set_stride, ld)
+    if "kmv_sums" in data:  # formed inside the McKean-Vlasov simulator (pdeinv_sde_simulate_mf_kmv)
+        mom, wst = data["kmv_sums"]
+    else:
+        z, n_sets, n_rows, set_stride, ld, tau = layout(data, d)
+        coef = pde_instance.coefficients(tau, z.device)
+        if d <= 8:  # one read of the rows for both sets of sums (pdeinv_kmv_moments_weights)
+            mom, wst = native.kmv_moments_weights(d, gamma, coef, z, n_sets, n_rows, set_stride, ld)
+        else:
+            mom = native.moments_batched(z, n_sets, n_rows, 2 * d, set_stride, ld)
+            wst, _ = native.kmv_weights(d, gamma, coef, z, n_sets, n_rows, set_stride, ld)
     theta = model.flat(params)
     F = pde_instance.initial_configuration["tilde_F"]
     if data.get("shared_time", False):

@@ -51,7 +51,8 @@ def stamp_times(seed: int, counter_offset: int, n_steps: int, dt: float, random_
 def simulate_mean_field(q0_p0: torch.Tensor, n_steps: int, dt: float, key: Key, potential, gamma: float, *,
                         particle_offset: int = 0, counter_offset: int = 0, noise_scale: float = math.sqrt(2.0),
                         random_shift: bool = True, noise: Optional[torch.Tensor] = None, traj: bool = True,
-                        tau: bool = True, exchange: str = "fused", out: Optional[dict] = None) -> dict:
+                        tau: bool = True, exchange: str = "fused", out: Optional[dict] = None,
+                        kmv_coef: Optional[torch.Tensor] = None, kmv_gamma: float = 1.0) -> dict:
     """Returns {"last" [N, 2d], "xsum" [n+2, 1+d] fp64 ([count, sum x] before each update and after the
     last, global over ranks), "traj" [n, N, 2d] time-major, "tau" [n, N]}. `out` may hold preallocated
     "traj" / "tau" / "last" buffers (fused path).
@@ -60,7 +61,11 @@ def simulate_mean_field(q0_p0: torch.Tensor, n_steps: int, dt: float, key: Key, 
     update (one all-reduce each). exchange="fused" (default): xsum = count * the closed-form fp64 mean
     path of DESIGN.md §4.3 (also returned as "xbar"), the model quantity the drift uses — equal to the
     measured ensemble mean in exact arithmetic and to fp32 rounding in practice (tested to 1e-6), but not
-    a measurement; take moments of "traj" / "last" for the measured means."""
+    a measurement; take moments of "traj" / "last" for the measured means.
+
+    kmv_coef [n, 3d + 2 + 2d^2] (fused path, Philox noise): the simulator also forms the quadratic-Phi KMV residual's
+    per-stamp sums of its own trajectory rows (pdeinv_sde_simulate_mf_kmv) — returned as "kmv_mom" / "kmv_wst"
+    (rank-local), with traj=False the trajectory is never written at all."""
     N, m = q0_p0.shape
     d = m // 2
     dev = q0_p0.device
@@ -79,8 +84,13 @@ def simulate_mean_field(q0_p0: torch.Tensor, n_steps: int, dt: float, key: Key, 
         sums = dist.allreduce_sum(native.mf_sums(desc, z0))  # the one collective of the simulate
         xbar, xs = native.mf_mean_path(desc, sums)
         desc.d_meanfield = ctypes.c_void_p(xbar.data_ptr())
-        native.sde_simulate_desc(desc, z0, res.get("traj") if traj else None, res.get("tau") if tau else None,
-                                 res["last"])
+        if kmv_coef is not None:
+            res["kmv_mom"], res["kmv_wst"] = native.sde_simulate_mf_kmv(
+                desc, z0, res.get("traj") if traj else None, res.get("tau") if tau else None, res["last"],
+                kmv_gamma, kmv_coef)
+        else:
+            native.sde_simulate_desc(desc, z0, res.get("traj") if traj else None, res.get("tau") if tau else None,
+                                     res["last"])
         del keep
         res["xsum"] = xs
         res["xbar"] = xbar

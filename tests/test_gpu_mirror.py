@@ -50,6 +50,42 @@ def test_kmv_residual_vs_pairwise_restatement(native):
     assert np.allclose(g.cpu().numpy(), g_fd, rtol=1e-3, atol=1e-3)
 
 
+@pytest.mark.parametrize("d", [2, 8])
+def test_kmv_sde_stamp_sums_product_path(native, d):
+    """The product path of the McKean-Vlasov SDE scheme with a quadratic model: sample_data takes the per-stamp sums
+    from the simulator (simulate_interacting(stamp_sums=True): pdeinv_sde_simulate_mf_kmv, no trajectory written),
+    value_and_grad_fn consumes data["kmv_sums"]; the same simulate with its trajectory written and the residual's own
+    pass over it gives the same loss / loss ground truth / gradient (fp32 reassociation: 1e-5 relative) and the same
+    stamps."""
+    from example_problems.kinetic_mckean_vlasov_example_quadratic import KineticMcKeanVlasov
+    from methods.consistency_instances import kinetic_mckean_vlasov as kmv
+    from core.model import QuadraticModel
+    from utils import prng
+    cfg = _cfg(["pde_instance=kinetic_mckean_vlasov", f"pde_instance.domain_dim={d}"])
+    pi = KineticMcKeanVlasov(cfg, prng.PRNGKey(0))
+    rng = np.random.default_rng(d)
+    model = QuadraticModel(d)
+    params = model.unflat(_t(np.concatenate([rng.standard_normal(d * d) * 0.3, rng.standard_normal(d) * 0.2])))
+    ctr = pi._counter
+    _, ra = pi.simulate_interacting(prng.PRNGKey(21), 3000)
+    pi._counter = ctr
+    _, rb = pi.simulate_interacting(prng.PRNGKey(21), 3000, stamp_sums=True)
+    assert "traj" not in rb
+    tau_a = ra["tau"][:, 0].double().cpu().numpy()
+    assert np.array_equal(tau_a, rb["tau_0T"])
+    res_a = kmv.value_and_grad_fn(model.apply, params, {"0T_tm": ra["traj"], "tau_0T": tau_a, "shared_time": True},
+                                  None, pi)
+    res_b = kmv.value_and_grad_fn(model.apply, params, {"kmv_sums": (rb["kmv_mom"], rb["kmv_wst"]),
+                                                        "tau_0T": rb["tau_0T"], "shared_time": True}, None, pi)
+    for k in ("loss", "loss ground truth"):
+        a, b = float(res_a[k]), float(res_b[k])
+        assert abs(a - b) < 1e-5 * (1 + abs(a)), (k, a, b)
+    ga = torch.cat([res_a["grad"]["params"]["tilde_F"]["kernel"].reshape(-1), res_a["grad"]["params"]["tilde_F"]["bias"]])
+    gb = torch.cat([res_b["grad"]["params"]["tilde_F"]["kernel"].reshape(-1), res_b["grad"]["params"]["tilde_F"]["bias"]])
+    assert (ga - gb).abs().max().item() < 1e-5 * (1 + ga.abs().max().item())
+    assert torch.equal(ra["last"], rb["last"])
+
+
 @pytest.mark.parametrize("d,n,chunk,W,L,impl", [(2, 40, 1 << 18, 20, 3, 0), (4, 37, 300, 20, 3, 1),
                                                 (4, 37, 300, 20, 3, 2), (3, 70, 300, 10, 2, 2),
                                                 (2, 130, 300, 20, 8, 2), (8, 65, 300, 28, 2, 2),
