@@ -33,9 +33,14 @@ def child(reps=20):
     runs = {
         "fused_sim_kmv": lambda: native.sde_simulate_mf_kmv(desc, z0, traj, tau, last, gamma, coef, nxt, z0),
         "fused_no_traj": lambda: native.sde_simulate_mf_kmv(desc, z0, None, None, last, gamma, coef, nxt, z0),
+        "sim_next_no_traj": lambda: native.sde_simulate_mf_next(desc, z0, None, None, last, nxt, z0),
         "sim_next": lambda: native.sde_simulate_mf_next(desc, z0, traj, tau, last, nxt, z0),
         "kmv_pass": lambda: native.kmv_moments_weights(d, gamma, coef, traj, n, N, N * 2 * d, 2 * d),
     }
+    only = os.environ.get("MFKMV_ONLY")
+    if only:  # e.g. under rocprofv3 --pmc: just these runs, fewer reps
+        runs = {k: v for k, v in runs.items() if k in only.split(",")}
+        reps = 3
     out = {}
     for name, fn in runs.items():
         for _ in range(3):
