@@ -27,6 +27,10 @@ from api import Method
 from utils import distributed as dist
 from utils import native, prng
 
+# McKean–Vlasov with a quadratic model: trajectories of at least this many bytes (n_steps x batch x 2d x 4) take the
+# per-stamp sums from the simulator instead of being written and read back by the KMV pass (a quarter of HBM)
+STAMP_SUMS_MIN_BYTES = 72 << 30
+
 INSTANCES = {
     "Fokker-Planck": fokker_planck,
     "Kinetic-Fokker-Planck": kinetic_fokker_planck,
@@ -82,11 +86,15 @@ class ConsistencyBased(Method):
                     data["tau_0T"] = pi.get_time_sample_ground_truth(rng_0T, spec)
             elif pi.sample_scheme == "SDE" and hasattr(pi, "simulate_interacting"):
                 # McKean–Vlasov: the interacting system on a shared clock (one tau per time stamp). For a quadratic
-                # model the residual needs only per-stamp sums, which the simulator forms from its own rows
-                # (data["kmv_sums"], even dim <= 8): no trajectory is written or re-read
+                # model the residual needs only per-stamp sums, which the simulator can form from its own rows
+                # (data["kmv_sums"], even dim <= 8: no trajectory written or re-read). That costs the simulator
+                # more than the KMV pass it saves (C4: 5.6 vs 5.4 ms), so it is taken only
+                # for a trajectory too large to keep beside the rest of HBM (STAMP_SUMS_MIN_BYTES).
                 B = int(tr.sample_per_time)
                 model = getattr(forward_fn, "__self__", forward_fn)
-                if getattr(model, "residual_kind", None) == "quadratic" and pi.dim % 2 == 0 and pi.dim <= 8:
+                traj_bytes = int(pi.n_steps) * B * 2 * pi.dim * 4
+                if (getattr(model, "residual_kind", None) == "quadratic" and pi.dim % 2 == 0 and pi.dim <= 8
+                        and traj_bytes >= STAMP_SUMS_MIN_BYTES):
                     _, r = pi.simulate_interacting(rng_0T, B, particle_offset=rank * B, stamp_sums=True)
                     data = {"kmv_sums": (r["kmv_mom"], r["kmv_wst"]), "tau_0T": r["tau_0T"], "shared_time": True}
                 else:

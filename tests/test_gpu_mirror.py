@@ -370,6 +370,22 @@ def test_trainer_kmv_exact_and_sde(native):
     assert all(np.isfinite(h["loss"]) for h in tr.history)
 
 
+def test_trainer_kmv_sde_stamp_sums_route(native, monkeypatch):
+    """The SDE scheme's two routes for a quadratic model (methods/consistency.py): trajectory + KMV pass (default at
+    this size) and the simulator's own stamp sums (STAMP_SUMS_MIN_BYTES = 0) train to the same losses (fp32
+    reassociation of the sums carried through the updates: 1e-4 relative)."""
+    import methods.consistency as mc
+    base = ["pde_instance=kinetic_mckean_vlasov", "pde_instance.domain_dim=2", "solver.train.sample_mode=grid_time",
+            "solver.train.sample_per_time=5000", "solver.train.n_time_stamps=1", "pde_instance.total_evolving_time=1",
+            "pde_instance.sample_scheme=SDE", "pde_instance.n_steps=20"]
+    ta = _run(base)
+    monkeypatch.setattr(mc, "STAMP_SUMS_MIN_BYTES", 0)
+    tb = _run(base)
+    la, lb = [h["loss"] for h in ta.history], [h["loss"] for h in tb.history]
+    assert len(la) == len(lb) > 0
+    assert np.allclose(la, lb, rtol=1e-4, atol=1e-6), (la, lb)
+
+
 def test_trainer_kmv_non_parametric(native):
     """estimation_mode=non-parametric under KMV (get_model -> V_hypothesis, the MLP.yaml net of
     width 20 x 8 layers): the general-Phi pair-row residual drives the trainer end to end."""
