@@ -7,15 +7,14 @@ using namespace pdeinv;
 // The quadratic-Phi KMV residual (kinetic_mckean_vlasov.py:11-120, kmv.hip) reads, per time stamp t = trajectory
 // row t, [count, sum z, sum z z^T] of z = [x, v] and the d_s log rho-weighted [sum w, sum w x, sum w x x^T] of x
 // (w = d_s^2 log rho + (d_s log rho)^2 + gamma d_s log rho, kinetic_mckean_vlasov.py:243-248). The simulator stages
-// each wave's 64 rows of update t in LDS for its coalesced store anyway; here the same staged rows feed two
-// v_mfma_f32_16x16x4_f32 products over K = the wave's rows, once per update:
-//   P1 = Z^T Z                            the Gram of z (features zero-padded to 16)
-//   P2 = A^T Z,  A = [w x (D), w, one, 0..]   sum w x x^T (rows < D), sum w x (row D), sum z (row D + 1)
-// (one = 1 on rows < N; staged rows past N are zero). A is staged beside z by each row's own lane, so the MFMA loop
-// is two LDS reads and two MFMAs per 4 rows; sum w is a wave sum and the count the block's valid rows. The waves of
-// a block add their tiles in LDS in a fixed order (one barrier per update, double-buffered) and the block writes one
-// partial column entry per sum (198 at d = 8); slab_reduce sums the blocks in fp64. Deterministic; no trajectory
-// re-read (the separate KMV pass reads the 13.4 GB C4 trajectory right after it was written).
+// each wave's 64 rows of update t in LDS for its coalesced store anyway; the same staged rows feed one
+// v_mfma_f32_16x16x4_f32 tile per stamp over K = the wave's rows (sde_mf_kmv_kernel below), the waves of a block add
+// their tiles in LDS in a fixed order (one barrier per 4 stamps), the block writes one partial column entry per sum
+// and slab_reduce sums the blocks in fp64. Deterministic; no trajectory re-read. The two blocks the residual uses
+// only summed over the stamps (sum w x x^T, the v v^T rest) come out as stamp totals.
+// Measured (profiles/r06_c4_fused_single_tile.txt): the kernel spends more on the stamp sums
+// (fp32 MFMA and the weight's VALU, which share the SIMD's issue) than the separate KMV pass spends streaming the
+// trajectory back, so the product path takes it only for trajectories too large to keep (methods/consistency.py).
 template <int D>
 constexpr int kmv_ncp() { return D + 2 + 2 * (D * (D + 1) / 2 + D); }
 template <int D>
@@ -124,7 +123,7 @@ __host__ __device__ constexpr int kmv_source(int e) {
   if (e == 0) return -1;                             // count
   if (e <= M) return word(D, e - 1);                 // sum z_k: row "one"
   if (e < LZ) {                                      // sum z_i z_j, i <= j
-    int i, j;
+    int i = 0, j = 0;
     tri(e - 1 - M, M, i, j);
     if (i < D) return word(i, j);                    // x x, x v
     const int va = i - D;
@@ -149,26 +148,14 @@ constexpr int kmv_nstamp() {
   return n;
 }
 
-#ifndef PDEINV_KMV_ABL
-#define PDEINV_KMV_ABL 0
-#endif
-#ifndef PDEINV_KMV_SPLIT
-#define PDEINV_KMV_SPLIT 0
-#endif
-#ifndef PDEINV_MF_KMV_BATCH
-#define PDEINV_MF_KMV_BATCH 4
-#endif
-#ifndef PDEINV_MF_KMV_MINW
-#define PDEINV_MF_KMV_MINW 1
-#endif
 template <int D, int WAVES, bool NXT>
-__global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(PDEINV_MF_KMV_MINW, 8))) void sde_mf_kmv_kernel(
+__global__ __launch_bounds__(64 * WAVES) void sde_mf_kmv_kernel(
     SdeArgs a, const float* __restrict__ z0, float* __restrict__ traj, float* __restrict__ tau,
     float* __restrict__ last, KmvStamps ks, MfNext nx) {
   constexpr int M = 2 * D, B = 64 * WAVES, NCP = kmv_ncp_pad<D>(), NA = kmv_na<D>();
   constexpr int LZ = moment_len(M), LW = moment_len(D), LT = LZ + LW;
   constexpr int NS = kmv_nstamp<D>(), NTOT = kmv_ntot<D>(), NVR = kmv_vv_rest<D>(), kRed = (NS + B - 1) / B;
-  constexpr int KB = PDEINV_MF_KMV_BATCH;  // stamps per block reduction (one barrier each)
+  constexpr int KB = 4;  // stamps per block reduction, one barrier each (2: the same time; 8: one block per CU)
   static_assert(KB > 0 && (KB & (KB - 1)) == 0, "power-of-two batch");
   static_assert(D % 2 == 0 && D <= 8, "even dim <= 8: 16-byte staged rows, a 16-feature tile");
   static_assert(D + 2 + NA <= 16, "A = [x, one, w, v_0..v_{nA-1}] in 16 features");
@@ -279,7 +266,7 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(PDEI
   auto stamp = [&](int s) {
     const float* cps = ks.cp + (int64_t)s * NCP;
     const bool live = n_valid == kWave || active;  // rows past N stage as zeros (weight 0, one = 0)
-    const float w = (PDEINV_KMV_ABL & 16) ? z[0] * cps[0] : (live ? kmv_weight<D>(z, cps, ks.gamma) : 0.f);
+    const float w = live ? kmv_weight<D>(z, cps, ks.gamma) : 0.f;
     const float one = live ? 1.f : 0.f;
     if (n_valid == kWave) {
 #pragma unroll
@@ -324,17 +311,15 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(PDEI
     int a_off = a_off0, b_off = b_off0;
     asm volatile("" : "+v"(a_off), "+v"(b_off));  // per stamp: not 32 addresses hoisted and held across stamps
 #pragma unroll
-    for (int j = 0; j < ((PDEINV_KMV_ABL & 8) ? 1 : 16); ++j) {
-      if (PDEINV_KMV_SPLIT && j > 0 && j % PDEINV_KMV_SPLIT == 0) __builtin_amdgcn_sched_barrier(0);
+    for (int j = 0; j < 16; ++j) {
       float av = stage[a_off + j * 4 * M];
       if constexpr (M < 16) av = c < M ? av : 0.f;
       // A[row][c] = [x (c < D) | one | w | v_(c-D-2)] from the same staged rows: x is av itself
       const float b = stage[b_off + j * b_str];
       const float a2 = c < D ? av : (c < D + 2 + NA ? b : 0.f);
-      if (PDEINV_KMV_ABL & 2) pt[j & 3] += a2 * av;
-      else pt = __builtin_amdgcn_mfma_f32_16x16x4f32(a2, av, pt, 0, 0, 0);
+      pt = __builtin_amdgcn_mfma_f32_16x16x4f32(a2, av, pt, 0, 0, 0);
     }
-    if (!(PDEINV_KMV_ABL & 4)) {
+    {
       int x_off = x_off0, w_off = w_off0;
       asm volatile("" : "+v"(x_off), "+v"(w_off));
 #pragma unroll
@@ -344,10 +329,6 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(PDEI
         const float wv = stage[w_off + 4 * j];
         pw = __builtin_amdgcn_mfma_f32_16x16x4f32(wv * xv, xv, pw, 0, 0, 0);
       }
-    }
-    if (PDEINV_KMV_ABL & 32) {
-      if (pt[0] + pt[1] + pt[2] + pt[3] + wsum == 12345.f) ks.partials[bid] = 1.f;
-      return;
     }
     const int kb = s & (KB - 1), buf = (s / KB) & 1;
     __builtin_amdgcn_wave_barrier();
@@ -371,7 +352,7 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(PDEI
 #pragma unroll
             for (int w2 = 0; w2 < WAVES; ++w2) sum += r[w2 * 256 + srcs[t]];
           }
-          if (!(PDEINV_KMV_ABL & 1) || sum == 12345.f) ks.partials[(st * NS + cols[t]) * nb + bid] = sum;
+          ks.partials[(st * NS + cols[t]) * nb + bid] = sum;
         }
       }
     }
@@ -459,10 +440,8 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(PDEI
   }
 }
 
-#ifndef PDEINV_MF_KMV_WAVES
-#define PDEINV_MF_KMV_WAVES 4  // waves per block of sde_mf_kmv_kernel (the stamp partials shrink with the block)
-#endif
-constexpr int kMfKmvBlock = 64 * PDEINV_MF_KMV_WAVES;
+constexpr int kMfKmvWaves = 4;  // waves per block of sde_mf_kmv_kernel
+constexpr int kMfKmvBlock = 64 * kMfKmvWaves;
 
 static int mf_kmv_grid(int64_t N) { return (int)((N + kMfKmvBlock - 1) / kMfKmvBlock); }
 
@@ -529,7 +508,7 @@ template <int D, bool NXT>
 static void launch_mf_kmv(const SdeArgs& a, const float* z0, float* traj, float* tau, float* last, const float* coef,
                           const KmvStamps& ks, const MfNext& nx, hipStream_t st) {
   hipLaunchKernelGGL(kmv_coef_pairs_kernel<D>, dim3((unsigned)a.n_steps), dim3(128), 0, st, coef, const_cast<float*>(ks.cp));
-  hipLaunchKernelGGL((sde_mf_kmv_kernel<D, PDEINV_MF_KMV_WAVES, NXT>), dim3(mf_kmv_grid(a.N)), dim3(kMfKmvBlock), 0,
+  hipLaunchKernelGGL((sde_mf_kmv_kernel<D, kMfKmvWaves, NXT>), dim3(mf_kmv_grid(a.N)), dim3(kMfKmvBlock), 0,
                      st, a, z0, traj, tau, last, ks, nx);
 }
 
