@@ -69,6 +69,21 @@ def gmm_residual_flops(d, K):
         + 6 * K * d
 
 
+def mf_sim_flops(d):
+    """Algorithmic fp32 FLOP of one particle-update of the McKean-Vlasov simulator (FMA = 2): y = x - xbar_s (d),
+    A y (2d^2), the EM update of v and x (8d). Box-Muller and the Philox integer work are not counted."""
+    return d + 2 * d * d + 8 * d
+
+
+def kmv_stamp_flops(d):
+    """Algorithmic fp32 FLOP of one particle-stamp of the quadratic-Phi KMV sums (kmv_moments_weights order): sum z
+    (2d), sum z z^T over the upper triangle (2 per entry, m = 2d), r = m1 - x (d), the two quadratic forms of the
+    weight over the symmetric pairs (4 per pair and per b_i: 4 (d(d+1)/2 + d)), w = q1 + q0^2 + gamma q0 (4),
+    sum w (1), sum w x (2d), sum w x x^T (d products + 2 per upper entry)."""
+    m, nt = 2 * d, d * (d + 1) // 2
+    return 2 * d + m * (m + 1) + d + 4 * (nt + d) + 4 + 1 + 2 * d + d + 2 * nt
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -98,15 +113,13 @@ def parse():
     p.add_argument("--c4-separate-sums", action="store_true",
                    help="C4: the next simulate's mean-path sums as their own launch (pdeinv_mf_sums) instead of "
                         "inside the KMV pass (pdeinv_kmv_moments_weights_mf_sums), for A/B")
-    p.add_argument("--c4-schedule", default="sim", choices=["fused", "concurrent", "sim", "simkmv"],
-                   help="C4 steady state: 'sim' (default) = the simulator draws the next simulate's noise sums "
-                        "(pdeinv_sde_simulate_mf_next), plain KMV pass; 'simkmv' = the simulator also forms the KMV "
-                        "per-stamp sums from its staged rows (pdeinv_sde_simulate_mf_kmv: no trajectory re-read, "
-                        "measured slower with the trajectory written, DESIGN.md §4.3 r06); 'fused' = the next "
-                        "simulate's mean-path "
-                        "sums inside the KMV pass; "
-                        "'concurrent' = the unfused KMV pass (HBM-bound) on the main stream and pdeinv_mf_sums "
-                        "(VALU-bound) on a side stream at the same time")
+    p.add_argument("--c4-schedule", default="simkmv", choices=["fused", "concurrent", "sim", "simkmv"],
+                   help="C4 steady state: 'simkmv' (default, the product path of methods/consistency.py) = the "
+                        "simulator forms the KMV per-stamp sums from its staged rows and draws the next simulate's "
+                        "noise sums (pdeinv_sde_simulate_mf_kmv): no trajectory written or read; 'sim' = the "
+                        "simulator writes the trajectory and draws the next sums (pdeinv_sde_simulate_mf_next), then "
+                        "one KMV pass reads it; 'fused' = the next sums inside the KMV pass; 'concurrent' = on a "
+                        "side stream (DESIGN.md §4.3)")
     p.add_argument("--cpu-procs", type=int, default=0,
                    help="CPU-baseline shard processes (0 = the per-GPU host share, os.cpu_count() // 8)")
     return p.parse_args()
@@ -479,7 +492,8 @@ def run_c4(a, rank, world, dev):
         if kmv_in_sim:  # the simulator also forms the KMV per-stamp sums and draws the next simulate's noise sums
             desc_n, keep_n = native.mf_desc(N, d, n, T / n, gamma, A, seed=key.seed,
                                             counter_offset=(counter[0] + n + 1) & 0xFFFFFFFF, particle_offset=poff)
-            mom, wst, sums_next[0] = native.sde_simulate_mf_kmv(desc, z0, bufs["traj"], bufs["tau"], bufs["last"],
+            # as the product path (methods/consistency.py): the residual needs only these sums, no trajectory
+            mom, wst, sums_next[0] = native.sde_simulate_mf_kmv(desc, z0, None, None, bufs["last"],
                                                                 gamma, coef, desc_n, z0)
             del keep_n
         elif sim_sums:  # the simulator also draws the NEXT simulate's mean-path noise sums (same z0 ensemble)
@@ -591,9 +605,20 @@ def run_c4(a, rank, world, dev):
                        "residual value_and_grad (one fused read of the trajectory)",
            "dim": d, "n_steps": n, "particles_per_gpu": N, "particles_total": total, "total_time": T, "gamma": gamma,
            "parallelism": f"dp{world}"}
-    out = base_record(a, world, value, ms, cfg, kern_ms, sim_bytes(N, n, d),
-                      "sde_simulate_kernel<8,MEANFIELD_QUADRATIC,staged> (all 101 updates)",
-                      traffic_from_profiles("sde_simulate_C4_bytes_per_launch") if (N, n) == (1 << 21, 100) else None)
+    kmv_in_sim = a.c4_schedule == "simkmv" and not a.c4_separate_sums and not pipeline
+    if kmv_in_sim:  # no trajectory: the launch is bound by its fp32 issue (VALU and the f32 MFMA share the SIMD)
+        cfg["workload"] = cfg["workload"].replace("KMV residual value_and_grad (one fused read of the trajectory)",
+                                                  "KMV residual value_and_grad from per-stamp sums the simulator "
+                                                  "forms (no trajectory written or read)")
+        out = base_record(a, world, value, ms, cfg, kern_ms, N * (8 * d + 8 * d),
+                          "sde_mf_kmv_kernel<8,4,next sums> (all 101 updates + the KMV per-stamp sums of 100 stamps "
+                          "+ the next simulate's 101 x 8 normals per particle) + slab reduce + mf_sums tail",
+                          None, flops_launch=N * ((n + 1) * mf_sim_flops(d) + n * kmv_stamp_flops(d)))
+    else:
+        out = base_record(a, world, value, ms, cfg, kern_ms, sim_bytes(N, n, d),
+                          "sde_simulate_kernel<8,MEANFIELD_QUADRATIC,staged> (all 101 updates)",
+                          traffic_from_profiles("sde_simulate_C4_bytes_per_launch") if (N, n) == (1 << 21, 100)
+                          else None)
     sums_ms = float(np.mean([s.elapsed_time(e) for s, e in ev["sums"]]))
     res_ms = float(np.mean([s.elapsed_time(e) for s, e in ev["res"]]))
     res_bytes = N * n * 8 * d
@@ -602,7 +627,9 @@ def run_c4(a, rank, world, dev):
                           "serial" + (", separate mean-path sums" if a.c4_separate_sums else
                                       (", mean-path sums of the next simulate on a side stream concurrent with the "
                                        "KMV pass" if a.c4_schedule == "concurrent" else
-                                       (", mean-path noise sums of the next simulate drawn inside the simulator"
+                                       (", the KMV per-stamp sums and the next simulate's mean-path noise sums "
+                                        "formed inside the simulator (no trajectory)" if kmv_in_sim else
+                                        ", mean-path noise sums of the next simulate drawn inside the simulator"
                                         if a.c4_schedule == "sim" else
                                         ", mean-path sums of the next simulate inside the KMV pass"))))
     if a.c4_separate_sums or pipeline:
@@ -610,6 +637,9 @@ def run_c4(a, rank, world, dev):
                             "ms": sums_ms, "normals_per_s": N * (n + 1) * d / (sums_ms / 1e3)}
         out["residual"] = {"kernel": "kmv_moments_weights_kernel<8> + slab reduce + split", "ms": res_ms,
                            "algorithmic_bytes": res_bytes, "GBps": res_bytes / (res_ms / 1e3) / 1e9}
+    elif kmv_in_sim:
+        out["mean_path"] = {"kernel": "all-reduce of the sums the previous simulate drew + mf_path_kernel", "ms": sums_ms}
+        out["residual"] = {"kernel": "all-reduce of the per-stamp sums + kmv_terms / kmv_combine", "ms": res_ms}
     elif a.c4_schedule == "sim":
         out["mean_path"] = {"kernel": "all-reduce of the sums the previous simulate drew + mf_path_kernel", "ms": sums_ms}
         out["roofline"]["kernel"] = ("sde_simulate_kernel<8,MEANFIELD_QUADRATIC,staged,next sums> (all 101 updates + the "

@@ -164,13 +164,10 @@ int pdeinv_sde_simulate_mf_next(const pdeinv_sde_desc* desc, const float* d_z0, 
                                 float* d_last, const pdeinv_sde_desc* next, const float* d_z0_next,
                                 void* d_workspace, double* d_sums_next, void* stream);
 /* ABI 10. pdeinv_sde_simulate (fused McKean–Vlasov path, desc->d_meanfield set) that also forms the quadratic-Φ
- * KMV residual's per-time-stamp sums of its own trajectory rows 0..n_steps-1 in the layout of
- * pdeinv_kmv_moments_weights(dim, gamma, d_coef, d_traj, n_steps, N, N*2d, 2d) (d_mom [n_steps, moment_len(2d)],
- * d_wstats [n_steps, moment_len(d)] fp64, rank-local), equal to it up to the fp32 summation order, with one
- * difference: the entries pdeinv_residual_kmv reads only summed over the stamps — Σ w x xᵀ (d_wstats entries
- * 1 + d …) and, at d = 8, the v vᵀ entries (a, b ≥ 6) — hold their total over the stamps on stamp 0 and zero on the
- * others (the residual and its gradient are unchanged). Formed from the rows the simulator stages for its
- * stores, so the trajectory is not read back (d_traj may be NULL). d_coef
+ * KMV residual's per-time-stamp sums of its own trajectory rows 0..n_steps-1 — exactly what
+ * pdeinv_kmv_moments_weights(dim, gamma, d_coef, d_traj, n_steps, N, N*2d, 2d) returns (d_mom [n_steps,
+ * moment_len(2d)], d_wstats [n_steps, moment_len(d)] fp64, rank-local), up to the fp32 summation order — from the
+ * rows the simulator stages for its stores, so the trajectory is not read back (d_traj may be NULL). d_coef
  * [n_steps, 3d + 2 + 2d^2] as pdeinv_kmv_weights. With `next` non-NULL it also returns the next simulate's
  * pdeinv_mf_sums in d_sums_next as pdeinv_sde_simulate_mf_next (same restrictions: counter offset only,
  * n_steps + 1 <= 128). Even dim <= 8, Philox noise (else PDEINV_ERR_UNSUPPORTED); deterministic. Replaces the

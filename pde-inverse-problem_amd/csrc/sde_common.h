@@ -68,38 +68,18 @@ __device__ __forceinline__ kfloat* kernarg_params() {
 // as 46 v_readlane per update (C4 step loop 208 -> 162 VALU instructions per update).
 // xbar_s through the constant address space: a scalar load (lgkmcnt). As a global load it was a vector load whose
 // vmcnt wait, on gfx950, also waited for every trajectory store of the previous update still in flight.
-// 16 uniform floats into scalar registers, waited for in place: the compiler can neither hoist nor batch these loads,
-// so one chunk is live at a time (a kernel whose other scalar operands leave no room for A's d^2 floats at once).
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-// `after` is a value computed from the previous chunk: the load is issued after it (an input of the asm), not
-// hoisted above the previous chunk's uses, which would put every chunk in the scalar file at once again.
-__device__ __forceinline__ f32x16 sgpr_chunk16(kfloat* p, float after) {
-  f32x16 r;
-  asm volatile("s_load_dwordx16 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(p), "v"(after) : "memory");
-  return r;
-}
-
-template <int D, bool CHUNKED = false>
+template <int D>
 __device__ __forceinline__ void grad_meanfield(const SdeArgs&, const float* q, const float* xbp, float* g) {
   kfloat* A = kernarg_params();
   kfloat* xb = (kfloat*)xbp;
   float y[D];
 #pragma unroll
   for (int c = 0; c < D; ++c) y[c] = q[c] - xb[c];
-  [[maybe_unused]] f32x16 ch;
 #pragma unroll
   for (int r = 0; r < D; ++r) {
     float acc = 0.f;
 #pragma unroll
-    for (int c = 0; c < D; ++c) {
-      const int e = r * D + c;
-      if constexpr (CHUNKED) {
-        if (e % 16 == 0) ch = sgpr_chunk16(A + e, r > 0 ? g[r - 1] : y[0]);
-        acc = fmaf(ch[e % 16], y[c], acc);
-      } else {
-        acc = fmaf(A[e], y[c], acc);
-      }
-    }
+    for (int c = 0; c < D; ++c) acc = fmaf(A[r * D + c], y[c], acc);
     g[r] = acc;
   }
 }

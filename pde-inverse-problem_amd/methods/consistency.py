@@ -27,9 +27,10 @@ from api import Method
 from utils import distributed as dist
 from utils import native, prng
 
-# McKean–Vlasov with a quadratic model: trajectories of at least this many bytes (n_steps x batch x 2d x 4) take the
-# per-stamp sums from the simulator instead of being written and read back by the KMV pass (a quarter of HBM)
-STAMP_SUMS_MIN_BYTES = 72 << 30
+# McKean–Vlasov with a quadratic model: trajectories of at least this many bytes (n_steps x batch x 2d x 4) are not
+# written; the simulator forms the KMV per-stamp sums from its own rows instead (0: always — C4 step 5.9 -> 5.7 ms,
+# DESIGN.md §4.3 r06). A large value restores trajectory + KMV pass (tests compare the two routes).
+STAMP_SUMS_MIN_BYTES = 0
 
 INSTANCES = {
     "Fokker-Planck": fokker_planck,
@@ -86,10 +87,8 @@ class ConsistencyBased(Method):
                     data["tau_0T"] = pi.get_time_sample_ground_truth(rng_0T, spec)
             elif pi.sample_scheme == "SDE" and hasattr(pi, "simulate_interacting"):
                 # McKean–Vlasov: the interacting system on a shared clock (one tau per time stamp). For a quadratic
-                # model the residual needs only per-stamp sums, which the simulator can form from its own rows
-                # (data["kmv_sums"], even dim <= 8: no trajectory written or re-read). That costs the simulator
-                # more than the KMV pass it saves (C4: 5.6 vs 5.4 ms), so it is taken only
-                # for a trajectory too large to keep beside the rest of HBM (STAMP_SUMS_MIN_BYTES).
+                # model the residual needs only per-stamp sums, which the simulator forms from its own rows
+                # (data["kmv_sums"], even dim <= 8: no trajectory written or re-read; STAMP_SUMS_MIN_BYTES).
                 B = int(tr.sample_per_time)
                 model = getattr(forward_fn, "__self__", forward_fn)
                 traj_bytes = int(pi.n_steps) * B * 2 * pi.dim * 4

@@ -371,15 +371,15 @@ def test_trainer_kmv_exact_and_sde(native):
 
 
 def test_trainer_kmv_sde_stamp_sums_route(native, monkeypatch):
-    """The SDE scheme's two routes for a quadratic model (methods/consistency.py): trajectory + KMV pass (default at
-    this size) and the simulator's own stamp sums (STAMP_SUMS_MIN_BYTES = 0) train to the same losses (fp32
+    """The SDE scheme's two routes for a quadratic model (methods/consistency.py): the simulator's own stamp sums
+    (default) and trajectory + KMV pass (STAMP_SUMS_MIN_BYTES raised past the trajectory) train to the same losses (fp32
     reassociation of the sums carried through the updates: 1e-4 relative)."""
     import methods.consistency as mc
     base = ["pde_instance=kinetic_mckean_vlasov", "pde_instance.domain_dim=2", "solver.train.sample_mode=grid_time",
             "solver.train.sample_per_time=5000", "solver.train.n_time_stamps=1", "pde_instance.total_evolving_time=1",
             "pde_instance.sample_scheme=SDE", "pde_instance.n_steps=20"]
     ta = _run(base)
-    monkeypatch.setattr(mc, "STAMP_SUMS_MIN_BYTES", 0)
+    monkeypatch.setattr(mc, "STAMP_SUMS_MIN_BYTES", 1 << 62)
     tb = _run(base)
     la, lb = [h["loss"] for h in ta.history], [h["loss"] for h in tb.history]
     assert len(la) == len(lb) > 0
