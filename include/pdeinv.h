@@ -364,13 +364,13 @@ int pdeinv_residual_kmv(const pdeinv_kmv_desc* desc, const double* d_mom, const 
  * reverse sweep and the weight-gradient outer products, as dense GEMMs (rocBLAS sgemm, fp32) plus
  * fused element-wise kernels, chunked over chunk_rows rows. impl selects the implementation:
  * PDEINV_MLP_IMPL_AUTO and PDEINV_MLP_IMPL_FUSED take the hand-written fused path for every d <= 16,
- * 1 <= L <= 16, W <= 512 and any out_features: fp32 MFMA GEMMs whose prologues and epilogues carry all of
+ * 1 <= L <= 16, W <= 1024 and any out_features: fp32 MFMA GEMMs whose prologues and epilogues carry all of
  * the element-wise algebra (layer 1 is recomputed from the rows, never stored; L = 1 runs the output layer
  * off the layer-1 prologue). The kernels are compiled for d in {2, 4, 8, 16} and W in {32, 64, 128, 256,
- * 512}; other d / W (e.g. the reference default 20 x 8 layers, MLP.yaml) run zero-padded to the next
+ * 512, 1024}; other d / W (e.g. the reference default 20 x 8 layers, MLP.yaml) run zero-padded to the next
  * compiled one (exact; rows, parameters and the true potential padded, the gradient unpadded, on the
- * device). PDEINV_MLP_IMPL_LIBRARY forces the rocBLAS + element-wise-kernel path (explicit opt-in; also
- * the only path for W > 512); FUSED on a shape outside the above returns PDEINV_ERR_UNSUPPORTED.
+ * device). PDEINV_MLP_IMPL_LIBRARY forces the rocBLAS + element-wise-kernel path (explicit opt-in, the
+ * only way rocBLAS is loaded); AUTO and FUSED on a shape outside the above return PDEINV_ERR_UNSUPPORTED.
  * d_params / d_grad: flat flax order [K_1 (d x W), b_1, K_2 (W x W), b_2, ..., K_o (W x out), b_o]
  * (pdeinv_mlp_param_count floats). d_acc [PDEINV_GMM_NACC] and d_grad are ACCUMULATED (+=): zero
  * them first. pdeinv_kfp_terms_finalize turns (acc, grad) into the PDEINV_KFP_* slots.
