@@ -100,9 +100,37 @@ def dp_residual(out_dir, shards="0", B=(3000, 2000, 40000)):
     np.savez(os.path.join(out_dir, f"rank{rank}.npz"), world=world, **res)
 
 
+def kmv_stamp_sums(out_dir, N="6000", d="8"):
+    """The McKean-Vlasov product route of methods/consistency.py on this rank's share of N particles: the simulator
+    forms the rank-local KMV per-stamp sums (simulate_interacting(stamp_sums=True), its mean field all-reduced
+    inside), value_and_grad_fn all-reduces them (shared clock). Saves loss / grad and this rank's last states."""
+    from core.model import QuadraticModel
+    from example_problems.kinetic_mckean_vlasov_example_quadratic import KineticMcKeanVlasov
+    from methods.consistency_instances import kinetic_mckean_vlasov as kmv
+    from utils import config, prng
+    from utils import distributed as dist
+    N, d = int(N), int(d)
+    rank, world = dist.rank(), dist.world_size()
+    dev = torch.device("cuda", dist.local_device())
+    off, cnt = dist.shard(N)
+    cfg = config.compose("config", ["pde_instance=kinetic_mckean_vlasov", f"pde_instance.domain_dim={d}"])
+    pi = KineticMcKeanVlasov(cfg, prng.PRNGKey(0))
+    _, r = pi.simulate_interacting(prng.PRNGKey(21), cnt, particle_offset=off, stamp_sums=True)
+    rng = np.random.default_rng(3)
+    net = QuadraticModel(d)
+    params = net.unflat(torch.as_tensor(np.concatenate([rng.standard_normal(d * d) * 0.3,
+                                                        rng.standard_normal(d) * 0.2]).astype(np.float32), device=dev))
+    out = kmv.value_and_grad_fn(net.apply, params, {"kmv_sums": (r["kmv_mom"], r["kmv_wst"]), "tau_0T": r["tau_0T"],
+                                                    "shared_time": True}, None, pi)
+    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), world=world, off=off, loss=float(out["loss"]),
+             loss_gt=float(out["loss ground truth"]), grad=_flat_grad(out["grad"]).double().cpu().numpy(),
+             last=r["last"].cpu().numpy(), tau=r["tau_0T"])
+
+
 if __name__ == "__main__":
     from utils import distributed as dist
     dist.init_from_env()
-    {"mean_field": mean_field, "dp_residual": dp_residual}[sys.argv[1]](*sys.argv[2:])
+    {"mean_field": mean_field, "dp_residual": dp_residual,
+     "kmv_stamp_sums": kmv_stamp_sums}[sys.argv[1]](*sys.argv[2:])
     if dist.is_distributed():
         torch.distributed.destroy_process_group()

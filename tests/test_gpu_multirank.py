@@ -137,6 +137,31 @@ def test_bench_strong_scaling_c4_two_ranks(native):
     assert abs(out["value"] * out["ms_per_step"] / 1e3 - total * 101) < 1e-6 * out["value"]
 
 
+def test_kmv_stamp_sums_route_is_rank_count_invariant(native, tmp_path):
+    """The McKean-Vlasov SDE product route (the simulator's own KMV stamp sums, no trajectory) over 2 ranks equals
+    the 1-rank run of the whole ensemble: the same stamps, the last states after concatenation to 2e-5 (ids are
+    rank-invariant; the mean field's fp64 partial sums add in another order), loss / ground truth / gradient from
+    the all-reduced stamp sums to the fp32 partial-sum order (1e-5 relative)."""
+    worker = [os.path.join(ROOT, "tests", "mp_gpu_worker.py"), "kmv_stamp_sums"]
+    ref = tmp_path / "w1"
+    ref.mkdir()
+    r = subprocess.run([sys.executable] + worker + [str(ref)], cwd=ROOT, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr[-3000:]
+    a = dict(np.load(ref / "rank0.npz"))
+    w2 = tmp_path / "w2"
+    w2.mkdir()
+    r = _launch(2, worker + [str(w2)], 29661)
+    assert r.returncode == 0, r.stderr[-3000:]
+    parts = [dict(np.load(w2 / f"rank{k}.npz")) for k in range(2)]
+    assert all(int(p["world"]) == 2 for p in parts)
+    assert np.array_equal(parts[0]["tau"], a["tau"])
+    assert np.allclose(np.concatenate([p["last"] for p in parts]), a["last"], rtol=0, atol=2e-5)
+    for p in parts:
+        for k in ("loss", "loss_gt"):
+            assert abs(float(p[k]) - float(a[k])) < 1e-5 * (1 + abs(float(a[k]))), (k, p[k], a[k])
+        assert np.abs(p["grad"] - a["grad"]).max() < 1e-5 * (1 + np.abs(a["grad"]).max())
+
+
 def test_dp_residual_matches_pmap_mean_of_shards(native, tmp_path):
     """2 ranks (gloo) vs the two shards evaluated one at a time: loss and grad = the shard means,
     grad_norm = the mean of the shard gradients' norms (trainer.py:44-53), for the quadratic, GMM and
