@@ -14,6 +14,7 @@
 #                                                        one --pmc pass per counter group over bench.py --config
 #   bash tools/lease.sh final <tag>                      tests + check + C3/C4/C5 lines + their profiles + RealNVP
 #                                                        + the pair recipe + the C5 traffic passes
+#   bash tools/lease.sh extra <tag>                      the last three alone
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" && mkdir -p gpurun_out
 R=$PWD
@@ -98,11 +99,13 @@ case $MODE in
   check) run_check ;;
   prof) run_prof "$@" ;;
   pmc) run_pmc "$@" ;;
-  final)
-    run_tests
-    run_check
-    run_bench C3 C4 C5
-    run_prof C3 C4 C5
+  final|extra)
+    if [ $MODE = final ]; then
+      run_tests
+      run_check
+      run_bench C3 C4 C5
+      run_prof C3 C4 C5
+    fi
     timeout -k 10 200 python3 tools/nvp_bench.py --steps 30 --warmup 5 --dims 2,4 > gpurun_out/final_${TAG}_nvp.jsonl 2>&1
     rc=$?; echo "nvp rc=$rc"; fatal $rc nvp
     timeout -k 10 300 python3 tools/kmv_mlp_time.py 2,5000,1,20,8,2 > gpurun_out/final_${TAG}_pairs.jsonl 2>&1
