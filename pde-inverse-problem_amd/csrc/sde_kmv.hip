@@ -16,6 +16,9 @@ using namespace pdeinv;
 // a block add their tiles in LDS in a fixed order (one barrier per update, double-buffered) and the block writes one
 // partial column entry per sum (198 at d = 8); slab_reduce sums the blocks in fp64. Deterministic; no trajectory
 // re-read (the separate KMV pass reads the 13.4 GB C4 trajectory right after it was written).
+// Measured at C4: 5.1 ms without the trajectory against 2.9 + 2.5 ms for simulate + KMV pass;
+// the launch is bound by fp32 issue (the f32 MFMA shares the SIMD's issue with the simulator's VALU). A one-tile
+// form with lane-private / split-K stamp totals and a spill-free form with chunked scalar operands measured slower.
 template <int D>
 constexpr int kmv_ncp() { return D + 2 + 2 * (D * (D + 1) / 2 + D); }
 
